@@ -1,0 +1,43 @@
+# Builds the MI355X codec library in-tree (it travels to the GPU box with the
+# snapshot) and the parity checker under oracle/.
+#
+#   make            -> coldforce_amd/libcfws.so + oracle/liboracle.so
+#   make ref        -> also oracle/_ref/ (reference codec, needs /root/reference)
+
+HIPCC    ?= /opt/rocm/bin/hipcc
+ARCH     ?= gfx950
+HIPFLAGS ?= -O3 -std=c++17 -fPIC -Wall -Wno-unused-result
+SRC      := coldforce_amd/csrc/cfws_device.hip coldforce_amd/csrc/cfws_frame.cpp
+HDR      := include/cfws.h include/cfws_co_ws_frame.h
+LIB      := coldforce_amd/libcfws.so
+OBJDIR   := build
+
+all: $(LIB) oracle
+
+$(OBJDIR)/cfws_device.o: coldforce_amd/csrc/cfws_device.hip $(HDR)
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) --offload-arch=$(ARCH) $(HIPFLAGS) -Iinclude -c $< -o $@
+
+$(OBJDIR)/cfws_frame.o: coldforce_amd/csrc/cfws_frame.cpp $(HDR)
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) --offload-arch=$(ARCH) $(HIPFLAGS) -Iinclude -c $< -o $@
+
+$(LIB): $(OBJDIR)/cfws_device.o $(OBJDIR)/cfws_frame.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $^
+
+oracle:
+	$(MAKE) -s -C oracle
+
+ref: all
+	$(MAKE) -s -C oracle ref
+
+asm: coldforce_amd/csrc/cfws_device.hip $(HDR)
+	@mkdir -p $(OBJDIR)/asm
+	$(HIPCC) --offload-arch=$(ARCH) $(HIPFLAGS) -Iinclude -c $< -o $(OBJDIR)/asm/cfws_device.o \
+	    -save-temps=obj -Rpass-analysis=kernel-resource-usage 2> $(OBJDIR)/asm/resource-usage.txt
+
+clean:
+	rm -rf $(OBJDIR) $(LIB)
+	$(MAKE) -s -C oracle clean
+
+.PHONY: all oracle ref asm clean

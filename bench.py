@@ -1,0 +1,222 @@
+#!/usr/bin/env python3
+"""bench.py -- BASELINE.json metric: device-resident WebSocket payload
+mask/unmask GiB/s on 64 KiB binary frames, one process per MI355X.
+
+Workload (BASELINE.json configs[1]): per GPU a batch
+of 65,536 binary frames x 64 KiB payload (4 GiB), client-mask then
+server-unmask, device resident. One step =
+  cfws_serialize_plan + cfws_serialize_execute    (co_ws_frame_serialize x 65,536,
+                                                   mask = true: header + XOR mask)
+  cfws_deserialize_plan + cfws_deserialize_execute (co_ws_frame_deserialize at every
+                                                   frame start: header parse + copy
+                                                   + XOR unmask)
+value = payload bytes processed by both ops on all ranks / wall time of the
+K timed steps (max over ranks), in GiB/s (2^30). With N GPUs each rank owns
+its own 65,536-frame shard of one global batch (weak scaling, no collective
+on the data path; the only collectives are the timing barrier and max).
+
+Usage: python bench.py [--gpus N --steps K --warmup W]
+       torchrun --nproc-per-node N bench.py --gpus N ...   (N > 1)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+GIB = float(1 << 30)
+METRIC = "WS payload mask/unmask GiB/s device-resident, 64KiB frames, 1/2/4/8 GPUs"
+PAYLOAD_SEED = 0x5EED0002
+KEY_SEED = 2
+
+
+def parse():
+    ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--frames", type=int, default=65536, help="frames per GPU")
+    ap.add_argument("--frame-size", type=int, default=65536)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0,
+                    help="target CPU time of the cpu_baseline sample")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+def cpu_baseline(frame_size: int, seconds: float):
+    """Reference codec (oracle/_ref, compiled from coldforce's own sources)
+    when it was built, else the clean-room port; timed on this host."""
+    import oracle
+    kind = "reference" if oracle.ref_lib("O2") is not None else "port"
+    try:
+        cpus = len(os.sched_getaffinity(0))
+    except AttributeError:
+        cpus = os.cpu_count() or 1
+    threads = max(1, min(16, cpus))
+    n = 1024 * threads // 4 if threads >= 4 else 1024
+    ms, us = oracle.cpu_bench(n, frame_size, threads, 1, kind)
+    iters = max(1, int(math.ceil(seconds / max(ms + us, 1e-3))))
+    if iters > 1:
+        ms, us = oracle.cpu_bench(n, frame_size, threads, iters, kind)
+    payload = n * frame_size * iters
+    return {
+        "value": round(2 * payload / (ms + us) / GIB, 3),
+        "unit": "GiB/s",
+        "cores": threads,
+        "kind": kind,
+        "sample": (f"{n} x {frame_size // 1024} KiB binary frames x {iters} iters, per-frame "
+                   f"co_ws_frame_serialize(mask) + co_ws_frame_deserialize"
+                   f"{' (reference -O2, oracle/_ref)' if kind == 'reference' else ' (port, -O2)'},"
+                   f" {threads} threads"),
+        "mask_gibs": round(payload / ms / GIB, 3),
+        "unmask_gibs": round(payload / us / GIB, 3),
+        "seconds": round(ms + us, 2),
+    }
+
+
+def load_traffic(kernel: str):
+    """HBM bytes per launch from the committed PMC pass (profiles/), if any."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            data = json.load(f)
+        return data.get(kernel, {}).get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    from coldforce_amd import cfws, shard
+    from coldforce_amd import workloads as W
+
+    rank, local_rank, world = shard.world()
+    if args.gpus != world and world == 1 and args.gpus > 1:
+        sys.exit("bench.py: --gpus > 1 needs torchrun (one process per GPU)")
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    cfws.init()
+
+    F, fs = args.frames, args.frame_size
+    desc_np, byte_base = shard.uniform_shard(F, fs, KEY_SEED, rank, world)
+    offs, wire_total = W.wire_layout(desc_np)
+    payload = torch.empty(F * fs, dtype=torch.uint8, device=dev)
+    cfws.fill_splitmix(payload, PAYLOAD_SEED, byte_base)
+    wire = torch.empty(W.round16(wire_total), dtype=torch.uint8, device=dev)
+    back = torch.empty(F * fs, dtype=torch.uint8, device=dev)
+    desc_ser = cfws.desc_to_device(desc_np, dev)
+    desc_de = torch.empty((F, 32), dtype=torch.uint8, device=dev)
+    status = torch.empty(F, dtype=torch.int32, device=dev)
+    index = torch.from_numpy(offs.astype("int64")).to(dev)
+    ws_ser = cfws.workspace(F, wire.numel(), dev)
+    ws_de = cfws.workspace(F, back.numel(), dev)
+    tot_ser = torch.zeros(1, dtype=torch.int64, device=dev)
+    tot_de = torch.zeros(1, dtype=torch.int64, device=dev)
+
+    def step(ev=None):
+        cfws.serialize_plan(desc_ser, wire.numel(), tot_ser, ws_ser)
+        if ev: ev[0].record()
+        cfws.serialize_execute(payload, desc_ser, wire, ws_ser)
+        if ev: ev[1].record()
+        cfws.deserialize_plan(wire, wire_total, index, desc_de, status, back.numel(), tot_de,
+                              ws_de, align=16)
+        if ev: ev[2].record()
+        cfws.deserialize_execute(wire, desc_de, status, back, ws_de)
+        if ev: ev[3].record()
+
+    for _ in range(args.warmup):
+        step()
+    events = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(args.steps)]
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(events[k])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = shard.max_over_ranks(time.perf_counter() - t0, dev)
+
+    # correctness of what was timed: unmask(mask(P)) == P, every frame COMPLETE
+    verified = (int(tot_ser.item()) == wire_total and int(tot_de.item()) == F * fs
+                and bool((status == 0).all().item()) and torch.equal(back, payload))
+    verified = shard.sum_over_ranks(1.0 if verified else 0.0, dev) == world
+
+    ser_ms = sum(e[0].elapsed_time(e[1]) for e in events) / args.steps
+    de_ms = sum(e[2].elapsed_time(e[3]) for e in events) / args.steps
+    hdr = int(wire_total - F * fs)
+    alg_bytes = 2 * F * fs + hdr            # read n + write n (+ headers) per launch
+    kern = {
+        "serialize_execute": {"ms": round(ser_ms, 4),
+                              "GBps": round(alg_bytes / (ser_ms * 1e-3) / 1e9, 1)},
+        "deserialize_execute": {"ms": round(de_ms, 4),
+                                "GBps": round(alg_bytes / (de_ms * 1e-3) / 1e9, 1)},
+    }
+    dom_name = "serialize_execute" if ser_ms >= de_ms else "deserialize_execute"
+    dom_ms = max(ser_ms, de_ms)
+    achieved = alg_bytes / (dom_ms * 1e-3) / 1e9
+    kernel_symbol = ("xform_kernel<true>" if dom_name == "serialize_execute"
+                     else "xform_kernel<false>")
+    total_payload = 2.0 * F * fs * world * args.steps
+    line = {
+        "metric": METRIC,
+        "value": round(total_payload / elapsed / GIB, 2),
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (splitmix64 payloads, glibc random() mask keys as co_ws_frame_serialize draws them)",
+        "config": {
+            "workload": f"config2: {F} binary frames x {fs // 1024} KiB per GPU, client-mask "
+                        f"(serialize) then server-unmask (deserialize), device resident",
+            "frames_per_gpu": F,
+            "payload_bytes_per_frame": fs,
+            "wire_bytes_per_gpu": wire_total,
+            "parallelism": f"shard-per-gpu x{world} (no collective)",
+        },
+        "roofline": {
+            "bound": "hbm",
+            "kernel": kernel_symbol,
+            "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": load_traffic(kernel_symbol),
+            "algorithmic_bytes_per_launch": alg_bytes,
+            "avg_launch_ms": round(dom_ms, 4),
+        },
+        "kernels": kern,
+        "verified": verified,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(fs, args.cpu_seconds)
+    else:
+        line["cpu_baseline"] = None
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    if not verified:
+        sys.exit(1)
+
+
+if __name__ == "__main__":
+    main()

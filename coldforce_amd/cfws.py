@@ -1,0 +1,327 @@
+"""Python binding of libcfws.so (the MI355X WebSocket frame codec).
+
+The product is the C ABI in ``include/cfws.h`` / ``include/cfws_co_ws_frame.h``;
+this module only exposes it to the tests and ``bench.py`` through ctypes,
+with torch supplying device memory and streams. It never falls back to a
+CPU implementation: if the library or a gfx950 device is missing, calls
+raise :class:`CodecError`.
+
+Names mirror the reference: ``serialize`` = ``co_ws_frame_serialize``
+(``src/ws/co_ws_frame.c:21-119``) over a batch, ``deserialize`` =
+``co_ws_frame_deserialize`` (``co_ws_frame.c:121-247``) at each frame start.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libcfws.so")
+
+OK = 0
+PARSE_COMPLETE = 0
+PARSE_MORE_DATA = 1
+ERROR_INVALID_FRAME = -7001
+ERROR_DATA_TOO_BIG = -7005
+ERROR_OUT_OF_MEMORY = -7006
+DEFAULT_MAX_PAYLOAD = 32 * 1024 * 1024          # co_ws_config.h:15
+
+OPCODE_CONTINUATION, OPCODE_TEXT, OPCODE_BINARY = 0x0, 0x1, 0x2
+OPCODE_CLOSE, OPCODE_PING, OPCODE_PONG = 0x8, 0x9, 0xA
+
+# cfws_frame_desc_t, 32 bytes.
+DESC_DTYPE = np.dtype([("payload_off", "<u8"), ("wire_off", "<u8"),
+                       ("payload_size", "<u8"), ("mask_key", "<u4"),
+                       ("fin", "u1"), ("opcode", "u1"), ("mask", "u1"),
+                       ("header_size", "u1")])
+assert DESC_DTYPE.itemsize == 32
+
+# Every function include/*.h declares (tests check the exports against the
+# headers themselves).
+BATCH_SYMBOLS = (
+    "cfws_init", "cfws_last_error", "cfws_version", "cfws_workspace_size",
+    "cfws_serialize_plan", "cfws_serialize_execute", "cfws_serialize_batch",
+    "cfws_deserialize_plan", "cfws_deserialize_execute", "cfws_deserialize_batch",
+    "cfws_xor_mask", "cfws_draw_mask_keys", "cfws_release_thread_resources",
+    "cfws_fill_splitmix",
+)
+DROPIN_SYMBOLS = (
+    "co_ws_frame_serialize", "co_ws_frame_deserialize", "co_ws_frame_create",
+    "co_ws_frame_destroy", "co_ws_frame_get_fin", "co_ws_frame_get_opcode",
+    "co_ws_frame_get_payload_size", "co_ws_frame_get_payload_data",
+    "co_ws_config_set_max_receive_payload_size", "co_ws_config_get_max_receive_payload_size",
+)
+
+
+class CodecError(RuntimeError):
+    pass
+
+
+class CoArray(C.Structure):
+    """co_array_t / co_byte_array_t (inc/coldforce/core/co_array.h:16-23)."""
+    _fields_ = [("capacity", C.c_size_t), ("count", C.c_size_t),
+                ("element_size", C.c_size_t), ("buffer", C.c_void_p)]
+
+
+class CoWsFrameHeader(C.Structure):
+    _fields_ = [("fin", C.c_bool), ("opcode", C.c_uint8), ("payload_size", C.c_uint64)]
+
+
+class CoWsFrame(C.Structure):
+    """co_ws_frame_t (inc/coldforce/ws/co_ws_frame.h:36-49)."""
+    _fields_ = [("header", CoWsFrameHeader), ("payload_data", C.c_void_p)]
+
+
+_vp, _u64, _sz, _u32 = C.c_void_p, C.c_uint64, C.c_size_t, C.c_uint32
+_lib = None
+
+
+def lib(path: str = LIB_PATH) -> C.CDLL:
+    """Load libcfws.so. torch is imported first so that the library binds to
+    the HIP runtime torch already loaded (one runtime per process)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    import torch  # noqa: F401  (HIP runtime first)
+    if not os.path.exists(path):
+        raise CodecError(f"{path} not built (run `make`); there is no CPU fallback")
+    L = C.CDLL(path)
+    sig = {
+        "cfws_init": ([], C.c_int),
+        "cfws_last_error": ([], C.c_char_p),
+        "cfws_version": ([], C.c_char_p),
+        "cfws_workspace_size": ([_sz, _u64], _sz),
+        "cfws_serialize_plan": ([_vp, _sz, _u64, _vp, _vp, _sz, _vp], C.c_int),
+        "cfws_serialize_execute": ([_vp, _vp, _sz, _vp, _u64, _vp, _vp], C.c_int),
+        "cfws_serialize_batch": ([_vp, _vp, _sz, _vp, _u64, _vp, _vp, _sz, _vp], C.c_int),
+        "cfws_deserialize_plan": ([_vp, _u64, _vp, _sz, _u64, _u32, _vp, _vp, _u64, _vp, _vp,
+                                   _sz, _vp], C.c_int),
+        "cfws_deserialize_execute": ([_vp, _vp, _vp, _sz, _vp, _u64, _vp, _vp], C.c_int),
+        "cfws_deserialize_batch": ([_vp, _u64, _vp, _sz, _u64, _u32, _vp, _vp, _vp, _u64, _vp,
+                                    _vp, _sz, _vp], C.c_int),
+        "cfws_xor_mask": ([_vp, _vp, _u64, _u32, _u32, _vp], C.c_int),
+        "cfws_draw_mask_keys": ([_sz, _vp, _vp], None),
+        "cfws_release_thread_resources": ([], None),
+        "cfws_fill_splitmix": ([_vp, _u64, _u64, _u64, _vp], C.c_int),
+        "co_ws_frame_serialize": ([C.c_bool, C.c_uint8, C.c_bool, _vp, _sz, C.POINTER(CoArray)],
+                                  C.c_bool),
+        "co_ws_frame_deserialize": ([C.POINTER(CoWsFrame), _vp, _sz, C.POINTER(C.c_size_t)],
+                                    C.c_int),
+        "co_ws_frame_create": ([], C.POINTER(CoWsFrame)),
+        "co_ws_frame_destroy": ([C.POINTER(CoWsFrame)], None),
+        "co_ws_frame_get_fin": ([C.POINTER(CoWsFrame)], C.c_bool),
+        "co_ws_frame_get_opcode": ([C.POINTER(CoWsFrame)], C.c_uint8),
+        "co_ws_frame_get_payload_size": ([C.POINTER(CoWsFrame)], C.c_uint64),
+        "co_ws_frame_get_payload_data": ([C.POINTER(CoWsFrame)], _vp),
+        "co_ws_config_set_max_receive_payload_size": ([_sz], None),
+        "co_ws_config_get_max_receive_payload_size": ([], _sz),
+    }
+    for name, (args, res) in sig.items():
+        f = getattr(L, name)
+        f.argtypes = args
+        f.restype = res
+    _lib = L
+    return L
+
+
+def _check(rc: int, what: str) -> None:
+    if rc != OK:
+        raise CodecError(f"{what} failed rc={rc}: {lib().cfws_last_error().decode()}")
+
+
+def init() -> None:
+    """Raise unless a gfx950 device is usable (no CPU fallback exists)."""
+    _check(lib().cfws_init(), "cfws_init")
+
+
+def _p(t) -> int | None:
+    return None if t is None else t.data_ptr()
+
+
+def _stream(stream) -> int | None:
+    import torch
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return s.cuda_stream
+
+
+# ---- host helpers ----------------------------------------------------------
+
+def draw_mask_keys(n: int, mask_flags=None, seed: int | None = None) -> np.ndarray:
+    """Keys exactly as n sequential co_ws_frame_serialize calls draw them
+    (after srandom(seed) when a seed is given)."""
+    if seed is not None:
+        C.CDLL(None).srandom(C.c_uint(seed))
+    keys = np.zeros(n, dtype=np.uint32)
+    mf = None if mask_flags is None else np.ascontiguousarray(mask_flags, dtype=np.uint8)
+    lib().cfws_draw_mask_keys(n, None if mf is None else mf.ctypes.data, keys.ctypes.data)
+    return keys
+
+
+def header_sizes(sizes: np.ndarray, masks: np.ndarray) -> np.ndarray:
+    sizes = np.asarray(sizes, dtype=np.uint64)
+    ext = np.where(sizes > 65535, 8, np.where(sizes > 125, 2, 0))
+    return (2 + ext + 4 * (np.asarray(masks) != 0)).astype(np.uint64)
+
+
+def desc_to_device(desc: np.ndarray, device="cuda"):
+    import torch
+    raw = np.ascontiguousarray(desc, dtype=DESC_DTYPE).view(np.uint8).reshape(-1, 32)
+    return torch.from_numpy(raw.copy()).to(device)
+
+
+def desc_from_device(t) -> np.ndarray:
+    return t.cpu().numpy().reshape(-1).view(DESC_DTYPE).copy()
+
+
+def workspace(n_frames: int, out_capacity: int, device="cuda"):
+    import torch
+    nbytes = lib().cfws_workspace_size(n_frames, out_capacity)
+    return torch.empty(nbytes, dtype=torch.uint8, device=device)
+
+
+# ---- batch API ---------------------------------------------------------------
+
+def serialize_plan(desc_t, wire_capacity: int, total_t, ws_t, stream=None) -> None:
+    _check(lib().cfws_serialize_plan(_p(desc_t), desc_t.shape[0], wire_capacity, _p(total_t),
+                                     _p(ws_t), ws_t.numel(), _stream(stream)),
+           "cfws_serialize_plan")
+
+
+def serialize_execute(payload_t, desc_t, wire_t, ws_t, wire_capacity: int | None = None,
+                      stream=None) -> None:
+    cap = wire_t.numel() if wire_capacity is None else wire_capacity
+    _check(lib().cfws_serialize_execute(_p(payload_t), _p(desc_t), desc_t.shape[0], _p(wire_t),
+                                        cap, _p(ws_t), _stream(stream)),
+           "cfws_serialize_execute")
+
+
+def serialize(payload_t, desc_t, wire_t, ws_t=None, total_t=None, stream=None):
+    """Serialize every frame of desc_t into wire_t; returns the total tensor."""
+    import torch
+    n = desc_t.shape[0]
+    if ws_t is None:
+        ws_t = workspace(n, wire_t.numel(), wire_t.device)
+    if total_t is None:
+        total_t = torch.zeros(1, dtype=torch.int64, device=wire_t.device)
+    _check(lib().cfws_serialize_batch(_p(payload_t), _p(desc_t), n, _p(wire_t), wire_t.numel(),
+                                      _p(total_t), _p(ws_t), ws_t.numel(), _stream(stream)),
+           "cfws_serialize_batch")
+    return total_t
+
+
+def deserialize_plan(wire_t, wire_size: int, index_t, desc_t, status_t, payload_capacity: int,
+                     total_t, ws_t, max_payload: int = DEFAULT_MAX_PAYLOAD, align: int = 16,
+                     stream=None) -> None:
+    _check(lib().cfws_deserialize_plan(_p(wire_t), wire_size, _p(index_t), index_t.numel(),
+                                       max_payload, align, _p(desc_t), _p(status_t),
+                                       payload_capacity, _p(total_t), _p(ws_t), ws_t.numel(),
+                                       _stream(stream)),
+           "cfws_deserialize_plan")
+
+
+def deserialize_execute(wire_t, desc_t, status_t, payload_t, ws_t,
+                        payload_capacity: int | None = None, stream=None) -> None:
+    cap = payload_t.numel() if payload_capacity is None else payload_capacity
+    _check(lib().cfws_deserialize_execute(_p(wire_t), _p(desc_t), _p(status_t), desc_t.shape[0],
+                                          _p(payload_t), cap, _p(ws_t), _stream(stream)),
+           "cfws_deserialize_execute")
+
+
+def deserialize(wire_t, wire_size: int, index_t, payload_t, desc_t=None, status_t=None,
+                ws_t=None, total_t=None, max_payload: int = DEFAULT_MAX_PAYLOAD,
+                align: int = 16, stream=None):
+    """Deserialize the frame starting at each index_t[i] of wire_t[:wire_size].
+    Returns (desc_t, status_t, total_t)."""
+    import torch
+    n = index_t.numel()
+    dev = wire_t.device
+    if desc_t is None:
+        desc_t = torch.empty((n, 32), dtype=torch.uint8, device=dev)
+    if status_t is None:
+        status_t = torch.empty(n, dtype=torch.int32, device=dev)
+    if ws_t is None:
+        ws_t = workspace(n, payload_t.numel(), dev)
+    if total_t is None:
+        total_t = torch.zeros(1, dtype=torch.int64, device=dev)
+    _check(lib().cfws_deserialize_batch(_p(wire_t), wire_size, _p(index_t), n, max_payload, align,
+                                        _p(desc_t), _p(status_t), _p(payload_t), payload_t.numel(),
+                                        _p(total_t), _p(ws_t), ws_t.numel(), _stream(stream)),
+           "cfws_deserialize_batch")
+    return desc_t, status_t, total_t
+
+
+def xor_mask(src_t, dst_t, n: int, key: int, phase: int = 0, stream=None) -> None:
+    _check(lib().cfws_xor_mask(_p(src_t), _p(dst_t), n, key, phase, _stream(stream)),
+           "cfws_xor_mask")
+
+
+def fill_splitmix(dst_t, seed: int, byte_base: int = 0, n: int | None = None, stream=None) -> None:
+    n = dst_t.numel() if n is None else n
+    _check(lib().cfws_fill_splitmix(_p(dst_t), n, seed, byte_base, _stream(stream)),
+           "cfws_fill_splitmix")
+
+
+# ---- drop-in per-frame API (co_ws_frame_*) ---------------------------------
+
+_libc = None
+
+
+def _c():
+    global _libc
+    if _libc is None:
+        _libc = C.CDLL(None)
+        _libc.malloc.restype = C.c_void_p
+        _libc.malloc.argtypes = [C.c_size_t]
+        _libc.free.argtypes = [C.c_void_p]
+    return _libc
+
+
+def byte_array_create() -> CoArray:
+    """co_byte_array_create(): capacity 8, element_size 1 (co_array.c:15-40)."""
+    a = CoArray()
+    a.capacity, a.count, a.element_size = 8, 0, 1
+    a.buffer = _c().malloc(8)
+    return a
+
+
+def byte_array_bytes(a: CoArray) -> bytes:
+    return C.string_at(a.buffer, a.count) if a.count else b""
+
+
+def byte_array_destroy(a: CoArray) -> None:
+    _c().free(a.buffer)
+    a.buffer = None
+
+
+def frame_serialize(fin: bool, opcode: int, mask: bool, data: bytes, buf: CoArray | None = None):
+    """co_ws_frame_serialize through the drop-in; returns (ok, wire bytes)."""
+    own = buf is None
+    if own:
+        buf = byte_array_create()
+    src = C.create_string_buffer(data, len(data)) if data else None
+    ok = lib().co_ws_frame_serialize(fin, opcode, mask, src, len(data), C.byref(buf))
+    out = byte_array_bytes(buf)
+    if own:
+        byte_array_destroy(buf)
+    return ok, out
+
+
+def frame_deserialize(data: bytes, index: int = 0):
+    """co_ws_frame_deserialize through the drop-in on a fresh frame.
+    Returns dict(rc, index, fin, opcode, payload_size, payload|None), the
+    payload including its NUL terminator, like oracle.ref_deserialize."""
+    L = lib()
+    f = L.co_ws_frame_create()
+    src = C.create_string_buffer(data, len(data))
+    idx = C.c_size_t(index)
+    rc = L.co_ws_frame_deserialize(f, src, len(data), C.byref(idx))
+    fr = f.contents
+    payload = None
+    if rc == 0 and fr.payload_data:
+        payload = C.string_at(fr.payload_data, fr.header.payload_size + 1)
+    out = dict(rc=rc, index=idx.value, fin=bool(fr.header.fin), opcode=fr.header.opcode,
+               payload_size=fr.header.payload_size, payload=payload)
+    L.co_ws_frame_destroy(f)
+    return out

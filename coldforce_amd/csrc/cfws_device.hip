@@ -1,0 +1,764 @@
+// cfws_device.hip -- MI355X (gfx950) kernels and batch C ABI of the
+// WebSocket frame codec (include/cfws.h).
+//
+// Reference behaviour restated on the device:
+//   header encode        co_ws_frame.c:34-68, :70-91
+//   payload mask         co_ws_frame.c:93-97    out[i] = in[i] ^ key[i % 4]
+//   header decode        co_ws_frame.c:131-213 (MORE_DATA before TOO_BIG)
+//   payload copy+unmask  co_ws_frame.c:214-242
+//
+// Design (DESIGN.md has the full story):
+//   * The output arena (wire arena for serialize, payload arena for
+//     deserialize) is cut into 16 KiB tiles of 16-byte chunks. Every chunk
+//     is produced by exactly one lane and written with one 16-byte store, so
+//     frame boundaries never need byte stores or read-modify-write.
+//   * A plan (prefix sum of frame sizes + a tile -> first-frame map) lets
+//     each workgroup find its frames with two scalar loads; a tile that lies
+//     inside one frame (the common case for 64 KiB frames) runs with the
+//     frame descriptor, key and alignment phase in SGPRs.
+//   * Source and destination are misaligned against each other (a masked
+//     64 KiB frame is 65,550 B on the wire). A lane loads the aligned 16-byte
+//     source block(s) covering its chunk and funnel-shifts them with
+//     v_alignbyte_b32; the key is pre-rotated once per frame.
+//   * Pure HBM streaming: 2 bytes of traffic per payload byte, no LDS on the
+//     fast path, no MFMA.
+#include <hip/hip_runtime.h>
+
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "cfws.h"
+
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kUnroll = 4;                                   // chunks per lane per tile
+constexpr uint64_t kChunk = 16;
+constexpr uint64_t kTileBytes = uint64_t(kThreads) * kUnroll * kChunk;  // 16 KiB
+constexpr uint32_t kLdsFrames = 1024;                        // frames staged per tile
+constexpr int kScanItems = 8;
+constexpr uint64_t kScanBlock = uint64_t(kThreads) * kScanItems;
+
+// ---------------------------------------------------------------------------
+// workspace layout (deterministic from n_frames and the output capacity)
+// ---------------------------------------------------------------------------
+struct WsLayout {
+    uint64_t total;      // u64: output bytes, clamped to capacity
+    uint64_t vals;       // u64[n]: per-frame sizes, then exclusive offsets
+    uint64_t partials;   // u64[scan blocks]
+    uint64_t tile_map;   // u32[tiles_max + 2]
+    uint64_t bytes;
+    uint64_t tiles_max;
+    uint64_t scan_blocks;
+};
+
+inline uint64_t align_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
+
+WsLayout ws_layout(uint64_t n, uint64_t capacity)
+{
+    WsLayout L;
+    L.tiles_max = (capacity + kTileBytes - 1) / kTileBytes;
+    L.scan_blocks = (n + kScanBlock - 1) / kScanBlock;
+    L.total = 0;
+    L.vals = 256;
+    L.partials = align_up(L.vals + 8 * n, 256);
+    L.tile_map = align_up(L.partials + 8 * (L.scan_blocks + 1), 256);
+    L.bytes = align_up(L.tile_map + 4 * (L.tiles_max + 2), 256);
+    return L;
+}
+
+// ---------------------------------------------------------------------------
+// device helpers
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t header_size_of(uint64_t n, bool mask)
+{
+    return 2u + (n > 65535u ? 8u : (n > 125u ? 2u : 0u)) + (mask ? 4u : 0u);
+}
+
+// Byte r of the serialized header (co_ws_frame.c:34-91).
+__device__ __forceinline__ uint32_t header_byte(const cfws_frame_desc_t& d, uint32_t r)
+{
+    const uint64_t n = d.payload_size;
+    const uint32_t ext = n > 65535u ? 8u : (n > 125u ? 2u : 0u);
+    if (r == 0) return (uint32_t)(uint8_t)(d.opcode | (d.fin ? 0x80u : 0u));
+    if (r == 1) {
+        const uint32_t l7 = ext == 8 ? 127u : (ext == 2 ? 126u : (uint32_t)n);
+        return (l7 | (d.mask ? 0x80u : 0u)) & 0xffu;
+    }
+    r -= 2;
+    if (r < ext) return (uint32_t)(n >> (8 * (ext - 1 - r))) & 0xffu;
+    r -= ext;
+    return (d.mask_key >> (8 * r)) & 0xffu;
+}
+
+__device__ __forceinline__ uint32_t rotr8(uint32_t key, uint32_t bytes)
+{
+    return __builtin_amdgcn_alignbyte(key, key, bytes & 3u);
+}
+
+// What one frame contributes to the output arena.
+//   [out_off, out_off + pre)              header bytes (serialize only)
+//   [out_off + pre, + body_len)           src[src_off + k] ^ key[k % 4]
+//   [.., next frame's out_off)            zero (deserialize alignment pad)
+struct FrameView {
+    uint64_t out_off;
+    uint64_t body_start;
+    uint64_t body_len;
+    uint64_t src_off;
+    uint32_t key;   // 0 when the frame is not masked: XOR becomes a copy
+    uint32_t pre;
+};
+
+template <bool kSer>
+__device__ __forceinline__ FrameView frame_view(const cfws_frame_desc_t* __restrict__ desc,
+                                                const int32_t* __restrict__ status, uint32_t f)
+{
+    const cfws_frame_desc_t d = desc[f];
+    FrameView v;
+    v.key = d.mask ? d.mask_key : 0u;
+    if (kSer) {
+        v.out_off = d.wire_off;
+        v.pre = d.header_size;
+        v.body_len = d.payload_size;
+        v.src_off = d.payload_off;
+    } else {
+        v.out_off = d.payload_off;
+        v.pre = 0;
+        v.body_len = (status[f] == CFWS_PARSE_COMPLETE) ? d.payload_size : 0;
+        v.src_off = d.wire_off + d.header_size;
+    }
+    v.body_start = v.out_off + v.pre;
+    return v;
+}
+
+template <bool kSer>
+__device__ __forceinline__ uint64_t out_off_of(const cfws_frame_desc_t* __restrict__ desc, uint32_t f)
+{
+    return kSer ? desc[f].wire_off : desc[f].payload_off;
+}
+
+// 16 output bytes starting `ph` bytes into the 32-byte window {A, B}.
+__device__ __forceinline__ uint4 funnel16(uint4 A, uint4 B, uint32_t ph)
+{
+    const bool s8 = (ph & 8u) != 0;
+    const bool s4 = (ph & 4u) != 0;
+    const uint32_t r = ph & 3u;
+    // shift by 8 bytes
+    const uint32_t a0 = s8 ? A.z : A.x, a1 = s8 ? A.w : A.y, a2 = s8 ? B.x : A.z;
+    const uint32_t a3 = s8 ? B.y : A.w, a4 = s8 ? B.z : B.x, a5 = s8 ? B.w : B.y;
+    // shift by 4 bytes
+    const uint32_t b0 = s4 ? a1 : a0, b1 = s4 ? a2 : a1, b2 = s4 ? a3 : a2;
+    const uint32_t b3 = s4 ? a4 : a3, b4 = s4 ? a5 : a4;
+    uint4 o;
+    o.x = __builtin_amdgcn_alignbyte(b1, b0, r);
+    o.y = __builtin_amdgcn_alignbyte(b2, b1, r);
+    o.z = __builtin_amdgcn_alignbyte(b3, b2, r);
+    o.w = __builtin_amdgcn_alignbyte(b4, b3, r);
+    return o;
+}
+
+// Fast path: the whole 16-byte chunk at D lies inside v's body.
+__device__ __forceinline__ uint4 body_chunk(const uint8_t* __restrict__ src, const FrameView& v,
+                                            uint64_t D)
+{
+    const uint64_t k0 = D - v.body_start;
+    const uint64_t s = v.src_off + k0;
+    const uint64_t sa = s & ~uint64_t(15);
+    const uint32_t ph = (uint32_t)(s & 15u);
+    const uint4 A = *reinterpret_cast<const uint4*>(src + sa);
+    uint4 o = A;
+    if (ph != 0) {
+        // The aligned block holding the chunk's last byte: always inside the
+        // same page as a valid source byte, never past the allocation's page.
+        const uint4 B = *reinterpret_cast<const uint4*>(src + sa + 16);
+        o = funnel16(A, B, ph);
+    }
+    const uint32_t kr = rotr8(v.key, (uint32_t)(k0 & 3u));
+    o.x ^= kr; o.y ^= kr; o.z ^= kr; o.w ^= kr;
+    return o;
+}
+
+// Slow path: a chunk that crosses a header, a frame boundary, padding or the
+// end of the arena. Built byte by byte, walking frames forward from f.
+template <bool kSer>
+__device__ __noinline__ uint4 edge_chunk(const uint8_t* __restrict__ src,
+                                         const cfws_frame_desc_t* __restrict__ desc,
+                                         const int32_t* __restrict__ status, uint32_t f,
+                                         uint32_t n_frames, uint64_t D, uint64_t total)
+{
+    FrameView v = frame_view<kSer>(desc, status, f);
+    uint64_t next = (f + 1 < n_frames) ? out_off_of<kSer>(desc, f + 1) : ~uint64_t(0);
+    uint32_t w[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        const uint64_t pos = D + j;
+        uint32_t b = 0;
+        if (pos < total) {
+            while (pos >= next) {
+                ++f;
+                v = frame_view<kSer>(desc, status, f);
+                next = (f + 1 < n_frames) ? out_off_of<kSer>(desc, f + 1) : ~uint64_t(0);
+            }
+            const uint64_t r = pos - v.out_off;
+            if (r < v.pre) {
+                b = header_byte(desc[f], (uint32_t)r);
+            } else {
+                const uint64_t k = r - v.pre;
+                if (k < v.body_len) b = (src[v.src_off + k] ^ (v.key >> (8 * (k & 3u)))) & 0xffu;
+            }
+        }
+        w[j >> 2] |= b << (8 * (j & 3));
+    }
+    return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+__device__ __forceinline__ void store_chunk(uint8_t* __restrict__ dst, uint64_t D, uint4 o,
+                                            uint64_t capacity)
+{
+    if (D + 16 <= capacity) {
+        *reinterpret_cast<uint4*>(dst + D) = o;
+    } else {
+        const uint32_t w[4] = {o.x, o.y, o.z, o.w};
+        for (uint32_t j = 0; D + j < capacity; ++j) dst[D + j] = (uint8_t)(w[j >> 2] >> (8 * (j & 3)));
+    }
+}
+
+// ---------------------------------------------------------------------------
+// the streaming kernel: serialize (kSer) = header + mask into the wire
+// arena; deserialize = copy + unmask into the payload arena
+// ---------------------------------------------------------------------------
+template <bool kSer>
+__global__ void __launch_bounds__(kThreads)
+xform_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+             const cfws_frame_desc_t* __restrict__ desc, const int32_t* __restrict__ status,
+             const uint32_t* __restrict__ tile_map, const uint64_t* __restrict__ total_p,
+             uint64_t capacity, uint32_t n_frames)
+{
+    __shared__ uint64_t s_off[kLdsFrames];
+    const uint64_t total = *total_p;                 // already clamped to capacity
+    const uint64_t n_tiles = (total + kTileBytes - 1) / kTileBytes;
+    const uint32_t tid = threadIdx.x;
+
+    for (uint64_t t = blockIdx.x; t < n_tiles; t += gridDim.x) {
+        const uint64_t base = t * kTileBytes;
+        const uint32_t f0 = tile_map[t];
+        uint32_t f1 = tile_map[t + 1];
+        if (f1 >= n_frames) f1 = n_frames - 1;
+
+        if (f0 == f1) {
+            // Whole tile inside one frame: descriptor is wave-uniform.
+            const FrameView v = frame_view<kSer>(desc, status, f0);
+            const uint64_t body_end = v.body_start + v.body_len;
+            uint4 o[kUnroll];
+            bool fast[kUnroll];
+#pragma unroll
+            for (int u = 0; u < kUnroll; ++u) {
+                const uint64_t D = base + (uint64_t(u) * kThreads + tid) * kChunk;
+                fast[u] = D >= v.body_start && D + kChunk <= body_end;
+                if (fast[u]) o[u] = body_chunk(src, v, D);
+            }
+#pragma unroll
+            for (int u = 0; u < kUnroll; ++u) {
+                const uint64_t D = base + (uint64_t(u) * kThreads + tid) * kChunk;
+                if (D >= total) continue;
+                if (!fast[u]) o[u] = edge_chunk<kSer>(src, desc, status, f0, n_frames, D, total);
+                store_chunk(dst, D, o[u], capacity);
+            }
+        } else {
+            // Several frames: stage their output offsets in LDS and search.
+            const uint32_t cnt = f1 - f0 + 1;
+            const bool staged = cnt <= kLdsFrames;
+            __syncthreads();
+            if (staged)
+                for (uint32_t i = tid; i < cnt; i += kThreads) s_off[i] = out_off_of<kSer>(desc, f0 + i);
+            __syncthreads();
+#pragma unroll
+            for (int u = 0; u < kUnroll; ++u) {
+                const uint64_t D = base + (uint64_t(u) * kThreads + tid) * kChunk;
+                if (D >= total) continue;
+                // largest f in [f0, f1] with out_off(f) <= D
+                uint32_t lo = 0, hi = cnt - 1;
+                while (lo < hi) {
+                    const uint32_t mid = (lo + hi + 1) >> 1;
+                    const uint64_t m = staged ? s_off[mid] : out_off_of<kSer>(desc, f0 + mid);
+                    if (m <= D) lo = mid; else hi = mid - 1;
+                }
+                const uint32_t f = f0 + lo;
+                const FrameView v = frame_view<kSer>(desc, status, f);
+                uint4 o;
+                if (D >= v.body_start && D + kChunk <= v.body_start + v.body_len)
+                    o = body_chunk(src, v, D);
+                else
+                    o = edge_chunk<kSer>(src, desc, status, f, n_frames, D, total);
+                store_chunk(dst, D, o, capacity);
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// plan kernels
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(kThreads)
+serialize_sizes_kernel(cfws_frame_desc_t* __restrict__ desc, uint64_t* __restrict__ vals, uint64_t n)
+{
+    const uint64_t f = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
+    if (f >= n) return;
+    const uint64_t len = desc[f].payload_size;
+    const uint32_t hs = header_size_of(len, desc[f].mask != 0);
+    desc[f].header_size = (uint8_t)hs;
+    vals[f] = hs + len;
+}
+
+// Header decode at d_index[f] (co_ws_frame.c:131-213), with the callers'
+// two-byte precheck (co_ws_client.c:202-206).
+__global__ void __launch_bounds__(kThreads)
+deserialize_parse_kernel(const uint8_t* __restrict__ wire, uint64_t wire_size,
+                         const uint64_t* __restrict__ index, uint64_t n, uint64_t max_payload,
+                         uint64_t align, cfws_frame_desc_t* __restrict__ desc,
+                         int32_t* __restrict__ status, uint64_t* __restrict__ vals)
+{
+    const uint64_t f = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
+    if (f >= n) return;
+    const uint64_t s = index[f];
+    cfws_frame_desc_t d;
+    d.payload_off = 0;
+    d.wire_off = s;
+    d.payload_size = 0;
+    d.mask_key = 0;
+    d.fin = 0;
+    d.opcode = 0;
+    d.mask = 0;
+    d.header_size = 0;
+    int32_t st = CFWS_PARSE_COMPLETE;
+    do {
+        if (s > wire_size || wire_size - s < 2) { st = CFWS_PARSE_MORE_DATA; break; }
+        const uint32_t b0 = wire[s], b1 = wire[s + 1];
+        d.fin = (uint8_t)(b0 >> 7);
+        d.opcode = (uint8_t)(b0 & 0x7fu);
+        if (d.opcode > 0x0f) { st = CFWS_ERROR_INVALID_FRAME; break; }
+        d.mask = (uint8_t)(b1 >> 7);
+        const uint32_t l7 = b1 & 0x7fu;
+        uint64_t p = s + 2;
+        if (l7 <= 125) {
+            d.payload_size = l7;
+        } else {
+            const uint32_t ext = (l7 == 126) ? 2u : 8u;
+            if (wire_size - p < ext) { st = CFWS_PARSE_MORE_DATA; break; }
+            uint64_t len = 0;
+            for (uint32_t i = 0; i < ext; ++i) len = (len << 8) | wire[p + i];
+            d.payload_size = len;
+            p += ext;
+        }
+        if (d.mask) {
+            if (wire_size - p < 4) { st = CFWS_PARSE_MORE_DATA; break; }
+            d.mask_key = (uint32_t)wire[p] | (uint32_t)wire[p + 1] << 8 |
+                         (uint32_t)wire[p + 2] << 16 | (uint32_t)wire[p + 3] << 24;
+            p += 4;
+        }
+        d.header_size = (uint8_t)(p - s);
+        if (wire_size - p < d.payload_size) { st = CFWS_PARSE_MORE_DATA; break; }
+        if (d.payload_size > max_payload) { st = CFWS_ERROR_DATA_TOO_BIG; break; }
+    } while (0);
+    desc[f] = d;
+    status[f] = st;
+    vals[f] = (st == CFWS_PARSE_COMPLETE) ? ((d.payload_size + align - 1) & ~(align - 1)) : 0;
+}
+
+// Exclusive block scan of one value per thread; *block_total gets the sum.
+__device__ __forceinline__ uint64_t block_exclusive_scan(uint64_t x, uint64_t* s_wave,
+                                                         uint64_t* block_total)
+{
+    const uint32_t lane = threadIdx.x & 63u, wid = threadIdx.x >> 6;
+    uint64_t inc = x;
+#pragma unroll
+    for (uint32_t o = 1; o < 64; o <<= 1) {
+        const uint64_t y = __shfl_up(inc, o, 64);
+        if (lane >= o) inc += y;
+    }
+    __syncthreads();
+    if (lane == 63) s_wave[wid] = inc;
+    __syncthreads();
+    uint64_t before = 0, all = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < kThreads / 64; ++w) {
+        if (w < wid) before += s_wave[w];
+        all += s_wave[w];
+    }
+    *block_total = all;
+    return before + inc - x;
+}
+
+__global__ void __launch_bounds__(kThreads)
+scan_reduce_kernel(const uint64_t* __restrict__ vals, uint64_t n, uint64_t* __restrict__ partials)
+{
+    __shared__ uint64_t s_wave[kThreads / 64];
+    const uint64_t b0 = uint64_t(blockIdx.x) * kScanBlock;
+    uint64_t sum = 0;
+#pragma unroll
+    for (int k = 0; k < kScanItems; ++k) {
+        const uint64_t i = b0 + uint64_t(k) * kThreads + threadIdx.x;
+        if (i < n) sum += vals[i];
+    }
+    uint64_t total;
+    block_exclusive_scan(sum, s_wave, &total);
+    if (threadIdx.x == 0) partials[blockIdx.x] = total;
+}
+
+__global__ void __launch_bounds__(kThreads)
+scan_partials_kernel(uint64_t* __restrict__ partials, uint64_t nb, uint64_t* __restrict__ grand)
+{
+    __shared__ uint64_t s_wave[kThreads / 64];
+    uint64_t carry = 0;
+    for (uint64_t b = 0; b < nb; b += kThreads) {
+        const uint64_t i = b + threadIdx.x;
+        const uint64_t x = i < nb ? partials[i] : 0;
+        uint64_t tot;
+        const uint64_t ex = block_exclusive_scan(x, s_wave, &tot);
+        if (i < nb) partials[i] = carry + ex;
+        carry += tot;
+    }
+    if (threadIdx.x == 0) *grand = carry;
+}
+
+__global__ void __launch_bounds__(kThreads)
+scan_apply_kernel(uint64_t* __restrict__ vals, uint64_t n, const uint64_t* __restrict__ partials)
+{
+    __shared__ uint64_t s_wave[kThreads / 64];
+    const uint64_t i0 = uint64_t(blockIdx.x) * kScanBlock + uint64_t(threadIdx.x) * kScanItems;
+    uint64_t v[kScanItems];
+    uint64_t sum = 0;
+#pragma unroll
+    for (int k = 0; k < kScanItems; ++k) {
+        v[k] = (i0 + k < n) ? vals[i0 + k] : 0;
+        sum += v[k];
+    }
+    uint64_t tot;
+    uint64_t run = block_exclusive_scan(sum, s_wave, &tot) + partials[blockIdx.x];
+#pragma unroll
+    for (int k = 0; k < kScanItems; ++k) {
+        if (i0 + k < n) vals[i0 + k] = run;
+        run += v[k];
+    }
+}
+
+// Writes offsets into the descriptors, applies the capacity rule and builds
+// the tile -> first frame map. `grand` = unclamped total from the scan.
+template <bool kSer>
+__global__ void __launch_bounds__(kThreads)
+finalize_kernel(cfws_frame_desc_t* __restrict__ desc, int32_t* __restrict__ status,
+                const uint64_t* __restrict__ offs, const uint64_t* __restrict__ grand,
+                uint64_t n, uint64_t capacity, uint32_t* __restrict__ tile_map,
+                uint64_t* __restrict__ ws_total, uint64_t* __restrict__ user_total)
+{
+    const uint64_t f = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
+    if (f >= n) return;
+    const uint64_t g = *grand;
+    const uint64_t total = g < capacity ? g : capacity;
+    const uint64_t lo = offs[f];
+    const uint64_t hi_raw = (f + 1 < n) ? offs[f + 1] : g;
+    if (kSer) {
+        desc[f].wire_off = lo;
+    } else {
+        desc[f].payload_off = lo;
+        if (status[f] == CFWS_PARSE_COMPLETE && lo + desc[f].payload_size > capacity)
+            status[f] = CFWS_ERROR_OUT_OF_MEMORY;
+    }
+    const uint64_t a = lo < total ? lo : total;
+    const uint64_t b = hi_raw < total ? hi_raw : total;
+    if (b > a) {
+        const uint64_t t0 = (a + kTileBytes - 1) / kTileBytes;
+        const uint64_t t1 = (b + kTileBytes - 1) / kTileBytes;
+        for (uint64_t t = t0; t < t1; ++t) tile_map[t] = (uint32_t)f;
+    }
+    if (f == n - 1) {
+        tile_map[(total + kTileBytes - 1) / kTileBytes] = (uint32_t)(n - 1);
+        *ws_total = total;
+        if (user_total) *user_total = kSer ? g : total;
+    }
+}
+
+__global__ void __launch_bounds__(kThreads)
+xor_mask_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, uint64_t n,
+                uint32_t key, uint32_t phase)
+{
+    const uint64_t stride = uint64_t(gridDim.x) * kThreads;
+    const uint64_t nv = n / 16;
+    const uint32_t kr = rotr8(key, phase);
+    const bool aligned = ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15u) == 0;
+    const uint64_t tid = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
+    if (aligned) {
+        for (uint64_t i = tid; i < nv; i += stride) {
+            uint4 v = reinterpret_cast<const uint4*>(src)[i];
+            v.x ^= kr; v.y ^= kr; v.z ^= kr; v.w ^= kr;
+            reinterpret_cast<uint4*>(dst)[i] = v;
+        }
+        for (uint64_t i = nv * 16 + tid; i < n; i += stride)
+            dst[i] = src[i] ^ (uint8_t)(kr >> (8 * (i & 3)));
+    } else {
+        for (uint64_t i = tid; i < n; i += stride)
+            dst[i] = src[i] ^ (uint8_t)(kr >> (8 * (i & 3)));
+    }
+}
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t seed, uint64_t i)
+{
+    uint64_t z = seed + (i + 1) * 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+__global__ void __launch_bounds__(kThreads)
+fill_splitmix_kernel(uint8_t* __restrict__ dst, uint64_t n, uint64_t seed, uint64_t word_base)
+{
+    const uint64_t stride = uint64_t(gridDim.x) * kThreads;
+    const uint64_t nv = n / 16;
+    for (uint64_t i = uint64_t(blockIdx.x) * kThreads + threadIdx.x; i < nv; i += stride) {
+        const uint64_t a = splitmix64(seed, word_base + 2 * i);
+        const uint64_t b = splitmix64(seed, word_base + 2 * i + 1);
+        reinterpret_cast<uint4*>(dst)[i] =
+            make_uint4((uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32));
+    }
+    const uint64_t t = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
+    if (t < (n & 15u)) {
+        const uint64_t o = nv * 16 + t;
+        dst[o] = (uint8_t)(splitmix64(seed, word_base + o / 8) >> (8 * (o & 7)));
+    }
+}
+
+// ---------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------
+thread_local char g_err[512] = "";
+int g_init_state = 0;   // 0 unknown, 1 ok, <0 error code
+
+int set_err(int code, const char* what, hipError_t e)
+{
+    snprintf(g_err, sizeof g_err, "%s: %s", what, e == hipSuccess ? "" : hipGetErrorString(e));
+    fprintf(stderr, "cfws: %s\n", g_err);
+    return code;
+}
+
+int check_init()
+{
+    if (g_init_state == 1) return CFWS_OK;
+    if (g_init_state < 0) return g_init_state;
+    int count = 0;
+    hipError_t e = hipGetDeviceCount(&count);
+    if (e != hipSuccess || count == 0) {
+        g_init_state = CFWS_ERROR_NO_DEVICE;
+        return set_err(CFWS_ERROR_NO_DEVICE, "no HIP device", e);
+    }
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    hipDeviceProp_t prop;
+    e = hipGetDeviceProperties(&prop, dev);
+    if (e != hipSuccess) return set_err(CFWS_ERROR_NO_DEVICE, "hipGetDeviceProperties", e);
+    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+        g_init_state = CFWS_ERROR_NO_DEVICE;
+        snprintf(g_err, sizeof g_err, "device arch %s is not gfx950", prop.gcnArchName);
+        fprintf(stderr, "cfws: %s\n", g_err);
+        return CFWS_ERROR_NO_DEVICE;
+    }
+    g_init_state = 1;
+    return CFWS_OK;
+}
+
+int launch_check(const char* what)
+{
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? CFWS_OK : set_err(CFWS_ERROR_HIP, what, e);
+}
+
+uint32_t grid_for(uint64_t items, uint64_t per_block)
+{
+    const uint64_t g = (items + per_block - 1) / per_block;
+    return (uint32_t)(g == 0 ? 1 : g);
+}
+
+uint32_t stream_grid(uint64_t tiles)
+{
+    static uint64_t cap = 0;
+    if (cap == 0) {
+        const char* s = getenv("CFWS_GRID");
+        cap = s ? strtoull(s, nullptr, 10) : 0;
+        if (cap == 0) cap = 8192;
+    }
+    const uint64_t g = tiles < cap ? tiles : cap;
+    return (uint32_t)(g == 0 ? 1 : g);
+}
+
+template <typename T>
+T* ws_ptr(const void* ws, uint64_t off)
+{
+    return reinterpret_cast<T*>(static_cast<char*>(const_cast<void*>(ws)) + off);
+}
+
+int run_scan(uint64_t* vals, uint64_t n, uint64_t* partials, uint64_t* grand, hipStream_t st)
+{
+    const uint32_t nb = grid_for(n, kScanBlock);
+    scan_reduce_kernel<<<nb, kThreads, 0, st>>>(vals, n, partials);
+    scan_partials_kernel<<<1, kThreads, 0, st>>>(partials, nb, grand);
+    scan_apply_kernel<<<nb, kThreads, 0, st>>>(vals, n, partials);
+    return launch_check("scan");
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// C ABI
+// ---------------------------------------------------------------------------
+extern "C" {
+
+int cfws_init(void) { return check_init(); }
+const char* cfws_last_error(void) { return g_err; }
+const char* cfws_version(void) { return "cfws 0.1 gfx950"; }
+
+size_t cfws_workspace_size(size_t n_frames, uint64_t out_capacity)
+{
+    return (size_t)ws_layout(n_frames, out_capacity).bytes;
+}
+
+int cfws_serialize_plan(cfws_frame_desc_t* d_desc, size_t n, uint64_t cap, uint64_t* d_total,
+                        void* ws, size_t ws_size, void* stream)
+{
+    if (int rc = check_init()) return rc;
+    const WsLayout L = ws_layout(n, cap);
+    if (!ws || ws_size < L.bytes) return set_err(CFWS_ERROR_WORKSPACE, "workspace too small", hipSuccess);
+    if (n > 0xffffffffull) return set_err(CFWS_ERROR_INVALID_ARGUMENT, "too many frames", hipSuccess);
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    if (n == 0) {
+        (void)hipMemsetAsync(ws_ptr<uint64_t>(ws, L.total), 0, 8, st);
+        if (d_total) (void)hipMemsetAsync(d_total, 0, 8, st);
+        return launch_check("serialize_plan(empty)");
+    }
+    if (!d_desc) return set_err(CFWS_ERROR_INVALID_ARGUMENT, "null descriptor table", hipSuccess);
+    uint64_t* vals = ws_ptr<uint64_t>(ws, L.vals);
+    uint64_t* partials = ws_ptr<uint64_t>(ws, L.partials);
+    uint64_t* grand = partials + L.scan_blocks;
+    serialize_sizes_kernel<<<grid_for(n, kThreads), kThreads, 0, st>>>(d_desc, vals, n);
+    if (int rc = run_scan(vals, n, partials, grand, st)) return rc;
+    finalize_kernel<true><<<grid_for(n, kThreads), kThreads, 0, st>>>(
+        d_desc, nullptr, vals, grand, n, cap, ws_ptr<uint32_t>(ws, L.tile_map),
+        ws_ptr<uint64_t>(ws, L.total), d_total);
+    return launch_check("serialize_plan");
+}
+
+int cfws_serialize_execute(const void* d_payload, const cfws_frame_desc_t* d_desc, size_t n,
+                           void* d_wire, uint64_t cap, const void* ws, void* stream)
+{
+    if (int rc = check_init()) return rc;
+    if (n == 0 || cap == 0) return CFWS_OK;
+    if (!d_payload || !d_desc || !d_wire || !ws)
+        return set_err(CFWS_ERROR_INVALID_ARGUMENT, "null pointer", hipSuccess);
+    if ((reinterpret_cast<uintptr_t>(d_payload) | reinterpret_cast<uintptr_t>(d_wire)) & 15u)
+        return set_err(CFWS_ERROR_INVALID_ARGUMENT, "arenas must be 16-byte aligned", hipSuccess);
+    const WsLayout L = ws_layout(n, cap);
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    xform_kernel<true><<<stream_grid(L.tiles_max), kThreads, 0, st>>>(
+        static_cast<const uint8_t*>(d_payload), static_cast<uint8_t*>(d_wire), d_desc, nullptr,
+        ws_ptr<const uint32_t>(ws, L.tile_map), ws_ptr<const uint64_t>(ws, L.total), cap,
+        (uint32_t)n);
+    return launch_check("serialize_execute");
+}
+
+int cfws_serialize_batch(const void* d_payload, cfws_frame_desc_t* d_desc, size_t n, void* d_wire,
+                         uint64_t cap, uint64_t* d_total, void* ws, size_t ws_size, void* stream)
+{
+    if (int rc = cfws_serialize_plan(d_desc, n, cap, d_total, ws, ws_size, stream)) return rc;
+    return cfws_serialize_execute(d_payload, d_desc, n, d_wire, cap, ws, stream);
+}
+
+int cfws_deserialize_plan(const void* d_wire, uint64_t wire_size, const uint64_t* d_index,
+                          size_t n, uint64_t max_payload, uint32_t align,
+                          cfws_frame_desc_t* d_desc, int32_t* d_status, uint64_t cap,
+                          uint64_t* d_total, void* ws, size_t ws_size, void* stream)
+{
+    if (int rc = check_init()) return rc;
+    if (align == 0 || (align & (align - 1)) || align > 4096)
+        return set_err(CFWS_ERROR_INVALID_ARGUMENT, "align must be a power of two <= 4096", hipSuccess);
+    const WsLayout L = ws_layout(n, cap);
+    if (!ws || ws_size < L.bytes) return set_err(CFWS_ERROR_WORKSPACE, "workspace too small", hipSuccess);
+    if (n > 0xffffffffull) return set_err(CFWS_ERROR_INVALID_ARGUMENT, "too many frames", hipSuccess);
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    if (n == 0) {
+        (void)hipMemsetAsync(ws_ptr<uint64_t>(ws, L.total), 0, 8, st);
+        if (d_total) (void)hipMemsetAsync(d_total, 0, 8, st);
+        return launch_check("deserialize_plan(empty)");
+    }
+    if (!d_wire || !d_index || !d_desc || !d_status)
+        return set_err(CFWS_ERROR_INVALID_ARGUMENT, "null pointer", hipSuccess);
+    uint64_t* vals = ws_ptr<uint64_t>(ws, L.vals);
+    uint64_t* partials = ws_ptr<uint64_t>(ws, L.partials);
+    uint64_t* grand = partials + L.scan_blocks;
+    deserialize_parse_kernel<<<grid_for(n, kThreads), kThreads, 0, st>>>(
+        static_cast<const uint8_t*>(d_wire), wire_size, d_index, n, max_payload, align, d_desc,
+        d_status, vals);
+    if (int rc = run_scan(vals, n, partials, grand, st)) return rc;
+    finalize_kernel<false><<<grid_for(n, kThreads), kThreads, 0, st>>>(
+        d_desc, d_status, vals, grand, n, cap, ws_ptr<uint32_t>(ws, L.tile_map),
+        ws_ptr<uint64_t>(ws, L.total), d_total);
+    return launch_check("deserialize_plan");
+}
+
+int cfws_deserialize_execute(const void* d_wire, const cfws_frame_desc_t* d_desc,
+                             const int32_t* d_status, size_t n, void* d_payload, uint64_t cap,
+                             const void* ws, void* stream)
+{
+    if (int rc = check_init()) return rc;
+    if (n == 0 || cap == 0) return CFWS_OK;
+    if (!d_wire || !d_desc || !d_status || !d_payload || !ws)
+        return set_err(CFWS_ERROR_INVALID_ARGUMENT, "null pointer", hipSuccess);
+    if ((reinterpret_cast<uintptr_t>(d_payload) | reinterpret_cast<uintptr_t>(d_wire)) & 15u)
+        return set_err(CFWS_ERROR_INVALID_ARGUMENT, "arenas must be 16-byte aligned", hipSuccess);
+    const WsLayout L = ws_layout(n, cap);
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    xform_kernel<false><<<stream_grid(L.tiles_max), kThreads, 0, st>>>(
+        static_cast<const uint8_t*>(d_wire), static_cast<uint8_t*>(d_payload), d_desc, d_status,
+        ws_ptr<const uint32_t>(ws, L.tile_map), ws_ptr<const uint64_t>(ws, L.total), cap,
+        (uint32_t)n);
+    return launch_check("deserialize_execute");
+}
+
+int cfws_deserialize_batch(const void* d_wire, uint64_t wire_size, const uint64_t* d_index,
+                           size_t n, uint64_t max_payload, uint32_t align,
+                           cfws_frame_desc_t* d_desc, int32_t* d_status, void* d_payload,
+                           uint64_t cap, uint64_t* d_total, void* ws, size_t ws_size,
+                           void* stream)
+{
+    if (int rc = cfws_deserialize_plan(d_wire, wire_size, d_index, n, max_payload, align, d_desc,
+                                       d_status, cap, d_total, ws, ws_size, stream))
+        return rc;
+    return cfws_deserialize_execute(d_wire, d_desc, d_status, n, d_payload, cap, ws, stream);
+}
+
+int cfws_xor_mask(const void* d_src, void* d_dst, uint64_t n, uint32_t key, uint32_t phase,
+                  void* stream)
+{
+    if (int rc = check_init()) return rc;
+    if (n == 0) return CFWS_OK;
+    const uint64_t blocks = (n / 16 + kThreads - 1) / kThreads;
+    const uint32_t g = (uint32_t)(blocks == 0 ? 1 : (blocks < 4096 ? blocks : 4096));
+    xor_mask_kernel<<<g, kThreads, 0, static_cast<hipStream_t>(stream)>>>(
+        static_cast<const uint8_t*>(d_src), static_cast<uint8_t*>(d_dst), n, key, phase & 3u);
+    return launch_check("xor_mask");
+}
+
+int cfws_fill_splitmix(void* d_dst, uint64_t n, uint64_t seed, uint64_t byte_base, void* stream)
+{
+    if (int rc = check_init()) return rc;
+    if (byte_base & 7u) return set_err(CFWS_ERROR_INVALID_ARGUMENT, "byte_base % 8 != 0", hipSuccess);
+    if (reinterpret_cast<uintptr_t>(d_dst) & 15u)
+        return set_err(CFWS_ERROR_INVALID_ARGUMENT, "destination must be 16-byte aligned", hipSuccess);
+    if (n == 0) return CFWS_OK;
+    const uint64_t blocks = (n / 16 + kThreads - 1) / kThreads;
+    const uint32_t g = (uint32_t)(blocks == 0 ? 1 : (blocks < 8192 ? blocks : 8192));
+    fill_splitmix_kernel<<<g, kThreads, 0, static_cast<hipStream_t>(stream)>>>(
+        static_cast<uint8_t*>(d_dst), n, seed, byte_base / 8);
+    return launch_check("fill_splitmix");
+}
+
+}  // extern "C"

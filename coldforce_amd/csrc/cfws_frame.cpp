@@ -1,0 +1,240 @@
+// cfws_frame.cpp -- the drop-in per-frame ABI (include/cfws_co_ws_frame.h).
+//
+// Same symbols, prototypes, struct layouts and return codes as coldforce's
+// src/ws/co_ws_frame.c + src/ws/co_ws_config.c, so libco_ws's callers
+// (co_ws_send, the receive loops, the ws_http2 extension) link against this
+// library unchanged. The payload XOR of a masked frame -- the reference's
+// scalar byte loops at co_ws_frame.c:93-97 and :234-242 -- runs on the
+// MI355X through cfws_xor_mask(); the 2-14 header bytes and the byte-array
+// bookkeeping stay on the calling thread. Unmasked frames are plain copies
+// in the reference too and stay plain copies here. There is no CPU XOR
+// path: without a gfx950 device a masked frame fails (serialize returns
+// false, deserialize CO_WS_ERROR_OUT_OF_MEMORY) and the reason goes to
+// stderr and cfws_last_error().
+#include <hip/hip_runtime.h>
+
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "cfws.h"
+#include "cfws_co_ws_frame.h"
+
+namespace {
+
+// co_ws_config.c:12-15 -- one process-wide, unsynchronised setting.
+size_t g_max_receive_payload_size = 32u * 1024u * 1024u;
+
+// Per calling thread: one stream and one device staging buffer, reused
+// across frames (coldforce runs each connection on one co_thread).
+struct ThreadDevice {
+    hipStream_t stream = nullptr;
+    void* buf = nullptr;
+    size_t cap = 0;
+};
+thread_local ThreadDevice t_dev;
+
+bool device_stage(size_t n)
+{
+    if (cfws_init() != CFWS_OK) return false;
+    if (!t_dev.stream && hipStreamCreateWithFlags(&t_dev.stream, hipStreamNonBlocking) != hipSuccess) {
+        fprintf(stderr, "cfws: hipStreamCreate failed\n");
+        t_dev.stream = nullptr;
+        return false;
+    }
+    if (t_dev.cap < n) {
+        size_t cap = 1u << 16;
+        while (cap < n) cap <<= 1;
+        if (t_dev.buf) (void)hipFree(t_dev.buf);
+        t_dev.buf = nullptr;
+        t_dev.cap = 0;
+        if (hipMalloc(&t_dev.buf, cap) != hipSuccess) {
+            fprintf(stderr, "cfws: hipMalloc(%zu) failed\n", cap);
+            return false;
+        }
+        t_dev.cap = cap;
+    }
+    return true;
+}
+
+// dst[i] = src[i] ^ key[i % 4] for a host buffer, through the device.
+bool device_xor(const uint8_t* src, uint8_t* dst, size_t n, uint32_t key)
+{
+    if (!device_stage(n)) return false;
+    hipStream_t st = t_dev.stream;
+    if (hipMemcpyAsync(t_dev.buf, src, n, hipMemcpyHostToDevice, st) != hipSuccess) return false;
+    if (cfws_xor_mask(t_dev.buf, t_dev.buf, n, key, 0, st) != CFWS_OK) return false;
+    if (hipMemcpyAsync(dst, t_dev.buf, n, hipMemcpyDeviceToHost, st) != hipSuccess) return false;
+    hipError_t e = hipStreamSynchronize(st);
+    if (e != hipSuccess) {
+        fprintf(stderr, "cfws: device XOR failed: %s\n", hipGetErrorString(e));
+        return false;
+    }
+    return true;
+}
+
+// co_array_set_count growth rule (src/core/co_array.c:83-112): capacity
+// doubles until it exceeds the new count.
+bool byte_array_reserve(co_byte_array_t* b, size_t count)
+{
+    if (b->capacity > count) return true;
+    size_t cap = b->capacity * 2;
+    while (cap <= count) cap *= 2;
+    void* nb = realloc(b->buffer, b->element_size * cap);
+    if (!nb) return false;
+    b->buffer = static_cast<uint8_t*>(nb);
+    b->capacity = cap;
+    return true;
+}
+
+// Header encode, co_ws_frame.c:34-91. Returns its size (2..14).
+uint32_t encode_header(bool fin, uint8_t opcode, bool mask, uint32_t key, uint64_t n, uint8_t* h)
+{
+    uint32_t k = 2;
+    h[0] = static_cast<uint8_t>(opcode | (fin ? 0x80u : 0u));
+    if (n <= 125u) {
+        h[1] = static_cast<uint8_t>(n);
+    } else if (n <= 0xffffu) {
+        h[1] = 126;
+        h[k++] = static_cast<uint8_t>(n >> 8);
+        h[k++] = static_cast<uint8_t>(n);
+    } else {
+        h[1] = 127;
+        for (int s = 56; s >= 0; s -= 8) h[k++] = static_cast<uint8_t>(n >> s);
+    }
+    if (mask) {
+        h[1] = static_cast<uint8_t>(h[1] | 0x80u);
+        for (int j = 0; j < 4; ++j) h[k++] = static_cast<uint8_t>(key >> (8 * j));
+    }
+    return k;
+}
+
+}  // namespace
+
+extern "C" {
+
+bool co_ws_frame_serialize(bool fin, uint8_t opcode, bool mask, const void* data, size_t n,
+                           co_byte_array_t* buffer)
+{
+    const size_t start = buffer->count;
+    const size_t hmax = 2 + (n > 0xffffu ? 8 : (n > 125u ? 2 : 0)) + (mask ? 4 : 0);
+    // The reference's only failure is malloc(n) before any key draw
+    // (co_ws_frame.c:74-80); reserving up front fails at the same point.
+    if (!byte_array_reserve(buffer, start + hmax + n)) return false;
+    uint32_t key = 0;
+    if (mask) {
+        // co_random(mask_key, 4): four (uint8_t)(random() % 256) draws.
+        for (int j = 0; j < 4; ++j) key |= static_cast<uint32_t>(static_cast<uint8_t>(random() % 256)) << (8 * j);
+    }
+    uint8_t* out = buffer->buffer + start;
+    const uint32_t hs = encode_header(fin, opcode, mask, key, n, out);
+    if (n > 0) {
+        if (mask) {
+            if (!device_xor(static_cast<const uint8_t*>(data), out + hs, n, key)) return false;
+        } else {
+            memcpy(out + hs, data, n);
+        }
+    }
+    buffer->count = start + hs + n;
+    return true;
+}
+
+int co_ws_frame_deserialize(co_ws_frame_t* frame, const uint8_t* data, const size_t data_size,
+                            size_t* index)
+{
+    size_t p = *index;
+    const uint8_t b0 = data[p++];
+    frame->header.fin = (b0 & 0x80u) != 0;
+    frame->header.opcode = static_cast<uint8_t>(b0 & 0x7fu);
+    if (frame->header.opcode > 0x0f) return CO_WS_ERROR_INVALID_FRAME;   // :139-142
+    frame->header.payload_size = 0;
+    frame->payload_data = nullptr;
+
+    const uint8_t b1 = data[p++];
+    const bool mask = (b1 & 0x80u) != 0;
+    const uint8_t l7 = static_cast<uint8_t>(b1 & 0x7fu);
+    if (l7 <= 125) {
+        frame->header.payload_size = l7;
+    } else {
+        const size_t ext = (l7 == 126) ? 2 : 8;
+        if (data_size - p < ext) return CO_WS_PARSE_MORE_DATA;           // :161-164, :176-179
+        uint64_t v = 0;
+        for (size_t i = 0; i < ext; ++i) v = (v << 8) | data[p + i];
+        frame->header.payload_size = v;
+        p += ext;
+    }
+    uint32_t key = 0;
+    if (mask) {
+        if (data_size - p < 4) return CO_WS_PARSE_MORE_DATA;             // :194-197
+        key = static_cast<uint32_t>(data[p]) | static_cast<uint32_t>(data[p + 1]) << 8 |
+              static_cast<uint32_t>(data[p + 2]) << 16 | static_cast<uint32_t>(data[p + 3]) << 24;
+        p += 4;
+    }
+    const uint64_t n = frame->header.payload_size;
+    if (static_cast<uint64_t>(data_size - p) < n) return CO_WS_PARSE_MORE_DATA;   // :203-206
+    if (n > g_max_receive_payload_size) return CO_WS_ERROR_DATA_TOO_BIG;         // :208-213
+    if (n > 0) {
+        uint8_t* payload = static_cast<uint8_t*>(malloc(static_cast<size_t>(n) + 1));
+        if (!payload) return CO_WS_ERROR_OUT_OF_MEMORY;
+        payload[n] = 0;
+        if (mask) {
+            if (!device_xor(data + p, payload, static_cast<size_t>(n), key)) {
+                free(payload);
+                return CO_WS_ERROR_OUT_OF_MEMORY;
+            }
+        } else {
+            memcpy(payload, data + p, static_cast<size_t>(n));
+        }
+        frame->payload_data = payload;
+        p += static_cast<size_t>(n);
+    }
+    *index = p;
+    return CO_WS_PARSE_COMPLETE;
+}
+
+co_ws_frame_t* co_ws_frame_create(void)
+{
+    co_ws_frame_t* f = static_cast<co_ws_frame_t*>(malloc(sizeof(co_ws_frame_t)));
+    if (!f) return nullptr;
+    f->header.fin = false;
+    f->header.opcode = 0xff;
+    f->header.payload_size = 0;
+    f->payload_data = nullptr;
+    return f;
+}
+
+void co_ws_frame_destroy(co_ws_frame_t* frame)
+{
+    if (!frame) return;
+    free(frame->payload_data);
+    free(frame);
+}
+
+bool co_ws_frame_get_fin(const co_ws_frame_t* frame) { return frame->header.fin; }
+uint8_t co_ws_frame_get_opcode(const co_ws_frame_t* frame) { return frame->header.opcode; }
+uint64_t co_ws_frame_get_payload_size(const co_ws_frame_t* frame) { return frame->header.payload_size; }
+const uint8_t* co_ws_frame_get_payload_data(const co_ws_frame_t* frame) { return frame->payload_data; }
+
+void co_ws_config_set_max_receive_payload_size(size_t v) { g_max_receive_payload_size = v; }
+size_t co_ws_config_get_max_receive_payload_size(void) { return g_max_receive_payload_size; }
+
+void cfws_draw_mask_keys(size_t n, const uint8_t* mask_flags, uint32_t* keys)
+{
+    for (size_t i = 0; i < n; ++i) {
+        uint32_t k = 0;
+        if (!mask_flags || mask_flags[i])
+            for (int j = 0; j < 4; ++j) k |= static_cast<uint32_t>(static_cast<uint8_t>(random() % 256)) << (8 * j);
+        keys[i] = k;
+    }
+}
+
+// Frees the calling thread's staging buffer and stream (optional; a thread
+// that exits without calling it leaks them until process exit).
+void cfws_release_thread_resources(void)
+{
+    if (t_dev.buf) (void)hipFree(t_dev.buf);
+    if (t_dev.stream) (void)hipStreamDestroy(t_dev.stream);
+    t_dev = ThreadDevice{};
+}
+
+}  // extern "C"

@@ -1,0 +1,154 @@
+/*
+ * cfws.h -- MI355X batch WebSocket frame codec: C ABI over device arenas.
+ *
+ * This is the batch entry point that sits beside the drop-in per-frame API
+ * (include/cfws_co_ws_frame.h). It covers the hot path of coldforce's
+ * src/ws/co_ws_frame.c for many independent frames at once:
+ *
+ *   cfws_serialize_*   = co_ws_frame_serialize   (co_ws_frame.c:21-119)
+ *                        for every frame of a batch: header encode + 4-byte
+ *                        key XOR mask, frames packed back to back in a wire
+ *                        arena exactly as sequential appends to one
+ *                        co_byte_array_t would lay them out.
+ *   cfws_deserialize_* = co_ws_frame_deserialize (co_ws_frame.c:121-247)
+ *                        at each given frame start of a wire arena (as the
+ *                        receive loops call it, co_ws_server.c:107-169):
+ *                        header decode, MORE_DATA / INVALID_FRAME /
+ *                        DATA_TOO_BIG decisions, copy + XOR unmask of every
+ *                        COMPLETE payload into a payload arena.
+ *
+ * Every pointer argument named d_* is device memory (hipMalloc); `stream` is
+ * a hipStream_t (NULL = default stream). Nothing here synchronises: results
+ * are valid once the stream has reached the end of the call. All arenas
+ * must be 16-byte aligned. The library needs a gfx950 device; with none it
+ * returns CFWS_ERROR_NO_DEVICE (there is no CPU fallback).
+ */
+#ifndef CFWS_H
+#define CFWS_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Return codes of the batch API. */
+#define CFWS_OK                       0
+#define CFWS_ERROR_INVALID_ARGUMENT  (-1)
+#define CFWS_ERROR_WORKSPACE         (-2)
+#define CFWS_ERROR_HIP               (-3)
+#define CFWS_ERROR_NO_DEVICE         (-4)
+
+/* Per-frame status codes written by deserialize: the reference's own values
+ * (inc/coldforce/ws/co_ws.h:25-39). */
+#define CFWS_PARSE_COMPLETE           0
+#define CFWS_PARSE_MORE_DATA          1
+#define CFWS_ERROR_INVALID_FRAME     (-7001)
+#define CFWS_ERROR_DATA_TOO_BIG      (-7005)
+#define CFWS_ERROR_OUT_OF_MEMORY     (-7006)
+
+/* Default max receive payload, co_ws_config.h:15. */
+#define CFWS_DEFAULT_MAX_RECEIVE_PAYLOAD_SIZE ((uint64_t)32 * 1024 * 1024)
+
+/*
+ * One frame of a batch (32 bytes, device resident, array-of-structs).
+ *   serialize:   in  payload_off, payload_size, mask_key, fin, opcode, mask
+ *                out wire_off, header_size
+ *   deserialize: in  wire_off (the frame start, from the caller's index)
+ *                out everything else, as far as the header was parsed
+ * mask_key holds the 4 key bytes in wire order: byte j = (mask_key >> 8j).
+ * opcode is written to the wire verbatim, OR 0x80 when fin (co_ws_frame.c
+ * :34-39); deserialize reports opcode = b0 & 0x7f (co_ws_frame.c:136-137).
+ */
+typedef struct cfws_frame_desc {
+    uint64_t payload_off;
+    uint64_t wire_off;
+    uint64_t payload_size;
+    uint32_t mask_key;
+    uint8_t  fin;
+    uint8_t  opcode;
+    uint8_t  mask;
+    uint8_t  header_size;
+} cfws_frame_desc_t;
+
+/* Library / device check: CFWS_OK when a gfx950 device is usable. */
+int cfws_init(void);
+const char* cfws_last_error(void);
+const char* cfws_version(void);
+
+/* Bytes of device workspace a plan+execute over n_frames frames producing
+ * at most out_capacity output bytes needs. */
+size_t cfws_workspace_size(size_t n_frames, uint64_t out_capacity);
+
+/* ---- serialize (client mask / server plain) ------------------------------
+ * plan:    header sizes, wire offsets (prefix sum), tile map, and
+ *          *d_wire_total = total wire bytes (not clamped to capacity).
+ * execute: writes headers + (masked) payloads; bytes past wire_capacity are
+ *          not written (check *d_wire_total <= wire_capacity).
+ * The workspace carries the plan from plan to execute. */
+int cfws_serialize_plan(cfws_frame_desc_t* d_desc, size_t n_frames,
+                        uint64_t wire_capacity, uint64_t* d_wire_total,
+                        void* d_workspace, size_t workspace_size, void* stream);
+int cfws_serialize_execute(const void* d_payload, const cfws_frame_desc_t* d_desc,
+                           size_t n_frames, void* d_wire, uint64_t wire_capacity,
+                           const void* d_workspace, void* stream);
+int cfws_serialize_batch(const void* d_payload, cfws_frame_desc_t* d_desc,
+                         size_t n_frames, void* d_wire, uint64_t wire_capacity,
+                         uint64_t* d_wire_total, void* d_workspace,
+                         size_t workspace_size, void* stream);
+
+/* ---- deserialize (server unmask / client plain) --------------------------
+ * plan:    parses the header at each d_frame_index[i] against wire_size,
+ *          writes d_desc[i] and d_status[i] (reference codes), lays COMPLETE
+ *          payloads out at payload_off = exclusive prefix sum of
+ *          round_up(payload_size, align) (align a power of two, 1..4096);
+ *          a COMPLETE frame whose payload does not fit payload_capacity gets
+ *          CFWS_ERROR_OUT_OF_MEMORY. *d_payload_total = min(sum, capacity).
+ * execute: copies + unmasks every COMPLETE payload; the bytes between one
+ *          payload's end and the next payload_off are written as zero. */
+int cfws_deserialize_plan(const void* d_wire, uint64_t wire_size,
+                          const uint64_t* d_frame_index, size_t n_frames,
+                          uint64_t max_payload, uint32_t align,
+                          cfws_frame_desc_t* d_desc, int32_t* d_status,
+                          uint64_t payload_capacity, uint64_t* d_payload_total,
+                          void* d_workspace, size_t workspace_size, void* stream);
+int cfws_deserialize_execute(const void* d_wire, const cfws_frame_desc_t* d_desc,
+                             const int32_t* d_status, size_t n_frames,
+                             void* d_payload, uint64_t payload_capacity,
+                             const void* d_workspace, void* stream);
+int cfws_deserialize_batch(const void* d_wire, uint64_t wire_size,
+                           const uint64_t* d_frame_index, size_t n_frames,
+                           uint64_t max_payload, uint32_t align,
+                           cfws_frame_desc_t* d_desc, int32_t* d_status,
+                           void* d_payload, uint64_t payload_capacity,
+                           uint64_t* d_payload_total, void* d_workspace,
+                           size_t workspace_size, void* stream);
+
+/* ---- single-buffer XOR (used by the per-frame drop-in path) --------------
+ * d_dst[i] = d_src[i] ^ key byte (i + key_phase) % 4, i < n. */
+int cfws_xor_mask(const void* d_src, void* d_dst, uint64_t n, uint32_t mask_key,
+                  uint32_t key_phase, void* stream);
+
+/* Mask keys for a batch, drawn exactly as sequential co_ws_frame_serialize
+ * calls would draw them: 4 x (random() % 256) per frame whose mask flag is
+ * set, in frame order, from the process's current random() state
+ * (co_ws_frame.c:84 -> src/core/co_random.c:32-35). mask_flags == NULL
+ * means every frame is masked; unmasked frames get key 0. Host memory. */
+void cfws_draw_mask_keys(size_t n_frames, const uint8_t* mask_flags, uint32_t* keys);
+
+/* Frees the calling thread's drop-in staging buffer and stream
+ * (cfws_frame.cpp); optional. */
+void cfws_release_thread_resources(void);
+
+/* ---- synthetic input (bench / tests) -------------------------------------
+ * d_dst[i] = byte ((byte_base + i) % 8) of splitmix64 output number
+ * (byte_base + i) / 8 for `seed`; byte_base must be a multiple of 8. */
+int cfws_fill_splitmix(void* d_dst, uint64_t n_bytes, uint64_t seed,
+                       uint64_t byte_base, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* CFWS_H */

@@ -1,0 +1,241 @@
+"""TEST INFRASTRUCTURE ONLY -- ctypes bindings for the parity checker.
+
+``liboracle.so`` is the clean-room CPU restatement of coldforce's frame codec
+(``oracle/cfws_oracle.c``); ``_ref/libcfws_ref*.so`` is the reference codec
+itself, compiled in place from ``/root/reference`` by ``oracle/Makefile``
+(absent on the GPU box unless built here first).
+
+Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s cpu_baseline
+leg may import this package; ``coldforce_amd`` never does.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ORACLE_SO = os.path.join(HERE, "liboracle.so")
+REF_SO = {"O2": os.path.join(HERE, "_ref", "libcfws_ref.so"),
+          "O0": os.path.join(HERE, "_ref", "libcfws_ref_O0.so")}
+
+PARSE_COMPLETE = 0
+PARSE_MORE_DATA = 1
+ERROR_INVALID_FRAME = -7001
+ERROR_DATA_TOO_BIG = -7005
+ERROR_OUT_OF_MEMORY = -7006
+DEFAULT_MAX_PAYLOAD = 32 * 1024 * 1024  # co_ws_config.h:15
+
+# Same 32-byte layout as cfws_frame_desc_t (include/cfws.h) / orc_desc_t.
+DESC_DTYPE = np.dtype([("payload_off", "<u8"), ("wire_off", "<u8"),
+                       ("payload_size", "<u8"), ("mask_key", "<u4"),
+                       ("fin", "u1"), ("opcode", "u1"), ("mask", "u1"),
+                       ("header_size", "u1")])
+assert DESC_DTYPE.itemsize == 32
+
+_u8p = C.POINTER(C.c_uint8)
+_vp = C.c_void_p
+_u64 = C.c_uint64
+_sz = C.c_size_t
+
+
+def _ptr(a):
+    return a.ctypes.data_as(_vp) if a is not None else None
+
+
+def build(ref: bool = True) -> None:
+    """Compile the restatement (and the reference when /root/reference exists)."""
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+    if ref and os.path.isdir("/root/reference"):
+        subprocess.run(["make", "-s", "-C", HERE, "ref"], check=True)
+
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(ORACLE_SO):
+            build(ref=False)
+        L = C.CDLL(ORACLE_SO)
+        L.orc_serialize_keyed.argtypes = [C.c_bool, C.c_uint8, C.c_bool, C.c_uint32, _vp, _sz, _vp]
+        L.orc_serialize_keyed.restype = _sz
+        L.orc_header_size.argtypes = [_u64, C.c_bool]
+        L.orc_header_size.restype = C.c_uint32
+        L.orc_keys.argtypes = [C.c_uint32, _sz, _vp, _vp]
+        L.orc_serialize_batch.argtypes = [_vp, _vp, _sz, _vp]
+        L.orc_serialize_batch.restype = _u64
+        L.orc_deserialize_batch.argtypes = [_vp, _u64, _vp, _sz, _u64, C.c_uint32, _vp, _vp, _vp, _u64]
+        L.orc_deserialize_batch.restype = _u64
+        L.orc_index_frames.argtypes = [_vp, _u64, _u64, _vp, _sz, C.POINTER(_u64)]
+        L.orc_index_frames.restype = _sz
+        L.orc_fill_splitmix.argtypes = [_vp, _u64, _u64, _u64]
+        L.orc_cpu_bench.argtypes = [_u64, _u64, C.c_int, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double)]
+        L.orc_cpu_bench.restype = C.c_int
+        _bind_flat(L, "orc")
+        _lib = L
+    return _lib
+
+
+def header_size(n: int, mask: bool) -> int:
+    return lib().orc_header_size(n, mask)
+
+
+def serialize_keyed(fin: bool, opcode: int, mask: bool, key: int, data: bytes) -> bytes:
+    src = np.frombuffer(data, dtype=np.uint8) if len(data) else np.zeros(1, np.uint8)
+    out = np.zeros(len(data) + 16, dtype=np.uint8)
+    n = lib().orc_serialize_keyed(fin, opcode, mask, key, _ptr(src), len(data), _ptr(out))
+    return out[:n].tobytes()
+
+
+def keys(seed: int, n: int, mask_flags=None) -> np.ndarray:
+    out = np.zeros(n, dtype=np.uint32)
+    mf = None if mask_flags is None else np.ascontiguousarray(mask_flags, dtype=np.uint8)
+    lib().orc_keys(seed, n, _ptr(mf), _ptr(out))
+    return out
+
+
+def serialize_batch(payload: np.ndarray, desc: np.ndarray):
+    """Returns (wire bytes ndarray, desc with wire_off/header_size filled)."""
+    desc = desc.copy()
+    total = int(sum(int(d["payload_size"]) + header_size(int(d["payload_size"]), bool(d["mask"]))
+                    for d in desc)) if len(desc) < 4096 else None
+    if total is None:
+        sizes = desc["payload_size"].astype(np.uint64)
+        hs = 2 + np.where(sizes > 65535, 8, np.where(sizes > 125, 2, 0)) + 4 * (desc["mask"] != 0)
+        total = int((sizes + hs.astype(np.uint64)).sum())
+    wire = np.zeros(max(total, 1), dtype=np.uint8)
+    pl = payload if payload.size else np.zeros(1, np.uint8)
+    n = lib().orc_serialize_batch(_ptr(pl), _ptr(desc), len(desc), _ptr(wire))
+    assert n == total
+    return wire[:total], desc
+
+
+def deserialize_batch(wire: np.ndarray, starts: np.ndarray, align: int = 16,
+                      max_payload: int = DEFAULT_MAX_PAYLOAD, capacity: int | None = None):
+    """Returns (payload arena, desc, status, total)."""
+    starts = np.ascontiguousarray(starts, dtype=np.uint64)
+    n = len(starts)
+    if capacity is None:
+        capacity = len(wire) + 16 * n + 16
+    desc = np.zeros(n, dtype=DESC_DTYPE)
+    status = np.zeros(n, dtype=np.int32)
+    out = np.zeros(max(capacity, 1), dtype=np.uint8)
+    w = wire if wire.size else np.zeros(1, np.uint8)
+    total = lib().orc_deserialize_batch(_ptr(w), len(wire), _ptr(starts), n, max_payload,
+                                        align, _ptr(desc), _ptr(status), _ptr(out), capacity)
+    return out, desc, status, int(total)
+
+
+def index_frames(wire: np.ndarray, max_frames: int, max_payload: int = DEFAULT_MAX_PAYLOAD):
+    starts = np.zeros(max(max_frames, 1), dtype=np.uint64)
+    consumed = _u64(0)
+    w = wire if wire.size else np.zeros(1, np.uint8)
+    k = lib().orc_index_frames(_ptr(w), len(wire), max_payload, _ptr(starts), max_frames,
+                               C.byref(consumed))
+    return starts[:k], int(consumed.value)
+
+
+def fill_splitmix(n_bytes: int, seed: int, byte_base: int = 0) -> np.ndarray:
+    out = np.zeros(max(n_bytes, 1), dtype=np.uint8)
+    lib().orc_fill_splitmix(_ptr(out), n_bytes, seed, byte_base)
+    return out[:n_bytes]
+
+
+def splitmix_words(seed: int, first_word: int, n_words: int) -> np.ndarray:
+    """Vectorised numpy splitmix64 (same function as orc_fill_splitmix)."""
+    i = np.arange(first_word, first_word + n_words, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        z = np.uint64(seed) + (i + np.uint64(1)) * np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z = z ^ (z >> np.uint64(31))
+    return z
+
+
+def cpu_bench(n_frames: int, frame_size: int, threads: int, iters: int, kind: str = "port"):
+    """Time per-frame serialize(mask)+deserialize. Returns (mask_s, unmask_s)."""
+    if kind == "port":
+        L, fn = lib(), "orc_cpu_bench"
+    else:
+        L, fn = ref_lib(kind[len("reference"):].strip("_-") or "O2"), "ref_cpu_bench"
+        if L is None:
+            raise FileNotFoundError("oracle/_ref not built")
+    f = getattr(L, fn)
+    f.argtypes = [_u64, _u64, C.c_int, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double)]
+    f.restype = C.c_int
+    ms, us = C.c_double(0), C.c_double(0)
+    rc = f(n_frames, frame_size, threads, iters, C.byref(ms), C.byref(us))
+    if rc != 0:
+        raise RuntimeError(f"cpu bench failed rc={rc}")
+    return ms.value, us.value
+
+
+# ---- the reference itself (oracle/_ref), when built -------------------------
+
+
+class _Flat:
+    """Uniform per-frame API over either library (prefix orc_ or ref_)."""
+
+    def __init__(self, L, prefix):
+        self.srandom = getattr(L, prefix + "_srandom")
+        self.serialize = getattr(L, prefix + "_serialize" + ("_flat" if prefix == "orc" else ""))
+        self.deserialize = getattr(L, prefix + "_deserialize" + ("_flat" if prefix == "orc" else ""))
+
+
+def _bind_flat(L, prefix):
+    f = _Flat(L, prefix)
+    f.srandom.argtypes = [C.c_uint]
+    f.srandom.restype = None
+    f.serialize.argtypes = [C.c_int, C.c_ubyte, C.c_int, _vp, C.c_ulonglong, _vp, C.c_ulonglong]
+    f.serialize.restype = C.c_longlong
+    f.deserialize.argtypes = [_vp, C.c_ulonglong, C.POINTER(C.c_ulonglong), C.c_ulonglong,
+                              C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_ulonglong),
+                              C.POINTER(C.c_int), _vp, C.c_ulonglong]
+    f.deserialize.restype = C.c_int
+    L.flat = f
+
+_ref = {}
+
+
+def ref_lib(opt: str = "O2"):
+    if opt not in _ref:
+        path = REF_SO[opt]
+        if not os.path.exists(path):
+            return None
+        L = C.CDLL(path)
+        _bind_flat(L, "ref")
+        _ref[opt] = L
+    return _ref[opt]
+
+
+def srandom(L, seed: int) -> None:
+    L.flat.srandom(seed)
+
+
+def ref_serialize(L, fin: bool, opcode: int, mask: bool, data: bytes) -> bytes:
+    """co_ws_frame_serialize through library L (oracle lib() or ref_lib())."""
+    src = np.frombuffer(data, dtype=np.uint8) if len(data) else np.zeros(1, np.uint8)
+    out = np.zeros(len(data) + 16, dtype=np.uint8)
+    n = L.flat.serialize(int(fin), opcode, int(mask), _ptr(src), len(data), _ptr(out), out.size)
+    assert n >= 0, n
+    return out[:n].tobytes()
+
+
+def ref_deserialize(L, data: bytes, index: int = 0, max_payload: int = DEFAULT_MAX_PAYLOAD):
+    """co_ws_frame_deserialize through library L. Returns dict(rc, index, fin, opcode, payload_size, payload|None)."""
+    src = np.frombuffer(data, dtype=np.uint8) if len(data) else np.zeros(1, np.uint8)
+    out = np.zeros(len(data) + 2, dtype=np.uint8)
+    idx = C.c_ulonglong(index)
+    fin, op, isnull = C.c_int(), C.c_int(), C.c_int()
+    psz = C.c_ulonglong()
+    rc = L.flat.deserialize(_ptr(src), len(data), C.byref(idx), max_payload, C.byref(fin),
+                           C.byref(op), C.byref(psz), C.byref(isnull), _ptr(out), out.size)
+    payload = None
+    if rc == 0 and not isnull.value:
+        payload = out[:psz.value + 1].tobytes()  # includes the NUL terminator
+    return dict(rc=rc, index=idx.value, fin=bool(fin.value), opcode=op.value,
+                payload_size=psz.value, payload=payload)

@@ -1,0 +1,366 @@
+/*
+ * cfws_oracle.c -- TEST INFRASTRUCTURE ONLY (see cfws_oracle.h).
+ *
+ * Clean-room CPU restatement of the coldforce RFC 6455 frame codec. Every
+ * function cites the reference lines whose behaviour it restates; the
+ * restatement is deliberately scalar (byte loop, key[i % 4]) so that it also
+ * serves as the "port" CPU baseline.
+ */
+#include "cfws_oracle.h"
+
+#include <stdlib.h>
+#include <string.h>
+
+/* ---- byte buffer: co_array_set_count / co_array_add growth rule ---------
+ * src/core/co_array.c:83-112 (capacity doubles from 8 until > count),
+ * :183-194 (append = grow + memcpy). */
+
+orc_bytes_t* orc_bytes_create(void)
+{
+    orc_bytes_t* b = (orc_bytes_t*)malloc(sizeof(*b));
+    if (!b) return NULL;
+    b->capacity = 8;
+    b->count = 0;
+    b->element_size = 1;
+    b->buffer = (uint8_t*)malloc(b->capacity);
+    if (!b->buffer) { free(b); return NULL; }
+    return b;
+}
+
+void orc_bytes_destroy(orc_bytes_t* b)
+{
+    if (b) { free(b->buffer); free(b); }
+}
+
+static bool orc_bytes_append(orc_bytes_t* b, const void* p, size_t n)
+{
+    size_t need = b->count + n;
+    if (b->capacity <= need) {
+        size_t cap = b->capacity * 2;
+        while (cap <= need) cap *= 2;
+        uint8_t* nb = (uint8_t*)realloc(b->buffer, cap);
+        if (!nb) return false;
+        b->buffer = nb;
+        b->capacity = cap;
+    }
+    memcpy(b->buffer + b->count, p, n);
+    b->count = need;
+    return true;
+}
+
+/* ---- header encode: co_ws_frame.c:34-68 (b0, 7/16/64-bit length) and
+ * :70-91 (mask bit + 4 key bytes after the length). The opcode byte is
+ * OR-ed verbatim with 0x80 when fin is set (no 4-bit masking). */
+
+uint32_t orc_header_size(uint64_t n, bool mask)
+{
+    uint32_t h = 2;
+    if (n > 65535u) h += 8;
+    else if (n > 125u) h += 2;
+    if (mask) h += 4;
+    return h;
+}
+
+static uint32_t orc_encode_header(bool fin, uint8_t opcode, bool mask,
+                                  uint32_t key, uint64_t n, uint8_t* h)
+{
+    uint32_t pos = 2;
+    h[0] = (uint8_t)(opcode | (fin ? 0x80u : 0u));
+    if (n <= 125u) {
+        h[1] = (uint8_t)n;
+    } else if (n <= 65535u) {
+        h[1] = 126;
+        h[pos++] = (uint8_t)(n >> 8);
+        h[pos++] = (uint8_t)n;
+    } else {
+        h[1] = 127;
+        for (int s = 56; s >= 0; s -= 8) h[pos++] = (uint8_t)(n >> s);
+    }
+    if (mask) {
+        h[1] |= 0x80u;
+        for (int j = 0; j < 4; ++j) h[pos++] = (uint8_t)(key >> (8 * j));
+    }
+    return pos;
+}
+
+/* Key draw: co_random(mask_key, 4) (co_ws_frame.c:84), i.e. 4 sequential
+ * (uint8_t)(random() % 256) (src/core/co_random.c:32-35). */
+static uint32_t orc_draw_key(void)
+{
+    uint32_t k = 0;
+    for (int j = 0; j < 4; ++j) k |= (uint32_t)(uint8_t)(random() % 256) << (8 * j);
+    return k;
+}
+
+static void orc_xor_bytes(uint8_t* dst, const uint8_t* src, uint64_t n, uint32_t key)
+{
+    uint8_t kb[4] = {(uint8_t)key, (uint8_t)(key >> 8), (uint8_t)(key >> 16),
+                     (uint8_t)(key >> 24)};
+    for (uint64_t i = 0; i < n; ++i) dst[i] = src[i] ^ kb[i % 4];
+}
+
+/* co_ws_frame_serialize, co_ws_frame.c:21-119. With mask: malloc(n) first
+ * (fails before anything is appended, :74-80), key, XOR (:93-97), append
+ * header then payload (:99-104). */
+bool orc_serialize(bool fin, uint8_t opcode, bool mask, const void* data,
+                   size_t n, orc_bytes_t* buffer)
+{
+    uint8_t h[16];
+    if (!mask) {
+        uint32_t hs = orc_encode_header(fin, opcode, false, 0, n, h);
+        orc_bytes_append(buffer, h, hs);
+        if (n > 0) orc_bytes_append(buffer, data, n);
+        return true;
+    }
+    uint8_t* tmp = (uint8_t*)malloc(n);
+    if (tmp == NULL && n > 0) return false;
+    uint32_t key = orc_draw_key();
+    uint32_t hs = orc_encode_header(fin, opcode, true, key, n, h);
+    orc_xor_bytes(tmp, (const uint8_t*)data, n, key);
+    orc_bytes_append(buffer, h, hs);
+    if (n > 0) orc_bytes_append(buffer, tmp, n);
+    free(tmp);
+    return true;
+}
+
+size_t orc_serialize_keyed(bool fin, uint8_t opcode, bool mask, uint32_t key,
+                           const uint8_t* data, size_t n, uint8_t* out)
+{
+    uint32_t hs = orc_encode_header(fin, opcode, mask, key, n, out);
+    if (mask) orc_xor_bytes(out + hs, data, n, key);
+    else if (n) memcpy(out + hs, data, n);
+    return hs + n;
+}
+
+/* ---- deserialize: co_ws_frame.c:121-247 ------------------------------- */
+
+void orc_frame_init(orc_frame_t* f)
+{   /* co_ws_frame_create, co_ws_frame.c:266-269 */
+    f->header.fin = false;
+    f->header.opcode = 0xff;
+    f->header.payload_size = 0;
+    f->payload_data = NULL;
+}
+
+void orc_frame_clear(orc_frame_t* f)
+{
+    free(f->payload_data);
+    f->payload_data = NULL;
+}
+
+static uint64_t orc_be(const uint8_t* p, int nbytes)
+{
+    uint64_t v = 0;
+    for (int i = 0; i < nbytes; ++i) v = (v << 8) | p[i];
+    return v;
+}
+
+int orc_deserialize(orc_frame_t* f, const uint8_t* data, size_t data_size,
+                    size_t* index, size_t max_payload)
+{
+    size_t p = *index;
+    uint8_t b0 = data[p++];
+    /* :136-142 -- RSV bits stay in the opcode, so any RSV bit => invalid. */
+    f->header.fin = (b0 & 0x80u) != 0;
+    f->header.opcode = (uint8_t)(b0 & 0x7fu);
+    if (f->header.opcode > 0x0f) return ORC_ERROR_INVALID_FRAME;
+    f->header.payload_size = 0;   /* :144-145 */
+    f->payload_data = NULL;
+
+    uint8_t b1 = data[p++];       /* :147-153 */
+    bool mask = (b1 & 0x80u) != 0;
+    uint8_t l7 = (uint8_t)(b1 & 0x7fu);
+    if (l7 <= 125) {               /* :155-158 */
+        f->header.payload_size = l7;
+    } else {                       /* :159-188, no minimal-encoding check */
+        int ext = (l7 == 126) ? 2 : 8;
+        if (data_size - p < (size_t)ext) return ORC_PARSE_MORE_DATA;
+        f->header.payload_size = orc_be(data + p, ext);
+        p += (size_t)ext;
+    }
+    uint32_t key = 0;
+    if (mask) {                    /* :190-201 */
+        if (data_size - p < 4) return ORC_PARSE_MORE_DATA;
+        key = (uint32_t)data[p] | (uint32_t)data[p + 1] << 8 |
+              (uint32_t)data[p + 2] << 16 | (uint32_t)data[p + 3] << 24;
+        p += 4;
+    }
+    uint64_t n = f->header.payload_size;
+    /* :203-206 MORE_DATA is decided before the size limit (:208-213). */
+    if ((uint64_t)(data_size - p) < n) return ORC_PARSE_MORE_DATA;
+    if (n > (uint64_t)max_payload) return ORC_ERROR_DATA_TOO_BIG;
+    if (n > 0) {                   /* :214-230 copy + NUL terminator */
+        f->payload_data = (uint8_t*)malloc((size_t)n + 1);
+        if (f->payload_data == NULL) return ORC_ERROR_OUT_OF_MEMORY;
+        f->payload_data[n] = 0;
+        if (mask) orc_xor_bytes(f->payload_data, data + p, n, key);  /* :232-242 */
+        else memcpy(f->payload_data, data + p, (size_t)n);
+        p += (size_t)n;
+    }
+    *index = p;                    /* :244, only on COMPLETE */
+    return ORC_PARSE_COMPLETE;
+}
+
+/* ---- batch mirrors of the device ABI ---------------------------------- */
+
+void orc_keys(uint32_t seed, size_t n, const uint8_t* mask_flags, uint32_t* keys)
+{
+    srandom(seed);
+    for (size_t i = 0; i < n; ++i)
+        keys[i] = (mask_flags == NULL || mask_flags[i]) ? orc_draw_key() : 0u;
+}
+
+uint64_t orc_serialize_batch(const uint8_t* payload, orc_desc_t* d, size_t n,
+                             uint8_t* wire)
+{
+    uint64_t off = 0;
+    for (size_t i = 0; i < n; ++i) {
+        d[i].wire_off = off;
+        d[i].header_size = (uint8_t)orc_header_size(d[i].payload_size, d[i].mask != 0);
+        off += orc_serialize_keyed(d[i].fin != 0, d[i].opcode, d[i].mask != 0,
+                                   d[i].mask_key, payload + d[i].payload_off,
+                                   (size_t)d[i].payload_size, wire + off);
+    }
+    return off;
+}
+
+/* Parse the header at `start` without copying the payload: the same
+ * decisions as orc_deserialize (co_ws_frame.c:131-213). */
+static int orc_parse_header(const uint8_t* w, uint64_t size, uint64_t start,
+                            uint64_t max_payload, orc_desc_t* d)
+{
+    memset(d, 0, sizeof(*d));
+    d->wire_off = start;
+    if (start > size || size - start < 2) return ORC_PARSE_MORE_DATA;  /* caller precheck */
+    uint8_t b0 = w[start], b1 = w[start + 1];
+    d->fin = (uint8_t)(b0 >> 7);
+    d->opcode = (uint8_t)(b0 & 0x7f);
+    if (d->opcode > 0x0f) return ORC_ERROR_INVALID_FRAME;
+    uint64_t p = start + 2;
+    uint8_t l7 = b1 & 0x7f;
+    d->mask = (uint8_t)(b1 >> 7);
+    if (l7 <= 125) {
+        d->payload_size = l7;
+    } else {
+        int ext = (l7 == 126) ? 2 : 8;
+        if (size - p < (uint64_t)ext) return ORC_PARSE_MORE_DATA;
+        d->payload_size = orc_be(w + p, ext);
+        p += (uint64_t)ext;
+    }
+    if (d->mask) {
+        if (size - p < 4) return ORC_PARSE_MORE_DATA;
+        d->mask_key = (uint32_t)w[p] | (uint32_t)w[p + 1] << 8 |
+                      (uint32_t)w[p + 2] << 16 | (uint32_t)w[p + 3] << 24;
+        p += 4;
+    }
+    d->header_size = (uint8_t)(p - start);
+    if (size - p < d->payload_size) return ORC_PARSE_MORE_DATA;
+    if (d->payload_size > max_payload) return ORC_ERROR_DATA_TOO_BIG;
+    return ORC_PARSE_COMPLETE;
+}
+
+uint64_t orc_deserialize_batch(const uint8_t* wire, uint64_t wire_size,
+                               const uint64_t* starts, size_t n,
+                               uint64_t max_payload, uint32_t align,
+                               orc_desc_t* d, int32_t* status,
+                               uint8_t* payload, uint64_t cap)
+{
+    if (align == 0) align = 1;
+    uint64_t off = 0;
+    for (size_t i = 0; i < n; ++i) {
+        int st = orc_parse_header(wire, wire_size, starts[i], max_payload, &d[i]);
+        uint64_t len = (st == ORC_PARSE_COMPLETE) ? d[i].payload_size : 0;
+        /* the layout is fixed by the parse results; capacity only marks */
+        uint64_t next = off + (len + align - 1) / align * align;
+        if (st == ORC_PARSE_COMPLETE && off + len > cap) {
+            st = ORC_ERROR_OUT_OF_MEMORY;
+            len = 0;
+        }
+        status[i] = st;
+        d[i].payload_off = off;
+        if (len) {
+            const uint8_t* src = wire + starts[i] + d[i].header_size;
+            if (d[i].mask) orc_xor_bytes(payload + off, src, len, d[i].mask_key);
+            else memcpy(payload + off, src, (size_t)len);
+        }
+        uint64_t pad_end = next < cap ? next : cap;
+        if (pad_end > off + len) memset(payload + off + len, 0, (size_t)(pad_end - off - len));
+        off = next;
+    }
+    return off < cap ? off : cap;
+}
+
+size_t orc_index_frames(const uint8_t* wire, uint64_t size, uint64_t max_payload,
+                        uint64_t* starts, size_t max_frames, uint64_t* consumed)
+{
+    size_t k = 0;
+    uint64_t p = 0;
+    orc_desc_t d;
+    while (k < max_frames && p < size) {
+        if (orc_parse_header(wire, size, p, max_payload, &d) != ORC_PARSE_COMPLETE) break;
+        starts[k++] = p;
+        p += d.header_size + d.payload_size;
+    }
+    if (consumed) *consumed = p;
+    return k;
+}
+
+/* ---- synthetic data ---------------------------------------------------- */
+
+static uint64_t orc_splitmix(uint64_t seed, uint64_t i)
+{
+    uint64_t z = seed + (i + 1) * 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+void orc_fill_splitmix(uint8_t* out, uint64_t n, uint64_t seed, uint64_t base)
+{
+    for (uint64_t i = 0; i < n; ++i) {
+        uint64_t o = base + i;
+        out[i] = (uint8_t)(orc_splitmix(seed, o >> 3) >> (8 * (o & 7)));
+    }
+}
+
+/* ---- flat entry points for ctypes (same shapes as ref_shim.c) ---------- */
+
+void orc_srandom(unsigned int seed) { srandom(seed); }
+
+long long orc_serialize_flat(int fin, unsigned char opcode, int mask, const void* data,
+                             unsigned long long n, unsigned char* out,
+                             unsigned long long cap)
+{
+    orc_bytes_t* b = orc_bytes_create();
+    if (!b) return -1;
+    if (!orc_serialize(fin != 0, opcode, mask != 0, data, (size_t)n, b)) {
+        orc_bytes_destroy(b);
+        return -1;
+    }
+    long long cnt = (long long)b->count;
+    if ((unsigned long long)cnt > cap) cnt = -2;
+    else memcpy(out, b->buffer, b->count);
+    orc_bytes_destroy(b);
+    return cnt;
+}
+
+int orc_deserialize_flat(const unsigned char* data, unsigned long long size,
+                         unsigned long long* index, unsigned long long max_payload,
+                         int* fin, int* opcode, unsigned long long* payload_size,
+                         int* payload_is_null, unsigned char* payload_out,
+                         unsigned long long cap)
+{
+    orc_frame_t f;
+    orc_frame_init(&f);
+    size_t idx = (size_t)*index;
+    int r = orc_deserialize(&f, data, (size_t)size, &idx, (size_t)max_payload);
+    *index = idx;
+    *fin = f.header.fin;
+    *opcode = f.header.opcode;
+    *payload_size = f.header.payload_size;
+    *payload_is_null = f.payload_data == NULL;
+    if (r == 0 && f.payload_data != NULL && f.header.payload_size + 1 <= cap)
+        memcpy(payload_out, f.payload_data, (size_t)f.header.payload_size + 1);
+    orc_frame_clear(&f);
+    return r;
+}

@@ -1,0 +1,65 @@
+/*
+ * ref_shim.c -- TEST INFRASTRUCTURE ONLY.
+ *
+ * Flat ctypes-friendly entry points around the REFERENCE codec, compiled by
+ * oracle/Makefile together with four reference translation units taken in
+ * place from /root/reference (src/ws/co_ws_frame.c, src/ws/co_ws_config.c,
+ * src/core/co_array.c, src/core/co_random.c). Output goes only to
+ * oracle/_ref/ (git-ignored). Used to pin the restatement (cfws_oracle.c)
+ * and to generate tests/golden/ fixtures; optionally the "reference" CPU
+ * baseline in bench.py.
+ */
+#include <stdlib.h>
+#include <string.h>
+
+#include <coldforce/core/co_byte_array.h>
+#include <coldforce/ws/co_ws_config.h>
+#include <coldforce/ws/co_ws_frame.h>
+
+void ref_srandom(unsigned int seed) { srandom(seed); }
+
+/* co_ws_frame_serialize into a fresh byte array (as co_ws_send does,
+ * co_ws_client.c:443-449); copies the wire bytes out. Returns the frame
+ * byte count, -1 if serialize failed, -2 if `cap` is too small. */
+long long ref_serialize(int fin, unsigned char opcode, int mask, const void* data,
+                        unsigned long long n, unsigned char* out,
+                        unsigned long long cap)
+{
+    co_byte_array_t* b = co_byte_array_create();
+    if (!co_ws_frame_serialize(fin != 0, opcode, mask != 0, data, (size_t)n, b)) {
+        co_byte_array_destroy(b);
+        return -1;
+    }
+    size_t cnt = co_byte_array_get_count(b);
+    if (cnt > cap) {
+        co_byte_array_destroy(b);
+        return -2;
+    }
+    memcpy(out, co_byte_array_get_ptr(b, 0), cnt);
+    co_byte_array_destroy(b);
+    return (long long)cnt;
+}
+
+/* co_ws_frame_deserialize on a fresh frame; reports the frame fields and
+ * copies the payload (plus its NUL terminator) when there is one. */
+int ref_deserialize(const unsigned char* data, unsigned long long size,
+                    unsigned long long* index, unsigned long long max_payload,
+                    int* fin, int* opcode, unsigned long long* payload_size,
+                    int* payload_is_null, unsigned char* payload_out,
+                    unsigned long long cap)
+{
+    co_ws_config_set_max_receive_payload_size((size_t)max_payload);
+    co_ws_frame_t* f = co_ws_frame_create();
+    size_t idx = (size_t)*index;
+    int r = co_ws_frame_deserialize(f, data, (size_t)size, &idx);
+    *index = idx;
+    *fin = f->header.fin;
+    *opcode = f->header.opcode;
+    *payload_size = f->header.payload_size;
+    *payload_is_null = f->payload_data == NULL;
+    if (r == 0 && f->payload_data != NULL && f->header.payload_size + 1 <= cap)
+        memcpy(payload_out, f->payload_data, (size_t)f->header.payload_size + 1);
+    co_ws_frame_destroy(f);
+    co_ws_config_set_max_receive_payload_size(CO_WS_CONFIG_DEFAULT_MAX_RECEIVE_PAYLOAD_SIZE);
+    return r;
+}

@@ -1,0 +1,206 @@
+#!/usr/bin/env python3
+"""Generate tests/golden/*.json from the REFERENCE codec itself.
+
+Runs coldforce's own co_ws_frame_serialize / co_ws_frame_deserialize,
+compiled in place from /root/reference by oracle/Makefile (`make -C oracle
+ref` -> oracle/_ref/libcfws_ref.so). Only this container has the reference;
+the committed JSON files are the data the GPU box checks against.
+
+Fixtures (inputs + expected outputs):
+  rfc6455_kat.json      RFC 6455 section 5.7 examples, decoded by the reference
+  serialize_cases.json  boundary payload sizes x mask x fin/opcode x seed:
+                        wire bytes (hex when small, SHA-256 always)
+  deserialize_cases.json  decode results incl. truncations, invalid opcodes,
+                        size limits, concatenated frames, non-minimal lengths
+  keys.json             mask-key stream after srandom(seed)
+  batch_digests.json    SHA-256 of whole serialized batches (config 2 full size)
+
+Payload bytes are synthetic: splitmix64 stream (oracle.fill_splitmix).
+Usage: python tests/golden/make_golden.py [--skip-full]
+"""
+from __future__ import annotations
+
+import argparse
+import hashlib
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+
+import oracle as O  # noqa: E402
+
+OUT = os.path.dirname(os.path.abspath(__file__))
+SIZES = [0, 1, 3, 4, 5, 124, 125, 126, 127, 128, 65535, 65536, 65537, 1 << 20]
+HEX_LIMIT = 300
+
+
+def sha(b: bytes) -> str:
+    return hashlib.sha256(b).hexdigest()
+
+
+def dump(name: str, obj) -> None:
+    with open(os.path.join(OUT, name), "w") as f:
+        json.dump(obj, f, indent=1)
+        f.write("\n")
+    print("wrote", name)
+
+
+def rfc6455(R):
+    cases = [
+        ("single-frame unmasked text", "810548656c6c6f"),
+        ("single-frame masked text", "818537fa213d7f9f4d5158"),
+        ("fragment 1 of unmasked text", "010348656c"),
+        ("fragment 2 of unmasked text", "80026c6f"),
+        ("unmasked ping", "890548656c6c6f"),
+        ("masked pong", "8a8537fa213d7f9f4d5158"),
+        ("256-byte unmasked binary", "827e0100" + "ab" * 256),
+        ("65536-byte unmasked binary", "827f0000000000010000" + "cd" * 65536),
+    ]
+    out = []
+    for name, hx in cases:
+        raw = bytes.fromhex(hx)
+        r = O.ref_deserialize(R, raw)
+        out.append(dict(name=name, wire=hx if len(raw) <= HEX_LIMIT else None,
+                        wire_sha256=sha(raw), wire_len=len(raw),
+                        wire_spec=None if len(raw) <= HEX_LIMIT else hx[:20] + "+repeat",
+                        rc=r["rc"], index=r["index"], fin=r["fin"], opcode=r["opcode"],
+                        payload_size=r["payload_size"],
+                        payload_hex=None if r["payload"] is None or len(r["payload"]) > HEX_LIMIT
+                        else r["payload"].hex(),
+                        payload_sha256=None if r["payload"] is None else sha(r["payload"])))
+    return out
+
+
+def serialize_cases(R):
+    out = []
+    variants = [(True, 0x2), (False, 0x0), (True, 0x1), (True, 0x9), (True, 0x7f), (False, 0xff)]
+    for seed in (1, 1234):
+        for n in SIZES:
+            for mask in (False, True):
+                for fin, op in variants:
+                    if n >= 65536 and (fin, op) not in [(True, 0x2), (False, 0x0)]:
+                        continue
+                    base = n * 8
+                    data = O.fill_splitmix(n, 0x5EEDF00D, base).tobytes()
+                    O.srandom(R, seed)
+                    w = O.ref_serialize(R, fin, op, mask, data)
+                    out.append(dict(seed=seed, n=n, mask=mask, fin=fin, opcode=op,
+                                    payload_seed=0x5EEDF00D, payload_byte_base=base,
+                                    header_hex=w[:O.header_size(n, mask)].hex(),
+                                    wire_hex=w.hex() if len(w) <= HEX_LIMIT else None,
+                                    wire_len=len(w), wire_sha256=sha(w)))
+    return out
+
+
+def deserialize_cases(R):
+    M = O.DEFAULT_MAX_PAYLOAD
+    cases = []
+
+    def add(name, wire: bytes, index=0, max_payload=M):
+        r = O.ref_deserialize(R, wire, index, max_payload)
+        p = r["payload"]
+        cases.append(dict(name=name, wire_hex=wire.hex() if len(wire) <= 4096 else None,
+                          wire_len=len(wire), wire_sha256=sha(wire),
+                          wire_spec=None, index=index, max_payload=max_payload,
+                          rc=r["rc"], index_out=r["index"], fin=r["fin"], opcode=r["opcode"],
+                          payload_size=r["payload_size"], payload_is_null=p is None,
+                          payload_hex=None if p is None or len(p) > 4096 else p.hex(),
+                          payload_sha256=None if p is None else sha(p)))
+
+    O.srandom(R, 77)
+    masked300 = O.ref_serialize(R, True, 2, True, bytes(range(256)) + bytes(44))
+    plain70k = O.ref_serialize(R, True, 2, False, b"\x5a" * 70000)
+    add("masked 300 B", masked300)
+    for cut in (2, 3, 4, 5, 7, 8, 100, len(masked300) - 1):
+        add(f"masked 300 B truncated to {cut}", masked300[:cut])
+    add("126-length header only", bytes([0x82, 0x7E]))
+    add("127-length header, 7 of 8 length bytes", bytes([0x82, 0x7F]) + bytes(7))
+    add("127-length header complete, no payload", bytes([0x82, 0x7F, 0, 0, 0, 0, 0, 1, 0, 0]))
+    add("masked, key truncated", bytes([0x81, 0x85, 0x37, 0xFA, 0x21]))
+    for b0 in (0xF2, 0xC1, 0xA1, 0x91, 0x47, 0x48, 0x10):
+        add(f"b0=0x{b0:02x} (RSV bits / HTTP text)", bytes([b0, 0x05]) + b"Hello")
+    for op in (3, 7, 0xB, 0xF):
+        add(f"reserved opcode {op}", bytes([0x80 | op, 0x03]) + b"abc")
+    add("zero-length masked", bytes([0x89, 0x80, 1, 2, 3, 4]))
+    add("zero-length unmasked", bytes([0x8A, 0x00]))
+    add("non-minimal 126 length of 5", bytes([0x81, 0x7E, 0x00, 0x05]) + b"Hello")
+    add("non-minimal 127 length of 5", bytes([0x81, 0x7F]) + (5).to_bytes(8, "big") + b"Hello")
+    add("64-bit length MSB set", bytes([0x82, 0x7F, 0x80, 0, 0, 0, 0, 0, 0, 1]) + b"xyz")
+    add("length 33554433 header only (MORE_DATA before TOO_BIG)",
+        bytes([0x82, 0x7F]) + (M + 1).to_bytes(8, "big"))
+    two = bytes([0x81, 0x01, 0x41]) + bytes([0x82, 0x85, 1, 2, 3, 4]) + bytes(5)
+    add("two frames, first", two, 0)
+    add("two frames, second", two, 3)
+    add("limit 300, payload 300", masked300, 0, 300)
+    add("limit 299, payload 300 (TOO_BIG)", masked300, 0, 299)
+    add("plain 70000 B", plain70k)
+    add("plain 70000 B, limit 69999", plain70k, 0, 69999)
+    # Full 33,554,433-byte payload -> DATA_TOO_BIG (described, not stored).
+    big = bytes([0x82, 0x7F]) + (M + 1).to_bytes(8, "big") + bytes(M + 1)
+    r = O.ref_deserialize(R, big)
+    cases.append(dict(name="zero payload of 33554433 B (TOO_BIG)", wire_hex=None,
+                      wire_spec="827f" + (M + 1).to_bytes(8, "big").hex() + "+zeros",
+                      wire_len=len(big), wire_sha256=sha(big), index=0, max_payload=M,
+                      rc=r["rc"], index_out=r["index"], fin=r["fin"], opcode=r["opcode"],
+                      payload_size=r["payload_size"], payload_is_null=r["payload"] is None,
+                      payload_hex=None, payload_sha256=None))
+    return cases
+
+
+def keys(R):
+    out = {}
+    for seed in (1, 2, 1234, 0x5EED):
+        O.srandom(R, seed)
+        ks = []
+        for _ in range(16):
+            w = O.ref_serialize(R, True, 2, True, b"")
+            ks.append(w[2:6].hex())
+        out[str(seed)] = ks
+    return out
+
+
+def batch_digest(R, n_frames, frame_size, payload_seed, key_seed, chunk=1024):
+    """Serialize n_frames frames through the reference, sequentially, one
+    co_byte_array per frame (co_ws_send), hashing the concatenated wire."""
+    h = hashlib.sha256()
+    hp = hashlib.sha256()
+    total = 0
+    O.srandom(R, key_seed)
+    for c0 in range(0, n_frames, chunk):
+        c1 = min(n_frames, c0 + chunk)
+        words = O.splitmix_words(payload_seed, c0 * frame_size // 8, (c1 - c0) * frame_size // 8)
+        arena = words.view(np.uint8)
+        hp.update(arena.tobytes())
+        for f in range(c1 - c0):
+            w = O.ref_serialize(R, True, 2, True, arena[f * frame_size:(f + 1) * frame_size].tobytes())
+            h.update(w)
+            total += len(w)
+    return dict(n_frames=n_frames, frame_size=frame_size, payload_seed=payload_seed,
+                key_seed=key_seed, fin=True, opcode=2, mask=True, wire_len=total,
+                wire_sha256=h.hexdigest(), payload_sha256=hp.hexdigest())
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--skip-full", action="store_true", help="skip the 4 GiB config-2 digest")
+    a = ap.parse_args()
+    O.build(ref=True)
+    R = O.ref_lib("O2")
+    assert R is not None, "oracle/_ref not built (needs /root/reference)"
+    dump("rfc6455_kat.json", rfc6455(R))
+    dump("serialize_cases.json", serialize_cases(R))
+    dump("deserialize_cases.json", deserialize_cases(R))
+    dump("keys.json", keys(R))
+    digests = [batch_digest(R, 1024, 65536, 0x5EED0002, 2),
+               batch_digest(R, 4096, 1000, 0x5EED00AA, 9)]
+    if not a.skip_full:
+        digests.append(batch_digest(R, 65536, 65536, 0x5EED0002, 2))
+    dump("batch_digests.json", digests)
+
+
+if __name__ == "__main__":
+    main()

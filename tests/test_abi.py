@@ -1,0 +1,108 @@
+"""CPU checks of the C-ABI boundary: libcfws.so loads, exports every function
+include/*.h declares, and its host-only parts behave like the reference
+(no compute call that needs a GPU is made here)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+import oracle as O
+from conftest import ROOT, golden, gpu_present
+
+LIB = os.path.join(ROOT, "coldforce_amd", "libcfws.so")
+
+
+def declared_functions():
+    names = set()
+    for h in ("cfws.h", "cfws_co_ws_frame.h"):
+        src = open(os.path.join(ROOT, "include", h)).read()
+        src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+        for m in re.finditer(r"^[A-Za-z_][\w \*]*?\b(\w+)\s*\(", src, flags=re.M):
+            if not m.group(0).lstrip().startswith(("#", "typedef", "return")):
+                names.add(m.group(1))
+    return sorted(names)
+
+
+def test_library_built():
+    assert os.path.exists(LIB), "run `make` (libcfws.so is the product)"
+
+
+def test_exports_every_declared_symbol():
+    names = declared_functions()
+    assert len(names) >= 24
+    out = subprocess.run(["nm", "-D", "--defined-only", LIB], capture_output=True, text=True,
+                         check=True).stdout
+    exported = {line.split()[-1] for line in out.splitlines() if " T " in line}
+    missing = [n for n in names if n not in exported]
+    assert not missing, missing
+    L = ctypes.CDLL(LIB)
+    for n in names:
+        getattr(L, n)
+
+
+def test_python_binding_lists_match_headers():
+    from coldforce_amd import cfws
+    assert sorted(cfws.BATCH_SYMBOLS + cfws.DROPIN_SYMBOLS) == declared_functions()
+
+
+def test_device_code_is_gfx950():
+    blob = open(LIB, "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in blob          # the embedded code object
+    for other in (b"--gfx942", b"--gfx90a", b"--gfx1100"):
+        assert other not in blob
+
+
+def test_workspace_size_host_only():
+    L = ctypes.CDLL(LIB)
+    L.cfws_workspace_size.restype = ctypes.c_size_t
+    L.cfws_workspace_size.argtypes = [ctypes.c_size_t, ctypes.c_uint64]
+    a = L.cfws_workspace_size(65536, 1 << 32)
+    assert 65536 * 8 < a < 65536 * 8 + (1 << 32) // 16384 * 4 + 8192
+    assert L.cfws_workspace_size(0, 0) > 0
+
+
+def test_draw_mask_keys_matches_reference_stream():
+    from coldforce_amd import cfws
+    for seed, ks in golden("keys.json").items():
+        got = cfws.draw_mask_keys(len(ks), seed=int(seed))
+        assert [int.from_bytes(bytes.fromhex(k), "little") for k in ks] == [int(x) for x in got]
+    # unmasked frames draw nothing and get key 0
+    flags = np.array([1, 0, 1, 0], np.uint8)
+    got = cfws.draw_mask_keys(4, flags, seed=1)
+    ref = golden("keys.json")["1"]
+    assert [int(x) for x in got] == [int.from_bytes(bytes.fromhex(ref[0]), "little"), 0,
+                                     int.from_bytes(bytes.fromhex(ref[1]), "little"), 0]
+
+
+def test_dropin_host_paths_without_device():
+    """Unmasked frames and header-only decisions never touch the device."""
+    from coldforce_amd import cfws
+    ok, w = cfws.frame_serialize(True, 1, False, b"Hello")
+    assert ok and w.hex() == "810548656c6c6f"
+    for c in golden("deserialize_cases.json"):
+        if c["wire_hex"] is None:
+            continue
+        raw = bytes.fromhex(c["wire_hex"])
+        masked_payload = c["rc"] == 0 and c["payload_size"] > 0 and (raw[c["index"] + 1] & 0x80)
+        if masked_payload:
+            continue
+        cfws.lib().co_ws_config_set_max_receive_payload_size(c["max_payload"])
+        r = cfws.frame_deserialize(raw, c["index"])
+        cfws.lib().co_ws_config_set_max_receive_payload_size(O.DEFAULT_MAX_PAYLOAD)
+        assert (r["rc"], r["index"], r["payload_size"], r["payload"] is None) == \
+            (c["rc"], c["index_out"], c["payload_size"], c["payload_is_null"]), c["name"]
+
+
+@pytest.mark.skipif(gpu_present(), reason="checks the no-device behaviour")
+def test_no_cpu_fallback():
+    from coldforce_amd import cfws
+    assert cfws.lib().cfws_init() == -4          # CFWS_ERROR_NO_DEVICE
+    with pytest.raises(cfws.CodecError):
+        cfws.init()
+    ok, _ = cfws.frame_serialize(True, 2, True, b"x" * 100)   # masked: needs the device
+    assert not ok
+    w = O.serialize_keyed(True, 2, True, 0x11223344, b"x" * 100)
+    assert cfws.frame_deserialize(w)["rc"] == -7006

@@ -1,0 +1,290 @@
+"""GPU parity: the MI355X batch codec (libcfws.so, include/cfws.h) against the
+oracle (CPU restatement, pinned to the reference) and against digests the
+reference codec itself produced (tests/golden/batch_digests.json).
+Bit-exact everywhere: this is byte work."""
+import hashlib
+import random
+
+import numpy as np
+import pytest
+
+import oracle as O
+from conftest import golden
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+from coldforce_amd import cfws  # noqa: E402
+from coldforce_amd import workloads as W  # noqa: E402
+
+SIZES = [0, 1, 3, 4, 5, 15, 16, 17, 124, 125, 126, 127, 128, 1000, 4095, 4096, 4097,
+         65535, 65536, 65537, 1 << 20]
+
+
+@pytest.fixture(scope="module", autouse=True)
+def device():
+    cfws.init()
+    return torch.device("cuda", 0)
+
+
+def sha(a) -> str:
+    return hashlib.sha256(a.tobytes() if hasattr(a, "tobytes") else a).hexdigest()
+
+
+def gpu_serialize(payload: np.ndarray, desc: np.ndarray, slack: int = 0, capacity=None,
+                  plan_execute=False):
+    pay = torch.from_numpy(payload if payload.size else np.zeros(16, np.uint8)).cuda()
+    d_t = cfws.desc_to_device(desc)
+    _, total = W.wire_layout(desc)
+    cap = W.round16(total) + slack if capacity is None else capacity
+    wire = torch.full((max(cap, 16),), 0xEE, dtype=torch.uint8, device="cuda")
+    if plan_execute:
+        ws = cfws.workspace(len(desc), cap)
+        tot = torch.zeros(1, dtype=torch.int64, device="cuda")
+        cfws.serialize_plan(d_t, cap, tot, ws)
+        cfws.serialize_execute(pay, d_t, wire, ws, cap)
+    else:
+        tot = cfws.serialize(pay, d_t, wire[:cap] if cap else wire[:0])
+    torch.cuda.synchronize()
+    return wire.cpu().numpy(), cfws.desc_from_device(d_t), int(tot.item()), total
+
+
+def random_desc(rng, n, payload_len, sizes=None, aligned=False):
+    d = np.zeros(n, dtype=cfws.DESC_DTYPE)
+    for i in range(n):
+        sz = rng.choice(sizes) if sizes else rng.randrange(0, 3000)
+        sz = min(sz, payload_len)
+        off = rng.randrange(0, payload_len - sz + 1)
+        if aligned:
+            off -= off % 16
+        d[i]["payload_off"] = off
+        d[i]["payload_size"] = sz
+        d[i]["fin"] = rng.random() < 0.7
+        d[i]["opcode"] = rng.randrange(256) if rng.random() < 0.1 else rng.choice([0, 1, 2, 8, 9, 10])
+        d[i]["mask"] = rng.random() < 0.6
+        d[i]["mask_key"] = rng.getrandbits(32) if d[i]["mask"] else 0
+    return d
+
+
+def check_serialize(payload, desc, **kw):
+    wire, d_out, tot, total = gpu_serialize(payload, desc, **kw)
+    exp, d_exp = O.serialize_batch(payload, desc.view(O.DESC_DTYPE))
+    assert tot == total == len(exp)
+    assert np.array_equal(d_out["wire_off"], d_exp["wire_off"])
+    assert np.array_equal(d_out["header_size"], d_exp["header_size"])
+    bad = np.nonzero(wire[:total] != exp)[0]
+    assert bad.size == 0, f"{bad.size} bytes differ, first at {bad[:8]}"
+    return wire, total
+
+
+def test_serialize_boundary_sizes():
+    rng = random.Random(1)
+    payload = O.fill_splitmix(3 << 20, 0x1234, 0)
+    d = []
+    for n in SIZES:
+        for mask in (False, True):
+            for fin, op in ((True, 2), (False, 0), (True, 0x7F), (False, 0xFF)):
+                d.append((rng.randrange(0, (3 << 20) - n), n, fin, op, mask, rng.getrandbits(32)))
+    desc = np.zeros(len(d), dtype=cfws.DESC_DTYPE)
+    for i, (off, n, fin, op, mask, key) in enumerate(d):
+        desc[i] = (off, 0, n, key if mask else 0, fin, op, mask, 0)
+    wire, total = check_serialize(payload, desc)
+    # bytes past the total inside the rounded-up capacity are written as zero
+    assert not wire[total:W.round16(total)].any()
+
+
+@pytest.mark.parametrize("seed", [2, 3, 4])
+def test_serialize_random_mix(seed):
+    rng = random.Random(seed)
+    payload = O.fill_splitmix(1 << 20, seed, 0)
+    desc = random_desc(rng, 4000, 1 << 20, aligned=seed == 4)
+    check_serialize(payload, desc, plan_execute=seed == 3)
+
+
+def test_serialize_tiny_frames_dense():
+    # > 1024 frames per 16 KiB tile (2-6 byte frames): exercises the
+    # global-search path of the tile scheduler.
+    rng = random.Random(9)
+    payload = O.fill_splitmix(4096, 9, 0)
+    desc = random_desc(rng, 20000, 4096, sizes=[0, 0, 1, 2, 3])
+    check_serialize(payload, desc)
+
+
+def test_serialize_keys_from_random():
+    # Keys drawn by cfws_draw_mask_keys after srandom(s) == reference key stream.
+    for seed, ks in golden("keys.json").items():
+        got = cfws.draw_mask_keys(len(ks), seed=int(seed))
+        assert [int.from_bytes(bytes.fromhex(k), "little") for k in ks] == list(map(int, got))
+
+
+def test_serialize_capacity_truncation():
+    rng = random.Random(5)
+    payload = O.fill_splitmix(1 << 16, 5, 0)
+    desc = random_desc(rng, 50, 1 << 16)
+    _, total = W.wire_layout(desc)
+    cap = total // 2 + 3
+    wire, _, tot, _ = gpu_serialize(payload, desc, capacity=cap)
+    exp, _ = O.serialize_batch(payload, desc.view(O.DESC_DTYPE))
+    assert tot == total                       # unclamped total is reported
+    assert np.array_equal(wire[:cap], exp[:cap])
+    assert (wire[cap:] == 0xEE).all()         # nothing written past capacity
+
+
+def gpu_deserialize(wire: np.ndarray, starts: np.ndarray, align=16, capacity=None,
+                    max_payload=O.DEFAULT_MAX_PAYLOAD, plan_execute=False):
+    w = torch.from_numpy(np.concatenate([wire, np.zeros(16, np.uint8)])).cuda()
+    idx = torch.from_numpy(starts.astype(np.int64)).cuda()
+    cap = capacity if capacity is not None else len(wire) + 16 * len(starts) + 16
+    out = torch.full((max(cap, 16),), 0xEE, dtype=torch.uint8, device="cuda")
+    if plan_execute:
+        n = len(starts)
+        ws = cfws.workspace(n, cap)
+        d_t = torch.empty((n, 32), dtype=torch.uint8, device="cuda")
+        st_t = torch.empty(n, dtype=torch.int32, device="cuda")
+        tot = torch.zeros(1, dtype=torch.int64, device="cuda")
+        cfws.deserialize_plan(w, len(wire), idx, d_t, st_t, cap, tot, ws, max_payload, align)
+        cfws.deserialize_execute(w, d_t, st_t, out, ws, cap)
+    else:
+        d_t, st_t, tot = cfws.deserialize(w, len(wire), idx, out[:cap], max_payload=max_payload,
+                                          align=align)
+    torch.cuda.synchronize()
+    return out.cpu().numpy(), cfws.desc_from_device(d_t), st_t.cpu().numpy(), int(tot.item())
+
+
+def check_deserialize(wire, starts, **kw):
+    out, d, st, tot = gpu_deserialize(wire, starts, **kw)
+    cap = kw.get("capacity") or len(wire) + 16 * len(starts) + 16
+    e_out, e_d, e_st, e_tot = O.deserialize_batch(wire, starts, align=kw.get("align", 16),
+                                                  max_payload=kw.get("max_payload",
+                                                                     O.DEFAULT_MAX_PAYLOAD),
+                                                  capacity=cap)
+    assert tot == e_tot
+    assert np.array_equal(st, e_st)
+    for f in ("payload_off", "wire_off", "payload_size", "mask_key", "fin", "opcode", "mask",
+              "header_size"):
+        assert np.array_equal(d[f], e_d[f]), f
+    bad = np.nonzero(out[:tot] != e_out[:tot])[0]
+    assert bad.size == 0, f"{bad.size} bytes differ, first at {bad[:8]}"
+    return out, d, st, tot
+
+
+def wire_stream(rng, n, sizes=None):
+    frames, payloads = [], []
+    for _ in range(n):
+        sz = rng.choice(sizes) if sizes else rng.randrange(0, 3000)
+        p = rng.randbytes(sz)
+        payloads.append(p)
+        frames.append(O.serialize_keyed(rng.random() < .7, rng.randrange(16), rng.random() < .6,
+                                        rng.getrandbits(32), p))
+    return np.frombuffer(b"".join(frames), dtype=np.uint8).copy(), payloads
+
+
+@pytest.mark.parametrize("align", [1, 16, 64, 4096])
+def test_deserialize_random_stream(align):
+    rng = random.Random(align)
+    wire, payloads = wire_stream(rng, 3000, sizes=SIZES[:-1] + [rng.randrange(70000)])
+    starts, consumed = O.index_frames(wire, 10000)
+    assert consumed == len(wire)
+    cap = len(wire) + align * (len(starts) + 1)
+    out, d, st, tot = check_deserialize(wire, starts, align=align, capacity=cap,
+                                        plan_execute=align == 64)
+    assert (st == 0).all()
+    for i, p in enumerate(payloads[:200]):
+        o = int(d["payload_off"][i])
+        assert out[o:o + len(p)].tobytes() == p
+
+
+def test_deserialize_error_frames():
+    rng = random.Random(7)
+    wire, _ = wire_stream(rng, 200)
+    starts, _ = O.index_frames(wire, 1000)
+    # corrupt some headers, add truncated / out-of-range starts, vary limits
+    wire = wire.copy()
+    for i in range(0, len(starts), 17):
+        wire[int(starts[i])] |= 0x40           # RSV2 -> INVALID_FRAME
+    extra = np.array([len(wire) - 1, len(wire), len(wire) + 7, int(starts[5]) + 1], dtype=np.uint64)
+    starts2 = np.concatenate([starts, extra])
+    check_deserialize(wire, starts2)
+    check_deserialize(wire, starts2, max_payload=1000)
+    check_deserialize(wire, starts2, capacity=10000)   # OUT_OF_MEMORY from some frame on
+
+
+def test_deserialize_golden_cases():
+    # every fixture case that is small enough, through the batch path
+    for c in golden("deserialize_cases.json"):
+        if c["wire_hex"] is None:
+            continue
+        raw = np.frombuffer(bytes.fromhex(c["wire_hex"]), dtype=np.uint8).copy()
+        out, d, st, tot = gpu_deserialize(raw, np.array([c["index"]], np.uint64), align=1,
+                                          max_payload=c["max_payload"])
+        exp_rc = c["rc"]
+        if len(raw) - c["index"] < 2:
+            exp_rc = O.PARSE_MORE_DATA
+        assert st[0] == exp_rc, c["name"]
+        if exp_rc == 0:
+            assert int(d["payload_size"][0]) == c["payload_size"]
+            if c["payload_hex"] is not None:
+                assert out[:c["payload_size"]].tobytes() + b"\0" == bytes.fromhex(c["payload_hex"])
+        if exp_rc in (0, O.ERROR_INVALID_FRAME):
+            assert bool(d["fin"][0]) == c["fin"] and int(d["opcode"][0]) == c["opcode"]
+
+
+def test_config2_reduced_digest():
+    g = golden("batch_digests.json")[0]
+    _roundtrip_digest(g)
+
+
+def test_config2_full_size_digest():
+    """65,536 x 64 KiB (BASELINE configs[1]) at full size: the wire arena is
+    bit-identical to the reference's serialize output (SHA-256 of 4.0009 GiB)
+    and deserialize restores every payload byte."""
+    g = golden("batch_digests.json")[2]
+    _roundtrip_digest(g, full=True)
+
+
+def _roundtrip_digest(g, full=False):
+    n, fs = g["n_frames"], g["frame_size"]
+    desc = W.uniform_batch(n, fs, g["key_seed"])
+    offs, total = W.wire_layout(desc)
+    assert total == g["wire_len"]
+    payload = torch.empty(n * fs, dtype=torch.uint8, device="cuda")
+    cfws.fill_splitmix(payload, g["payload_seed"])
+    d_t = cfws.desc_to_device(desc)
+    wire = torch.empty(W.round16(total), dtype=torch.uint8, device="cuda")
+    tot = cfws.serialize(payload, d_t, wire)
+    torch.cuda.synchronize()
+    assert tot.item() == total
+    h = hashlib.sha256()
+    step = 1 << 28
+    for o in range(0, total, step):
+        h.update(wire[o:min(total, o + step)].cpu().numpy().tobytes())
+    assert h.hexdigest() == g["wire_sha256"]
+    idx = torch.from_numpy(offs.astype(np.int64)).cuda()
+    back = torch.empty(n * fs, dtype=torch.uint8, device="cuda")
+    _, st, ptot = cfws.deserialize(wire, total, idx, back, align=16)
+    torch.cuda.synchronize()
+    assert ptot.item() == n * fs and bool((st == 0).all())
+    assert torch.equal(back, payload)
+    if not full:
+        assert sha(back.cpu().numpy()) == g["payload_sha256"]
+
+
+def test_fill_splitmix_matches_oracle():
+    for n, base in ((1000, 0), (4096, 8), (77777, 1 << 20)):
+        t = torch.empty(n, dtype=torch.uint8, device="cuda")
+        cfws.fill_splitmix(t, 0xABCDEF, base)
+        assert np.array_equal(t.cpu().numpy(), O.fill_splitmix(n, 0xABCDEF, base))
+
+
+@pytest.mark.parametrize("n", [1, 5, 16, 17, 1000, 65536, 65550, 1 << 20])
+def test_xor_mask(n):
+    src = torch.randint(0, 256, (n + 32,), dtype=torch.uint8, device="cuda")
+    for phase in range(4):
+        for so in (0, 3):
+            dst = torch.zeros(n + 32, dtype=torch.uint8, device="cuda")
+            cfws.xor_mask(src[so:], dst[so:], n, 0xA1B2C3D4, phase)
+            s = src.cpu().numpy()[so:so + n]
+            kb = np.array([0xD4, 0xC3, 0xB2, 0xA1], np.uint8)
+            exp = s ^ kb[(np.arange(n) + phase) % 4]
+            assert np.array_equal(dst.cpu().numpy()[so:so + n], exp)

@@ -1,0 +1,111 @@
+"""GPU parity of the drop-in per-frame ABI (co_ws_frame_* exported by
+libcfws.so, include/cfws_co_ws_frame.h) against the reference's golden
+vectors: same wire bytes for the same random() stream, same decode results,
+same NUL-terminated payloads."""
+import hashlib
+import random
+
+import pytest
+
+import oracle as O
+from conftest import golden
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+from coldforce_amd import cfws  # noqa: E402
+
+
+def sha(b):
+    return hashlib.sha256(b).hexdigest()
+
+
+@pytest.fixture(scope="module", autouse=True)
+def device():
+    cfws.init()
+
+
+def test_serialize_golden_cases():
+    import ctypes
+    libc = ctypes.CDLL(None)
+    for c in golden("serialize_cases.json"):
+        data = O.fill_splitmix(c["n"], c["payload_seed"], c["payload_byte_base"]).tobytes()
+        libc.srandom(c["seed"])
+        ok, w = cfws.frame_serialize(c["fin"], c["opcode"], c["mask"], data)
+        assert ok
+        assert len(w) == c["wire_len"] and sha(w) == c["wire_sha256"], (c["n"], c["mask"])
+
+
+def test_serialize_appends_with_reference_growth():
+    # Several frames appended to one byte array: same bytes as one frame after
+    # another, capacity = the co_array doubling rule (co_array.c:83-112).
+    import ctypes
+    libc = ctypes.CDLL(None)
+    buf = cfws.byte_array_create()
+    libc.srandom(5)
+    expect = b""
+    sizes = [0, 10, 200, 70000, 3]
+    for n in sizes:
+        ok, _ = cfws.frame_serialize(True, 2, True, bytes(range(256)) * (n // 256) + bytes(n % 256), buf)
+        assert ok
+    out = cfws.byte_array_bytes(buf)
+    oracle_lib = O.lib()
+    O.srandom(oracle_lib, 5)
+    for n in sizes:
+        expect += O.ref_serialize(oracle_lib, True, 2, True, bytes(range(256)) * (n // 256) + bytes(n % 256))
+    assert out == expect
+    cap = 8
+    while cap <= len(expect):
+        cap *= 2
+    assert buf.capacity == cap and buf.count == len(expect)
+    cfws.byte_array_destroy(buf)
+
+
+def test_deserialize_golden_cases():
+    for c in golden("deserialize_cases.json"):
+        if c["wire_hex"] is None:
+            continue
+        raw = bytes.fromhex(c["wire_hex"])
+        cfws.lib().co_ws_config_set_max_receive_payload_size(c["max_payload"])
+        r = cfws.frame_deserialize(raw, c["index"])
+        cfws.lib().co_ws_config_set_max_receive_payload_size(O.DEFAULT_MAX_PAYLOAD)
+        got = (r["rc"], r["index"], r["fin"], r["opcode"], r["payload_size"], r["payload"] is None)
+        exp = (c["rc"], c["index_out"], c["fin"], c["opcode"], c["payload_size"], c["payload_is_null"])
+        assert got == exp, c["name"]
+        if c["payload_sha256"] is not None:
+            assert sha(r["payload"]) == c["payload_sha256"], c["name"]
+
+
+def test_rfc6455_golden():
+    for c in golden("rfc6455_kat.json"):
+        if c["wire"] is None:
+            continue
+        r = cfws.frame_deserialize(bytes.fromhex(c["wire"]))
+        assert (r["rc"], r["index"], r["fin"], r["opcode"], r["payload_size"]) == \
+            (c["rc"], c["index"], c["fin"], c["opcode"], c["payload_size"])
+        assert sha(r["payload"]) == c["payload_sha256"]
+
+
+def test_random_roundtrip_vs_oracle():
+    import ctypes
+    libc = ctypes.CDLL(None)
+    rng = random.Random(4)
+    L = O.lib()
+    for trial in range(60):
+        n = rng.choice([1, 2, 125, 126, 65535, 65536, 65537, rng.randrange(300000)])
+        data = rng.randbytes(n)
+        libc.srandom(trial)
+        ok, w = cfws.frame_serialize(rng.random() < .5, rng.randrange(16), True, data)
+        assert ok
+        O.srandom(L, trial)
+        assert w == O.ref_serialize(L, bool(w[0] & 0x80), w[0] & 0x7F, True, data)
+        assert cfws.frame_deserialize(w) == O.ref_deserialize(L, w)
+
+
+def test_frame_object_api():
+    L = cfws.lib()
+    f = L.co_ws_frame_create()
+    assert L.co_ws_frame_get_opcode(f) == 0xFF and not L.co_ws_frame_get_fin(f)
+    assert L.co_ws_frame_get_payload_size(f) == 0 and not L.co_ws_frame_get_payload_data(f)
+    L.co_ws_frame_destroy(f)
