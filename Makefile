@@ -41,3 +41,12 @@ clean:
 	$(MAKE) -s -C oracle clean
 
 .PHONY: all oracle ref asm clean
+
+# A/B build variants (kept out of git under build/): make variant V=nt F="-DCFWS_NT_STORE"
+variant: $(HDR)
+	@mkdir -p $(OBJDIR)/variants/$(V)
+	$(HIPCC) --offload-arch=$(ARCH) $(HIPFLAGS) $(F) -Iinclude -c coldforce_amd/csrc/cfws_device.hip -o $(OBJDIR)/variants/$(V)/cfws_device.o
+	$(HIPCC) --offload-arch=$(ARCH) $(HIPFLAGS) $(F) -Iinclude -c coldforce_amd/csrc/cfws_frame.cpp -o $(OBJDIR)/variants/$(V)/cfws_frame.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o $(OBJDIR)/variants/libcfws_$(V).so $(OBJDIR)/variants/$(V)/cfws_device.o $(OBJDIR)/variants/$(V)/cfws_frame.o
+
+.PHONY: variant

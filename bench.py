@@ -155,6 +155,16 @@ def main():
                 and bool((status == 0).all().item()) and torch.equal(back, payload))
     verified = shard.sum_over_ranks(1.0 if verified else 0.0, dev) == world
 
+    # practical ceiling: a plain device-to-device copy of the same byte count
+    c0, c1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    back.copy_(payload)
+    c0.record()
+    for _ in range(5):
+        back.copy_(payload)
+    c1.record()
+    torch.cuda.synchronize()
+    copy_gbps = 2 * F * fs / (c0.elapsed_time(c1) / 5 * 1e-3) / 1e9
+
     ser_ms = sum(e[0].elapsed_time(e[1]) for e in events) / args.steps
     de_ms = sum(e[2].elapsed_time(e[3]) for e in events) / args.steps
     hdr = int(wire_total - F * fs)
@@ -204,6 +214,8 @@ def main():
             "avg_launch_ms": round(dom_ms, 4),
         },
         "kernels": kern,
+        "copy_ceiling": {"GBps": round(copy_gbps, 1), "frac_of_copy": round(achieved / copy_gbps, 4),
+                         "how": "torch.Tensor.copy_ of the 4 GiB payload arena, device to device"},
         "verified": verified,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

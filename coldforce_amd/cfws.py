@@ -18,7 +18,7 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libcfws.so")
+LIB_PATH = os.environ.get("CFWS_LIB") or os.path.join(HERE, "libcfws.so")   # CFWS_LIB: A/B builds
 
 OK = 0
 PARSE_COMPLETE = 0

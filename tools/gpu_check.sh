@@ -1,0 +1,18 @@
+#!/bin/bash
+# One GPU-box session: parity tests, smoke, bench, rocprof kernel stats.
+# Every GPU step has its own time limit; the chain stops at the first failure.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+export TMPDIR=/tmp
+OUT=gpurun_out/${TAG:-run}
+mkdir -p "$OUT"
+rocm-smi --showproductname > "$OUT/smi.txt" 2>&1 || true
+nproc > "$OUT/nproc.txt"
+timeout -k 10 900 python -m pytest tests -x -q -m gpu > "$OUT/pytest_gpu.txt" 2>&1 &&
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.txt" 2>&1 &&
+timeout -k 10 600 python bench.py ${BENCH_ARGS:-} > "$OUT/bench.json" 2> "$OUT/bench.err" &&
+( cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/$OUT/prof" -o run -- \
+      python3 "$GRAFT_REPO_ROOT/bench.py" --steps 10 --warmup 2 --no-cpu-baseline ) > "$OUT/rocprof.txt" 2>&1
+rc=$?
+echo "exit $rc"
+exit $rc
