@@ -47,6 +47,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="target CPU time of the cpu_baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--workload", choices=["config2", "config3"], default="config2",
+                    help="config2: uniform 64 KiB frames (the metric's config); config3: Zipf "
+                         "64 B-1 MiB messages in 1-8 continuation fragments, reassembled")
     return ap.parse_args()
 
 
@@ -110,12 +113,24 @@ def main():
     cfws.init()
 
     F, fs = args.frames, args.frame_size
-    desc_np, byte_base = shard.uniform_shard(F, fs, KEY_SEED, rank, world)
+    flags = 0
+    if args.workload == "config3":
+        # each rank: its own 4 GiB Zipf batch (independent seed per rank)
+        c3 = W.CONFIG3
+        desc_np, msgs = W.zipf_batch(c3["target_bytes"], c3["seed"] + rank, c3["key_seed"] + rank)
+        arena_bytes = int(msgs["arena_bytes"])
+        payload = torch.empty(W.round16(arena_bytes), dtype=torch.uint8, device=dev)
+        cfws.fill_splitmix(payload, c3["seed"] + rank)
+        flags = cfws.DESERIALIZE_REASSEMBLE
+        F = len(desc_np)
+    else:
+        desc_np, byte_base = shard.uniform_shard(F, fs, KEY_SEED, rank, world)
+        arena_bytes = F * fs
+        payload = torch.empty(arena_bytes, dtype=torch.uint8, device=dev)
+        cfws.fill_splitmix(payload, PAYLOAD_SEED, byte_base)
     offs, wire_total = W.wire_layout(desc_np)
-    payload = torch.empty(F * fs, dtype=torch.uint8, device=dev)
-    cfws.fill_splitmix(payload, PAYLOAD_SEED, byte_base)
     wire = torch.empty(W.round16(wire_total), dtype=torch.uint8, device=dev)
-    back = torch.empty(F * fs, dtype=torch.uint8, device=dev)
+    back = torch.empty(payload.numel() + 64, dtype=torch.uint8, device=dev)
     desc_ser = cfws.desc_to_device(desc_np, dev)
     desc_de = torch.empty((F, 32), dtype=torch.uint8, device=dev)
     status = torch.empty(F, dtype=torch.int32, device=dev)
@@ -131,9 +146,9 @@ def main():
         cfws.serialize_execute(payload, desc_ser, wire, ws_ser)
         if ev: ev[1].record()
         cfws.deserialize_plan(wire, wire_total, index, desc_de, status, back.numel(), tot_de,
-                              ws_de, align=16)
+                              ws_de, align=16, flags=flags)
         if ev: ev[2].record()
-        cfws.deserialize_execute(wire, desc_de, status, back, ws_de)
+        cfws.deserialize_execute(wire, desc_de, status, back, ws_de, flags=flags)
         if ev: ev[3].record()
 
     for _ in range(args.warmup):
@@ -151,24 +166,25 @@ def main():
     elapsed = shard.max_over_ranks(time.perf_counter() - t0, dev)
 
     # correctness of what was timed: unmask(mask(P)) == P, every frame COMPLETE
-    verified = (int(tot_ser.item()) == wire_total and int(tot_de.item()) == F * fs
-                and bool((status == 0).all().item()) and torch.equal(back, payload))
+    verified = (int(tot_ser.item()) == wire_total and int(tot_de.item()) == arena_bytes
+                and bool((status == 0).all().item())
+                and torch.equal(back[:arena_bytes], payload[:arena_bytes]))
     verified = shard.sum_over_ranks(1.0 if verified else 0.0, dev) == world
 
     # practical ceiling: a plain device-to-device copy of the same byte count
     c0, c1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    back.copy_(payload)
+    back[:payload.numel()].copy_(payload)
     c0.record()
     for _ in range(5):
-        back.copy_(payload)
+        back[:payload.numel()].copy_(payload)
     c1.record()
     torch.cuda.synchronize()
-    copy_gbps = 2 * F * fs / (c0.elapsed_time(c1) / 5 * 1e-3) / 1e9
+    copy_gbps = 2 * payload.numel() / (c0.elapsed_time(c1) / 5 * 1e-3) / 1e9
 
     ser_ms = sum(e[0].elapsed_time(e[1]) for e in events) / args.steps
     de_ms = sum(e[2].elapsed_time(e[3]) for e in events) / args.steps
-    hdr = int(wire_total - F * fs)
-    alg_bytes = 2 * F * fs + hdr            # read n + write n (+ headers) per launch
+    hdr = int(wire_total - arena_bytes)
+    alg_bytes = 2 * arena_bytes + hdr       # read n + write n (+ headers) per launch
     kern = {
         "serialize_execute": {"ms": round(ser_ms, 4),
                               "GBps": round(alg_bytes / (ser_ms * 1e-3) / 1e9, 1)},
@@ -180,7 +196,7 @@ def main():
     achieved = alg_bytes / (dom_ms * 1e-3) / 1e9
     kernel_symbol = ("xform_kernel<true>" if dom_name == "serialize_execute"
                      else "xform_kernel<false>")
-    total_payload = 2.0 * F * fs * world * args.steps
+    total_payload = 2.0 * arena_bytes * world * args.steps
     line = {
         "metric": METRIC,
         "value": round(total_payload / elapsed / GIB, 2),
@@ -195,10 +211,14 @@ def main():
         "dtype": "u8",
         "data": "synthetic (splitmix64 payloads, glibc random() mask keys as co_ws_frame_serialize draws them)",
         "config": {
-            "workload": f"config2: {F} binary frames x {fs // 1024} KiB per GPU, client-mask "
-                        f"(serialize) then server-unmask (deserialize), device resident",
+            "workload": (f"config2: {F} binary frames x {fs // 1024} KiB per GPU, client-mask "
+                         f"(serialize) then server-unmask (deserialize), device resident"
+                         if args.workload == "config2" else
+                         f"config3: {F} frames / {len(msgs['len'])} Zipf messages (64 B-1 MiB, "
+                         f"1-8 fragments) per GPU, client-mask then server-unmask with "
+                         f"continuation reassembly, device resident"),
             "frames_per_gpu": F,
-            "payload_bytes_per_frame": fs,
+            "payload_bytes_per_gpu": arena_bytes,
             "wire_bytes_per_gpu": wire_total,
             "parallelism": f"shard-per-gpu x{world} (no collective)",
         },
@@ -218,7 +238,7 @@ def main():
                          "how": "torch.Tensor.copy_ of the 4 GiB payload arena, device to device"},
         "verified": verified,
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload == "config2":
         line["cpu_baseline"] = cpu_baseline(fs, args.cpu_seconds)
     else:
         line["cpu_baseline"] = None

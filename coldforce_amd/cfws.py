@@ -27,6 +27,7 @@ ERROR_INVALID_FRAME = -7001
 ERROR_DATA_TOO_BIG = -7005
 ERROR_OUT_OF_MEMORY = -7006
 DEFAULT_MAX_PAYLOAD = 32 * 1024 * 1024          # co_ws_config.h:15
+DESERIALIZE_REASSEMBLE = 1                      # include/cfws.h
 
 OPCODE_CONTINUATION, OPCODE_TEXT, OPCODE_BINARY = 0x0, 0x1, 0x2
 OPCODE_CLOSE, OPCODE_PING, OPCODE_PONG = 0x8, 0x9, 0xA
@@ -96,11 +97,11 @@ def lib(path: str = LIB_PATH) -> C.CDLL:
         "cfws_serialize_plan": ([_vp, _sz, _u64, _vp, _vp, _sz, _vp], C.c_int),
         "cfws_serialize_execute": ([_vp, _vp, _sz, _vp, _u64, _vp, _vp], C.c_int),
         "cfws_serialize_batch": ([_vp, _vp, _sz, _vp, _u64, _vp, _vp, _sz, _vp], C.c_int),
-        "cfws_deserialize_plan": ([_vp, _u64, _vp, _sz, _u64, _u32, _vp, _vp, _u64, _vp, _vp,
-                                   _sz, _vp], C.c_int),
-        "cfws_deserialize_execute": ([_vp, _vp, _vp, _sz, _vp, _u64, _vp, _vp], C.c_int),
-        "cfws_deserialize_batch": ([_vp, _u64, _vp, _sz, _u64, _u32, _vp, _vp, _vp, _u64, _vp,
-                                    _vp, _sz, _vp], C.c_int),
+        "cfws_deserialize_plan": ([_vp, _u64, _vp, _sz, _u64, _u32, _u32, _vp, _vp, _u64, _vp,
+                                   _vp, _sz, _vp], C.c_int),
+        "cfws_deserialize_execute": ([_vp, _vp, _vp, _sz, _u32, _vp, _u64, _vp, _vp], C.c_int),
+        "cfws_deserialize_batch": ([_vp, _u64, _vp, _sz, _u64, _u32, _u32, _vp, _vp, _vp, _u64,
+                                    _vp, _vp, _sz, _vp], C.c_int),
         "cfws_xor_mask": ([_vp, _vp, _u64, _u32, _u32, _vp], C.c_int),
         "cfws_draw_mask_keys": ([_sz, _vp, _vp], None),
         "cfws_release_thread_resources": ([], None),
@@ -213,25 +214,26 @@ def serialize(payload_t, desc_t, wire_t, ws_t=None, total_t=None, stream=None):
 
 def deserialize_plan(wire_t, wire_size: int, index_t, desc_t, status_t, payload_capacity: int,
                      total_t, ws_t, max_payload: int = DEFAULT_MAX_PAYLOAD, align: int = 16,
-                     stream=None) -> None:
+                     flags: int = 0, stream=None) -> None:
     _check(lib().cfws_deserialize_plan(_p(wire_t), wire_size, _p(index_t), index_t.numel(),
-                                       max_payload, align, _p(desc_t), _p(status_t),
+                                       max_payload, align, flags, _p(desc_t), _p(status_t),
                                        payload_capacity, _p(total_t), _p(ws_t), ws_t.numel(),
                                        _stream(stream)),
            "cfws_deserialize_plan")
 
 
 def deserialize_execute(wire_t, desc_t, status_t, payload_t, ws_t,
-                        payload_capacity: int | None = None, stream=None) -> None:
+                        payload_capacity: int | None = None, flags: int = 0,
+                        stream=None) -> None:
     cap = payload_t.numel() if payload_capacity is None else payload_capacity
     _check(lib().cfws_deserialize_execute(_p(wire_t), _p(desc_t), _p(status_t), desc_t.shape[0],
-                                          _p(payload_t), cap, _p(ws_t), _stream(stream)),
+                                          flags, _p(payload_t), cap, _p(ws_t), _stream(stream)),
            "cfws_deserialize_execute")
 
 
 def deserialize(wire_t, wire_size: int, index_t, payload_t, desc_t=None, status_t=None,
                 ws_t=None, total_t=None, max_payload: int = DEFAULT_MAX_PAYLOAD,
-                align: int = 16, stream=None):
+                align: int = 16, flags: int = 0, stream=None):
     """Deserialize the frame starting at each index_t[i] of wire_t[:wire_size].
     Returns (desc_t, status_t, total_t)."""
     import torch
@@ -246,8 +248,9 @@ def deserialize(wire_t, wire_size: int, index_t, payload_t, desc_t=None, status_
     if total_t is None:
         total_t = torch.zeros(1, dtype=torch.int64, device=dev)
     _check(lib().cfws_deserialize_batch(_p(wire_t), wire_size, _p(index_t), n, max_payload, align,
-                                        _p(desc_t), _p(status_t), _p(payload_t), payload_t.numel(),
-                                        _p(total_t), _p(ws_t), ws_t.numel(), _stream(stream)),
+                                        flags, _p(desc_t), _p(status_t), _p(payload_t),
+                                        payload_t.numel(), _p(total_t), _p(ws_t), ws_t.numel(),
+                                        _stream(stream)),
            "cfws_deserialize_batch")
     return desc_t, status_t, total_t
 

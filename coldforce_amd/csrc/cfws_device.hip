@@ -7,21 +7,24 @@
 //   header decode        co_ws_frame.c:131-213 (MORE_DATA before TOO_BIG)
 //   payload copy+unmask  co_ws_frame.c:214-242
 //
-// Design (DESIGN.md has the full story):
+// Design (DESIGN.md §3 has the full story):
 //   * The output arena (wire arena for serialize, payload arena for
-//     deserialize) is cut into 16 KiB tiles of 16-byte chunks. Every chunk
-//     is produced by exactly one lane and written with one 16-byte store, so
-//     frame boundaries never need byte stores or read-modify-write.
-//   * A plan (prefix sum of frame sizes + a tile -> first-frame map) lets
-//     each workgroup find its frames with two scalar loads; a tile that lies
-//     inside one frame (the common case for 64 KiB frames) runs with the
-//     frame descriptor, key and alignment phase in SGPRs.
+//     deserialize) is cut into 4 KiB regions, one per wave; every 16-byte
+//     chunk is produced by exactly one lane and written with one 16-byte
+//     store, so frame boundaries never need byte stores or read-modify-write.
+//   * A plan (prefix sum of frame sizes + a region -> first-frame map) lets a
+//     wave find its frames with two scalar loads; a region inside one frame
+//     runs with the frame's descriptor, key and alignment phase in SGPRs.
 //   * Source and destination are misaligned against each other (a masked
-//     64 KiB frame is 65,550 B on the wire). A lane loads the aligned 16-byte
-//     source block(s) covering its chunk and funnel-shifts them with
-//     v_alignbyte_b32; the key is pre-rotated once per frame.
+//     64 KiB frame is 65,550 B on the wire); a lane funnel-shifts the two
+//     aligned 16-byte source blocks covering its chunk (v_alignbyte_b32) and
+//     XORs with the key pre-rotated once per frame.
 //   * Pure HBM streaming: 2 bytes of traffic per payload byte, no LDS on the
 //     fast path, no MFMA.
+//   * A pass writes output bytes [base, base + total) from per-frame output
+//     offsets `offs` (monotone). Deserialize with CFWS_DESERIALIZE_REASSEMBLE
+//     runs two passes: data frames packed (messages contiguous), then control
+//     frames after them.
 #include <hip/hip_runtime.h>
 
 #include <stdint.h>
@@ -41,20 +44,25 @@ constexpr int kWaves = kThreads / 64;
 constexpr int kUnroll = CFWS_UNROLL;                         // chunks per lane per region
 constexpr uint64_t kChunk = 16;
 constexpr uint64_t kSlice = 64 * kChunk;                     // one wave-instruction: 1 KiB
-constexpr uint64_t kTileBytes = kSlice * kUnroll;            // one wave's region: 4 KiB
+constexpr uint64_t kRegion = kSlice * kUnroll;               // one wave's region: 4 KiB
 constexpr int kScanItems = 8;
 constexpr uint64_t kScanBlock = uint64_t(kThreads) * kScanItems;
+
+// Frame classes a pass copies (deserialize): all, data only, control only.
+enum : uint32_t { kClassAll = 0, kClassData = 1, kClassControl = 2 };
 
 // ---------------------------------------------------------------------------
 // workspace layout (deterministic from n_frames and the output capacity)
 // ---------------------------------------------------------------------------
+// hdr[0] pass-0 total (clamped)   hdr[1] pass-1 total (clamped)
+// hdr[2] pass-1 output base       hdr[3] pass-0 grand total   hdr[4] pass-1 grand
 struct WsLayout {
-    uint64_t total;      // u64: output bytes, clamped to capacity
-    uint64_t vals;       // u64[n]: per-frame sizes, then exclusive offsets
-    uint64_t partials;   // u64[scan blocks]
-    uint64_t tile_map;   // u32[tiles_max + 2]
+    uint64_t hdr;
+    uint64_t offs[2];      // u64[n] per pass: sizes, then exclusive offsets
+    uint64_t partials[2];  // u64[scan blocks + 1] per pass
+    uint64_t map[2];       // u32[regions + 2] per pass
     uint64_t bytes;
-    uint64_t tiles_max;
+    uint64_t regions;
     uint64_t scan_blocks;
 };
 
@@ -63,13 +71,15 @@ inline uint64_t align_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
 WsLayout ws_layout(uint64_t n, uint64_t capacity)
 {
     WsLayout L;
-    L.tiles_max = (capacity + kTileBytes - 1) / kTileBytes;
+    L.regions = (capacity + kRegion - 1) / kRegion;
     L.scan_blocks = (n + kScanBlock - 1) / kScanBlock;
-    L.total = 0;
-    L.vals = 256;
-    L.partials = align_up(L.vals + 8 * n, 256);
-    L.tile_map = align_up(L.partials + 8 * (L.scan_blocks + 1), 256);
-    L.bytes = align_up(L.tile_map + 4 * (L.tiles_max + 2), 256);
+    uint64_t at = 0;
+    L.hdr = at;
+    at += 256;
+    for (int p = 0; p < 2; ++p) { L.offs[p] = at; at = align_up(at + 8 * n, 256); }
+    for (int p = 0; p < 2; ++p) { L.partials[p] = at; at = align_up(at + 8 * (L.scan_blocks + 1), 256); }
+    for (int p = 0; p < 2; ++p) { L.map[p] = at; at = align_up(at + 4 * (L.regions + 2), 256); }
+    L.bytes = at;
     return L;
 }
 
@@ -81,39 +91,15 @@ __device__ __forceinline__ uint32_t header_size_of(uint64_t n, bool mask)
     return 2u + (n > 65535u ? 8u : (n > 125u ? 2u : 0u)) + (mask ? 4u : 0u);
 }
 
-// Byte r of the serialized header (co_ws_frame.c:34-91).
-__device__ __forceinline__ uint32_t header_byte(const cfws_frame_desc_t& d, uint32_t r)
+__device__ __forceinline__ bool is_control(uint32_t opcode)
 {
-    const uint64_t n = d.payload_size;
-    const uint32_t ext = n > 65535u ? 8u : (n > 125u ? 2u : 0u);
-    if (r == 0) return (uint32_t)(uint8_t)(d.opcode | (d.fin ? 0x80u : 0u));
-    if (r == 1) {
-        const uint32_t l7 = ext == 8 ? 127u : (ext == 2 ? 126u : (uint32_t)n);
-        return (l7 | (d.mask ? 0x80u : 0u)) & 0xffu;
-    }
-    r -= 2;
-    if (r < ext) return (uint32_t)(n >> (8 * (ext - 1 - r))) & 0xffu;
-    r -= ext;
-    return (d.mask_key >> (8 * r)) & 0xffu;
+    return opcode <= 0x0fu && (opcode & 0x08u) != 0;       // co_ws_frame.h:32-34
 }
 
 __device__ __forceinline__ uint32_t rotr8(uint32_t key, uint32_t bytes)
 {
     return __builtin_amdgcn_alignbyte(key, key, bytes & 3u);
 }
-
-// What one frame contributes to the output arena.
-//   [out_off, out_off + pre)              header bytes (serialize only)
-//   [out_off + pre, + body_len)           src[src_off + k] ^ key[k % 4]
-//   [.., next frame's out_off)            zero (deserialize alignment pad)
-struct FrameView {
-    uint64_t out_off;
-    uint64_t body_start;
-    uint64_t body_len;
-    uint64_t src_off;
-    uint32_t key;   // 0 when the frame is not masked: XOR becomes a copy
-    uint32_t pre;
-};
 
 // The descriptor is read as four 64-bit words so that a wave-uniform f
 // becomes one s_load_dwordx8 (byte-field loads would be vector loads).
@@ -132,33 +118,68 @@ __device__ __forceinline__ DescWords load_desc(const cfws_frame_desc_t* __restri
     return DescWords{q[0], q[1], q[2], q[3]};
 }
 
-template <bool kSer>
-__device__ __forceinline__ FrameView frame_view(const cfws_frame_desc_t* __restrict__ desc,
-                                                const int32_t* __restrict__ status, uint32_t f)
+// Byte r of the serialized header (co_ws_frame.c:34-91).
+__device__ __forceinline__ uint32_t header_byte(const DescWords& d, uint32_t r)
 {
-    const DescWords d = load_desc(desc, f);
+    const uint64_t n = d.payload_size;
+    const uint32_t ext = n > 65535u ? 8u : (n > 125u ? 2u : 0u);
+    if (r == 0) return (d.opcode() | (d.fin() ? 0x80u : 0u)) & 0xffu;
+    if (r == 1) {
+        const uint32_t l7 = ext == 8 ? 127u : (ext == 2 ? 126u : (uint32_t)n);
+        return (l7 | (d.mask() ? 0x80u : 0u)) & 0xffu;
+    }
+    r -= 2;
+    if (r < ext) return (uint32_t)(n >> (8 * (ext - 1 - r))) & 0xffu;
+    r -= ext;
+    return (d.key() >> (8 * r)) & 0xffu;
+}
+
+// Arguments of one streaming pass.
+struct Pass {
+    const uint8_t* src;
+    uint8_t* dst;                 // already offset by the pass base
+    const cfws_frame_desc_t* desc;
+    const int32_t* status;        // deserialize only
+    const uint64_t* offs;         // per-frame output offsets of this pass
+    uint64_t total;               // output bytes of this pass
+    uint64_t capacity;            // writable bytes from dst
+    uint32_t n_frames;
+    uint32_t klass;
+};
+
+// What one frame contributes to a pass's output.
+//   [out_off, out_off + pre)              header bytes (serialize only)
+//   [out_off + pre, + body_len)           src[src_off + k] ^ key[k % 4]
+//   [.., next frame's out_off)            zero (deserialize alignment pad)
+struct FrameView {
+    uint64_t out_off;
+    uint64_t body_start;
+    uint64_t body_len;
+    uint64_t src_off;
+    uint32_t key;   // 0 when the frame is not masked: XOR becomes a copy
+    uint32_t pre;
+};
+
+template <bool kSer>
+__device__ __forceinline__ FrameView frame_view(const Pass& P, uint32_t f)
+{
+    const DescWords d = load_desc(P.desc, f);
     FrameView v;
     v.key = d.mask() ? d.key() : 0u;
+    v.out_off = P.offs[f];
     if (kSer) {
-        v.out_off = d.wire_off;
         v.pre = d.header_size();
         v.body_len = d.payload_size;
         v.src_off = d.payload_off;
     } else {
-        v.out_off = d.payload_off;
+        const bool ctl = is_control(d.opcode());
+        const bool take = P.klass == kClassAll || (P.klass == kClassControl) == ctl;
         v.pre = 0;
-        v.body_len = (status[f] == CFWS_PARSE_COMPLETE) ? d.payload_size : 0;
+        v.body_len = (take && P.status[f] == CFWS_PARSE_COMPLETE) ? d.payload_size : 0;
         v.src_off = d.wire_off + d.header_size();
     }
     v.body_start = v.out_off + v.pre;
     return v;
-}
-
-template <bool kSer>
-__device__ __forceinline__ uint64_t out_off_of(const cfws_frame_desc_t* __restrict__ desc, uint32_t f)
-{
-    const uint64_t* q = reinterpret_cast<const uint64_t*>(desc) + 4 * uint64_t(f);
-    return kSer ? q[1] : q[0];
 }
 
 // 16-byte global accesses of the streaming paths. Output is written once and
@@ -196,10 +217,8 @@ __device__ __forceinline__ uint4 funnel16(uint4 A, uint4 B, uint32_t ph)
     const bool s8 = (ph & 8u) != 0;
     const bool s4 = (ph & 4u) != 0;
     const uint32_t r = ph & 3u;
-    // shift by 8 bytes
     const uint32_t a0 = s8 ? A.z : A.x, a1 = s8 ? A.w : A.y, a2 = s8 ? B.x : A.z;
     const uint32_t a3 = s8 ? B.y : A.w, a4 = s8 ? B.z : B.x, a5 = s8 ? B.w : B.y;
-    // shift by 4 bytes
     const uint32_t b0 = s4 ? a1 : a0, b1 = s4 ? a2 : a1, b2 = s4 ? a3 : a2;
     const uint32_t b3 = s4 ? a4 : a3, b4 = s4 ? a5 : a4;
     uint4 o;
@@ -210,97 +229,95 @@ __device__ __forceinline__ uint4 funnel16(uint4 A, uint4 B, uint32_t ph)
     return o;
 }
 
-// Fast path: the whole 16-byte chunk at D lies inside v's body.
+__device__ __forceinline__ void xor4(uint4& o, uint32_t k)
+{
+    o.x ^= k; o.y ^= k; o.z ^= k; o.w ^= k;
+}
+
+// One chunk entirely inside v's body.
 __device__ __forceinline__ uint4 body_chunk(const uint8_t* __restrict__ src, const FrameView& v,
                                             uint64_t D)
 {
     const uint64_t k0 = D - v.body_start;
     const uint64_t s = v.src_off + k0;
-    const uint64_t sa = s & ~uint64_t(15);
+    const uint8_t* sp = src + (s & ~uint64_t(15));
     const uint32_t ph = (uint32_t)(s & 15u);
-    const uint4 A = *reinterpret_cast<const uint4*>(src + sa);
-    uint4 o = A;
-    if (ph != 0) {
-        // The aligned block holding the chunk's last byte: always inside the
-        // same page as a valid source byte, never past the allocation's page.
-        const uint4 B = *reinterpret_cast<const uint4*>(src + sa + 16);
-        o = funnel16(A, B, ph);
-    }
-    const uint32_t kr = rotr8(v.key, (uint32_t)(k0 & 3u));
-    o.x ^= kr; o.y ^= kr; o.z ^= kr; o.w ^= kr;
+    uint4 o = ld16(sp);
+    // The aligned block holding the chunk's last byte: it contains a valid
+    // source byte, so it never lies past the allocation's last page.
+    if (ph != 0) o = funnel16(o, ld16(sp + 16), ph);
+    xor4(o, rotr8(v.key, (uint32_t)(k0 & 3u)));
     return o;
 }
 
-// Slow path: a chunk that crosses a header, a frame boundary, padding or the
-// end of the arena. Built byte by byte, walking frames forward from f.
+// A chunk that crosses a header, a frame boundary, padding or the end of
+// the pass: built byte by byte, walking frames forward from f.
 template <bool kSer>
-__device__ __noinline__ uint4 edge_chunk(const uint8_t* __restrict__ src,
-                                         const cfws_frame_desc_t* __restrict__ desc,
-                                         const int32_t* __restrict__ status, uint32_t f,
-                                         uint32_t n_frames, uint64_t D, uint64_t total)
+__device__ __noinline__ uint4 edge_chunk(const Pass& P, uint32_t f, uint64_t D)
 {
-    FrameView v = frame_view<kSer>(desc, status, f);
-    uint64_t next = (f + 1 < n_frames) ? out_off_of<kSer>(desc, f + 1) : ~uint64_t(0);
-    uint32_t w[4] = {0u, 0u, 0u, 0u};
+    FrameView v = frame_view<kSer>(P, f);
+    uint64_t next = (f + 1 < P.n_frames) ? P.offs[f + 1] : ~uint64_t(0);
+    uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
         const uint64_t pos = D + j;
         uint32_t b = 0;
-        if (pos < total) {
+        if (pos < P.total) {
             while (pos >= next) {
                 ++f;
-                v = frame_view<kSer>(desc, status, f);
-                next = (f + 1 < n_frames) ? out_off_of<kSer>(desc, f + 1) : ~uint64_t(0);
+                v = frame_view<kSer>(P, f);
+                next = (f + 1 < P.n_frames) ? P.offs[f + 1] : ~uint64_t(0);
             }
             const uint64_t r = pos - v.out_off;
             if (r < v.pre) {
-                b = header_byte(desc[f], (uint32_t)r);
+                b = header_byte(load_desc(P.desc, f), (uint32_t)r);
             } else {
                 const uint64_t k = r - v.pre;
-                if (k < v.body_len) b = (src[v.src_off + k] ^ (v.key >> (8 * (k & 3u)))) & 0xffu;
+                if (k < v.body_len) b = (P.src[v.src_off + k] ^ (v.key >> (8 * (k & 3u)))) & 0xffu;
             }
         }
-        w[j >> 2] |= b << (8 * (j & 3));
+        const uint32_t sh = 8 * (j & 3);
+        if (j < 4) w0 |= b << sh;
+        else if (j < 8) w1 |= b << sh;
+        else if (j < 12) w2 |= b << sh;
+        else w3 |= b << sh;
     }
-    return make_uint4(w[0], w[1], w[2], w[3]);
+    return make_uint4(w0, w1, w2, w3);
 }
 
-__device__ __forceinline__ void store_chunk(uint8_t* __restrict__ dst, uint64_t D, uint4 o,
-                                            uint64_t capacity)
+__device__ __forceinline__ void store_chunk(const Pass& P, uint64_t D, uint4 o)
 {
-    if (D + 16 <= capacity) {
-        *reinterpret_cast<uint4*>(dst + D) = o;
+    if (D + 16 <= P.capacity) {
+        st16(P.dst + D, o);
     } else {
         const uint32_t w[4] = {o.x, o.y, o.z, o.w};
-        for (uint32_t j = 0; D + j < capacity; ++j) dst[D + j] = (uint8_t)(w[j >> 2] >> (8 * (j & 3)));
+        for (uint32_t j = 0; D + j < P.capacity; ++j) P.dst[D + j] = (uint8_t)(w[j >> 2] >> (8 * (j & 3)));
     }
 }
 
 // ---------------------------------------------------------------------------
-// the streaming kernel: serialize (kSer) = header + mask into the wire
-// arena; deserialize = copy + unmask into the payload arena
+// the streaming kernel
 // ---------------------------------------------------------------------------
 
-// A 4 KiB region that lies inside one frame's body: frame, source phase and
-// rotated key are wave-uniform (SGPRs); kUnroll 1 KiB wave-instructions of
-// loads are all in flight before the first store.
-__device__ __forceinline__ void fast_region(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
-                                            const FrameView& v, uint64_t base, uint32_t lane)
+// A region inside one frame's body: frame, source phase and rotated key are
+// wave-uniform (SGPRs); all kUnroll x {A, B} loads are in flight before the
+// first store.
+__device__ __forceinline__ void fast_region(const Pass& P, const FrameView& v, uint64_t base,
+                                            uint32_t lane)
 {
     const uint64_t delta = v.src_off - v.body_start;           // src = out + delta
     const uint32_t ph = (uint32_t)(delta & 15u);
     const uint32_t kr = rotr8(v.key, (uint32_t)((0 - v.body_start) & 3u));
-    const uint8_t* s0 = src + ((base + delta) & ~uint64_t(15)) + lane * kChunk;
-    uint8_t* d0 = dst + base + lane * kChunk;
+    const uint8_t* s0 = P.src + ((base + delta) & ~uint64_t(15)) + lane * kChunk;
+    uint8_t* d0 = P.dst + base + lane * kChunk;
     if (ph == 0) {
         uint4 a[kUnroll];
 #pragma unroll
         for (int u = 0; u < kUnroll; ++u) a[u] = ld16(s0 + u * kSlice);
 #pragma unroll
         for (int u = 0; u < kUnroll; ++u) {
-            uint4 o = a[u];
-            o.x ^= kr; o.y ^= kr; o.z ^= kr; o.w ^= kr;
-            st16(d0 + u * kSlice, o);
+            xor4(a[u], kr);
+            st16(d0 + u * kSlice, a[u]);
         }
     } else {
         uint4 a[kUnroll], b[kUnroll];
@@ -312,23 +329,20 @@ __device__ __forceinline__ void fast_region(const uint8_t* __restrict__ src, uin
 #pragma unroll
         for (int u = 0; u < kUnroll; ++u) {
             uint4 o = funnel16(a[u], b[u], ph);
-            o.x ^= kr; o.y ^= kr; o.z ^= kr; o.w ^= kr;
+            xor4(o, kr);
             st16(d0 + u * kSlice, o);
         }
     }
 }
 
-// A region crossed by exactly one frame boundary (the common boundary case
-// for large frames): both frames' views are wave-uniform, each lane picks
-// one by comparing its chunk with the boundary; only the chunk holding the
-// boundary / header bytes takes the byte-wise edge path.
+// A region crossed by exactly one frame boundary (the boundary case of large
+// frames): both views are wave-uniform, each lane picks one by comparing its
+// chunk with the boundary; only chunks holding the boundary or header bytes
+// go byte-wise.
 template <bool kSer>
-__device__ __forceinline__ void two_frame_region(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
-                                                 const cfws_frame_desc_t* __restrict__ desc,
-                                                 const int32_t* __restrict__ status,
-                                                 const FrameView& va, const FrameView& vb,
-                                                 uint32_t fa, uint32_t n_frames, uint64_t base,
-                                                 uint64_t total, uint64_t capacity, uint32_t lane)
+__device__ __forceinline__ void two_frame_region(const Pass& P, const FrameView& va,
+                                                 const FrameView& vb, uint32_t fa,
+                                                 uint64_t base, uint32_t lane)
 {
     uint4 a[kUnroll], b[kUnroll];
     bool fast[kUnroll];
@@ -338,10 +352,9 @@ __device__ __forceinline__ void two_frame_region(const uint8_t* __restrict__ src
         const bool hi = D >= vb.out_off;
         const uint64_t bs = hi ? vb.body_start : va.body_start;
         const uint64_t be = bs + (hi ? vb.body_len : va.body_len);
-        const uint64_t so = hi ? vb.src_off : va.src_off;
+        const uint64_t s = (hi ? vb.src_off : va.src_off) + (D - bs);
+        const uint8_t* sp = P.src + (s & ~uint64_t(15));
         fast[u] = D >= bs && D + kChunk <= be;
-        const uint64_t s = so + (D - bs);
-        const uint8_t* sp = src + (s & ~uint64_t(15));
         if (fast[u]) {
             a[u] = ld16(sp);
             if (s & 15u) b[u] = ld16(sp + 16);
@@ -350,93 +363,92 @@ __device__ __forceinline__ void two_frame_region(const uint8_t* __restrict__ src
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u) {
         const uint64_t D = base + u * kSlice + lane * kChunk;
-        if (D >= total) continue;
+        if (D >= P.total) continue;
         const bool hi = D >= vb.out_off;
-        uint4 o;
         if (fast[u]) {
-            const uint64_t bs = hi ? vb.body_start : va.body_start;
-            const uint64_t so = hi ? vb.src_off : va.src_off;
-            const uint32_t key = hi ? vb.key : va.key;
-            const uint64_t k0 = D - bs;
-            const uint32_t ph = (uint32_t)((so + k0) & 15u);
-            o = ph ? funnel16(a[u], b[u], ph) : a[u];
-            const uint32_t kr = rotr8(key, (uint32_t)(k0 & 3u));
-            o.x ^= kr; o.y ^= kr; o.z ^= kr; o.w ^= kr;
-            st16(dst + D, o);
+            const uint64_t k0 = D - (hi ? vb.body_start : va.body_start);
+            const uint32_t ph = (uint32_t)(((hi ? vb.src_off : va.src_off) + k0) & 15u);
+            uint4 o = ph ? funnel16(a[u], b[u], ph) : a[u];
+            xor4(o, rotr8(hi ? vb.key : va.key, (uint32_t)(k0 & 3u)));
+            st16(P.dst + D, o);
         } else {
-            o = edge_chunk<kSer>(src, desc, status, hi ? fa + 1 : fa, n_frames, D, total);
-            store_chunk(dst, D, o, capacity);
+            store_chunk(P, D, edge_chunk<kSer>(P, hi ? fa + 1 : fa, D));
         }
     }
 }
 
-// A region that touches a header, a frame boundary, padding or the arena
-// end: every lane finds the frame of each of its chunks (binary search over
-// the region's frames [f0, f1]) and builds the chunk from it.
+// Any other region (small frames, padding, pass end): every lane finds the
+// frame of each of its chunks by binary search over the region's frames.
 template <bool kSer>
-__device__ __noinline__ void general_region(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
-                                            const cfws_frame_desc_t* __restrict__ desc,
-                                            const int32_t* __restrict__ status, uint32_t f0,
-                                            uint32_t f1, uint32_t n_frames, uint64_t base,
-                                            uint64_t total, uint64_t capacity, uint32_t lane)
+__device__ __noinline__ void general_region(const Pass& P, uint32_t f0, uint32_t f1,
+                                            uint64_t base, uint32_t lane)
 {
 #pragma unroll 1
     for (int u = 0; u < kUnroll; ++u) {
         const uint64_t D = base + u * kSlice + lane * kChunk;
-        if (D >= total) continue;
-        uint32_t lo = f0, hi = f1;                  // largest f with out_off(f) <= D
+        if (D >= P.total) continue;
+        uint32_t lo = f0, hi = f1;                  // largest f with offs[f] <= D
         while (lo < hi) {
             const uint32_t mid = (lo + hi + 1) >> 1;
-            if (out_off_of<kSer>(desc, mid) <= D) lo = mid; else hi = mid - 1;
+            if (P.offs[mid] <= D) lo = mid; else hi = mid - 1;
         }
-        const FrameView v = frame_view<kSer>(desc, status, lo);
-        uint4 o;
-        if (D >= v.body_start && D + kChunk <= v.body_start + v.body_len)
-            o = body_chunk(src, v, D);
-        else
-            o = edge_chunk<kSer>(src, desc, status, lo, n_frames, D, total);
-        store_chunk(dst, D, o, capacity);
+        const FrameView v = frame_view<kSer>(P, lo);
+        const uint4 o = (D >= v.body_start && D + kChunk <= v.body_start + v.body_len)
+                            ? body_chunk(P.src, v, D)
+                            : edge_chunk<kSer>(P, lo, D);
+        store_chunk(P, D, o);
     }
 }
 
+// serialize (kSer): header + (masked) payload into the wire arena;
+// deserialize: copy + unmask into the payload arena.
 template <bool kSer>
 __global__ void __launch_bounds__(kThreads)
 xform_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
              const cfws_frame_desc_t* __restrict__ desc, const int32_t* __restrict__ status,
-             const uint32_t* __restrict__ tile_map, const uint64_t* __restrict__ total_p,
-             uint64_t capacity, uint32_t n_frames)
+             const uint64_t* __restrict__ offs, const uint32_t* __restrict__ region_map,
+             const uint64_t* __restrict__ total_p, const uint64_t* __restrict__ base_p,
+             uint64_t capacity, uint32_t n_frames, uint32_t klass)
 {
-    const uint64_t total = *total_p;                 // already clamped to capacity
-    const uint64_t n_regions = (total + kTileBytes - 1) / kTileBytes;
+    const uint64_t out_base = base_p ? *base_p : 0;
+    Pass P;
+    P.src = src;
+    P.dst = dst + out_base;
+    P.desc = desc;
+    P.status = status;
+    P.offs = offs;
+    P.total = *total_p;                              // clamped by the plan
+    P.capacity = capacity - out_base;
+    P.n_frames = n_frames;
+    P.klass = klass;
+    const uint64_t n_regions = (P.total + kRegion - 1) / kRegion;
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t stride = uint64_t(gridDim.x) * kWaves;
 
     for (uint64_t r = uint64_t(blockIdx.x) * kWaves + wave; r < n_regions; r += stride) {
-        const uint64_t base = r * kTileBytes;
+        const uint64_t base = r * kRegion;
+        const uint64_t end = base + kRegion;
         // The plan writes every entry in [0, n_regions]; the clamps only keep
         // a corrupted workspace from turning into an out-of-bounds read.
-        uint32_t f0 = tile_map[r];
-        uint32_t f1 = tile_map[r + 1];
+        uint32_t f0 = region_map[r];
+        uint32_t f1 = region_map[r + 1];
         if (f1 >= n_frames) f1 = n_frames - 1;
         if (f0 > f1) f0 = f1;
-        const uint64_t end = base + kTileBytes;
-        // tile_map[r + 1] is the frame holding the NEXT region's first byte;
-        // frames that start at or after this region's end do not touch it.
-        if (f1 > f0 && out_off_of<kSer>(desc, f0 + 1) >= end) f1 = f0;
-        const FrameView va = frame_view<kSer>(desc, status, f0);
+        // region_map[r + 1] holds the NEXT region's first byte; frames that
+        // start at or after this region's end do not touch it.
+        if (f1 > f0 && offs[f0 + 1] >= end) f1 = f0;
+        const FrameView va = frame_view<kSer>(P, f0);
         if (f0 == f1) {
             if (base >= va.body_start && end <= va.body_start + va.body_len) {
-                fast_region(src, dst, va, base, lane);
+                fast_region(P, va, base, lane);
                 continue;
             }
-        } else if (f1 == f0 + 1 || out_off_of<kSer>(desc, f0 + 2) >= end) {
-            const FrameView vb = frame_view<kSer>(desc, status, f0 + 1);
-            two_frame_region<kSer>(src, dst, desc, status, va, vb, f0, n_frames, base, total,
-                                   capacity, lane);
+        } else if (f1 == f0 + 1 || offs[f0 + 2] >= end) {
+            two_frame_region<kSer>(P, va, frame_view<kSer>(P, f0 + 1), f0, base, lane);
             continue;
         }
-        general_region<kSer>(src, dst, desc, status, f0, f1, n_frames, base, total, capacity, lane);
+        general_region<kSer>(P, f0, f1, base, lane);
     }
 }
 
@@ -454,13 +466,16 @@ serialize_sizes_kernel(cfws_frame_desc_t* __restrict__ desc, uint64_t* __restric
     vals[f] = hs + len;
 }
 
-// Header decode at d_index[f] (co_ws_frame.c:131-213), with the callers'
-// two-byte precheck (co_ws_client.c:202-206).
+// Header decode at index[f] (co_ws_frame.c:131-213), with the callers'
+// two-byte precheck (co_ws_client.c:202-206). Writes the layout sizes of
+// both passes: vals0 = data (or every frame without reassembly), vals1 =
+// control frames when reassembling.
 __global__ void __launch_bounds__(kThreads)
 deserialize_parse_kernel(const uint8_t* __restrict__ wire, uint64_t wire_size,
                          const uint64_t* __restrict__ index, uint64_t n, uint64_t max_payload,
-                         uint64_t align, cfws_frame_desc_t* __restrict__ desc,
-                         int32_t* __restrict__ status, uint64_t* __restrict__ vals)
+                         uint64_t align, uint32_t reassemble, cfws_frame_desc_t* __restrict__ desc,
+                         int32_t* __restrict__ status, uint64_t* __restrict__ vals0,
+                         uint64_t* __restrict__ vals1)
 {
     const uint64_t f = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
     if (f >= n) return;
@@ -506,7 +521,14 @@ deserialize_parse_kernel(const uint8_t* __restrict__ wire, uint64_t wire_size,
     } while (0);
     desc[f] = d;
     status[f] = st;
-    vals[f] = (st == CFWS_PARSE_COMPLETE) ? ((d.payload_size + align - 1) & ~(align - 1)) : 0;
+    const uint64_t len = (st == CFWS_PARSE_COMPLETE) ? d.payload_size : 0;
+    if (reassemble) {
+        const bool ctl = is_control(d.opcode);
+        vals0[f] = ctl ? 0 : len;
+        vals1[f] = ctl ? len : 0;
+    } else {
+        vals0[f] = (len + align - 1) & ~(align - 1);
+    }
 }
 
 // Exclusive block scan of one value per thread; *block_total gets the sum.
@@ -525,7 +547,7 @@ __device__ __forceinline__ uint64_t block_exclusive_scan(uint64_t x, uint64_t* s
     __syncthreads();
     uint64_t before = 0, all = 0;
 #pragma unroll
-    for (uint32_t w = 0; w < kThreads / 64; ++w) {
+    for (uint32_t w = 0; w < kWaves; ++w) {
         if (w < wid) before += s_wave[w];
         all += s_wave[w];
     }
@@ -536,7 +558,7 @@ __device__ __forceinline__ uint64_t block_exclusive_scan(uint64_t x, uint64_t* s
 __global__ void __launch_bounds__(kThreads)
 scan_reduce_kernel(const uint64_t* __restrict__ vals, uint64_t n, uint64_t* __restrict__ partials)
 {
-    __shared__ uint64_t s_wave[kThreads / 64];
+    __shared__ uint64_t s_wave[kWaves];
     const uint64_t b0 = uint64_t(blockIdx.x) * kScanBlock;
     uint64_t sum = 0;
 #pragma unroll
@@ -552,7 +574,7 @@ scan_reduce_kernel(const uint64_t* __restrict__ vals, uint64_t n, uint64_t* __re
 __global__ void __launch_bounds__(kThreads)
 scan_partials_kernel(uint64_t* __restrict__ partials, uint64_t nb, uint64_t* __restrict__ grand)
 {
-    __shared__ uint64_t s_wave[kThreads / 64];
+    __shared__ uint64_t s_wave[kWaves];
     uint64_t carry = 0;
     for (uint64_t b = 0; b < nb; b += kThreads) {
         const uint64_t i = b + threadIdx.x;
@@ -568,7 +590,7 @@ scan_partials_kernel(uint64_t* __restrict__ partials, uint64_t nb, uint64_t* __r
 __global__ void __launch_bounds__(kThreads)
 scan_apply_kernel(uint64_t* __restrict__ vals, uint64_t n, const uint64_t* __restrict__ partials)
 {
-    __shared__ uint64_t s_wave[kThreads / 64];
+    __shared__ uint64_t s_wave[kWaves];
     const uint64_t i0 = uint64_t(blockIdx.x) * kScanBlock + uint64_t(threadIdx.x) * kScanItems;
     uint64_t v[kScanItems];
     uint64_t sum = 0;
@@ -586,39 +608,68 @@ scan_apply_kernel(uint64_t* __restrict__ vals, uint64_t n, const uint64_t* __res
     }
 }
 
-// Writes offsets into the descriptors, applies the capacity rule and builds
-// the tile -> first frame map. `grand` = unclamped total from the scan.
-template <bool kSer>
+// Fills the region -> first-frame map of one pass over [0, total).
+__device__ __forceinline__ void map_regions(const uint64_t* __restrict__ offs, uint64_t f, uint64_t n,
+                                            uint64_t grand, uint64_t total, uint32_t* __restrict__ map)
+{
+    const uint64_t lo = offs[f];
+    const uint64_t hi = (f + 1 < n) ? offs[f + 1] : grand;
+    const uint64_t a = lo < total ? lo : total;
+    const uint64_t b = hi < total ? hi : total;
+    if (b > a) {
+        const uint64_t r1 = (b + kRegion - 1) / kRegion;
+        for (uint64_t r = (a + kRegion - 1) / kRegion; r < r1; ++r) map[r] = (uint32_t)f;
+    }
+    if (f == n - 1) map[(total + kRegion - 1) / kRegion] = (uint32_t)(n - 1);
+}
+
 __global__ void __launch_bounds__(kThreads)
-finalize_kernel(cfws_frame_desc_t* __restrict__ desc, int32_t* __restrict__ status,
-                const uint64_t* __restrict__ offs, const uint64_t* __restrict__ grand,
-                uint64_t n, uint64_t capacity, uint32_t* __restrict__ tile_map,
-                uint64_t* __restrict__ ws_total, uint64_t* __restrict__ user_total)
+serialize_finalize_kernel(cfws_frame_desc_t* __restrict__ desc, const uint64_t* __restrict__ offs,
+                          uint64_t* __restrict__ hdr, uint64_t n, uint64_t capacity,
+                          uint32_t* __restrict__ map, uint64_t* __restrict__ user_total)
 {
     const uint64_t f = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
     if (f >= n) return;
-    const uint64_t g = *grand;
+    const uint64_t g = hdr[3];
     const uint64_t total = g < capacity ? g : capacity;
-    const uint64_t lo = offs[f];
-    const uint64_t hi_raw = (f + 1 < n) ? offs[f + 1] : g;
-    if (kSer) {
-        desc[f].wire_off = lo;
-    } else {
-        desc[f].payload_off = lo;
-        if (status[f] == CFWS_PARSE_COMPLETE && lo + desc[f].payload_size > capacity)
-            status[f] = CFWS_ERROR_OUT_OF_MEMORY;
-    }
-    const uint64_t a = lo < total ? lo : total;
-    const uint64_t b = hi_raw < total ? hi_raw : total;
-    if (b > a) {
-        const uint64_t t0 = (a + kTileBytes - 1) / kTileBytes;
-        const uint64_t t1 = (b + kTileBytes - 1) / kTileBytes;
-        for (uint64_t t = t0; t < t1; ++t) tile_map[t] = (uint32_t)f;
-    }
+    desc[f].wire_off = offs[f];
+    map_regions(offs, f, n, g, total, map);
     if (f == n - 1) {
-        tile_map[(total + kTileBytes - 1) / kTileBytes] = (uint32_t)(n - 1);
-        *ws_total = total;
-        if (user_total) *user_total = kSer ? g : total;
+        hdr[0] = total;
+        if (user_total) *user_total = g;
+    }
+}
+
+// Offsets into the descriptors, the capacity rule (a COMPLETE frame with a
+// payload that does not fit gets CFWS_ERROR_OUT_OF_MEMORY, like the
+// reference's failed malloc, co_ws_frame.c:216-223), region maps.
+__global__ void __launch_bounds__(kThreads)
+deserialize_finalize_kernel(cfws_frame_desc_t* __restrict__ desc, int32_t* __restrict__ status,
+                            const uint64_t* __restrict__ offs0, const uint64_t* __restrict__ offs1,
+                            uint64_t* __restrict__ hdr, uint64_t n, uint64_t capacity,
+                            uint32_t reassemble, uint32_t* __restrict__ map0,
+                            uint32_t* __restrict__ map1, uint64_t* __restrict__ user_total)
+{
+    const uint64_t f = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
+    if (f >= n) return;
+    const uint64_t g0 = hdr[3];
+    const uint64_t g1 = reassemble ? hdr[4] : 0;
+    const uint64_t t0 = g0 < capacity ? g0 : capacity;
+    const uint64_t room1 = capacity - t0;
+    const uint64_t t1 = g1 < room1 ? g1 : room1;
+    const bool ctl = reassemble && is_control(desc[f].opcode);
+    const uint64_t off = ctl ? g0 + offs1[f] : offs0[f];
+    desc[f].payload_off = off;
+    const uint64_t len = desc[f].payload_size;
+    if (status[f] == CFWS_PARSE_COMPLETE && len > 0 && off + len > capacity)
+        status[f] = CFWS_ERROR_OUT_OF_MEMORY;
+    map_regions(offs0, f, n, g0, t0, map0);
+    if (reassemble) map_regions(offs1, f, n, g1, t1, map1);
+    if (f == n - 1) {
+        hdr[0] = t0;
+        hdr[1] = t1;
+        hdr[2] = t0;
+        if (user_total) *user_total = t0 + t1;
     }
 }
 
@@ -634,7 +685,7 @@ xor_mask_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, uint
     if (aligned) {
         for (uint64_t i = tid; i < nv; i += stride) {
             uint4 v = reinterpret_cast<const uint4*>(src)[i];
-            v.x ^= kr; v.y ^= kr; v.z ^= kr; v.w ^= kr;
+            xor4(v, kr);
             reinterpret_cast<uint4*>(dst)[i] = v;
         }
         for (uint64_t i = nv * 16 + tid; i < n; i += stride)
@@ -679,7 +730,8 @@ int g_init_state = 0;   // 0 unknown, 1 ok, <0 error code
 
 int set_err(int code, const char* what, hipError_t e)
 {
-    snprintf(g_err, sizeof g_err, "%s: %s", what, e == hipSuccess ? "" : hipGetErrorString(e));
+    snprintf(g_err, sizeof g_err, "%s%s%s", what, e == hipSuccess ? "" : ": ",
+             e == hipSuccess ? "" : hipGetErrorString(e));
     fprintf(stderr, "cfws: %s\n", g_err);
     return code;
 }
@@ -751,6 +803,30 @@ int run_scan(uint64_t* vals, uint64_t n, uint64_t* partials, uint64_t* grand, hi
     return launch_check("scan");
 }
 
+bool misaligned(const void* a, const void* b)
+{
+    return ((reinterpret_cast<uintptr_t>(a) | reinterpret_cast<uintptr_t>(b)) & 15u) != 0;
+}
+
+int zero_totals(const WsLayout& L, void* ws, uint64_t* d_total, hipStream_t st)
+{
+    (void)hipMemsetAsync(ws_ptr<uint64_t>(ws, L.hdr), 0, 64, st);
+    if (d_total) (void)hipMemsetAsync(d_total, 0, 8, st);
+    return launch_check("zero totals");
+}
+
+template <bool kSer>
+void launch_pass(const WsLayout& L, int p, const void* src, void* dst, const cfws_frame_desc_t* desc,
+                 const int32_t* status, const void* ws, uint64_t cap, size_t n, uint32_t klass,
+                 hipStream_t st)
+{
+    const uint64_t* hdr = ws_ptr<const uint64_t>(ws, L.hdr);
+    xform_kernel<kSer><<<stream_grid(L.regions), kThreads, 0, st>>>(
+        static_cast<const uint8_t*>(src), static_cast<uint8_t*>(dst), desc, status,
+        ws_ptr<const uint64_t>(ws, L.offs[p]), ws_ptr<const uint32_t>(ws, L.map[p]), hdr + p,
+        p == 1 ? hdr + 2 : nullptr, cap, (uint32_t)n, klass);
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------
@@ -760,7 +836,7 @@ extern "C" {
 
 int cfws_init(void) { return check_init(); }
 const char* cfws_last_error(void) { return g_err; }
-const char* cfws_version(void) { return "cfws 0.1 gfx950"; }
+const char* cfws_version(void) { return "cfws 0.2 gfx950"; }
 
 size_t cfws_workspace_size(size_t n_frames, uint64_t out_capacity)
 {
@@ -775,20 +851,14 @@ int cfws_serialize_plan(cfws_frame_desc_t* d_desc, size_t n, uint64_t cap, uint6
     if (!ws || ws_size < L.bytes) return set_err(CFWS_ERROR_WORKSPACE, "workspace too small", hipSuccess);
     if (n > 0xffffffffull) return set_err(CFWS_ERROR_INVALID_ARGUMENT, "too many frames", hipSuccess);
     hipStream_t st = static_cast<hipStream_t>(stream);
-    if (n == 0) {
-        (void)hipMemsetAsync(ws_ptr<uint64_t>(ws, L.total), 0, 8, st);
-        if (d_total) (void)hipMemsetAsync(d_total, 0, 8, st);
-        return launch_check("serialize_plan(empty)");
-    }
+    if (n == 0) return zero_totals(L, ws, d_total, st);
     if (!d_desc) return set_err(CFWS_ERROR_INVALID_ARGUMENT, "null descriptor table", hipSuccess);
-    uint64_t* vals = ws_ptr<uint64_t>(ws, L.vals);
-    uint64_t* partials = ws_ptr<uint64_t>(ws, L.partials);
-    uint64_t* grand = partials + L.scan_blocks;
-    serialize_sizes_kernel<<<grid_for(n, kThreads), kThreads, 0, st>>>(d_desc, vals, n);
-    if (int rc = run_scan(vals, n, partials, grand, st)) return rc;
-    finalize_kernel<true><<<grid_for(n, kThreads), kThreads, 0, st>>>(
-        d_desc, nullptr, vals, grand, n, cap, ws_ptr<uint32_t>(ws, L.tile_map),
-        ws_ptr<uint64_t>(ws, L.total), d_total);
+    uint64_t* hdr = ws_ptr<uint64_t>(ws, L.hdr);
+    uint64_t* offs = ws_ptr<uint64_t>(ws, L.offs[0]);
+    serialize_sizes_kernel<<<grid_for(n, kThreads), kThreads, 0, st>>>(d_desc, offs, n);
+    if (int rc = run_scan(offs, n, ws_ptr<uint64_t>(ws, L.partials[0]), hdr + 3, st)) return rc;
+    serialize_finalize_kernel<<<grid_for(n, kThreads), kThreads, 0, st>>>(
+        d_desc, offs, hdr, n, cap, ws_ptr<uint32_t>(ws, L.map[0]), d_total);
     return launch_check("serialize_plan");
 }
 
@@ -799,14 +869,11 @@ int cfws_serialize_execute(const void* d_payload, const cfws_frame_desc_t* d_des
     if (n == 0 || cap == 0) return CFWS_OK;
     if (!d_payload || !d_desc || !d_wire || !ws)
         return set_err(CFWS_ERROR_INVALID_ARGUMENT, "null pointer", hipSuccess);
-    if ((reinterpret_cast<uintptr_t>(d_payload) | reinterpret_cast<uintptr_t>(d_wire)) & 15u)
+    if (misaligned(d_payload, d_wire))
         return set_err(CFWS_ERROR_INVALID_ARGUMENT, "arenas must be 16-byte aligned", hipSuccess);
     const WsLayout L = ws_layout(n, cap);
-    hipStream_t st = static_cast<hipStream_t>(stream);
-    xform_kernel<true><<<stream_grid(L.tiles_max), kThreads, 0, st>>>(
-        static_cast<const uint8_t*>(d_payload), static_cast<uint8_t*>(d_wire), d_desc, nullptr,
-        ws_ptr<const uint32_t>(ws, L.tile_map), ws_ptr<const uint64_t>(ws, L.total), cap,
-        (uint32_t)n);
+    launch_pass<true>(L, 0, d_payload, d_wire, d_desc, nullptr, ws, cap, n, kClassAll,
+                      static_cast<hipStream_t>(stream));
     return launch_check("serialize_execute");
 }
 
@@ -818,66 +885,69 @@ int cfws_serialize_batch(const void* d_payload, cfws_frame_desc_t* d_desc, size_
 }
 
 int cfws_deserialize_plan(const void* d_wire, uint64_t wire_size, const uint64_t* d_index,
-                          size_t n, uint64_t max_payload, uint32_t align,
+                          size_t n, uint64_t max_payload, uint32_t align, uint32_t flags,
                           cfws_frame_desc_t* d_desc, int32_t* d_status, uint64_t cap,
                           uint64_t* d_total, void* ws, size_t ws_size, void* stream)
 {
     if (int rc = check_init()) return rc;
     if (align == 0 || (align & (align - 1)) || align > 4096)
         return set_err(CFWS_ERROR_INVALID_ARGUMENT, "align must be a power of two <= 4096", hipSuccess);
+    if (flags & ~CFWS_DESERIALIZE_REASSEMBLE)
+        return set_err(CFWS_ERROR_INVALID_ARGUMENT, "unknown flags", hipSuccess);
     const WsLayout L = ws_layout(n, cap);
     if (!ws || ws_size < L.bytes) return set_err(CFWS_ERROR_WORKSPACE, "workspace too small", hipSuccess);
     if (n > 0xffffffffull) return set_err(CFWS_ERROR_INVALID_ARGUMENT, "too many frames", hipSuccess);
     hipStream_t st = static_cast<hipStream_t>(stream);
-    if (n == 0) {
-        (void)hipMemsetAsync(ws_ptr<uint64_t>(ws, L.total), 0, 8, st);
-        if (d_total) (void)hipMemsetAsync(d_total, 0, 8, st);
-        return launch_check("deserialize_plan(empty)");
-    }
+    if (n == 0) return zero_totals(L, ws, d_total, st);
     if (!d_wire || !d_index || !d_desc || !d_status)
         return set_err(CFWS_ERROR_INVALID_ARGUMENT, "null pointer", hipSuccess);
-    uint64_t* vals = ws_ptr<uint64_t>(ws, L.vals);
-    uint64_t* partials = ws_ptr<uint64_t>(ws, L.partials);
-    uint64_t* grand = partials + L.scan_blocks;
+    const uint32_t reasm = (flags & CFWS_DESERIALIZE_REASSEMBLE) ? 1u : 0u;
+    uint64_t* hdr = ws_ptr<uint64_t>(ws, L.hdr);
+    uint64_t* offs0 = ws_ptr<uint64_t>(ws, L.offs[0]);
+    uint64_t* offs1 = ws_ptr<uint64_t>(ws, L.offs[1]);
     deserialize_parse_kernel<<<grid_for(n, kThreads), kThreads, 0, st>>>(
-        static_cast<const uint8_t*>(d_wire), wire_size, d_index, n, max_payload, align, d_desc,
-        d_status, vals);
-    if (int rc = run_scan(vals, n, partials, grand, st)) return rc;
-    finalize_kernel<false><<<grid_for(n, kThreads), kThreads, 0, st>>>(
-        d_desc, d_status, vals, grand, n, cap, ws_ptr<uint32_t>(ws, L.tile_map),
-        ws_ptr<uint64_t>(ws, L.total), d_total);
+        static_cast<const uint8_t*>(d_wire), wire_size, d_index, n, max_payload, align, reasm,
+        d_desc, d_status, offs0, offs1);
+    if (int rc = run_scan(offs0, n, ws_ptr<uint64_t>(ws, L.partials[0]), hdr + 3, st)) return rc;
+    if (reasm)
+        if (int rc = run_scan(offs1, n, ws_ptr<uint64_t>(ws, L.partials[1]), hdr + 4, st)) return rc;
+    deserialize_finalize_kernel<<<grid_for(n, kThreads), kThreads, 0, st>>>(
+        d_desc, d_status, offs0, offs1, hdr, n, cap, reasm, ws_ptr<uint32_t>(ws, L.map[0]),
+        ws_ptr<uint32_t>(ws, L.map[1]), d_total);
     return launch_check("deserialize_plan");
 }
 
 int cfws_deserialize_execute(const void* d_wire, const cfws_frame_desc_t* d_desc,
-                             const int32_t* d_status, size_t n, void* d_payload, uint64_t cap,
-                             const void* ws, void* stream)
+                             const int32_t* d_status, size_t n, uint32_t flags, void* d_payload,
+                             uint64_t cap, const void* ws, void* stream)
 {
     if (int rc = check_init()) return rc;
     if (n == 0 || cap == 0) return CFWS_OK;
     if (!d_wire || !d_desc || !d_status || !d_payload || !ws)
         return set_err(CFWS_ERROR_INVALID_ARGUMENT, "null pointer", hipSuccess);
-    if ((reinterpret_cast<uintptr_t>(d_payload) | reinterpret_cast<uintptr_t>(d_wire)) & 15u)
+    if (misaligned(d_payload, d_wire))
         return set_err(CFWS_ERROR_INVALID_ARGUMENT, "arenas must be 16-byte aligned", hipSuccess);
     const WsLayout L = ws_layout(n, cap);
     hipStream_t st = static_cast<hipStream_t>(stream);
-    xform_kernel<false><<<stream_grid(L.tiles_max), kThreads, 0, st>>>(
-        static_cast<const uint8_t*>(d_wire), static_cast<uint8_t*>(d_payload), d_desc, d_status,
-        ws_ptr<const uint32_t>(ws, L.tile_map), ws_ptr<const uint64_t>(ws, L.total), cap,
-        (uint32_t)n);
+    if (flags & CFWS_DESERIALIZE_REASSEMBLE) {
+        launch_pass<false>(L, 0, d_wire, d_payload, d_desc, d_status, ws, cap, n, kClassData, st);
+        launch_pass<false>(L, 1, d_wire, d_payload, d_desc, d_status, ws, cap, n, kClassControl, st);
+    } else {
+        launch_pass<false>(L, 0, d_wire, d_payload, d_desc, d_status, ws, cap, n, kClassAll, st);
+    }
     return launch_check("deserialize_execute");
 }
 
 int cfws_deserialize_batch(const void* d_wire, uint64_t wire_size, const uint64_t* d_index,
-                           size_t n, uint64_t max_payload, uint32_t align,
+                           size_t n, uint64_t max_payload, uint32_t align, uint32_t flags,
                            cfws_frame_desc_t* d_desc, int32_t* d_status, void* d_payload,
                            uint64_t cap, uint64_t* d_total, void* ws, size_t ws_size,
                            void* stream)
 {
-    if (int rc = cfws_deserialize_plan(d_wire, wire_size, d_index, n, max_payload, align, d_desc,
-                                       d_status, cap, d_total, ws, ws_size, stream))
+    if (int rc = cfws_deserialize_plan(d_wire, wire_size, d_index, n, max_payload, align, flags,
+                                       d_desc, d_status, cap, d_total, ws, ws_size, stream))
         return rc;
-    return cfws_deserialize_execute(d_wire, d_desc, d_status, n, d_payload, cap, ws, stream);
+    return cfws_deserialize_execute(d_wire, d_desc, d_status, n, flags, d_payload, cap, ws, stream);
 }
 
 int cfws_xor_mask(const void* d_src, void* d_dst, uint64_t n, uint32_t key, uint32_t phase,

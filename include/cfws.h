@@ -100,26 +100,36 @@ int cfws_serialize_batch(const void* d_payload, cfws_frame_desc_t* d_desc,
 
 /* ---- deserialize (server unmask / client plain) --------------------------
  * plan:    parses the header at each d_frame_index[i] against wire_size,
- *          writes d_desc[i] and d_status[i] (reference codes), lays COMPLETE
- *          payloads out at payload_off = exclusive prefix sum of
- *          round_up(payload_size, align) (align a power of two, 1..4096);
- *          a COMPLETE frame whose payload does not fit payload_capacity gets
- *          CFWS_ERROR_OUT_OF_MEMORY. *d_payload_total = min(sum, capacity).
- * execute: copies + unmasks every COMPLETE payload; the bytes between one
- *          payload's end and the next payload_off are written as zero. */
+ *          writes d_desc[i] and d_status[i] (reference codes) and lays the
+ *          COMPLETE payloads out:
+ *            flags = 0: payload_off = exclusive prefix sum of
+ *              round_up(payload_size, align) (align a power of two, 1..4096);
+ *            flags = CFWS_DESERIALIZE_REASSEMBLE: data frames (opcode < 8)
+ *              packed back to back in stream order, so the fragments of every
+ *              message (TEXT/BINARY then CONTINUATION..., co_ws_frame.h:28-30)
+ *              are contiguous; control frames (opcode 8-15) packed after all
+ *              data bytes; align is ignored.
+ *          A COMPLETE frame with a non-empty payload that does not fit
+ *          payload_capacity gets CFWS_ERROR_OUT_OF_MEMORY (layout unchanged).
+ *          *d_payload_total = min(sum, capacity).
+ * execute: copies + unmasks every COMPLETE payload; bytes of the layout not
+ *          covered by a payload (alignment padding, OOM frames) are zero.
+ *          `flags` must be the plan's. */
+#define CFWS_DESERIALIZE_REASSEMBLE 1u
+
 int cfws_deserialize_plan(const void* d_wire, uint64_t wire_size,
                           const uint64_t* d_frame_index, size_t n_frames,
-                          uint64_t max_payload, uint32_t align,
+                          uint64_t max_payload, uint32_t align, uint32_t flags,
                           cfws_frame_desc_t* d_desc, int32_t* d_status,
                           uint64_t payload_capacity, uint64_t* d_payload_total,
                           void* d_workspace, size_t workspace_size, void* stream);
 int cfws_deserialize_execute(const void* d_wire, const cfws_frame_desc_t* d_desc,
-                             const int32_t* d_status, size_t n_frames,
+                             const int32_t* d_status, size_t n_frames, uint32_t flags,
                              void* d_payload, uint64_t payload_capacity,
                              const void* d_workspace, void* stream);
 int cfws_deserialize_batch(const void* d_wire, uint64_t wire_size,
                            const uint64_t* d_frame_index, size_t n_frames,
-                           uint64_t max_payload, uint32_t align,
+                           uint64_t max_payload, uint32_t align, uint32_t flags,
                            cfws_frame_desc_t* d_desc, int32_t* d_status,
                            void* d_payload, uint64_t payload_capacity,
                            uint64_t* d_payload_total, void* d_workspace,

@@ -68,7 +68,8 @@ def lib() -> C.CDLL:
         L.orc_keys.argtypes = [C.c_uint32, _sz, _vp, _vp]
         L.orc_serialize_batch.argtypes = [_vp, _vp, _sz, _vp]
         L.orc_serialize_batch.restype = _u64
-        L.orc_deserialize_batch.argtypes = [_vp, _u64, _vp, _sz, _u64, C.c_uint32, _vp, _vp, _vp, _u64]
+        L.orc_deserialize_batch.argtypes = [_vp, _u64, _vp, _sz, _u64, C.c_uint32, C.c_uint32,
+                                            _vp, _vp, _vp, _u64]
         L.orc_deserialize_batch.restype = _u64
         L.orc_index_frames.argtypes = [_vp, _u64, _u64, _vp, _sz, C.POINTER(_u64)]
         L.orc_index_frames.restype = _sz
@@ -114,8 +115,12 @@ def serialize_batch(payload: np.ndarray, desc: np.ndarray):
     return wire[:total], desc
 
 
+DESERIALIZE_REASSEMBLE = 1
+
+
 def deserialize_batch(wire: np.ndarray, starts: np.ndarray, align: int = 16,
-                      max_payload: int = DEFAULT_MAX_PAYLOAD, capacity: int | None = None):
+                      max_payload: int = DEFAULT_MAX_PAYLOAD, capacity: int | None = None,
+                      flags: int = 0):
     """Returns (payload arena, desc, status, total)."""
     starts = np.ascontiguousarray(starts, dtype=np.uint64)
     n = len(starts)
@@ -126,7 +131,8 @@ def deserialize_batch(wire: np.ndarray, starts: np.ndarray, align: int = 16,
     out = np.zeros(max(capacity, 1), dtype=np.uint8)
     w = wire if wire.size else np.zeros(1, np.uint8)
     total = lib().orc_deserialize_batch(_ptr(w), len(wire), _ptr(starts), n, max_payload,
-                                        align, _ptr(desc), _ptr(status), _ptr(out), capacity)
+                                        align, flags, _ptr(desc), _ptr(status), _ptr(out),
+                                        capacity)
     return out, desc, status, int(total)
 
 

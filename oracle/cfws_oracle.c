@@ -259,35 +259,56 @@ static int orc_parse_header(const uint8_t* w, uint64_t size, uint64_t start,
     return ORC_PARSE_COMPLETE;
 }
 
+static int orc_is_control(const orc_desc_t* d)
+{   /* co_ws_frame.h:32-34: opcodes 0x8-0xF are control frames */
+    return d->opcode <= 0x0f && (d->opcode & 0x08) != 0;
+}
+
 uint64_t orc_deserialize_batch(const uint8_t* wire, uint64_t wire_size,
                                const uint64_t* starts, size_t n,
-                               uint64_t max_payload, uint32_t align,
+                               uint64_t max_payload, uint32_t align, uint32_t flags,
                                orc_desc_t* d, int32_t* status,
                                uint8_t* payload, uint64_t cap)
 {
-    if (align == 0) align = 1;
+    const int reasm = (flags & ORC_DESERIALIZE_REASSEMBLE) != 0;
+    if (align == 0 || reasm) align = 1;
+    /* layout first: it depends only on the parse results */
     uint64_t off = 0;
     for (size_t i = 0; i < n; ++i) {
-        int st = orc_parse_header(wire, wire_size, starts[i], max_payload, &d[i]);
-        uint64_t len = (st == ORC_PARSE_COMPLETE) ? d[i].payload_size : 0;
-        /* the layout is fixed by the parse results; capacity only marks */
-        uint64_t next = off + (len + align - 1) / align * align;
-        if (st == ORC_PARSE_COMPLETE && off + len > cap) {
-            st = ORC_ERROR_OUT_OF_MEMORY;
+        status[i] = orc_parse_header(wire, wire_size, starts[i], max_payload, &d[i]);
+        int ok = status[i] == ORC_PARSE_COMPLETE && !(reasm && orc_is_control(&d[i]));
+        uint64_t len = ok ? d[i].payload_size : 0;
+        d[i].payload_off = off;
+        off += (len + align - 1) / align * align;
+    }
+    uint64_t data_total = off, ctrl = 0;
+    if (reasm) {
+        for (size_t i = 0; i < n; ++i) {
+            if (!orc_is_control(&d[i])) continue;
+            d[i].payload_off = data_total + ctrl;
+            if (status[i] == ORC_PARSE_COMPLETE) ctrl += d[i].payload_size;
+        }
+    }
+    uint64_t total = data_total + ctrl;
+    if (total > cap) total = cap;
+    /* then the bytes: payloads, zero padding, capacity rule */
+    for (size_t i = 0; i < n; ++i) {
+        uint64_t o = d[i].payload_off;
+        uint64_t len = status[i] == ORC_PARSE_COMPLETE ? d[i].payload_size : 0;
+        uint64_t span = reasm ? len : (len + align - 1) / align * align;
+        if (len && o + len > cap) {
+            status[i] = ORC_ERROR_OUT_OF_MEMORY;
             len = 0;
         }
-        status[i] = st;
-        d[i].payload_off = off;
         if (len) {
             const uint8_t* src = wire + starts[i] + d[i].header_size;
-            if (d[i].mask) orc_xor_bytes(payload + off, src, len, d[i].mask_key);
-            else memcpy(payload + off, src, (size_t)len);
+            if (d[i].mask) orc_xor_bytes(payload + o, src, len, d[i].mask_key);
+            else memcpy(payload + o, src, (size_t)len);
         }
-        uint64_t pad_end = next < cap ? next : cap;
-        if (pad_end > off + len) memset(payload + off + len, 0, (size_t)(pad_end - off - len));
-        off = next;
+        uint64_t end = o + span < cap ? o + span : cap;
+        if (end > o + len) memset(payload + o + len, 0, (size_t)(end - o - len));
     }
-    return off < cap ? off : cap;
+    return total;
 }
 
 size_t orc_index_frames(const uint8_t* wire, uint64_t size, uint64_t max_payload,

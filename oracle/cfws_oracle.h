@@ -97,11 +97,17 @@ uint64_t orc_serialize_batch(const uint8_t* payload, orc_desc_t* desc, size_t n,
  * wire_size, &starts[i]) preceded by the callers' 2-byte precheck
  * (co_ws_client.c:202-206). COMPLETE payloads are unmasked into `payload`
  * at offsets = exclusive scan of round_up(size, align); bytes between a
- * payload's end and the next offset are zero. A frame that does not fit
- * payload_capacity gets ORC_ERROR_OUT_OF_MEMORY. Returns total bytes. */
+ * payload's end and the next offset are zero. With
+ * ORC_DESERIALIZE_REASSEMBLE, data frames (opcode < 8) are packed with no
+ * padding in stream order -- every fragmented message (TEXT/BINARY +
+ * CONTINUATION..., co_ws_frame.h:28-30) comes out contiguous -- and control
+ * frames (opcode 8-15) are packed after all data bytes. A COMPLETE frame
+ * whose payload does not fit payload_capacity gets ORC_ERROR_OUT_OF_MEMORY
+ * (the layout is unchanged). Returns min(total, capacity). */
+#define ORC_DESERIALIZE_REASSEMBLE 1u
 uint64_t orc_deserialize_batch(const uint8_t* wire, uint64_t wire_size,
                                const uint64_t* starts, size_t n,
-                               uint64_t max_payload, uint32_t align,
+                               uint64_t max_payload, uint32_t align, uint32_t flags,
                                orc_desc_t* desc, int32_t* status,
                                uint8_t* payload, uint64_t payload_capacity);
 

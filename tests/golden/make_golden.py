@@ -184,6 +184,29 @@ def batch_digest(R, n_frames, frame_size, payload_seed, key_seed, chunk=1024):
                 wire_sha256=h.hexdigest(), payload_sha256=hp.hexdigest())
 
 
+def zipf_digest(R, target, seed, key_seed, ping_every=0):
+    """Config 3: the Zipf message/fragment schedule (coldforce_amd.workloads,
+    schedule only -- the keys come from the reference's own random() calls),
+    serialized frame by frame through the reference."""
+    from coldforce_amd import workloads as W
+    desc, msgs = W.zipf_batch(target, seed, key_seed, ping_every=ping_every)
+    arena_n = int(msgs["arena_bytes"])
+    arena = O.splitmix_words(seed, 0, (arena_n + 7) // 8).view(np.uint8)[:arena_n]
+    h = hashlib.sha256()
+    total = 0
+    O.srandom(R, key_seed)
+    for d in desc:
+        o, n = int(d["payload_off"]), int(d["payload_size"])
+        w = O.ref_serialize(R, bool(d["fin"]), int(d["opcode"]), True, arena[o:o + n].tobytes())
+        h.update(w)
+        total += len(w)
+    return dict(kind="zipf", target_bytes=target, seed=seed, key_seed=key_seed,
+                ping_every=ping_every, n_frames=len(desc), n_messages=len(msgs["len"]),
+                first_message_sizes=[int(x) for x in msgs["len"][:16]],
+                arena_bytes=arena_n, arena_sha256=hashlib.sha256(arena.tobytes()).hexdigest(),
+                wire_len=total, wire_sha256=h.hexdigest())
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--skip-full", action="store_true", help="skip the 4 GiB config-2 digest")
@@ -200,6 +223,10 @@ def main():
     if not a.skip_full:
         digests.append(batch_digest(R, 65536, 65536, 0x5EED0002, 2))
     dump("batch_digests.json", digests)
+    zipf = [zipf_digest(R, 64 << 20, 0x5EED0003, 3), zipf_digest(R, 8 << 20, 0x5EED0033, 33, ping_every=3)]
+    if not a.skip_full:
+        zipf.append(zipf_digest(R, 4 << 30, 0x5EED0003, 3))
+    dump("zipf_digests.json", zipf)
 
 
 if __name__ == "__main__":

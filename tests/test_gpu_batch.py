@@ -132,7 +132,7 @@ def test_serialize_capacity_truncation():
 
 
 def gpu_deserialize(wire: np.ndarray, starts: np.ndarray, align=16, capacity=None,
-                    max_payload=O.DEFAULT_MAX_PAYLOAD, plan_execute=False):
+                    max_payload=O.DEFAULT_MAX_PAYLOAD, plan_execute=False, flags=0):
     w = torch.from_numpy(np.concatenate([wire, np.zeros(16, np.uint8)])).cuda()
     idx = torch.from_numpy(starts.astype(np.int64)).cuda()
     cap = capacity if capacity is not None else len(wire) + 16 * len(starts) + 16
@@ -143,11 +143,12 @@ def gpu_deserialize(wire: np.ndarray, starts: np.ndarray, align=16, capacity=Non
         d_t = torch.empty((n, 32), dtype=torch.uint8, device="cuda")
         st_t = torch.empty(n, dtype=torch.int32, device="cuda")
         tot = torch.zeros(1, dtype=torch.int64, device="cuda")
-        cfws.deserialize_plan(w, len(wire), idx, d_t, st_t, cap, tot, ws, max_payload, align)
-        cfws.deserialize_execute(w, d_t, st_t, out, ws, cap)
+        cfws.deserialize_plan(w, len(wire), idx, d_t, st_t, cap, tot, ws, max_payload, align,
+                              flags=flags)
+        cfws.deserialize_execute(w, d_t, st_t, out, ws, cap, flags=flags)
     else:
         d_t, st_t, tot = cfws.deserialize(w, len(wire), idx, out[:cap], max_payload=max_payload,
-                                          align=align)
+                                          align=align, flags=flags)
     torch.cuda.synchronize()
     return out.cpu().numpy(), cfws.desc_from_device(d_t), st_t.cpu().numpy(), int(tot.item())
 
@@ -158,7 +159,7 @@ def check_deserialize(wire, starts, **kw):
     e_out, e_d, e_st, e_tot = O.deserialize_batch(wire, starts, align=kw.get("align", 16),
                                                   max_payload=kw.get("max_payload",
                                                                      O.DEFAULT_MAX_PAYLOAD),
-                                                  capacity=cap)
+                                                  capacity=cap, flags=kw.get("flags", 0))
     assert tot == e_tot
     assert np.array_equal(st, e_st)
     for f in ("payload_off", "wire_off", "payload_size", "mask_key", "fin", "opcode", "mask",
@@ -193,6 +194,30 @@ def test_deserialize_random_stream(align):
     for i, p in enumerate(payloads[:200]):
         o = int(d["payload_off"][i])
         assert out[o:o + len(p)].tobytes() == p
+
+
+@pytest.mark.parametrize("plan_execute", [False, True])
+def test_deserialize_reassemble(plan_execute):
+    """Fragmented messages with control frames interleaved (RFC 6455 5.4):
+    data payloads come out packed in stream order, controls after them."""
+    rng = random.Random(21 + plan_execute)
+    frames = []
+    for m in range(400):
+        nfrag = rng.randrange(1, 6)
+        for j in range(nfrag):
+            op = (rng.choice([1, 2]) if j == 0 else 0)
+            p = rng.randbytes(rng.choice([0, 1, 17, 125, 126, 4000, 70000]))
+            frames.append(O.serialize_keyed(j == nfrag - 1, op, rng.random() < .8,
+                                            rng.getrandbits(32), p))
+            if rng.random() < 0.2:
+                frames.append(O.serialize_keyed(True, rng.choice([8, 9, 10]), True,
+                                                rng.getrandbits(32), rng.randbytes(rng.randrange(126))))
+    wire = np.frombuffer(b"".join(frames), dtype=np.uint8).copy()
+    starts, _ = O.index_frames(wire, 100000)
+    check_deserialize(wire, starts, flags=1, plan_execute=plan_execute)
+    # errors and a tight capacity under reassembly
+    wire[int(starts[7])] |= 0x20
+    check_deserialize(wire, starts, flags=1, capacity=len(wire) // 3)
 
 
 def test_deserialize_error_frames():
