@@ -118,22 +118,6 @@ __device__ __forceinline__ DescWords load_desc(const cfws_frame_desc_t* __restri
     return DescWords{q[0], q[1], q[2], q[3]};
 }
 
-// Byte r of the serialized header (co_ws_frame.c:34-91).
-__device__ __forceinline__ uint32_t header_byte(const DescWords& d, uint32_t r)
-{
-    const uint64_t n = d.payload_size;
-    const uint32_t ext = n > 65535u ? 8u : (n > 125u ? 2u : 0u);
-    if (r == 0) return (d.opcode() | (d.fin() ? 0x80u : 0u)) & 0xffu;
-    if (r == 1) {
-        const uint32_t l7 = ext == 8 ? 127u : (ext == 2 ? 126u : (uint32_t)n);
-        return (l7 | (d.mask() ? 0x80u : 0u)) & 0xffu;
-    }
-    r -= 2;
-    if (r < ext) return (uint32_t)(n >> (8 * (ext - 1 - r))) & 0xffu;
-    r -= ext;
-    return (d.key() >> (8 * r)) & 0xffu;
-}
-
 // Arguments of one streaming pass.
 struct Pass {
     const uint8_t* src;
@@ -158,7 +142,21 @@ struct FrameView {
     uint64_t src_off;
     uint32_t key;   // 0 when the frame is not masked: XOR becomes a copy
     uint32_t pre;
+    uint32_t hb;    // serialize: header byte 0 | mask bit << 8
 };
+
+// Byte r < pre of a serialize frame's header, from its view (co_ws_frame.c:34-91).
+__device__ __forceinline__ uint32_t view_header_byte(const FrameView& v, uint32_t r)
+{
+    const uint64_t n = v.body_len;
+    const uint32_t ext = n > 65535u ? 8u : (n > 125u ? 2u : 0u);
+    const uint32_t l7 = ext == 8 ? 127u : (ext == 2 ? 126u : (uint32_t)n);
+    const uint32_t key_b = (v.key >> (8 * ((r - 2 - ext) & 3u))) & 0xffu;
+    const uint32_t len_b = (uint32_t)(n >> (8 * ((ext - 1 - (r - 2)) & 7u))) & 0xffu;
+    return r == 0 ? (v.hb & 0xffu)
+         : r == 1 ? ((l7 | ((v.hb >> 1) & 0x80u)) & 0xffu)
+         : (r - 2 < ext) ? len_b : key_b;
+}
 
 template <bool kSer>
 __device__ __forceinline__ FrameView frame_view(const Pass& P, uint32_t f)
@@ -167,10 +165,12 @@ __device__ __forceinline__ FrameView frame_view(const Pass& P, uint32_t f)
     FrameView v;
     v.key = d.mask() ? d.key() : 0u;
     v.out_off = P.offs[f];
+    v.hb = 0;
     if (kSer) {
         v.pre = d.header_size();
         v.body_len = d.payload_size;
         v.src_off = d.payload_off;
+        v.hb = ((d.opcode() | (d.fin() ? 0x80u : 0u)) & 0xffu) | (d.mask() ? 0x100u : 0u);
     } else {
         const bool ctl = is_control(d.opcode());
         const bool take = P.klass == kClassAll || (P.klass == kClassControl) == ctl;
@@ -250,10 +250,20 @@ __device__ __forceinline__ uint4 body_chunk(const uint8_t* __restrict__ src, con
     return o;
 }
 
-// A chunk that crosses a header, a frame boundary, padding or the end of
-// the pass: built byte by byte, walking frames forward from f.
+// Byte idx (0..31) of the 32-byte window {A, B}, without dynamic register
+// indexing (which would go to scratch).
+__device__ __forceinline__ uint32_t window_byte(const uint4& A, const uint4& B, uint32_t idx)
+{
+    const bool q1 = (idx & 4u) != 0, q2 = (idx & 8u) != 0;
+    const uint32_t a = q2 ? (q1 ? A.w : A.z) : (q1 ? A.y : A.x);
+    const uint32_t b = q2 ? (q1 ? B.w : B.z) : (q1 ? B.y : B.x);
+    return (((idx & 16u) ? b : a) >> (8 * (idx & 3u))) & 0xffu;
+}
+
+// Slow fallback: byte by byte, walking frames forward from f (chunks that
+// hold more than two frames: runs of frames shorter than ~14 bytes).
 template <bool kSer>
-__device__ __noinline__ uint4 edge_chunk(const Pass& P, uint32_t f, uint64_t D)
+__device__ __noinline__ uint4 edge_chunk_bytes(const Pass P, uint32_t f, uint64_t D)
 {
     FrameView v = frame_view<kSer>(P, f);
     uint64_t next = (f + 1 < P.n_frames) ? P.offs[f + 1] : ~uint64_t(0);
@@ -270,12 +280,79 @@ __device__ __noinline__ uint4 edge_chunk(const Pass& P, uint32_t f, uint64_t D)
             }
             const uint64_t r = pos - v.out_off;
             if (r < v.pre) {
-                b = header_byte(load_desc(P.desc, f), (uint32_t)r);
+                b = view_header_byte(v, (uint32_t)r);
             } else {
                 const uint64_t k = r - v.pre;
                 if (k < v.body_len) b = (P.src[v.src_off + k] ^ (v.key >> (8 * (k & 3u)))) & 0xffu;
             }
         }
+        const uint32_t sh = 8 * (j & 3);
+        if (j < 4) w0 |= b << sh;
+        else if (j < 8) w1 |= b << sh;
+        else if (j < 12) w2 |= b << sh;
+        else w3 |= b << sh;
+    }
+    return make_uint4(w0, w1, w2, w3);
+}
+
+// Where frame v's body overlaps [D, lim): the aligned source block holding
+// the first overlapping byte (and the next one when the overlap spans two).
+// Only blocks that hold a valid source byte are read.
+__device__ __forceinline__ void edge_blocks(const uint8_t* __restrict__ src, const FrameView& v,
+                                            uint64_t D, uint64_t lim, uint4& A, uint4& B,
+                                            uint64_t& abase)
+{
+    const uint64_t be = v.body_start + v.body_len;
+    const uint64_t lo = D > v.body_start ? D : v.body_start;
+    const uint64_t hi = lim < be ? lim : be;
+    abase = 0;
+    if (hi > lo) {
+        const uint64_t s_first = v.src_off + (lo - v.body_start);
+        const uint64_t s_last = v.src_off + (hi - 1 - v.body_start);
+        abase = s_first & ~uint64_t(15);
+        A = ld16(src + abase);
+        B = ((s_last & ~uint64_t(15)) != abase) ? ld16(src + abase + 16) : A;
+    }
+}
+
+// Byte at output position pos of frame v (pos inside v's output range).
+__device__ __forceinline__ uint32_t edge_byte(const FrameView& v, uint64_t pos, const uint4& A,
+                                              const uint4& B, uint64_t abase)
+{
+    const uint64_t r = pos - v.out_off;
+    if (r < v.pre) return view_header_byte(v, (uint32_t)r);
+    const uint64_t k = r - v.pre;
+    if (k >= v.body_len) return 0;
+    const uint32_t idx = (uint32_t)(v.src_off + k - abase);
+    return (window_byte(A, B, idx) ^ (v.key >> (8 * (k & 3u)))) & 0xffu;
+}
+
+// A chunk that crosses a header, a frame boundary, padding or the end of
+// the pass. With at most two frames in it (every boundary of frames larger
+// than the chunk) all source blocks are loaded up front and the bytes are
+// assembled in registers: one memory round trip instead of sixteen.
+template <bool kSer>
+__device__ __noinline__ uint4 edge_chunk(const Pass P, uint32_t f, uint64_t D)
+{
+    const uint64_t lim = D + 16 < P.total ? D + 16 : P.total;
+    const uint64_t o1 = (f + 1 < P.n_frames) ? P.offs[f + 1] : ~uint64_t(0);
+    const uint64_t o2 = (f + 2 < P.n_frames) ? P.offs[f + 2] : ~uint64_t(0);
+    if (o2 < lim) return edge_chunk_bytes<kSer>(P, f, D);
+    const FrameView va = frame_view<kSer>(P, f);
+    const bool two = o1 < lim;
+    FrameView vb = va;
+    if (two) vb = frame_view<kSer>(P, f + 1);
+    uint4 Aa = make_uint4(0, 0, 0, 0), Ba = Aa, Ab = Aa, Bb = Aa;
+    uint64_t ba = 0, bb = 0;
+    edge_blocks(P.src, va, D, lim, Aa, Ba, ba);
+    if (two) edge_blocks(P.src, vb, D, lim, Ab, Bb, bb);
+    uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        const uint64_t pos = D + j;
+        uint32_t b = 0;
+        if (pos < lim)
+            b = (two && pos >= o1) ? edge_byte(vb, pos, Ab, Bb, bb) : edge_byte(va, pos, Aa, Ba, ba);
         const uint32_t sh = 8 * (j & 3);
         if (j < 4) w0 |= b << sh;
         else if (j < 8) w1 |= b << sh;
@@ -337,12 +414,11 @@ __device__ __forceinline__ void fast_region(const Pass& P, const FrameView& v, u
 
 // A region crossed by exactly one frame boundary (the boundary case of large
 // frames): both views are wave-uniform, each lane picks one by comparing its
-// chunk with the boundary; only chunks holding the boundary or header bytes
-// go byte-wise.
+// chunk with the boundary. Chunks not entirely inside a body are left to
+// edge_kernel.
 template <bool kSer>
 __device__ __forceinline__ void two_frame_region(const Pass& P, const FrameView& va,
-                                                 const FrameView& vb, uint32_t fa,
-                                                 uint64_t base, uint32_t lane)
+                                                 const FrameView& vb, uint64_t base, uint32_t lane)
 {
     uint4 a[kUnroll], b[kUnroll];
     bool fast[kUnroll];
@@ -362,46 +438,49 @@ __device__ __forceinline__ void two_frame_region(const Pass& P, const FrameView&
     }
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u) {
+        if (!fast[u]) continue;
         const uint64_t D = base + u * kSlice + lane * kChunk;
-        if (D >= P.total) continue;
         const bool hi = D >= vb.out_off;
-        if (fast[u]) {
-            const uint64_t k0 = D - (hi ? vb.body_start : va.body_start);
-            const uint32_t ph = (uint32_t)(((hi ? vb.src_off : va.src_off) + k0) & 15u);
-            uint4 o = ph ? funnel16(a[u], b[u], ph) : a[u];
-            xor4(o, rotr8(hi ? vb.key : va.key, (uint32_t)(k0 & 3u)));
-            st16(P.dst + D, o);
-        } else {
-            store_chunk(P, D, edge_chunk<kSer>(P, hi ? fa + 1 : fa, D));
-        }
+        const uint64_t k0 = D - (hi ? vb.body_start : va.body_start);
+        const uint32_t ph = (uint32_t)(((hi ? vb.src_off : va.src_off) + k0) & 15u);
+        uint4 o = ph ? funnel16(a[u], b[u], ph) : a[u];
+        xor4(o, rotr8(hi ? vb.key : va.key, (uint32_t)(k0 & 3u)));
+        st16(P.dst + D, o);
     }
 }
 
 // Any other region (small frames, padding, pass end): every lane finds the
-// frame of each of its chunks by binary search over the region's frames.
+// frame of each of its chunks by binary search over the region's frames and
+// writes it when it lies inside that frame's body.
 template <bool kSer>
-__device__ __noinline__ void general_region(const Pass& P, uint32_t f0, uint32_t f1,
-                                            uint64_t base, uint32_t lane)
+__device__ __forceinline__ void general_region(const Pass& P, uint32_t f0, uint32_t f1,
+                                               uint64_t base, uint32_t lane)
 {
-#pragma unroll 1
+    uint32_t fr[kUnroll];
+#pragma unroll
     for (int u = 0; u < kUnroll; ++u) {
         const uint64_t D = base + u * kSlice + lane * kChunk;
-        if (D >= P.total) continue;
         uint32_t lo = f0, hi = f1;                  // largest f with offs[f] <= D
         while (lo < hi) {
             const uint32_t mid = (lo + hi + 1) >> 1;
             if (P.offs[mid] <= D) lo = mid; else hi = mid - 1;
         }
-        const FrameView v = frame_view<kSer>(P, lo);
-        const uint4 o = (D >= v.body_start && D + kChunk <= v.body_start + v.body_len)
-                            ? body_chunk(P.src, v, D)
-                            : edge_chunk<kSer>(P, lo, D);
-        store_chunk(P, D, o);
+        fr[u] = lo;
+    }
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+        const uint64_t D = base + u * kSlice + lane * kChunk;
+        const FrameView v = frame_view<kSer>(P, fr[u]);
+        if (D >= v.body_start && D + kChunk <= v.body_start + v.body_len)
+            st16(P.dst + D, body_chunk(P.src, v, D));
     }
 }
 
-// serialize (kSer): header + (masked) payload into the wire arena;
-// deserialize: copy + unmask into the payload arena.
+// The streaming kernel: serialize (kSer) = header + (masked) payload into
+// the wire arena; deserialize = copy + unmask into the payload arena. It
+// writes every 16-byte chunk that lies inside one frame's body; the chunks
+// holding headers, boundaries, padding or the pass end belong to
+// edge_kernel. Both read the same plan; their chunk sets are disjoint.
 template <bool kSer>
 __global__ void __launch_bounds__(kThreads)
 xform_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
@@ -440,15 +519,61 @@ xform_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
         if (f1 > f0 && offs[f0 + 1] >= end) f1 = f0;
         const FrameView va = frame_view<kSer>(P, f0);
         if (f0 == f1) {
-            if (base >= va.body_start && end <= va.body_start + va.body_len) {
+            if (base >= va.body_start && end <= va.body_start + va.body_len)
                 fast_region(P, va, base, lane);
-                continue;
-            }
+            else
+                two_frame_region<kSer>(P, va, va, base, lane);   // partial body, one frame
         } else if (f1 == f0 + 1 || offs[f0 + 2] >= end) {
-            two_frame_region<kSer>(P, va, frame_view<kSer>(P, f0 + 1), f0, base, lane);
-            continue;
+            two_frame_region<kSer>(P, va, frame_view<kSer>(P, f0 + 1), base, lane);
+        } else {
+            general_region<kSer>(P, f0, f1, base, lane);
         }
-        general_region<kSer>(P, f0, f1, base, lane);
+    }
+}
+
+// One thread per frame: the 16-byte chunks that START inside the frame's
+// output range and do not lie entirely inside its body -- header chunks,
+// the chunk that crosses into the next frame, padding, the pass end.
+template <bool kSer>
+__global__ void __launch_bounds__(kThreads)
+edge_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+            const cfws_frame_desc_t* __restrict__ desc, const int32_t* __restrict__ status,
+            const uint64_t* __restrict__ offs, const uint64_t* __restrict__ total_p,
+            const uint64_t* __restrict__ base_p, uint64_t capacity, uint32_t n_frames,
+            uint32_t klass)
+{
+    const uint64_t f = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
+    if (f >= n_frames) return;
+    const uint64_t out_base = base_p ? *base_p : 0;
+    Pass P;
+    P.src = src;
+    P.dst = dst + out_base;
+    P.desc = desc;
+    P.status = status;
+    P.offs = offs;
+    P.total = *total_p;
+    P.capacity = capacity - out_base;
+    P.n_frames = n_frames;
+    P.klass = klass;
+    const uint64_t lo = offs[f];
+    uint64_t hi = (f + 1 < n_frames) ? offs[f + 1] : P.total;
+    if (hi > P.total) hi = P.total;
+    if (lo >= hi) return;
+    const FrameView v = frame_view<kSer>(P, (uint32_t)f);
+    const uint64_t be = v.body_start + v.body_len;
+    const uint64_t first = (lo + 15) & ~uint64_t(15);
+    // chunks before the body (headers): D < body_start
+    for (uint64_t D = first; D < hi && D < v.body_start; D += 16)
+        store_chunk(P, D, edge_chunk<kSer>(P, (uint32_t)f, D));
+    // chunks reaching past the body end (boundary, padding, pass end)
+    uint64_t t = be >= 15 ? ((be - 15 + 15) & ~uint64_t(15)) : 0;   // first D with D + 16 > be
+    if (t < first) t = first;
+    if (t < v.body_start) t = (v.body_start + 15) & ~uint64_t(15);  // header chunks done above
+    for (uint64_t D = t; D < hi; D += 16) {
+        if (D >= be && D + 16 <= hi)          // pure alignment padding / OOM body
+            store_chunk(P, D, make_uint4(0, 0, 0, 0));
+        else
+            store_chunk(P, D, edge_chunk<kSer>(P, (uint32_t)f, D));
     }
 }
 
@@ -815,16 +940,38 @@ int zero_totals(const WsLayout& L, void* ws, uint64_t* d_total, hipStream_t st)
     return launch_check("zero totals");
 }
 
+// Dynamic LDS the streaming kernel reserves per workgroup. It is never
+// touched: it only caps residency at 6 workgroups (24 waves) per CU. At the
+// register-limited 8 workgroups per CU the kernel ran 8-12 % slower (more
+// streams contending for HBM pages); 6 measured best on config 2 and 3
+// (sweep 3..8 per CU, tools/envab.sh). CFWS_XFORM_LDS overrides (0 = none).
+constexpr uint32_t kXformLdsDefault = 27000;     // 53 x 512 B granules; 6 x fits 160 KiB
+
+uint32_t xform_lds_bytes()
+{
+    static int64_t v = -1;
+    if (v < 0) {
+        const char* s = getenv("CFWS_XFORM_LDS");
+        v = s ? (int64_t)strtoull(s, nullptr, 10) : kXformLdsDefault;
+        if (v > 65536) v = 65536;
+    }
+    return (uint32_t)v;
+}
+
 template <bool kSer>
 void launch_pass(const WsLayout& L, int p, const void* src, void* dst, const cfws_frame_desc_t* desc,
                  const int32_t* status, const void* ws, uint64_t cap, size_t n, uint32_t klass,
                  hipStream_t st)
 {
     const uint64_t* hdr = ws_ptr<const uint64_t>(ws, L.hdr);
-    xform_kernel<kSer><<<stream_grid(L.regions), kThreads, 0, st>>>(
+    xform_kernel<kSer><<<stream_grid(L.regions), kThreads, xform_lds_bytes(), st>>>(
         static_cast<const uint8_t*>(src), static_cast<uint8_t*>(dst), desc, status,
         ws_ptr<const uint64_t>(ws, L.offs[p]), ws_ptr<const uint32_t>(ws, L.map[p]), hdr + p,
         p == 1 ? hdr + 2 : nullptr, cap, (uint32_t)n, klass);
+    edge_kernel<kSer><<<grid_for(n, kThreads), kThreads, 0, st>>>(
+        static_cast<const uint8_t*>(src), static_cast<uint8_t*>(dst), desc, status,
+        ws_ptr<const uint64_t>(ws, L.offs[p]), hdr + p, p == 1 ? hdr + 2 : nullptr, cap,
+        (uint32_t)n, klass);
 }
 
 }  // namespace
