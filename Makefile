@@ -7,8 +7,9 @@
 HIPCC    ?= /opt/rocm/bin/hipcc
 ARCH     ?= gfx950
 HIPFLAGS ?= -O3 -std=c++17 -fPIC -Wall -Wno-unused-result
-SRC      := coldforce_amd/csrc/cfws_device.hip coldforce_amd/csrc/cfws_frame.cpp
-HDR      := include/cfws.h include/cfws_co_ws_frame.h
+SRC      := coldforce_amd/csrc/cfws_device.hip coldforce_amd/csrc/cfws_frame.cpp \
+            coldforce_amd/csrc/cfws_pipeline.cpp
+HDR      := include/cfws.h include/cfws_co_ws_frame.h coldforce_amd/csrc/cfws_internal.h
 LIB      := coldforce_amd/libcfws.so
 OBJDIR   := build
 
@@ -16,13 +17,17 @@ all: $(LIB) oracle
 
 $(OBJDIR)/cfws_device.o: coldforce_amd/csrc/cfws_device.hip $(HDR)
 	@mkdir -p $(OBJDIR)
-	$(HIPCC) --offload-arch=$(ARCH) $(HIPFLAGS) -Iinclude -c $< -o $@
+	$(HIPCC) --offload-arch=$(ARCH) $(HIPFLAGS) -Iinclude -Icoldforce_amd/csrc -c $< -o $@
 
 $(OBJDIR)/cfws_frame.o: coldforce_amd/csrc/cfws_frame.cpp $(HDR)
 	@mkdir -p $(OBJDIR)
-	$(HIPCC) --offload-arch=$(ARCH) $(HIPFLAGS) -Iinclude -c $< -o $@
+	$(HIPCC) --offload-arch=$(ARCH) $(HIPFLAGS) -Iinclude -Icoldforce_amd/csrc -c $< -o $@
 
-$(LIB): $(OBJDIR)/cfws_device.o $(OBJDIR)/cfws_frame.o
+$(OBJDIR)/cfws_pipeline.o: coldforce_amd/csrc/cfws_pipeline.cpp $(HDR)
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) --offload-arch=$(ARCH) $(HIPFLAGS) -Iinclude -Icoldforce_amd/csrc -c $< -o $@
+
+$(LIB): $(OBJDIR)/cfws_device.o $(OBJDIR)/cfws_frame.o $(OBJDIR)/cfws_pipeline.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $^
 
 oracle:
@@ -33,7 +38,7 @@ ref: all
 
 asm: coldforce_amd/csrc/cfws_device.hip $(HDR)
 	@mkdir -p $(OBJDIR)/asm
-	$(HIPCC) --offload-arch=$(ARCH) $(HIPFLAGS) -Iinclude -c $< -o $(OBJDIR)/asm/cfws_device.o \
+	$(HIPCC) --offload-arch=$(ARCH) $(HIPFLAGS) -Iinclude -Icoldforce_amd/csrc -c $< -o $(OBJDIR)/asm/cfws_device.o \
 	    -save-temps=obj -Rpass-analysis=kernel-resource-usage 2> $(OBJDIR)/asm/resource-usage.txt
 
 clean:
@@ -45,8 +50,9 @@ clean:
 # A/B build variants (kept out of git under build/): make variant V=nt F="-DCFWS_NT_STORE"
 variant: $(HDR)
 	@mkdir -p $(OBJDIR)/variants/$(V)
-	$(HIPCC) --offload-arch=$(ARCH) $(HIPFLAGS) $(F) -Iinclude -c coldforce_amd/csrc/cfws_device.hip -o $(OBJDIR)/variants/$(V)/cfws_device.o
-	$(HIPCC) --offload-arch=$(ARCH) $(HIPFLAGS) $(F) -Iinclude -c coldforce_amd/csrc/cfws_frame.cpp -o $(OBJDIR)/variants/$(V)/cfws_frame.o
-	$(HIPCC) --offload-arch=$(ARCH) -shared -o $(OBJDIR)/variants/libcfws_$(V).so $(OBJDIR)/variants/$(V)/cfws_device.o $(OBJDIR)/variants/$(V)/cfws_frame.o
+	$(HIPCC) --offload-arch=$(ARCH) $(HIPFLAGS) $(F) -Iinclude -Icoldforce_amd/csrc -c coldforce_amd/csrc/cfws_device.hip -o $(OBJDIR)/variants/$(V)/cfws_device.o
+	$(HIPCC) --offload-arch=$(ARCH) $(HIPFLAGS) $(F) -Iinclude -Icoldforce_amd/csrc -c coldforce_amd/csrc/cfws_frame.cpp -o $(OBJDIR)/variants/$(V)/cfws_frame.o
+	$(HIPCC) --offload-arch=$(ARCH) $(HIPFLAGS) $(F) -Iinclude -Icoldforce_amd/csrc -c coldforce_amd/csrc/cfws_pipeline.cpp -o $(OBJDIR)/variants/$(V)/cfws_pipeline.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o $(OBJDIR)/variants/libcfws_$(V).so $(OBJDIR)/variants/$(V)/cfws_device.o $(OBJDIR)/variants/$(V)/cfws_frame.o $(OBJDIR)/variants/$(V)/cfws_pipeline.o
 
 .PHONY: variant

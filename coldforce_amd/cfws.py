@@ -46,7 +46,8 @@ BATCH_SYMBOLS = (
     "cfws_serialize_plan", "cfws_serialize_execute", "cfws_serialize_batch",
     "cfws_deserialize_plan", "cfws_deserialize_execute", "cfws_deserialize_batch",
     "cfws_xor_mask", "cfws_draw_mask_keys", "cfws_release_thread_resources",
-    "cfws_fill_splitmix",
+    "cfws_fill_splitmix", "cfws_pipeline_create", "cfws_pipeline_destroy",
+    "cfws_pipeline_serialize", "cfws_pipeline_deserialize",
 )
 DROPIN_SYMBOLS = (
     "co_ws_frame_serialize", "co_ws_frame_deserialize", "co_ws_frame_create",
@@ -106,6 +107,11 @@ def lib(path: str = LIB_PATH) -> C.CDLL:
         "cfws_draw_mask_keys": ([_sz, _vp, _vp], None),
         "cfws_release_thread_resources": ([], None),
         "cfws_fill_splitmix": ([_vp, _u64, _u64, _u64, _vp], C.c_int),
+        "cfws_pipeline_create": ([_u64, _sz, C.c_int, C.POINTER(_vp)], C.c_int),
+        "cfws_pipeline_destroy": ([_vp], None),
+        "cfws_pipeline_serialize": ([_vp, _vp, _vp, _sz, _vp, _u64, C.POINTER(_u64)], C.c_int),
+        "cfws_pipeline_deserialize": ([_vp, _vp, _u64, _vp, _sz, _u64, _u32, _u32, _vp, _vp, _vp,
+                                       _u64, C.POINTER(_u64)], C.c_int),
         "co_ws_frame_serialize": ([C.c_bool, C.c_uint8, C.c_bool, _vp, _sz, C.POINTER(CoArray)],
                                   C.c_bool),
         "co_ws_frame_deserialize": ([C.POINTER(CoWsFrame), _vp, _sz, C.POINTER(C.c_size_t)],
@@ -328,3 +334,49 @@ def frame_deserialize(data: bytes, index: int = 0):
                payload_size=fr.header.payload_size, payload=payload)
     L.co_ws_frame_destroy(f)
     return out
+
+
+# ---- host-memory pipeline --------------------------------------------------
+
+class Pipeline:
+    """cfws_pipeline_*: the codec over host buffers (pinned numpy/torch
+    memory recommended), H2D / kernels / D2H overlapped across `depth` slots."""
+
+    def __init__(self, chunk_bytes: int = 64 << 20, max_frames: int = 1 << 18, depth: int = 3):
+        h = C.c_void_p()
+        _check(lib().cfws_pipeline_create(chunk_bytes, max_frames, depth, C.byref(h)),
+               "cfws_pipeline_create")
+        self.h = h
+
+    def close(self):
+        if self.h:
+            lib().cfws_pipeline_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def serialize(self, payload_ptr: int, desc: np.ndarray, wire_ptr: int, wire_capacity: int) -> int:
+        """desc: host DESC_DTYPE array (wire_off/header_size filled in place)."""
+        tot = C.c_uint64()
+        _check(lib().cfws_pipeline_serialize(self.h, payload_ptr, desc.ctypes.data, len(desc),
+                                             wire_ptr, wire_capacity, C.byref(tot)),
+               "cfws_pipeline_serialize")
+        return tot.value
+
+    def deserialize(self, wire_ptr: int, wire_size: int, index: np.ndarray, payload_ptr: int,
+                    payload_capacity: int, align: int = 16, max_payload: int = DEFAULT_MAX_PAYLOAD):
+        """Returns (desc, status, total)."""
+        index = np.ascontiguousarray(index, dtype=np.uint64)
+        desc = np.zeros(len(index), dtype=DESC_DTYPE)
+        status = np.zeros(len(index), dtype=np.int32)
+        tot = C.c_uint64()
+        _check(lib().cfws_pipeline_deserialize(self.h, wire_ptr, wire_size, index.ctypes.data,
+                                               len(index), max_payload, align, 0,
+                                               desc.ctypes.data, status.ctypes.data, payload_ptr,
+                                               payload_capacity, C.byref(tot)),
+               "cfws_pipeline_deserialize")
+        return desc, status, tot.value

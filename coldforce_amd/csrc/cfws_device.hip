@@ -33,6 +33,7 @@
 #include <string.h>
 
 #include "cfws.h"
+#include "cfws_internal.h"
 
 namespace {
 
@@ -975,6 +976,8 @@ void launch_pass(const WsLayout& L, int p, const void* src, void* dst, const cfw
 }
 
 }  // namespace
+
+uint64_t cfws_internal_grand_total_offset() { return ws_layout(0, 0).hdr + 3 * sizeof(uint64_t); }
 
 // ---------------------------------------------------------------------------
 // C ABI

@@ -1,0 +1,314 @@
+// cfws_pipeline.cpp -- host-memory batch codec (include/cfws.h, cfws_pipeline_*).
+//
+// coldforce's frames start and end in host memory: socket receive buffers
+// (co_tcp_receive_all, src/net/co_tcp_client.c:695-721) and send buffers
+// (co_ws_send -> module.send, src/ws/co_ws_client.c:427-460). This pipeline
+// runs the device batch codec over host buffers: the batch is cut into
+// chunks of frames, and `depth` slots, each with its own stream and device
+// staging, overlap H2D copies, the plan + streaming kernels and D2H copies of
+// consecutive chunks (the two DMA directions run concurrently). The host
+// buffers should be pinned (hipHostMalloc / hipHostRegister) for full PCIe
+// rate. All codec decisions (header encode/decode, layout, status codes) are
+// the device plan's; the host only cuts chunks and rebases offsets.
+#include <hip/hip_runtime.h>
+
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "cfws.h"
+#include "cfws_internal.h"
+
+namespace {
+
+constexpr int kMaxDepth = 4;
+
+struct Slot {
+    hipStream_t st = nullptr;
+    void* d_in = nullptr;              // chunk source (payload or wire)
+    void* d_out = nullptr;             // chunk output
+    cfws_frame_desc_t* d_desc = nullptr;
+    int32_t* d_status = nullptr;
+    uint64_t* d_index = nullptr;
+    uint64_t* d_total = nullptr;
+    void* d_ws = nullptr;
+    size_t ws_size = 0;
+    void* h_stage = nullptr;           // pinned: descriptors / index / status staging
+    uint64_t* h_total = nullptr;       // pinned
+    hipEvent_t ev_done = nullptr;      // slot free again (its last D2H finished)
+    hipEvent_t ev_total = nullptr;     // the chunk's layout total is on the host
+};
+
+uint32_t hdr_size(uint64_t n, bool mask)
+{
+    return 2u + (n > 65535u ? 8u : (n > 125u ? 2u : 0u)) + (mask ? 4u : 0u);
+}
+
+int fail(const char* what, hipError_t e = hipSuccess)
+{
+    fprintf(stderr, "cfws pipeline: %s%s%s\n", what, e == hipSuccess ? "" : ": ",
+            e == hipSuccess ? "" : hipGetErrorString(e));
+    return e == hipSuccess ? CFWS_ERROR_INVALID_ARGUMENT : CFWS_ERROR_HIP;
+}
+
+#define CFWS_HIP(call)                                   \
+    do {                                                 \
+        hipError_t e_ = (call);                          \
+        if (e_ != hipSuccess) return fail(#call, e_);    \
+    } while (0)
+
+}  // namespace
+
+struct cfws_pipeline {
+    int depth = 0;
+    uint64_t chunk = 0;        // staging bytes per slot and direction
+    size_t max_frames = 0;     // frames per chunk
+    Slot slot[kMaxDepth];
+};
+
+extern "C" {
+
+int cfws_pipeline_create(uint64_t chunk_bytes, size_t max_frames, int depth, cfws_pipeline_t** out)
+{
+    if (int rc = cfws_init()) return rc;
+    if (!out || depth < 1 || depth > kMaxDepth || chunk_bytes < 4096 || max_frames == 0)
+        return fail("bad pipeline parameters");
+    auto* p = new cfws_pipeline;
+    p->depth = depth;
+    p->chunk = (chunk_bytes + 255) & ~uint64_t(255);
+    p->max_frames = max_frames;
+    // The deserialize output of a chunk can exceed its wire bytes only by
+    // the alignment padding; reserve one 4 KiB pad per frame at most.
+    const uint64_t out_bytes = p->chunk + 64;
+    for (int s = 0; s < depth; ++s) {
+        Slot& S = p->slot[s];
+        S.ws_size = cfws_workspace_size(max_frames, out_bytes);
+        if (hipStreamCreateWithFlags(&S.st, hipStreamNonBlocking) != hipSuccess ||
+            hipMalloc(&S.d_in, p->chunk + 64) != hipSuccess ||
+            hipMalloc(&S.d_out, out_bytes) != hipSuccess ||
+            hipMalloc(&S.d_desc, max_frames * sizeof(cfws_frame_desc_t)) != hipSuccess ||
+            hipMalloc(&S.d_status, max_frames * sizeof(int32_t)) != hipSuccess ||
+            hipMalloc(&S.d_index, max_frames * sizeof(uint64_t)) != hipSuccess ||
+            hipMalloc(&S.d_total, 64) != hipSuccess ||
+            hipMalloc(&S.d_ws, S.ws_size) != hipSuccess ||
+            hipHostMalloc(&S.h_stage, max_frames * (sizeof(cfws_frame_desc_t) + sizeof(int32_t))) != hipSuccess ||
+            hipHostMalloc(reinterpret_cast<void**>(&S.h_total), 64) != hipSuccess ||
+            hipEventCreateWithFlags(&S.ev_done, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&S.ev_total, hipEventDisableTiming) != hipSuccess) {
+            cfws_pipeline_destroy(p);
+            return fail("pipeline allocation failed");
+        }
+        (void)hipEventRecord(S.ev_done, S.st);
+    }
+    *out = p;
+    return CFWS_OK;
+}
+
+void cfws_pipeline_destroy(cfws_pipeline_t* p)
+{
+    if (!p) return;
+    for (int s = 0; s < kMaxDepth; ++s) {
+        Slot& S = p->slot[s];
+        if (S.st) (void)hipStreamSynchronize(S.st);
+        if (S.d_in) (void)hipFree(S.d_in);
+        if (S.d_out) (void)hipFree(S.d_out);
+        if (S.d_desc) (void)hipFree(S.d_desc);
+        if (S.d_status) (void)hipFree(S.d_status);
+        if (S.d_index) (void)hipFree(S.d_index);
+        if (S.d_total) (void)hipFree(S.d_total);
+        if (S.d_ws) (void)hipFree(S.d_ws);
+        if (S.h_stage) (void)hipHostFree(S.h_stage);
+        if (S.h_total) (void)hipHostFree(S.h_total);
+        if (S.ev_done) (void)hipEventDestroy(S.ev_done);
+        if (S.ev_total) (void)hipEventDestroy(S.ev_total);
+        if (S.st) (void)hipStreamDestroy(S.st);
+    }
+    delete p;
+}
+
+// co_ws_frame_serialize over a host batch: host payload arena -> host wire
+// arena. h_desc is updated like cfws_serialize_plan updates d_desc.
+int cfws_pipeline_serialize(cfws_pipeline_t* p, const void* h_payload, cfws_frame_desc_t* h_desc,
+                            size_t n, void* h_wire, uint64_t wire_capacity, uint64_t* wire_total)
+{
+    if (!p || (n && (!h_payload || !h_desc || !h_wire))) return fail("null argument");
+    // Layout on the host copy of the descriptors (same rule as the device
+    // plan) so that chunks can be cut by wire bytes.
+    uint64_t off = 0;
+    for (size_t i = 0; i < n; ++i) {
+        h_desc[i].header_size = (uint8_t)hdr_size(h_desc[i].payload_size, h_desc[i].mask != 0);
+        h_desc[i].wire_off = off;
+        off += h_desc[i].header_size + h_desc[i].payload_size;
+    }
+    if (wire_total) *wire_total = off;
+    const uint8_t* src = static_cast<const uint8_t*>(h_payload);
+    uint8_t* dst = static_cast<uint8_t*>(h_wire);
+    size_t i = 0;
+    int c = 0;
+    while (i < n) {
+        // chunk = frames [i, j): source span and wire bytes within the staging
+        uint64_t lo = h_desc[i].payload_off, hi = lo + h_desc[i].payload_size;
+        size_t j = i;
+        while (j < n && j - i < p->max_frames) {
+            const uint64_t a = std::min(lo, (uint64_t)h_desc[j].payload_off);
+            const uint64_t b = std::max(hi, (uint64_t)(h_desc[j].payload_off + h_desc[j].payload_size));
+            const uint64_t wire = h_desc[j].wire_off + h_desc[j].header_size + h_desc[j].payload_size -
+                                  h_desc[i].wire_off;
+            if (j > i && ((b - (a & ~uint64_t(15))) > p->chunk || wire > p->chunk)) break;
+            lo = a;
+            hi = b;
+            ++j;
+        }
+        const uint64_t src_lo = lo & ~uint64_t(15);
+        const uint64_t wire_lo = h_desc[i].wire_off;
+        const uint64_t wire_bytes = h_desc[j - 1].wire_off + h_desc[j - 1].header_size +
+                                    h_desc[j - 1].payload_size - wire_lo;
+        if (hi - src_lo > p->chunk || wire_bytes > p->chunk)
+            return fail("a frame is larger than the pipeline chunk");
+        Slot& S = p->slot[c % p->depth];
+        CFWS_HIP(hipEventSynchronize(S.ev_done));
+        auto* stage = static_cast<cfws_frame_desc_t*>(S.h_stage);
+        for (size_t k = i; k < j; ++k) {
+            stage[k - i] = h_desc[k];
+            stage[k - i].payload_off -= src_lo;
+        }
+        CFWS_HIP(hipMemcpyAsync(S.d_in, src + src_lo, hi - src_lo, hipMemcpyHostToDevice, S.st));
+        CFWS_HIP(hipMemcpyAsync(S.d_desc, stage, (j - i) * sizeof(cfws_frame_desc_t),
+                                hipMemcpyHostToDevice, S.st));
+        if (int rc = cfws_serialize_batch(S.d_in, S.d_desc, j - i, S.d_out, p->chunk + 64, S.d_total,
+                                          S.d_ws, S.ws_size, S.st))
+            return rc;
+        if (wire_lo < wire_capacity) {
+            const uint64_t m = std::min(wire_bytes, wire_capacity - wire_lo);
+            CFWS_HIP(hipMemcpyAsync(dst + wire_lo, S.d_out, m, hipMemcpyDeviceToHost, S.st));
+        }
+        CFWS_HIP(hipEventRecord(S.ev_done, S.st));
+        i = j;
+        ++c;
+    }
+    for (int s = 0; s < p->depth; ++s) CFWS_HIP(hipStreamSynchronize(p->slot[s].st));
+    return CFWS_OK;
+}
+
+// co_ws_frame_deserialize at every h_index[i] of a host wire buffer: header
+// decode, status, copy + unmask into the host payload arena laid out as
+// cfws_deserialize_plan lays it out (flags must be 0: the reassembly layout
+// puts control frames after ALL data, which a chunked pass cannot know).
+// Precondition (what a receive loop's index satisfies): h_index increasing
+// and every frame ending at or before the next frame's start.
+int cfws_pipeline_deserialize(cfws_pipeline_t* p, const void* h_wire, uint64_t wire_size,
+                              const uint64_t* h_index, size_t n, uint64_t max_payload,
+                              uint32_t align, uint32_t flags, cfws_frame_desc_t* h_desc,
+                              int32_t* h_status, void* h_payload, uint64_t payload_capacity,
+                              uint64_t* payload_total)
+{
+    if (!p || (n && (!h_wire || !h_index || !h_desc || !h_status || !h_payload)))
+        return fail("null argument");
+    if (flags != 0) return fail("the pipeline supports flags = 0 only");
+    if (align == 0 || (align & (align - 1)) || align > 4096) return fail("bad align");
+    for (size_t i = 1; i < n; ++i)
+        if (h_index[i] < h_index[i - 1]) return fail("frame index must be increasing");
+    const uint8_t* src = static_cast<const uint8_t*>(h_wire);
+    uint8_t* dst = static_cast<uint8_t*>(h_payload);
+
+    struct Chunk { size_t i, j; int slot; uint64_t wire_lo; };
+    std::vector<Chunk> pend;         // chunks whose layout total is not consumed yet
+    uint64_t base = 0;               // payload bytes laid out by earlier chunks
+    uint64_t out_slot = p->chunk + 64;
+
+    // Finish chunk k: its layout total is known -> D2H payload, descriptors
+    // and status, then rebase on the host once they land.
+    std::vector<Chunk> done;
+    auto drain = [&](const Chunk& k) -> int {
+        Slot& S = p->slot[k.slot];
+        CFWS_HIP(hipEventSynchronize(S.ev_total));
+        const uint64_t tot = *S.h_total;          // unclamped chunk layout bytes
+        if (base < payload_capacity && tot) {
+            const uint64_t m = std::min(tot, payload_capacity - base);
+            CFWS_HIP(hipMemcpyAsync(dst + base, S.d_out, m, hipMemcpyDeviceToHost, S.st));
+        }
+        auto* sdesc = static_cast<cfws_frame_desc_t*>(S.h_stage);
+        auto* sstat = reinterpret_cast<int32_t*>(sdesc + p->max_frames);
+        CFWS_HIP(hipMemcpyAsync(sdesc, S.d_desc, (k.j - k.i) * sizeof(cfws_frame_desc_t),
+                                hipMemcpyDeviceToHost, S.st));
+        CFWS_HIP(hipMemcpyAsync(sstat, S.d_status, (k.j - k.i) * sizeof(int32_t),
+                                hipMemcpyDeviceToHost, S.st));
+        CFWS_HIP(hipEventRecord(S.ev_done, S.st));
+        CFWS_HIP(hipEventSynchronize(S.ev_done));
+        for (size_t f = k.i; f < k.j; ++f) {
+            h_desc[f] = sdesc[f - k.i];
+            h_desc[f].wire_off += k.wire_lo;
+            h_desc[f].payload_off += base;
+            h_status[f] = sstat[f - k.i];
+        }
+        base += tot;
+        return CFWS_OK;
+    };
+
+    size_t i = 0;
+    int c = 0;
+    while (i < n) {
+        const uint64_t lo = std::min(h_index[i], wire_size);
+        // a frame's bytes end at the next frame's start (the index precondition)
+        auto end_of = [&](size_t k) { return k + 1 < n ? std::min(h_index[k + 1], wire_size) : wire_size; };
+        // frames [i, j): their wire bytes plus the worst-case alignment
+        // padding of their payloads must fit the slot's staging
+        size_t j = i + 1;
+        while (j < n && j - i < p->max_frames &&
+               end_of(j) - (lo & ~uint64_t(15)) + (j + 1 - i) * uint64_t(align - 1) <= p->chunk)
+            ++j;
+        const uint64_t hi = end_of(j - 1);
+        const uint64_t wire_lo = lo & ~uint64_t(15);
+        if (hi - wire_lo + (j - i) * uint64_t(align - 1) > p->chunk)
+            return fail("a frame is larger than the pipeline chunk");
+        const int s = c % p->depth;
+        Slot& S = p->slot[s];
+        // slot reuse: its previous chunk must be fully drained first
+        for (size_t q = 0; q < pend.size(); ++q)
+            if (pend[q].slot == s) {
+                while (!pend.empty() && pend.front().slot != s) {
+                    if (int rc = drain(pend.front())) return rc;
+                    pend.erase(pend.begin());
+                }
+                if (int rc = drain(pend.front())) return rc;
+                pend.erase(pend.begin());
+                break;
+            }
+        auto* sidx = static_cast<uint64_t*>(S.h_stage);
+        for (size_t k = i; k < j; ++k) sidx[k - i] = h_index[k] - wire_lo;
+        CFWS_HIP(hipMemcpyAsync(S.d_in, src + wire_lo, hi - wire_lo, hipMemcpyHostToDevice, S.st));
+        CFWS_HIP(hipMemcpyAsync(S.d_index, sidx, (j - i) * sizeof(uint64_t), hipMemcpyHostToDevice, S.st));
+        // The capacity rule needs this chunk's payload base: everything laid
+        // out before it must be known (drain all pending chunks first).
+        while (!pend.empty()) {
+            if (int rc = drain(pend.front())) return rc;
+            pend.erase(pend.begin());
+        }
+        const uint64_t cap = base >= payload_capacity ? 0 : std::min(out_slot, payload_capacity - base);
+        // cap == 0 (capacity exhausted): the plan marks every non-empty
+        // COMPLETE frame OUT_OF_MEMORY, exactly the batch rule.
+        if (int rc = cfws_deserialize_batch(S.d_in, hi - wire_lo, S.d_index, j - i, max_payload,
+                                            align, 0, S.d_desc, S.d_status, S.d_out, cap,
+                                            S.d_total, S.d_ws, S.ws_size, S.st))
+            return rc;
+        // the unclamped layout total: offsets keep counting past the capacity
+        CFWS_HIP(hipMemcpyAsync(S.h_total,
+                                static_cast<char*>(S.d_ws) + cfws_internal_grand_total_offset(), 8,
+                                hipMemcpyDeviceToHost, S.st));
+        CFWS_HIP(hipEventRecord(S.ev_total, S.st));
+        pend.push_back(Chunk{i, j, s, wire_lo});
+        i = j;
+        ++c;
+    }
+    while (!pend.empty()) {
+        if (int rc = drain(pend.front())) return rc;
+        pend.erase(pend.begin());
+    }
+    if (payload_total) *payload_total = std::min(base, payload_capacity);
+    return CFWS_OK;
+}
+
+}  // extern "C"

@@ -135,6 +135,32 @@ int cfws_deserialize_batch(const void* d_wire, uint64_t wire_size,
                            uint64_t* d_payload_total, void* d_workspace,
                            size_t workspace_size, void* stream);
 
+/* ---- host-memory pipeline ------------------------------------------------
+ * The same codec over HOST buffers (socket send/receive side): the batch is
+ * cut into chunks of frames; `depth` slots (1..4), each with a stream and
+ * device staging of chunk_bytes per direction, overlap H2D, the device plan +
+ * kernels and D2H of consecutive chunks. Host buffers should be pinned.
+ * Synchronous: results are in host memory on return.
+ * max_frames bounds the frames per chunk (descriptor staging). */
+typedef struct cfws_pipeline cfws_pipeline_t;
+int cfws_pipeline_create(uint64_t chunk_bytes, size_t max_frames, int depth,
+                         cfws_pipeline_t** out);
+void cfws_pipeline_destroy(cfws_pipeline_t* pipeline);
+/* cfws_serialize_batch over host arenas; h_desc gets wire_off/header_size. */
+int cfws_pipeline_serialize(cfws_pipeline_t* pipeline, const void* h_payload,
+                            cfws_frame_desc_t* h_desc, size_t n_frames, void* h_wire,
+                            uint64_t wire_capacity, uint64_t* wire_total);
+/* cfws_deserialize_batch over host buffers, flags = 0 (the reassembly layout
+ * needs the whole batch). Precondition: h_frame_index increasing, every
+ * frame ending at or before the next start (what a receive loop's index
+ * satisfies). */
+int cfws_pipeline_deserialize(cfws_pipeline_t* pipeline, const void* h_wire,
+                              uint64_t wire_size, const uint64_t* h_frame_index,
+                              size_t n_frames, uint64_t max_payload, uint32_t align,
+                              uint32_t flags, cfws_frame_desc_t* h_desc, int32_t* h_status,
+                              void* h_payload, uint64_t payload_capacity,
+                              uint64_t* payload_total);
+
 /* ---- single-buffer XOR (used by the per-frame drop-in path) --------------
  * d_dst[i] = d_src[i] ^ key byte (i + key_phase) % 4, i < n. */
 int cfws_xor_mask(const void* d_src, void* d_dst, uint64_t n, uint32_t mask_key,

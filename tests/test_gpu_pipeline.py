@@ -1,0 +1,103 @@
+"""GPU parity of the host-memory pipeline (cfws_pipeline_*): host buffers in,
+host buffers out, H2D / kernels / D2H overlapped over several slots; results
+must equal the oracle's (which is pinned to the reference) byte for byte,
+however the batch is cut into chunks."""
+import random
+
+import numpy as np
+import pytest
+
+import oracle as O
+from conftest import golden
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+from coldforce_amd import cfws  # noqa: E402
+from coldforce_amd import workloads as W  # noqa: E402
+
+
+def pinned(n: int):
+    t = torch.zeros(max(n, 16), dtype=torch.uint8, pin_memory=True)
+    return t, t.numpy()
+
+
+@pytest.fixture(scope="module", autouse=True)
+def device():
+    cfws.init()
+
+
+@pytest.mark.parametrize("chunk,depth", [(69632, 1), (69632, 3), (1 << 20, 2)])
+def test_pipeline_serialize_matches_oracle(chunk, depth):
+    rng = random.Random(chunk + depth)
+    payload_t, payload = pinned(3 << 20)
+    payload[:] = O.fill_splitmix(payload.size, 77, 0)
+    n = 3000
+    d = np.zeros(n, dtype=cfws.DESC_DTYPE)
+    off = 0
+    for i in range(n):
+        sz = rng.choice([0, 1, 5, 125, 126, 1000, 4000, 20000, 65535, 65536, 65537 - 40000])
+        if rng.random() < 0.5:
+            off = rng.randrange(0, payload.size - sz)       # jump around
+        d[i] = (off, 0, sz, rng.getrandbits(32), rng.random() < .7, rng.choice([0, 1, 2, 9]),
+                rng.random() < .6, 0)
+        off = min(off + sz, payload.size - 70000)
+    exp, exp_d = O.serialize_batch(payload, d.view(O.DESC_DTYPE))
+    wire_t, wire = pinned(len(exp) + 64)
+    p = cfws.Pipeline(chunk_bytes=chunk, max_frames=512, depth=depth)
+    tot = p.serialize(payload_t.data_ptr(), d, wire_t.data_ptr(), wire.size)
+    p.close()
+    assert tot == len(exp)
+    assert np.array_equal(d["wire_off"], exp_d["wire_off"])
+    assert np.array_equal(wire[:tot], exp)
+
+
+@pytest.mark.parametrize("chunk,depth,align", [(69632, 1, 16), (69632, 3, 1), (1 << 20, 2, 64)])
+def test_pipeline_deserialize_matches_oracle(chunk, depth, align):
+    rng = random.Random(chunk + depth + align)
+    frames = []
+    for _ in range(2500):
+        p = rng.randbytes(rng.choice([0, 1, 7, 125, 126, 3000, 20000, 40000]))
+        frames.append(O.serialize_keyed(rng.random() < .7, rng.randrange(16), rng.random() < .6,
+                                        rng.getrandbits(32), p))
+    raw = b"".join(frames)
+    wire_t, wire = pinned(len(raw))
+    wire[:len(raw)] = np.frombuffer(raw, np.uint8)
+    starts, _ = O.index_frames(wire[:len(raw)], 100000)
+    starts = np.concatenate([starts, [len(raw) - 1, len(raw)]]).astype(np.uint64)  # truncated tails
+    pl = cfws.Pipeline(chunk_bytes=chunk, max_frames=300, depth=depth)
+    for cap in (len(raw) + align * len(starts) + 64, len(raw) // 2):
+        out_t, out = pinned(cap)
+        desc, st, tot = pl.deserialize(wire_t.data_ptr(), len(raw), starts, out_t.data_ptr(), cap,
+                                       align=align)
+        e_out, e_d, e_st, e_tot = O.deserialize_batch(wire[:len(raw)], starts, align=align,
+                                                      capacity=cap)
+        assert tot == e_tot
+        assert np.array_equal(st, e_st)
+        for f in ("payload_off", "wire_off", "payload_size", "mask_key", "fin", "opcode", "mask",
+                  "header_size"):
+            assert np.array_equal(desc[f], e_d[f]), f
+        assert np.array_equal(out[:tot], e_out[:tot])
+    pl.close()
+
+
+def test_pipeline_config2_reduced_digest():
+    """1,024 x 64 KiB through host memory: the wire equals the reference's."""
+    import hashlib
+    g = golden("batch_digests.json")[0]
+    n, fs = g["n_frames"], g["frame_size"]
+    desc = W.uniform_batch(n, fs, g["key_seed"])
+    payload_t, payload = pinned(n * fs)
+    payload[:] = O.splitmix_words(g["payload_seed"], 0, n * fs // 8).view(np.uint8)
+    wire_t, wire = pinned(g["wire_len"])
+    pl = cfws.Pipeline(chunk_bytes=8 << 20, max_frames=4096, depth=3)
+    tot = pl.serialize(payload_t.data_ptr(), desc, wire_t.data_ptr(), wire.size)
+    assert tot == g["wire_len"]
+    assert hashlib.sha256(wire[:tot].tobytes()).hexdigest() == g["wire_sha256"]
+    back_t, back = pinned(n * fs)
+    d2, st, ptot = pl.deserialize(wire_t.data_ptr(), tot, desc["wire_off"], back_t.data_ptr(),
+                                  back.size)
+    pl.close()
+    assert ptot == n * fs and (st == 0).all()
+    assert np.array_equal(back, payload)
