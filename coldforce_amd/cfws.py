@@ -48,6 +48,8 @@ BATCH_SYMBOLS = (
     "cfws_xor_mask", "cfws_draw_mask_keys", "cfws_release_thread_resources",
     "cfws_fill_splitmix", "cfws_pipeline_create", "cfws_pipeline_destroy",
     "cfws_pipeline_serialize", "cfws_pipeline_deserialize",
+    "cfws_h2_serialize_workspace_size", "cfws_h2_serialize_batch",
+    "cfws_h2_deserialize_workspace_size", "cfws_h2_deserialize_batch",
 )
 DROPIN_SYMBOLS = (
     "co_ws_frame_serialize", "co_ws_frame_deserialize", "co_ws_frame_create",
@@ -107,6 +109,13 @@ def lib(path: str = LIB_PATH) -> C.CDLL:
         "cfws_draw_mask_keys": ([_sz, _vp, _vp], None),
         "cfws_release_thread_resources": ([], None),
         "cfws_fill_splitmix": ([_vp, _u64, _u64, _u64, _vp], C.c_int),
+        "cfws_h2_serialize_workspace_size": ([_sz, _u64, _u64, _u32], _sz),
+        "cfws_h2_serialize_batch": ([_vp, _vp, _sz, _u32, _u32, _vp, _u64, _vp, _u64, _vp, _vp,
+                                     _sz, _vp], C.c_int),
+        "cfws_h2_deserialize_workspace_size": ([_sz, _u64, _u64], _sz),
+        "cfws_h2_deserialize_batch": ([_vp, _u64, _vp, _sz, _u32, _vp, _vp, _u64, _u64, _u32, _vp,
+                                       _vp, _vp, _u64, _vp, C.POINTER(_sz), _vp, _sz, _vp],
+                                      C.c_int),
         "cfws_pipeline_create": ([_u64, _sz, C.c_int, C.POINTER(_vp)], C.c_int),
         "cfws_pipeline_destroy": ([_vp], None),
         "cfws_pipeline_serialize": ([_vp, _vp, _vp, _sz, _vp, _u64, C.POINTER(_u64)], C.c_int),
@@ -334,6 +343,59 @@ def frame_deserialize(data: bytes, index: int = 0):
                payload_size=fr.header.payload_size, payload=payload)
     L.co_ws_frame_destroy(f)
     return out
+
+
+# ---- WebSocket over HTTP/2 ---------------------------------------------------
+
+H2_DEFAULT_MAX_FRAME_SIZE = 16384
+H2_PARSE_COMPLETE, H2_PARSE_MORE_DATA, H2_PARSE_ERROR, H2_NOT_DATA = 0, 1, -1, 3
+
+
+def h2_wrapped_bound(wire_capacity: int, n_frames: int, S: int = H2_DEFAULT_MAX_FRAME_SIZE) -> int:
+    return wire_capacity + 9 * (n_frames + wire_capacity // S + 1)
+
+
+def h2_serialize(payload_t, desc_t, wire_t, h2_t, sid: int = 1, S: int = H2_DEFAULT_MAX_FRAME_SIZE,
+                 ws_t=None, total_t=None, stream=None):
+    """WS frames -> HTTP/2 DATA frames (co_http2_stream_send_ws_frame over a
+    batch). wire_t is scratch for the WS wire bytes. Returns total_t."""
+    import torch
+    n = desc_t.shape[0]
+    if ws_t is None:
+        ws_t = torch.empty(lib().cfws_h2_serialize_workspace_size(n, wire_t.numel(), h2_t.numel(), S),
+                           dtype=torch.uint8, device=h2_t.device)
+    if total_t is None:
+        total_t = torch.zeros(1, dtype=torch.int64, device=h2_t.device)
+    _check(lib().cfws_h2_serialize_batch(_p(payload_t), _p(desc_t), n, sid, S, _p(wire_t),
+                                         wire_t.numel(), _p(h2_t), h2_t.numel(), _p(total_t),
+                                         _p(ws_t), ws_t.numel(), _stream(stream)),
+           "cfws_h2_serialize_batch")
+    return total_t
+
+
+def h2_deserialize(h2_t, h2_size: int, index_t, pool_t, payload_t, S: int = H2_DEFAULT_MAX_FRAME_SIZE,
+                   max_payload: int = DEFAULT_MAX_PAYLOAD, align: int = 16, ws_t=None, stream=None):
+    """HTTP/2 DATA frames at index_t -> pooled WS messages -> payloads.
+    Returns (h2_status_t, msg_desc_t, msg_status_t, total_t, n_messages)."""
+    import torch
+    n = index_t.numel()
+    dev = h2_t.device
+    h2_status = torch.empty(n, dtype=torch.int32, device=dev)
+    msg_desc = torch.empty((max(n, 1), 32), dtype=torch.uint8, device=dev)
+    msg_status = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+    total = torch.zeros(1, dtype=torch.int64, device=dev)
+    if ws_t is None:
+        ws_t = torch.empty(lib().cfws_h2_deserialize_workspace_size(n, pool_t.numel(), payload_t.numel()),
+                           dtype=torch.uint8, device=dev)
+    n_msg = C.c_size_t(0)
+    _check(lib().cfws_h2_deserialize_batch(_p(h2_t), h2_size, _p(index_t), n, S, _p(h2_status),
+                                           _p(pool_t), pool_t.numel(), max_payload, align,
+                                           _p(msg_desc), _p(msg_status), _p(payload_t),
+                                           payload_t.numel(), _p(total), C.byref(n_msg), _p(ws_t),
+                                           ws_t.numel(), _stream(stream)),
+           "cfws_h2_deserialize_batch")
+    m = n_msg.value
+    return h2_status, msg_desc[:m], msg_status[:m], total, m
 
 
 # ---- host-memory pipeline --------------------------------------------------

@@ -52,6 +52,15 @@ constexpr uint64_t kScanBlock = uint64_t(kThreads) * kScanItems;
 // Frame classes a pass copies (deserialize): all, data only, control only.
 enum : uint32_t { kClassAll = 0, kClassData = 1, kClassControl = 2 };
 
+// What a streaming pass produces.
+//   kModeSer:    WS serialize    -- header (2-14 B) + masked payload per frame
+//   kModeDeser:  WS deserialize  -- unmasked payload per frame (or any
+//                                   "strip a prefix, copy the body" pass:
+//                                   HTTP/2 DATA unwrap uses it too)
+//   kModeH2Wrap: HTTP/2 DATA wrap -- 9-byte DATA header + a slice of WS wire
+enum : int { kModeSer = 0, kModeDeser = 1, kModeH2Wrap = 2 };
+__host__ __device__ constexpr bool is_ser(int mode) { return mode != kModeDeser; }
+
 // ---------------------------------------------------------------------------
 // workspace layout (deterministic from n_frames and the output capacity)
 // ---------------------------------------------------------------------------
@@ -130,6 +139,7 @@ struct Pass {
     uint64_t capacity;            // writable bytes from dst
     uint32_t n_frames;
     uint32_t klass;
+    uint32_t sid;                 // HTTP/2 stream id (kModeH2Wrap)
 };
 
 // What one frame contributes to a pass's output.
@@ -159,7 +169,7 @@ __device__ __forceinline__ uint32_t view_header_byte(const FrameView& v, uint32_
          : (r - 2 < ext) ? len_b : key_b;
 }
 
-template <bool kSer>
+template <int kMode>
 __device__ __forceinline__ FrameView frame_view(const Pass& P, uint32_t f)
 {
     const DescWords d = load_desc(P.desc, f);
@@ -167,11 +177,13 @@ __device__ __forceinline__ FrameView frame_view(const Pass& P, uint32_t f)
     v.key = d.mask() ? d.key() : 0u;
     v.out_off = P.offs[f];
     v.hb = 0;
-    if (kSer) {
+    if (is_ser(kMode)) {
         v.pre = d.header_size();
         v.body_len = d.payload_size;
         v.src_off = d.payload_off;
-        v.hb = ((d.opcode() | (d.fin() ? 0x80u : 0u)) & 0xffu) | (d.mask() ? 0x100u : 0u);
+        v.hb = kMode == kModeH2Wrap
+                   ? (d.fin() ? 0x1u : 0u)                         // DATA flags: END_STREAM
+                   : ((d.opcode() | (d.fin() ? 0x80u : 0u)) & 0xffu) | (d.mask() ? 0x100u : 0u);
     } else {
         const bool ctl = is_control(d.opcode());
         const bool take = P.klass == kClassAll || (P.klass == kClassControl) == ctl;
@@ -235,6 +247,26 @@ __device__ __forceinline__ void xor4(uint4& o, uint32_t k)
     o.x ^= k; o.y ^= k; o.z ^= k; o.w ^= k;
 }
 
+// Byte r of an HTTP/2 DATA frame header (co_http2_frame.c:33-72: 24-bit BE
+// length, type 0, flags, 31-bit BE stream id).
+__device__ __forceinline__ uint32_t h2_header_byte(const FrameView& v, uint32_t sid, uint32_t r)
+{
+    const uint32_t len = (uint32_t)v.body_len;
+    const uint32_t sidm = sid & 0x7fffffffu;
+    return r == 0 ? (len >> 16) & 0xffu
+         : r == 1 ? (len >> 8) & 0xffu
+         : r == 2 ? len & 0xffu
+         : r == 3 ? 0u
+         : r == 4 ? (v.hb & 0xffu)
+         : (sidm >> (8 * (8 - r))) & 0xffu;
+}
+
+template <int kMode>
+__device__ __forceinline__ uint32_t header_byte_of(const Pass& P, const FrameView& v, uint32_t r)
+{
+    return kMode == kModeH2Wrap ? h2_header_byte(v, P.sid, r) : view_header_byte(v, r);
+}
+
 // One chunk entirely inside v's body.
 __device__ __forceinline__ uint4 body_chunk(const uint8_t* __restrict__ src, const FrameView& v,
                                             uint64_t D)
@@ -263,10 +295,10 @@ __device__ __forceinline__ uint32_t window_byte(const uint4& A, const uint4& B, 
 
 // Slow fallback: byte by byte, walking frames forward from f (chunks that
 // hold more than two frames: runs of frames shorter than ~14 bytes).
-template <bool kSer>
+template <int kMode>
 __device__ __noinline__ uint4 edge_chunk_bytes(const Pass P, uint32_t f, uint64_t D)
 {
-    FrameView v = frame_view<kSer>(P, f);
+    FrameView v = frame_view<kMode>(P, f);
     uint64_t next = (f + 1 < P.n_frames) ? P.offs[f + 1] : ~uint64_t(0);
     uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;
 #pragma unroll
@@ -276,12 +308,12 @@ __device__ __noinline__ uint4 edge_chunk_bytes(const Pass P, uint32_t f, uint64_
         if (pos < P.total) {
             while (pos >= next) {
                 ++f;
-                v = frame_view<kSer>(P, f);
+                v = frame_view<kMode>(P, f);
                 next = (f + 1 < P.n_frames) ? P.offs[f + 1] : ~uint64_t(0);
             }
             const uint64_t r = pos - v.out_off;
             if (r < v.pre) {
-                b = view_header_byte(v, (uint32_t)r);
+                b = header_byte_of<kMode>(P, v, (uint32_t)r);
             } else {
                 const uint64_t k = r - v.pre;
                 if (k < v.body_len) b = (P.src[v.src_off + k] ^ (v.key >> (8 * (k & 3u)))) & 0xffu;
@@ -317,11 +349,12 @@ __device__ __forceinline__ void edge_blocks(const uint8_t* __restrict__ src, con
 }
 
 // Byte at output position pos of frame v (pos inside v's output range).
-__device__ __forceinline__ uint32_t edge_byte(const FrameView& v, uint64_t pos, const uint4& A,
-                                              const uint4& B, uint64_t abase)
+template <int kMode>
+__device__ __forceinline__ uint32_t edge_byte(const Pass& P, const FrameView& v, uint64_t pos,
+                                              const uint4& A, const uint4& B, uint64_t abase)
 {
     const uint64_t r = pos - v.out_off;
-    if (r < v.pre) return view_header_byte(v, (uint32_t)r);
+    if (r < v.pre) return header_byte_of<kMode>(P, v, (uint32_t)r);
     const uint64_t k = r - v.pre;
     if (k >= v.body_len) return 0;
     const uint32_t idx = (uint32_t)(v.src_off + k - abase);
@@ -332,17 +365,17 @@ __device__ __forceinline__ uint32_t edge_byte(const FrameView& v, uint64_t pos, 
 // the pass. With at most two frames in it (every boundary of frames larger
 // than the chunk) all source blocks are loaded up front and the bytes are
 // assembled in registers: one memory round trip instead of sixteen.
-template <bool kSer>
+template <int kMode>
 __device__ __noinline__ uint4 edge_chunk(const Pass P, uint32_t f, uint64_t D)
 {
     const uint64_t lim = D + 16 < P.total ? D + 16 : P.total;
     const uint64_t o1 = (f + 1 < P.n_frames) ? P.offs[f + 1] : ~uint64_t(0);
     const uint64_t o2 = (f + 2 < P.n_frames) ? P.offs[f + 2] : ~uint64_t(0);
-    if (o2 < lim) return edge_chunk_bytes<kSer>(P, f, D);
-    const FrameView va = frame_view<kSer>(P, f);
+    if (o2 < lim) return edge_chunk_bytes<kMode>(P, f, D);
+    const FrameView va = frame_view<kMode>(P, f);
     const bool two = o1 < lim;
     FrameView vb = va;
-    if (two) vb = frame_view<kSer>(P, f + 1);
+    if (two) vb = frame_view<kMode>(P, f + 1);
     uint4 Aa = make_uint4(0, 0, 0, 0), Ba = Aa, Ab = Aa, Bb = Aa;
     uint64_t ba = 0, bb = 0;
     edge_blocks(P.src, va, D, lim, Aa, Ba, ba);
@@ -353,7 +386,8 @@ __device__ __noinline__ uint4 edge_chunk(const Pass P, uint32_t f, uint64_t D)
         const uint64_t pos = D + j;
         uint32_t b = 0;
         if (pos < lim)
-            b = (two && pos >= o1) ? edge_byte(vb, pos, Ab, Bb, bb) : edge_byte(va, pos, Aa, Ba, ba);
+            b = (two && pos >= o1) ? edge_byte<kMode>(P, vb, pos, Ab, Bb, bb)
+                                   : edge_byte<kMode>(P, va, pos, Aa, Ba, ba);
         const uint32_t sh = 8 * (j & 3);
         if (j < 4) w0 |= b << sh;
         else if (j < 8) w1 |= b << sh;
@@ -417,7 +451,7 @@ __device__ __forceinline__ void fast_region(const Pass& P, const FrameView& v, u
 // frames): both views are wave-uniform, each lane picks one by comparing its
 // chunk with the boundary. Chunks not entirely inside a body are left to
 // edge_kernel.
-template <bool kSer>
+template <int kMode>
 __device__ __forceinline__ void two_frame_region(const Pass& P, const FrameView& va,
                                                  const FrameView& vb, uint64_t base, uint32_t lane)
 {
@@ -453,7 +487,7 @@ __device__ __forceinline__ void two_frame_region(const Pass& P, const FrameView&
 // Any other region (small frames, padding, pass end): every lane finds the
 // frame of each of its chunks by binary search over the region's frames and
 // writes it when it lies inside that frame's body.
-template <bool kSer>
+template <int kMode>
 __device__ __forceinline__ void general_region(const Pass& P, uint32_t f0, uint32_t f1,
                                                uint64_t base, uint32_t lane)
 {
@@ -471,7 +505,7 @@ __device__ __forceinline__ void general_region(const Pass& P, uint32_t f0, uint3
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u) {
         const uint64_t D = base + u * kSlice + lane * kChunk;
-        const FrameView v = frame_view<kSer>(P, fr[u]);
+        const FrameView v = frame_view<kMode>(P, fr[u]);
         if (D >= v.body_start && D + kChunk <= v.body_start + v.body_len)
             st16(P.dst + D, body_chunk(P.src, v, D));
     }
@@ -482,13 +516,13 @@ __device__ __forceinline__ void general_region(const Pass& P, uint32_t f0, uint3
 // writes every 16-byte chunk that lies inside one frame's body; the chunks
 // holding headers, boundaries, padding or the pass end belong to
 // edge_kernel. Both read the same plan; their chunk sets are disjoint.
-template <bool kSer>
+template <int kMode>
 __global__ void __launch_bounds__(kThreads)
 xform_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
              const cfws_frame_desc_t* __restrict__ desc, const int32_t* __restrict__ status,
              const uint64_t* __restrict__ offs, const uint32_t* __restrict__ region_map,
              const uint64_t* __restrict__ total_p, const uint64_t* __restrict__ base_p,
-             uint64_t capacity, uint32_t n_frames, uint32_t klass)
+             uint64_t capacity, uint32_t n_frames, uint32_t klass, uint32_t sid)
 {
     const uint64_t out_base = base_p ? *base_p : 0;
     Pass P;
@@ -501,6 +535,7 @@ xform_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
     P.capacity = capacity - out_base;
     P.n_frames = n_frames;
     P.klass = klass;
+    P.sid = sid;
     const uint64_t n_regions = (P.total + kRegion - 1) / kRegion;
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -518,16 +553,16 @@ xform_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
         // region_map[r + 1] holds the NEXT region's first byte; frames that
         // start at or after this region's end do not touch it.
         if (f1 > f0 && offs[f0 + 1] >= end) f1 = f0;
-        const FrameView va = frame_view<kSer>(P, f0);
+        const FrameView va = frame_view<kMode>(P, f0);
         if (f0 == f1) {
             if (base >= va.body_start && end <= va.body_start + va.body_len)
                 fast_region(P, va, base, lane);
             else
-                two_frame_region<kSer>(P, va, va, base, lane);   // partial body, one frame
+                two_frame_region<kMode>(P, va, va, base, lane);   // partial body, one frame
         } else if (f1 == f0 + 1 || offs[f0 + 2] >= end) {
-            two_frame_region<kSer>(P, va, frame_view<kSer>(P, f0 + 1), base, lane);
+            two_frame_region<kMode>(P, va, frame_view<kMode>(P, f0 + 1), base, lane);
         } else {
-            general_region<kSer>(P, f0, f1, base, lane);
+            general_region<kMode>(P, f0, f1, base, lane);
         }
     }
 }
@@ -535,13 +570,13 @@ xform_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
 // One thread per frame: the 16-byte chunks that START inside the frame's
 // output range and do not lie entirely inside its body -- header chunks,
 // the chunk that crosses into the next frame, padding, the pass end.
-template <bool kSer>
+template <int kMode>
 __global__ void __launch_bounds__(kThreads)
 edge_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
             const cfws_frame_desc_t* __restrict__ desc, const int32_t* __restrict__ status,
             const uint64_t* __restrict__ offs, const uint64_t* __restrict__ total_p,
             const uint64_t* __restrict__ base_p, uint64_t capacity, uint32_t n_frames,
-            uint32_t klass)
+            uint32_t klass, uint32_t sid)
 {
     const uint64_t f = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
     if (f >= n_frames) return;
@@ -556,16 +591,17 @@ edge_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
     P.capacity = capacity - out_base;
     P.n_frames = n_frames;
     P.klass = klass;
+    P.sid = sid;
     const uint64_t lo = offs[f];
     uint64_t hi = (f + 1 < n_frames) ? offs[f + 1] : P.total;
     if (hi > P.total) hi = P.total;
     if (lo >= hi) return;
-    const FrameView v = frame_view<kSer>(P, (uint32_t)f);
+    const FrameView v = frame_view<kMode>(P, (uint32_t)f);
     const uint64_t be = v.body_start + v.body_len;
     const uint64_t first = (lo + 15) & ~uint64_t(15);
     // chunks before the body (headers): D < body_start
     for (uint64_t D = first; D < hi && D < v.body_start; D += 16)
-        store_chunk(P, D, edge_chunk<kSer>(P, (uint32_t)f, D));
+        store_chunk(P, D, edge_chunk<kMode>(P, (uint32_t)f, D));
     // chunks reaching past the body end (boundary, padding, pass end)
     uint64_t t = be >= 15 ? ((be - 15 + 15) & ~uint64_t(15)) : 0;   // first D with D + 16 > be
     if (t < first) t = first;
@@ -574,7 +610,7 @@ edge_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
         if (D >= be && D + 16 <= hi)          // pure alignment padding / OOM body
             store_chunk(P, D, make_uint4(0, 0, 0, 0));
         else
-            store_chunk(P, D, edge_chunk<kSer>(P, (uint32_t)f, D));
+            store_chunk(P, D, edge_chunk<kMode>(P, (uint32_t)f, D));
     }
 }
 
@@ -597,8 +633,9 @@ serialize_sizes_kernel(cfws_frame_desc_t* __restrict__ desc, uint64_t* __restric
 // both passes: vals0 = data (or every frame without reassembly), vals1 =
 // control frames when reassembling.
 __global__ void __launch_bounds__(kThreads)
-deserialize_parse_kernel(const uint8_t* __restrict__ wire, uint64_t wire_size,
-                         const uint64_t* __restrict__ index, uint64_t n, uint64_t max_payload,
+deserialize_parse_kernel(const uint8_t* __restrict__ wire, uint64_t wire_size_all,
+                         const uint64_t* __restrict__ index, const uint64_t* __restrict__ ends,
+                         uint64_t n, uint64_t max_payload,
                          uint64_t align, uint32_t reassemble, cfws_frame_desc_t* __restrict__ desc,
                          int32_t* __restrict__ status, uint64_t* __restrict__ vals0,
                          uint64_t* __restrict__ vals1)
@@ -606,6 +643,9 @@ deserialize_parse_kernel(const uint8_t* __restrict__ wire, uint64_t wire_size,
     const uint64_t f = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
     if (f >= n) return;
     const uint64_t s = index[f];
+    // data_size of the call: the whole buffer, or this frame's own message
+    // (co_http2_stream_receive_ws_frame passes the pooled DATA, :144-146)
+    const uint64_t wire_size = ends && ends[f] < wire_size_all ? ends[f] : wire_size_all;
     cfws_frame_desc_t d;
     d.payload_off = 0;
     d.wire_off = s;
@@ -849,6 +889,159 @@ fill_splitmix_kernel(uint8_t* __restrict__ dst, uint64_t n, uint64_t seed, uint6
 }
 
 // ---------------------------------------------------------------------------
+// WebSocket over HTTP/2 (src/ws_http2): DATA-frame wrap and unwrap
+// ---------------------------------------------------------------------------
+
+// DATA frames a serialized WS frame becomes: co_http2_stream_send_data splits
+// its bytes into frames of at most max_frame_size (co_http2_stream.c:964-1010).
+__global__ void __launch_bounds__(kThreads)
+h2_count_kernel(const cfws_frame_desc_t* __restrict__ desc, uint64_t n, uint64_t S,
+                uint64_t* __restrict__ vals)
+{
+    const uint64_t f = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
+    if (f >= n) return;
+    const uint64_t W = desc[f].header_size + desc[f].payload_size;
+    vals[f] = W <= S ? 1 : (W + S - 1) / S;
+}
+
+// One DATA-frame descriptor per slice: payload_off = slice start in the WS
+// wire arena, payload_size = slice length, fin = END_STREAM (last slice;
+// co_ws_http2_extension.c:190-194 sends every WS frame with end_stream).
+// Output offset of DATA frame d = 9 d + its wire offset.
+__global__ void __launch_bounds__(kThreads)
+h2_expand_kernel(const cfws_frame_desc_t* __restrict__ desc, const uint64_t* __restrict__ first,
+                 uint64_t n, uint64_t S, uint64_t n_max, cfws_frame_desc_t* __restrict__ ddesc,
+                 uint64_t* __restrict__ doffs)
+{
+    const uint64_t f = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
+    if (f >= n) return;
+    const uint64_t W = desc[f].header_size + desc[f].payload_size;
+    const uint64_t w0 = desc[f].wire_off;
+    const uint64_t k = W <= S ? 1 : (W + S - 1) / S;
+    for (uint64_t j = 0; j < k; ++j) {
+        const uint64_t d = first[f] + j;
+        if (d >= n_max) break;
+        cfws_frame_desc_t e;
+        e.payload_off = w0 + j * S;
+        e.wire_off = 9 * d + e.payload_off;
+        e.payload_size = (j + 1 < k) ? S : W - j * S;
+        e.mask_key = 0;
+        e.fin = (j + 1 == k) ? 1 : 0;
+        e.opcode = 0;
+        e.mask = 0;
+        e.header_size = 9;
+        ddesc[d] = e;
+        doffs[d] = e.wire_off;
+    }
+}
+
+// Unused descriptor slots past the real DATA-frame count become empty frames
+// at the end; then the region map of the wrapped arena.
+__global__ void __launch_bounds__(kThreads)
+h2_finalize_kernel(cfws_frame_desc_t* __restrict__ ddesc, uint64_t* __restrict__ doffs,
+                   uint64_t n_max, const uint64_t* __restrict__ n_data_p,
+                   const uint64_t* __restrict__ wire_total_p, uint64_t capacity,
+                   uint32_t* __restrict__ map, uint64_t* __restrict__ hdr,
+                   uint64_t* __restrict__ user_total)
+{
+    const uint64_t d = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
+    if (d >= n_max) return;
+    const uint64_t nd = *n_data_p;
+    const uint64_t T = *wire_total_p + 9 * nd;
+    const uint64_t total = T < capacity ? T : capacity;
+    if (d >= nd) {
+        cfws_frame_desc_t e = {};
+        e.payload_off = 0;
+        e.wire_off = T;
+        ddesc[d] = e;
+        doffs[d] = T;
+    }
+    const uint64_t lo = d < nd ? doffs[d] : T;
+    const uint64_t hi = d + 1 < nd ? doffs[d + 1] : T;
+    const uint64_t a = lo < total ? lo : total, b = hi < total ? hi : total;
+    if (b > a) {
+        const uint64_t r1 = (b + kRegion - 1) / kRegion;
+        for (uint64_t r = (a + kRegion - 1) / kRegion; r < r1; ++r) map[r] = (uint32_t)d;
+    }
+    if (d == n_max - 1) {
+        map[(total + kRegion - 1) / kRegion] = (uint32_t)(n_max - 1);
+        hdr[0] = total;
+        if (user_total) *user_total = T;
+    }
+}
+
+// HTTP/2 frame header at index[i] (co_http2_frame.c:211-300): MORE_DATA under
+// 9 bytes, PARSE_ERROR when length > max_frame_size, MORE_DATA when the
+// payload is incomplete; DATA payload after the optional pad length byte and
+// without the padding. Non-DATA frames are CFWS_H2_NOT_DATA (no bytes).
+__global__ void __launch_bounds__(kThreads)
+h2_parse_kernel(const uint8_t* __restrict__ h2, uint64_t size, const uint64_t* __restrict__ index,
+                uint64_t n, uint64_t max_frame, cfws_frame_desc_t* __restrict__ desc,
+                int32_t* __restrict__ status, uint64_t* __restrict__ vals)
+{
+    const uint64_t i = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t s = index[i];
+    cfws_frame_desc_t d = {};
+    d.wire_off = s;
+    int32_t st = CFWS_H2_PARSE_COMPLETE;
+    do {
+        if (s > size || size - s < 9) { st = CFWS_H2_PARSE_MORE_DATA; break; }
+        const uint64_t len = (uint64_t)h2[s] << 16 | (uint64_t)h2[s + 1] << 8 | h2[s + 2];
+        if (len > max_frame) { st = CFWS_H2_PARSE_ERROR; break; }
+        if (size - s - 9 < len) { st = CFWS_H2_PARSE_MORE_DATA; break; }
+        const uint32_t type = h2[s + 3], flags = h2[s + 4];
+        d.opcode = (uint8_t)type;
+        d.fin = (uint8_t)(flags & 0x1u);
+        if (type != 0) { st = CFWS_H2_NOT_DATA; break; }
+        uint64_t pad = 0, hs = 9;
+        if (flags & 0x8u) {                               // PADDED
+            if (len < 1) { st = CFWS_H2_PARSE_ERROR; break; }
+            pad = h2[s + 9];
+            hs = 10;
+            if (pad + 1 > len) { st = CFWS_H2_PARSE_ERROR; break; }
+        }
+        d.header_size = (uint8_t)hs;
+        d.payload_size = len - (hs - 9) - pad;
+    } while (0);
+    desc[i] = d;
+    status[i] = st;
+    vals[i] = st == CFWS_H2_PARSE_COMPLETE ? d.payload_size : 0;
+}
+
+// A WS message = the pooled payloads of DATA frames up to and including one
+// with END_STREAM (co_http2_stream.c:550-608). es[i] = 1 for those frames.
+__global__ void __launch_bounds__(kThreads)
+h2_end_flags_kernel(const cfws_frame_desc_t* __restrict__ desc, const int32_t* __restrict__ status,
+                    uint64_t n, uint64_t* __restrict__ es)
+{
+    const uint64_t i = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
+    if (i >= n) return;
+    es[i] = (status[i] == CFWS_H2_PARSE_COMPLETE && desc[i].fin) ? 1 : 0;
+}
+
+// Message m ends after its END_STREAM frame's data; it starts where message
+// m - 1 ended (pooled offsets are monotone, failed frames add no bytes).
+__global__ void __launch_bounds__(kThreads)
+h2_messages_kernel(const cfws_frame_desc_t* __restrict__ desc, const int32_t* __restrict__ status,
+                   const uint64_t* __restrict__ msg_id, uint64_t n, uint64_t* __restrict__ ends)
+{
+    const uint64_t i = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
+    if (i >= n) return;
+    if (status[i] == CFWS_H2_PARSE_COMPLETE && desc[i].fin)
+        ends[msg_id[i]] = desc[i].payload_off + desc[i].payload_size;
+}
+
+__global__ void __launch_bounds__(kThreads)
+h2_starts_kernel(const uint64_t* __restrict__ ends, const uint64_t* __restrict__ n_msg_p,
+                 uint64_t n, uint64_t* __restrict__ starts)
+{
+    const uint64_t m = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
+    if (m >= n || m >= *n_msg_p) return;
+    starts[m] = m == 0 ? 0 : ends[m - 1];
+}
+
+// ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
 thread_local char g_err[512] = "";
@@ -959,20 +1152,30 @@ uint32_t xform_lds_bytes()
     return (uint32_t)v;
 }
 
-template <bool kSer>
+// The streaming kernel plus the edge kernel of one pass.
+template <int kMode>
+void launch_streaming(const void* src, void* dst, const cfws_frame_desc_t* desc,
+                      const int32_t* status, const uint64_t* offs, const uint32_t* map,
+                      const uint64_t* total_p, const uint64_t* base_p, uint64_t regions,
+                      uint64_t cap, size_t n, uint32_t klass, uint32_t sid, hipStream_t st)
+{
+    xform_kernel<kMode><<<stream_grid(regions), kThreads, xform_lds_bytes(), st>>>(
+        static_cast<const uint8_t*>(src), static_cast<uint8_t*>(dst), desc, status, offs, map,
+        total_p, base_p, cap, (uint32_t)n, klass, sid);
+    edge_kernel<kMode><<<grid_for(n, kThreads), kThreads, 0, st>>>(
+        static_cast<const uint8_t*>(src), static_cast<uint8_t*>(dst), desc, status, offs,
+        total_p, base_p, cap, (uint32_t)n, klass, sid);
+}
+
+template <int kMode>
 void launch_pass(const WsLayout& L, int p, const void* src, void* dst, const cfws_frame_desc_t* desc,
                  const int32_t* status, const void* ws, uint64_t cap, size_t n, uint32_t klass,
-                 hipStream_t st)
+                 hipStream_t st, uint32_t sid = 0)
 {
     const uint64_t* hdr = ws_ptr<const uint64_t>(ws, L.hdr);
-    xform_kernel<kSer><<<stream_grid(L.regions), kThreads, xform_lds_bytes(), st>>>(
-        static_cast<const uint8_t*>(src), static_cast<uint8_t*>(dst), desc, status,
-        ws_ptr<const uint64_t>(ws, L.offs[p]), ws_ptr<const uint32_t>(ws, L.map[p]), hdr + p,
-        p == 1 ? hdr + 2 : nullptr, cap, (uint32_t)n, klass);
-    edge_kernel<kSer><<<grid_for(n, kThreads), kThreads, 0, st>>>(
-        static_cast<const uint8_t*>(src), static_cast<uint8_t*>(dst), desc, status,
-        ws_ptr<const uint64_t>(ws, L.offs[p]), hdr + p, p == 1 ? hdr + 2 : nullptr, cap,
-        (uint32_t)n, klass);
+    launch_streaming<kMode>(src, dst, desc, status, ws_ptr<const uint64_t>(ws, L.offs[p]),
+                            ws_ptr<const uint32_t>(ws, L.map[p]), hdr + p,
+                            p == 1 ? hdr + 2 : nullptr, L.regions, cap, n, klass, sid, st);
 }
 
 }  // namespace
@@ -1022,7 +1225,7 @@ int cfws_serialize_execute(const void* d_payload, const cfws_frame_desc_t* d_des
     if (misaligned(d_payload, d_wire))
         return set_err(CFWS_ERROR_INVALID_ARGUMENT, "arenas must be 16-byte aligned", hipSuccess);
     const WsLayout L = ws_layout(n, cap);
-    launch_pass<true>(L, 0, d_payload, d_wire, d_desc, nullptr, ws, cap, n, kClassAll,
+    launch_pass<kModeSer>(L, 0, d_payload, d_wire, d_desc, nullptr, ws, cap, n, kClassAll,
                       static_cast<hipStream_t>(stream));
     return launch_check("serialize_execute");
 }
@@ -1034,8 +1237,8 @@ int cfws_serialize_batch(const void* d_payload, cfws_frame_desc_t* d_desc, size_
     return cfws_serialize_execute(d_payload, d_desc, n, d_wire, cap, ws, stream);
 }
 
-int cfws_deserialize_plan(const void* d_wire, uint64_t wire_size, const uint64_t* d_index,
-                          size_t n, uint64_t max_payload, uint32_t align, uint32_t flags,
+static int deserialize_plan_impl(const void* d_wire, uint64_t wire_size, const uint64_t* d_index,
+                                 const uint64_t* d_ends, size_t n, uint64_t max_payload, uint32_t align, uint32_t flags,
                           cfws_frame_desc_t* d_desc, int32_t* d_status, uint64_t cap,
                           uint64_t* d_total, void* ws, size_t ws_size, void* stream)
 {
@@ -1056,7 +1259,7 @@ int cfws_deserialize_plan(const void* d_wire, uint64_t wire_size, const uint64_t
     uint64_t* offs0 = ws_ptr<uint64_t>(ws, L.offs[0]);
     uint64_t* offs1 = ws_ptr<uint64_t>(ws, L.offs[1]);
     deserialize_parse_kernel<<<grid_for(n, kThreads), kThreads, 0, st>>>(
-        static_cast<const uint8_t*>(d_wire), wire_size, d_index, n, max_payload, align, reasm,
+        static_cast<const uint8_t*>(d_wire), wire_size, d_index, d_ends, n, max_payload, align, reasm,
         d_desc, d_status, offs0, offs1);
     if (int rc = run_scan(offs0, n, ws_ptr<uint64_t>(ws, L.partials[0]), hdr + 3, st)) return rc;
     if (reasm)
@@ -1065,6 +1268,15 @@ int cfws_deserialize_plan(const void* d_wire, uint64_t wire_size, const uint64_t
         d_desc, d_status, offs0, offs1, hdr, n, cap, reasm, ws_ptr<uint32_t>(ws, L.map[0]),
         ws_ptr<uint32_t>(ws, L.map[1]), d_total);
     return launch_check("deserialize_plan");
+}
+
+int cfws_deserialize_plan(const void* d_wire, uint64_t wire_size, const uint64_t* d_index,
+                          size_t n, uint64_t max_payload, uint32_t align, uint32_t flags,
+                          cfws_frame_desc_t* d_desc, int32_t* d_status, uint64_t cap,
+                          uint64_t* d_total, void* ws, size_t ws_size, void* stream)
+{
+    return deserialize_plan_impl(d_wire, wire_size, d_index, nullptr, n, max_payload, align, flags,
+                                 d_desc, d_status, cap, d_total, ws, ws_size, stream);
 }
 
 int cfws_deserialize_execute(const void* d_wire, const cfws_frame_desc_t* d_desc,
@@ -1080,10 +1292,10 @@ int cfws_deserialize_execute(const void* d_wire, const cfws_frame_desc_t* d_desc
     const WsLayout L = ws_layout(n, cap);
     hipStream_t st = static_cast<hipStream_t>(stream);
     if (flags & CFWS_DESERIALIZE_REASSEMBLE) {
-        launch_pass<false>(L, 0, d_wire, d_payload, d_desc, d_status, ws, cap, n, kClassData, st);
-        launch_pass<false>(L, 1, d_wire, d_payload, d_desc, d_status, ws, cap, n, kClassControl, st);
+        launch_pass<kModeDeser>(L, 0, d_wire, d_payload, d_desc, d_status, ws, cap, n, kClassData, st);
+        launch_pass<kModeDeser>(L, 1, d_wire, d_payload, d_desc, d_status, ws, cap, n, kClassControl, st);
     } else {
-        launch_pass<false>(L, 0, d_wire, d_payload, d_desc, d_status, ws, cap, n, kClassAll, st);
+        launch_pass<kModeDeser>(L, 0, d_wire, d_payload, d_desc, d_status, ws, cap, n, kClassAll, st);
     }
     return launch_check("deserialize_execute");
 }
@@ -1098,6 +1310,174 @@ int cfws_deserialize_batch(const void* d_wire, uint64_t wire_size, const uint64_
                                        d_desc, d_status, cap, d_total, ws, ws_size, stream))
         return rc;
     return cfws_deserialize_execute(d_wire, d_desc, d_status, n, flags, d_payload, cap, ws, stream);
+}
+
+// ---- WebSocket over HTTP/2 -------------------------------------------------
+
+namespace {
+
+struct H2SerLayout {
+    uint64_t ser;        // WS serialize workspace
+    uint64_t hdr;        // [0] wrapped total (clamped) [3] DATA-frame count
+    uint64_t vals;       // u64[n]: DATA frames per WS frame -> first DATA frame
+    uint64_t partials;
+    uint64_t ddesc;      // cfws_frame_desc_t[n_max]
+    uint64_t doffs;      // u64[n_max]
+    uint64_t map;        // u32[regions + 2]
+    uint64_t bytes, n_max, regions;
+};
+
+H2SerLayout h2_ser_layout(uint64_t n, uint64_t wire_cap, uint64_t h2_cap, uint64_t S)
+{
+    H2SerLayout L;
+    L.n_max = n + wire_cap / S + 1;
+    L.regions = (h2_cap + kRegion - 1) / kRegion;
+    uint64_t at = align_up(ws_layout(n, wire_cap).bytes, 256);
+    L.ser = 0;
+    L.hdr = at; at += 256;
+    L.vals = at; at = align_up(at + 8 * n, 256);
+    L.partials = at; at = align_up(at + 8 * ((n + kScanBlock - 1) / kScanBlock + 1), 256);
+    L.ddesc = at; at = align_up(at + sizeof(cfws_frame_desc_t) * L.n_max, 256);
+    L.doffs = at; at = align_up(at + 8 * L.n_max, 256);
+    L.map = at; at = align_up(at + 4 * (L.regions + 2), 256);
+    L.bytes = at;
+    return L;
+}
+
+struct H2DeLayout {
+    uint64_t pool;       // pool pass (DATA unwrap): a WsLayout over n_h2 frames
+    uint64_t pdesc;      // cfws_frame_desc_t[n_h2]
+    uint64_t es;         // u64[n_h2]: END_STREAM flags -> message ids
+    uint64_t es_part;
+    uint64_t es_total;   // u64: message count
+    uint64_t starts, ends;   // u64[n_h2]
+    uint64_t wsd;        // WS deserialize workspace
+    uint64_t bytes;
+};
+
+H2DeLayout h2_de_layout(uint64_t n, uint64_t pool_cap, uint64_t payload_cap)
+{
+    H2DeLayout L;
+    uint64_t at = 0;
+    L.pool = at; at = align_up(at + ws_layout(n, pool_cap).bytes, 256);
+    L.pdesc = at; at = align_up(at + sizeof(cfws_frame_desc_t) * n, 256);
+    L.es = at; at = align_up(at + 8 * n, 256);
+    L.es_part = at; at = align_up(at + 8 * ((n + kScanBlock - 1) / kScanBlock + 1), 256);
+    L.es_total = at; at += 256;
+    L.starts = at; at = align_up(at + 8 * n, 256);
+    L.ends = at; at = align_up(at + 8 * n, 256);
+    L.wsd = at; at = align_up(at + ws_layout(n, payload_cap).bytes, 256);
+    L.bytes = at;
+    return L;
+}
+
+}  // namespace
+
+size_t cfws_h2_serialize_workspace_size(size_t n, uint64_t wire_cap, uint64_t h2_cap, uint32_t S)
+{
+    return (size_t)h2_ser_layout(n, wire_cap, h2_cap, S ? S : CFWS_H2_DEFAULT_MAX_FRAME_SIZE).bytes;
+}
+
+size_t cfws_h2_deserialize_workspace_size(size_t n_h2, uint64_t pool_cap, uint64_t payload_cap)
+{
+    return (size_t)h2_de_layout(n_h2, pool_cap, payload_cap).bytes;
+}
+
+int cfws_h2_serialize_batch(const void* d_payload, cfws_frame_desc_t* d_desc, size_t n,
+                            uint32_t stream_id, uint32_t S, void* d_wire, uint64_t wire_cap,
+                            void* d_h2, uint64_t h2_cap, uint64_t* d_h2_total, void* ws,
+                            size_t ws_size, void* stream)
+{
+    if (int rc = check_init()) return rc;
+    if (S == 0) S = CFWS_H2_DEFAULT_MAX_FRAME_SIZE;
+    if (S > 0xffffff) return set_err(CFWS_ERROR_INVALID_ARGUMENT, "max_frame_size > 2^24-1", hipSuccess);
+    const H2SerLayout L = h2_ser_layout(n, wire_cap, h2_cap, S);
+    if (!ws || ws_size < L.bytes) return set_err(CFWS_ERROR_WORKSPACE, "workspace too small", hipSuccess);
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    if (n == 0) {
+        if (d_h2_total) (void)hipMemsetAsync(d_h2_total, 0, 8, st);
+        return launch_check("h2_serialize(empty)");
+    }
+    // 1. the WS frames, exactly as cfws_serialize_batch writes them
+    const WsLayout WL = ws_layout(n, wire_cap);
+    if (int rc = cfws_serialize_batch(d_payload, d_desc, n, d_wire, wire_cap, nullptr, ws, WL.bytes, stream))
+        return rc;
+    // 2. their DATA frames
+    uint64_t* hdr = ws_ptr<uint64_t>(ws, L.hdr);
+    uint64_t* vals = ws_ptr<uint64_t>(ws, L.vals);
+    cfws_frame_desc_t* ddesc = ws_ptr<cfws_frame_desc_t>(ws, L.ddesc);
+    uint64_t* doffs = ws_ptr<uint64_t>(ws, L.doffs);
+    uint32_t* map = ws_ptr<uint32_t>(ws, L.map);
+    h2_count_kernel<<<grid_for(n, kThreads), kThreads, 0, st>>>(d_desc, n, S, vals);
+    if (int rc = run_scan(vals, n, ws_ptr<uint64_t>(ws, L.partials), hdr + 3, st)) return rc;
+    h2_expand_kernel<<<grid_for(n, kThreads), kThreads, 0, st>>>(d_desc, vals, n, S, L.n_max, ddesc, doffs);
+    h2_finalize_kernel<<<grid_for(L.n_max, kThreads), kThreads, 0, st>>>(
+        ddesc, doffs, L.n_max, hdr + 3, ws_ptr<const uint64_t>(ws, WL.hdr + 24), h2_cap, map, hdr,
+        d_h2_total);
+    // 3. wrap: 9-byte DATA header + slice, one streaming pass
+    if (h2_cap)
+        launch_streaming<kModeH2Wrap>(d_wire, d_h2, ddesc, nullptr, doffs, map, hdr, nullptr,
+                                      L.regions, h2_cap, L.n_max, kClassAll, stream_id, st);
+    return launch_check("h2_serialize");
+}
+
+int cfws_h2_deserialize_batch(const void* d_h2, uint64_t h2_size, const uint64_t* d_h2_index,
+                              size_t n, uint32_t S, int32_t* d_h2_status, void* d_pool,
+                              uint64_t pool_cap, uint64_t max_payload, uint32_t align,
+                              cfws_frame_desc_t* d_msg_desc, int32_t* d_msg_status,
+                              void* d_payload, uint64_t payload_cap, uint64_t* d_payload_total,
+                              size_t* n_messages, void* ws, size_t ws_size, void* stream)
+{
+    if (int rc = check_init()) return rc;
+    if (S == 0) S = CFWS_H2_DEFAULT_MAX_FRAME_SIZE;
+    const H2DeLayout L = h2_de_layout(n, pool_cap, payload_cap);
+    if (!ws || ws_size < L.bytes) return set_err(CFWS_ERROR_WORKSPACE, "workspace too small", hipSuccess);
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    if (n_messages) *n_messages = 0;
+    if (n == 0) {
+        if (d_payload_total) (void)hipMemsetAsync(d_payload_total, 0, 8, st);
+        return launch_check("h2_deserialize(empty)");
+    }
+    if (!d_h2 || !d_h2_index || !d_h2_status || !d_pool || !d_msg_desc || !d_msg_status || !d_payload)
+        return set_err(CFWS_ERROR_INVALID_ARGUMENT, "null pointer", hipSuccess);
+    // 1. unwrap: DATA payloads pooled back to back (a prefix-strip pass)
+    const WsLayout PL = ws_layout(n, pool_cap);
+    void* pws = ws_ptr<void>(ws, L.pool);
+    uint64_t* phdr = ws_ptr<uint64_t>(pws, PL.hdr);
+    uint64_t* poffs = ws_ptr<uint64_t>(pws, PL.offs[0]);
+    cfws_frame_desc_t* pdesc = ws_ptr<cfws_frame_desc_t>(ws, L.pdesc);
+    h2_parse_kernel<<<grid_for(n, kThreads), kThreads, 0, st>>>(
+        static_cast<const uint8_t*>(d_h2), h2_size, d_h2_index, n, S, pdesc, d_h2_status, poffs);
+    if (int rc = run_scan(poffs, n, ws_ptr<uint64_t>(pws, PL.partials[0]), phdr + 3, st)) return rc;
+    deserialize_finalize_kernel<<<grid_for(n, kThreads), kThreads, 0, st>>>(
+        pdesc, d_h2_status, poffs, poffs, phdr, n, pool_cap, 0, ws_ptr<uint32_t>(pws, PL.map[0]),
+        ws_ptr<uint32_t>(pws, PL.map[1]), nullptr);
+    if (pool_cap)
+        launch_pass<kModeDeser>(PL, 0, d_h2, d_pool, pdesc, d_h2_status, pws, pool_cap, n, kClassAll, st);
+    // 2. messages: END_STREAM closes one (co_http2_stream.c:550-608)
+    uint64_t* es = ws_ptr<uint64_t>(ws, L.es);
+    uint64_t* n_msg_d = ws_ptr<uint64_t>(ws, L.es_total);
+    uint64_t* starts = ws_ptr<uint64_t>(ws, L.starts);
+    uint64_t* ends = ws_ptr<uint64_t>(ws, L.ends);
+    h2_end_flags_kernel<<<grid_for(n, kThreads), kThreads, 0, st>>>(pdesc, d_h2_status, n, es);
+    if (int rc = run_scan(es, n, ws_ptr<uint64_t>(ws, L.es_part), n_msg_d, st)) return rc;
+    h2_messages_kernel<<<grid_for(n, kThreads), kThreads, 0, st>>>(pdesc, d_h2_status, es, n, ends);
+    h2_starts_kernel<<<grid_for(n, kThreads), kThreads, 0, st>>>(ends, n_msg_d, n, starts);
+    uint64_t n_msg = 0;
+    hipError_t e = hipMemcpyAsync(&n_msg, n_msg_d, 8, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) return set_err(CFWS_ERROR_HIP, "h2_deserialize message count", e);
+    if (n_messages) *n_messages = (size_t)n_msg;
+    // 3. each pooled message through co_ws_frame_deserialize, against its
+    //    own size (co_ws_http2_extension.c:134-164)
+    void* wsd = ws_ptr<void>(ws, L.wsd);
+    const size_t wsd_size = ws_layout(n, payload_cap).bytes;
+    if (int rc = deserialize_plan_impl(d_pool, pool_cap, starts, ends, n_msg, max_payload, align, 0,
+                                       d_msg_desc, d_msg_status, payload_cap, d_payload_total, wsd,
+                                       wsd_size, stream))
+        return rc;
+    return cfws_deserialize_execute(d_pool, d_msg_desc, d_msg_status, n_msg, 0, d_payload,
+                                    payload_cap, wsd, stream);
 }
 
 int cfws_xor_mask(const void* d_src, void* d_dst, uint64_t n, uint32_t key, uint32_t phase,

@@ -135,6 +135,46 @@ int cfws_deserialize_batch(const void* d_wire, uint64_t wire_size,
                            uint64_t* d_payload_total, void* d_workspace,
                            size_t workspace_size, void* stream);
 
+/* ---- WebSocket over HTTP/2 (src/ws_http2) ---------------------------------
+ * Send: every WS frame of the batch is serialized (cfws_serialize_batch, into
+ * d_wire) and carried in HTTP/2 DATA frames of at most max_frame_size payload
+ * bytes (0 = the default 16384, co_http2.h:55), END_STREAM on the last DATA
+ * frame of each WS frame -- co_http2_stream_send_ws_frame
+ * (co_ws_http2_extension.c:166-199) -> co_http2_stream_send_data
+ * (co_http2_stream.c:933-1013), DATA layout co_http2_frame.c:33-72 (9-byte
+ * header: 24-bit BE length, type 0, flags, 31-bit BE stream id). The flow
+ * control window is assumed to admit every frame. *d_h2_total is unclamped.
+ * Receive: the DATA frames starting at d_h2_index[i] (one stream, in order)
+ * are parsed (co_http2_frame.c:211-300; status per DATA frame below), their
+ * payloads pooled into d_pool until END_STREAM (co_http2_stream.c:550-608),
+ * and every pooled message goes through co_ws_frame_deserialize against its
+ * own size (co_ws_http2_extension.c:134-164): d_msg_desc / d_msg_status get
+ * one entry per message (room for n_h2 entries), payloads land in d_payload
+ * as cfws_deserialize_batch lays them out (flags = 0). Synchronises the
+ * stream to return *n_messages. */
+#define CFWS_H2_DEFAULT_MAX_FRAME_SIZE 16384u
+#define CFWS_H2_PARSE_COMPLETE    0     /* co_http.h:40-42 */
+#define CFWS_H2_PARSE_MORE_DATA   1
+#define CFWS_H2_PARSE_ERROR      (-1)
+#define CFWS_H2_NOT_DATA          3     /* a complete non-DATA frame: no bytes */
+
+size_t cfws_h2_serialize_workspace_size(size_t n_frames, uint64_t wire_capacity,
+                                        uint64_t h2_capacity, uint32_t max_frame_size);
+int cfws_h2_serialize_batch(const void* d_payload, cfws_frame_desc_t* d_desc, size_t n_frames,
+                            uint32_t stream_id, uint32_t max_frame_size, void* d_wire,
+                            uint64_t wire_capacity, void* d_h2, uint64_t h2_capacity,
+                            uint64_t* d_h2_total, void* d_workspace, size_t workspace_size,
+                            void* stream);
+size_t cfws_h2_deserialize_workspace_size(size_t n_h2_frames, uint64_t pool_capacity,
+                                          uint64_t payload_capacity);
+int cfws_h2_deserialize_batch(const void* d_h2, uint64_t h2_size, const uint64_t* d_h2_index,
+                              size_t n_h2_frames, uint32_t max_frame_size, int32_t* d_h2_status,
+                              void* d_pool, uint64_t pool_capacity, uint64_t max_payload,
+                              uint32_t align, cfws_frame_desc_t* d_msg_desc,
+                              int32_t* d_msg_status, void* d_payload, uint64_t payload_capacity,
+                              uint64_t* d_payload_total, size_t* n_messages,
+                              void* d_workspace, size_t workspace_size, void* stream);
+
 /* ---- host-memory pipeline ------------------------------------------------
  * The same codec over HOST buffers (socket send/receive side): the batch is
  * cut into chunks of frames; `depth` slots (1..4), each with a stream and

@@ -245,3 +245,100 @@ def ref_deserialize(L, data: bytes, index: int = 0, max_payload: int = DEFAULT_M
         payload = out[:psz.value + 1].tobytes()  # includes the NUL terminator
     return dict(rc=rc, index=idx.value, fin=bool(fin.value), opcode=op.value,
                 payload_size=psz.value, payload=payload)
+
+
+# ---- WebSocket over HTTP/2 ----------------------------------------------------
+
+def _bind_h2():
+    L = lib()
+    if not hasattr(L, "_h2_bound"):
+        L.orc_h2_send.argtypes = [_vp, _u64, C.c_uint32, C.c_uint32, _vp]
+        L.orc_h2_send.restype = _u64
+        L.orc_h2_serialize_batch.argtypes = [_vp, _vp, _sz, C.c_uint32, C.c_uint32, _vp, _vp]
+        L.orc_h2_serialize_batch.restype = _u64
+        L.orc_h2_deserialize_batch.argtypes = [_vp, _u64, _vp, _sz, C.c_uint32, _vp, _vp, _u64,
+                                               _u64, C.c_uint32, _vp, _vp, _vp, _u64,
+                                               C.POINTER(_u64)]
+        L.orc_h2_deserialize_batch.restype = _u64
+        L._h2_bound = True
+    return L
+
+
+def h2_frames_bound(ws_len: int, S: int) -> int:
+    return 9 * (ws_len // S + 2) + ws_len
+
+
+def h2_serialize_batch(payload: np.ndarray, desc: np.ndarray, sid: int = 1, S: int = 16384):
+    """Returns (h2 bytes, desc with header_size filled)."""
+    L = _bind_h2()
+    desc = desc.copy()
+    sizes = desc["payload_size"].astype(np.uint64)
+    w = sizes + 14
+    bound = int((w + 9 * (w // S + 1)).sum()) + 64
+    out = np.zeros(bound, dtype=np.uint8)
+    tmp = np.zeros(int(w.max()) + 16 if len(w) else 16, dtype=np.uint8)
+    pl = payload if payload.size else np.zeros(1, np.uint8)
+    n = L.orc_h2_serialize_batch(_ptr(pl), _ptr(desc), len(desc), sid, S, _ptr(tmp), _ptr(out))
+    return out[:n], desc
+
+
+def h2_deserialize_batch(h2: np.ndarray, index: np.ndarray, S: int = 16384,
+                         max_payload: int = DEFAULT_MAX_PAYLOAD, align: int = 16,
+                         pool_capacity: int | None = None, payload_capacity: int | None = None):
+    """Returns dict(h2_status, pool, msg_desc, msg_status, payload, total, n_msg)."""
+    L = _bind_h2()
+    index = np.ascontiguousarray(index, dtype=np.uint64)
+    n = len(index)
+    pool_capacity = len(h2) if pool_capacity is None else pool_capacity
+    payload_capacity = len(h2) + 16 * n + 16 if payload_capacity is None else payload_capacity
+    h2_status = np.zeros(n, dtype=np.int32)
+    pool = np.zeros(max(pool_capacity, 1), dtype=np.uint8)
+    msg_desc = np.zeros(max(n, 1), dtype=DESC_DTYPE)
+    msg_status = np.zeros(max(n, 1), dtype=np.int32)
+    payload = np.zeros(max(payload_capacity, 1), dtype=np.uint8)
+    n_msg = _u64(0)
+    h = h2 if h2.size else np.zeros(1, np.uint8)
+    total = L.orc_h2_deserialize_batch(_ptr(h), len(h2), _ptr(index), n, S, _ptr(h2_status),
+                                       _ptr(pool), pool_capacity, max_payload, align,
+                                       _ptr(msg_desc), _ptr(msg_status), _ptr(payload),
+                                       payload_capacity, C.byref(n_msg))
+    m = n_msg.value
+    return dict(h2_status=h2_status, pool=pool, msg_desc=msg_desc[:m], msg_status=msg_status[:m],
+                payload=payload, total=int(total), n_msg=m)
+
+
+def h2_index(h2: np.ndarray) -> np.ndarray:
+    """Frame starts of a well-formed HTTP/2 frame stream (sequential walk)."""
+    starts, p, n = [], 0, len(h2)
+    while p + 9 <= n:
+        starts.append(p)
+        p += 9 + (int(h2[p]) << 16 | int(h2[p + 1]) << 8 | int(h2[p + 2]))
+    return np.array(starts, dtype=np.uint64)
+
+
+def ref_h2_send(R, ws: bytes, S: int = 16384, sid: int = 1) -> bytes:
+    f = R.ref_h2_send
+    f.argtypes = [_vp, C.c_ulonglong, C.c_uint, C.c_uint, _vp, C.c_ulonglong]
+    f.restype = C.c_longlong
+    src = np.frombuffer(ws, dtype=np.uint8) if ws else np.zeros(1, np.uint8)
+    out = np.zeros(len(ws) + 9 * (len(ws) // S + 2), dtype=np.uint8)
+    k = f(_ptr(src), len(ws), S, sid, _ptr(out), out.size)
+    assert k >= 0
+    return out[:k].tobytes()
+
+
+def ref_h2_recv(R, data: bytes, index: int = 0, S: int = 16384):
+    f = R.ref_h2_recv
+    f.argtypes = [_vp, C.c_ulonglong, C.POINTER(C.c_ulonglong), C.c_uint,
+                  C.POINTER(C.c_uint), C.POINTER(C.c_uint), C.POINTER(C.c_uint),
+                  C.POINTER(C.c_uint), _vp, C.c_ulonglong, C.POINTER(C.c_ulonglong)]
+    f.restype = C.c_int
+    src = np.frombuffer(data, dtype=np.uint8)
+    out = np.zeros(len(data) + 1, dtype=np.uint8)
+    idx = C.c_ulonglong(index)
+    ln, ty, fl, sid = C.c_uint(), C.c_uint(), C.c_uint(), C.c_uint()
+    plen = C.c_ulonglong()
+    r = f(_ptr(src), len(data), C.byref(idx), S, C.byref(ln), C.byref(ty), C.byref(fl),
+          C.byref(sid), _ptr(out), out.size, C.byref(plen))
+    return dict(rc=r, index=idx.value, length=ln.value, type=ty.value, flags=fl.value,
+                sid=sid.value, payload=out[:plen.value].tobytes())

@@ -385,3 +385,138 @@ int orc_deserialize_flat(const unsigned char* data, unsigned long long size,
     orc_frame_clear(&f);
     return r;
 }
+
+/* ---- WebSocket over HTTP/2 --------------------------------------------- */
+
+/* DATA frame encode, co_http2_frame.c:33-72 (no padding on send,
+ * co_http2_create_data_frame(..., NULL, 0), co_http2_frame.c:628-700). */
+static uint64_t orc_h2_data_frame(const uint8_t* data, uint32_t len, int end_stream,
+                                  uint32_t sid, uint8_t* out)
+{
+    out[0] = (uint8_t)(len >> 16);
+    out[1] = (uint8_t)(len >> 8);
+    out[2] = (uint8_t)len;
+    out[3] = 0;                                   /* DATA */
+    out[4] = end_stream ? 0x1 : 0x0;              /* END_STREAM */
+    sid &= 0x7fffffffu;
+    out[5] = (uint8_t)(sid >> 24);
+    out[6] = (uint8_t)(sid >> 16);
+    out[7] = (uint8_t)(sid >> 8);
+    out[8] = (uint8_t)sid;
+    if (len) memcpy(out + 9, data, len);
+    return 9 + (uint64_t)len;
+}
+
+/* co_http2_stream_send_data (co_http2_stream.c:933-1013) with end_stream and
+ * a window that admits the frame: first frame max_frame_size, then full
+ * frames, the last one END_STREAM; one frame when it fits. */
+uint64_t orc_h2_send(const uint8_t* ws, uint64_t len, uint32_t S, uint32_t sid, uint8_t* out)
+{
+    if (len <= S) return orc_h2_data_frame(ws, (uint32_t)len, 1, sid, out);
+    uint64_t at = orc_h2_data_frame(ws, S, 0, sid, out), idx = S;
+    while (len > idx) {
+        uint32_t sz = (len - idx > S) ? S : (uint32_t)(len - idx);
+        at += orc_h2_data_frame(ws + idx, sz, len - idx <= S, sid, out + at);
+        idx += sz;
+    }
+    return at;
+}
+
+uint64_t orc_h2_serialize_batch(const uint8_t* payload, orc_desc_t* d, size_t n, uint32_t sid,
+                                uint32_t S, uint8_t* tmp, uint8_t* out)
+{
+    uint64_t at = 0;
+    for (size_t i = 0; i < n; ++i) {
+        d[i].header_size = (uint8_t)orc_header_size(d[i].payload_size, d[i].mask != 0);
+        size_t w = orc_serialize_keyed(d[i].fin != 0, d[i].opcode, d[i].mask != 0, d[i].mask_key,
+                                       payload + d[i].payload_off, (size_t)d[i].payload_size, tmp);
+        at += orc_h2_send(tmp, w, S, sid, out + at);
+    }
+    return at;
+}
+
+/* co_http2_frame_deserialize's DATA path (co_http2_frame.c:211-300): status
+ * 0 / 1 (MORE_DATA) / -1 (PARSE_ERROR: length > max frame size; also a pad
+ * length that does not fit, where the reference underflows) / 3 (not DATA).
+ * DATA payloads (padding stripped) are pooled until END_STREAM
+ * (co_http2_stream.c:550-608); each pooled message is then parsed by
+ * co_ws_frame_deserialize against its own size (co_ws_http2_extension.c:
+ * 134-164). Layout of the WS payloads as orc_deserialize_batch (flags 0). */
+uint64_t orc_h2_deserialize_batch(const uint8_t* h2, uint64_t size, const uint64_t* index,
+                                  size_t n, uint32_t S, int32_t* h2_status, uint8_t* pool,
+                                  uint64_t pool_cap, uint64_t max_payload, uint32_t align,
+                                  orc_desc_t* msg_desc, int32_t* msg_status, uint8_t* payload,
+                                  uint64_t payload_cap, uint64_t* n_msg_out)
+{
+    uint64_t pooled = 0, n_msg = 0, msg_start = 0;
+    uint64_t* starts = (uint64_t*)malloc(sizeof(uint64_t) * (n + 1));
+    uint64_t* ends = (uint64_t*)malloc(sizeof(uint64_t) * (n + 1));
+    for (size_t i = 0; i < n; ++i) {
+        uint64_t s = index[i];
+        int st = 0;
+        uint64_t dlen = 0, hs = 9;
+        int es = 0;
+        if (s > size || size - s < 9) st = 1;
+        else {
+            uint64_t len = (uint64_t)h2[s] << 16 | (uint64_t)h2[s + 1] << 8 | h2[s + 2];
+            if (len > S) st = -1;
+            else if (size - s - 9 < len) st = 1;
+            else if (h2[s + 3] != 0) st = 3;
+            else {
+                uint64_t pad = 0;
+                if (h2[s + 4] & 0x8) {
+                    if (len < 1) st = -1;
+                    else {
+                        pad = h2[s + 9];
+                        hs = 10;
+                        if (pad + 1 > len) st = -1;
+                    }
+                }
+                if (st == 0) {
+                    dlen = len - (hs - 9) - pad;
+                    es = h2[s + 4] & 0x1;
+                }
+            }
+        }
+        if (st == 0 && dlen && pooled + dlen > pool_cap) st = ORC_ERROR_OUT_OF_MEMORY;
+        h2_status[i] = st;
+        if (st == 0) {
+            memcpy(pool + pooled, h2 + s + hs, (size_t)dlen);
+            pooled += dlen;
+            if (es) {
+                starts[n_msg] = msg_start;
+                ends[n_msg] = pooled;
+                ++n_msg;
+                msg_start = pooled;
+            }
+        }
+    }
+    /* each message: co_ws_frame_deserialize(frame, msg, msg_size, &0) */
+    uint64_t off = 0, total;
+    if (align == 0) align = 1;
+    for (uint64_t m = 0; m < n_msg; ++m) {
+        int st = orc_parse_header(pool + starts[m], ends[m] - starts[m], 0, max_payload, &msg_desc[m]);
+        msg_desc[m].wire_off = starts[m];
+        uint64_t len = st == ORC_PARSE_COMPLETE ? msg_desc[m].payload_size : 0;
+        uint64_t next = off + (len + align - 1) / align * align;
+        if (len && off + len > payload_cap) {
+            st = ORC_ERROR_OUT_OF_MEMORY;
+            len = 0;
+        }
+        msg_status[m] = st;
+        msg_desc[m].payload_off = off;
+        if (len) {
+            const uint8_t* src = pool + starts[m] + msg_desc[m].header_size;
+            if (msg_desc[m].mask) orc_xor_bytes(payload + off, src, len, msg_desc[m].mask_key);
+            else memcpy(payload + off, src, (size_t)len);
+        }
+        uint64_t pad_end = next < payload_cap ? next : payload_cap;
+        if (pad_end > off + len) memset(payload + off + len, 0, (size_t)(pad_end - off - len));
+        off = next;
+    }
+    total = off < payload_cap ? off : payload_cap;
+    free(starts);
+    free(ends);
+    if (n_msg_out) *n_msg_out = n_msg;
+    return total;
+}

@@ -111,6 +111,17 @@ uint64_t orc_deserialize_batch(const uint8_t* wire, uint64_t wire_size,
                                orc_desc_t* desc, int32_t* status,
                                uint8_t* payload, uint64_t payload_capacity);
 
+/* WebSocket over HTTP/2 (src/ws_http2): see cfws_oracle.c. */
+uint64_t orc_h2_send(const uint8_t* ws, uint64_t len, uint32_t max_frame, uint32_t sid,
+                     uint8_t* out);
+uint64_t orc_h2_serialize_batch(const uint8_t* payload, orc_desc_t* desc, size_t n,
+                                uint32_t sid, uint32_t max_frame, uint8_t* tmp, uint8_t* out);
+uint64_t orc_h2_deserialize_batch(const uint8_t* h2, uint64_t size, const uint64_t* index,
+                                  size_t n, uint32_t max_frame, int32_t* h2_status,
+                                  uint8_t* pool, uint64_t pool_cap, uint64_t max_payload,
+                                  uint32_t align, orc_desc_t* msg_desc, int32_t* msg_status,
+                                  uint8_t* payload, uint64_t payload_cap, uint64_t* n_msg);
+
 /* Sequential frame-boundary walk of a packed wire stream, as the receive
  * loops do (co_ws_server.c:107-169): writes up to max_frames starts of
  * COMPLETE frames, returns the count; *consumed = bytes of whole frames. */

@@ -63,3 +63,71 @@ int ref_deserialize(const unsigned char* data, unsigned long long size,
     co_ws_config_set_max_receive_payload_size(CO_WS_CONFIG_DEFAULT_MAX_RECEIVE_PAYLOAD_SIZE);
     return r;
 }
+
+/* ---- HTTP/2 DATA framing through the reference's frame codec ------------
+ * co_http2_frame.c (compiled in place) encodes / decodes each frame; the
+ * split of one buffer into DATA frames restates co_http2_stream_send_data
+ * (co_http2_stream.c:933-1013: first frame max_frame_size, then full frames,
+ * END_STREAM on the last, one frame when it fits; window assumed open),
+ * whose stream machinery needs a live connection. */
+#include <coldforce/http2/co_http2_frame.h>
+
+static void ref_h2_one(const uint8_t* data, uint32_t len, int end_stream, uint32_t sid,
+                       co_byte_array_t* out)
+{
+    co_http2_frame_t* f = co_http2_create_data_frame(false, end_stream != 0, data, len, NULL, 0);
+    f->header.stream_id = sid;
+    co_http2_frame_serialize(f, out);
+    co_http2_frame_destroy(f);
+}
+
+long long ref_h2_send(const unsigned char* ws, unsigned long long len, unsigned int max_frame,
+                      unsigned int sid, unsigned char* out, unsigned long long cap)
+{
+    co_byte_array_t* b = co_byte_array_create();
+    if (len <= max_frame) {
+        ref_h2_one(ws, (uint32_t)len, 1, sid, b);
+    } else {
+        uint32_t index = max_frame;
+        ref_h2_one(ws, max_frame, 0, sid, b);
+        do {
+            uint32_t sz = (len - index > max_frame) ? max_frame : (uint32_t)(len - index);
+            ref_h2_one(ws + index, sz, len - index <= max_frame, sid, b);
+            index += sz;
+        } while (len > index);
+    }
+    size_t cnt = co_byte_array_get_count(b);
+    long long r = (long long)cnt;
+    if (cnt > cap) r = -2;
+    else memcpy(out, co_byte_array_get_ptr(b, 0), cnt);
+    co_byte_array_destroy(b);
+    return r;
+}
+
+/* co_http2_frame_deserialize on buffer[index..]: result, header fields and
+ * the DATA payload (padding stripped). */
+int ref_h2_recv(const unsigned char* data, unsigned long long size, unsigned long long* index,
+                unsigned int max_frame, unsigned int* length, unsigned int* type,
+                unsigned int* flags, unsigned int* sid, unsigned char* payload,
+                unsigned long long cap, unsigned long long* payload_len)
+{
+    co_byte_array_t* b = co_byte_array_create();
+    co_byte_array_add(b, data, (size_t)size);
+    co_http2_frame_t* f = co_http2_frame_create();
+    size_t idx = (size_t)*index;
+    int r = co_http2_frame_deserialize(b, &idx, max_frame, f);
+    *index = idx;
+    *length = f->header.length;
+    *type = f->header.type;
+    *flags = f->header.flags;
+    *sid = f->header.stream_id;
+    *payload_len = 0;
+    if (r == 0 && f->header.type == 0 && f->payload.data.data_length <= cap) {
+        *payload_len = f->payload.data.data_length;
+        if (f->payload.data.data_length) memcpy(payload, f->payload.data.data, f->payload.data.data_length);
+    }
+    if (r == 0) co_http2_frame_destroy(f);
+    else free(f);
+    co_byte_array_destroy(b);
+    return r;
+}

@@ -207,6 +207,99 @@ def zipf_digest(R, target, seed, key_seed, ping_every=0):
                 wire_len=total, wire_sha256=h.hexdigest())
 
 
+def h2_cases(R):
+    """WebSocket over HTTP/2 through the reference: co_ws_frame_serialize +
+    co_http2_frame.c DATA frames (split as co_http2_stream_send_data does),
+    DATA decode cases through co_http2_frame_deserialize, and message-level
+    results composed from the reference's DATA decode, the pooling rule of
+    co_http2_stream.c:550-608 and co_ws_frame_deserialize."""
+    out = {"wrap": [], "recv": [], "messages": []}
+    for S, sid in ((16384, 1), (100, 3)):
+        O.srandom(R, 5)
+        h2 = b""
+        frames = []
+        for n, fin, op in ((0, 1, 9), (5, 1, 1), (125, 0, 1), (126, 0, 0), (16376, 1, 0),
+                           (16377, 1, 2), (65536, 1, 2), (100000, 1, 2)):
+            data = O.fill_splitmix(n, 0x5EED0005, 8 * n).tobytes()
+            ws = O.ref_serialize(R, bool(fin), op, True, data)
+            h2 += O.ref_h2_send(R, ws, S, sid)
+            frames.append(dict(n=n, fin=fin, opcode=op, payload_seed=0x5EED0005, payload_byte_base=8 * n))
+        out["wrap"].append(dict(max_frame=S, sid=sid, key_seed=5, frames=frames, h2_len=len(h2),
+                                h2_sha256=sha(h2)))
+
+    def hdr(length, typ, flags, sid):
+        return bytes([length >> 16 & 255, length >> 8 & 255, length & 255, typ, flags]) + \
+            (sid & 0x7fffffff).to_bytes(4, "big")
+    data = bytes(range(40))
+    cases = [
+        ("DATA", hdr(40, 0, 0, 1) + data),
+        ("DATA END_STREAM", hdr(40, 0, 1, 1) + data),
+        ("DATA padded 7", hdr(48, 0, 8 | 1, 1) + bytes([7]) + data + bytes(7)),
+        ("DATA padded 0", hdr(41, 0, 8, 1) + bytes([0]) + data),
+        ("DATA empty END_STREAM", hdr(0, 0, 1, 1)),
+        ("8-byte header", hdr(40, 0, 0, 1)[:8]),
+        ("payload truncated", hdr(40, 0, 0, 1) + data[:39]),
+        ("length over max_frame_size", hdr(16385, 0, 0, 1) + bytes(16385)),
+        ("PING", hdr(8, 6, 0, 0) + bytes(8)),
+    ]
+    for name, raw in cases:
+        r = O.ref_h2_recv(R, raw, 0, 16384)
+        out["recv"].append(dict(name=name, raw_hex=raw.hex(), rc=r["rc"], index=r["index"],
+                                length=r["length"], type=r["type"], flags=r["flags"],
+                                payload_hex=r["payload"].hex()))
+    # messages: DATA frames -> pool until END_STREAM -> co_ws_frame_deserialize
+    O.srandom(R, 6)
+    stream = b""
+    ws_msgs = [O.ref_serialize(R, True, 1, True, b"hello"),
+               O.ref_serialize(R, True, 2, True, bytes(range(256)) * 150),
+               O.ref_serialize(R, False, 2, True, bytes(300)),
+               bytes([0x82, 0x85, 1, 2, 3, 4]) + b"ab",                # WS frame longer than its message
+               O.ref_serialize(R, True, 9, False, b"")]
+    for k, ws in enumerate(ws_msgs):
+        if k == 2:   # one message split with padded DATA frames
+            stream += hdr(100 + 1 + 3, 0, 8, 1) + bytes([3]) + ws[:100] + bytes(3)
+            stream += hdr(len(ws) - 100, 0, 1, 1) + ws[100:]
+        else:
+            stream += O.ref_h2_send(R, ws, 16384 if k != 1 else 1000, 1)
+    idx, pool, msgs = 0, b"", []
+    while idx < len(stream):
+        r = O.ref_h2_recv(R, stream, idx, 16384)
+        assert r["rc"] == 0
+        idx = r["index"]
+        pool += r["payload"]
+        if r["flags"] & 1:
+            msgs.append(pool)
+            pool = b""
+    res = []
+    for m in msgs:
+        d = O.ref_deserialize(R, m, 0)
+        res.append(dict(rc=d["rc"], fin=d["fin"], opcode=d["opcode"], payload_size=d["payload_size"],
+                        payload_sha256=None if d["payload"] is None else sha(d["payload"][:-1]),
+                        message_len=len(m)))
+    out["messages"].append(dict(stream_hex=stream.hex(), max_frame=16384, results=res))
+    return out
+
+
+def h2_digest(R, n_frames, frame_size, payload_seed, key_seed, S=16384, sid=1):
+    """Config 5: n_frames binary frames, client-masked, each carried in
+    HTTP/2 DATA frames of at most S bytes, through the reference."""
+    h = hashlib.sha256()
+    total = 0
+    O.srandom(R, key_seed)
+    chunk = 1024
+    for c0 in range(0, n_frames, chunk):
+        c1 = min(n_frames, c0 + chunk)
+        arena = O.splitmix_words(payload_seed, c0 * frame_size // 8,
+                                 (c1 - c0) * frame_size // 8 + 1).view(np.uint8)
+        for f in range(c1 - c0):
+            ws = O.ref_serialize(R, True, 2, True, arena[f * frame_size:(f + 1) * frame_size].tobytes())
+            h2 = O.ref_h2_send(R, ws, S, sid)
+            h.update(h2)
+            total += len(h2)
+    return dict(n_frames=n_frames, frame_size=frame_size, payload_seed=payload_seed,
+                key_seed=key_seed, max_frame=S, sid=sid, h2_len=total, h2_sha256=h.hexdigest())
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--skip-full", action="store_true", help="skip the 4 GiB config-2 digest")
@@ -227,6 +320,11 @@ def main():
     if not a.skip_full:
         zipf.append(zipf_digest(R, 4 << 30, 0x5EED0003, 3))
     dump("zipf_digests.json", zipf)
+    dump("h2_cases.json", h2_cases(R))
+    h2d = [h2_digest(R, 1024, 16376, 0x5EED0005, 5), h2_digest(R, 1024, 65536, 0x5EED0005, 5)]
+    if not a.skip_full:
+        h2d += [h2_digest(R, 65536, 16376, 0x5EED0005, 5), h2_digest(R, 65536, 65536, 0x5EED0005, 5)]
+    dump("h2_digests.json", h2d)
 
 
 if __name__ == "__main__":

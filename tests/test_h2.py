@@ -1,0 +1,247 @@
+"""WebSocket over HTTP/2 (BASELINE.json configs[4]):
+WS frames carried in HTTP/2 DATA frames (co_ws_http2_extension.c:134-199,
+co_http2_stream.c:933-1013 and :550-608, co_http2_frame.c:33-72 and
+:211-300). CPU tests pin the oracle to the reference's own DATA encoder /
+decoder (tests/golden/h2_*.json); GPU tests hold the device path to both."""
+import hashlib
+import random
+
+import numpy as np
+import pytest
+
+import oracle as O
+from conftest import golden, gpu_present
+
+
+def sha(b) -> str:
+    return hashlib.sha256(b.tobytes() if hasattr(b, "tobytes") else b).hexdigest()
+
+
+def wrap_desc(case):
+    frames = case["frames"]
+    sizes = [f["n"] for f in frames]
+    arena = b"".join(O.fill_splitmix(f["n"], f["payload_seed"], f["payload_byte_base"]).tobytes()
+                     for f in frames)
+    d = np.zeros(len(frames), dtype=O.DESC_DTYPE)
+    d["payload_off"] = np.concatenate([[0], np.cumsum(sizes[:-1])]).astype(np.uint64)
+    d["payload_size"] = sizes
+    d["fin"] = [f["fin"] for f in frames]
+    d["opcode"] = [f["opcode"] for f in frames]
+    d["mask"] = 1
+    d["mask_key"] = O.keys(case["key_seed"], len(frames))
+    return np.frombuffer(arena, np.uint8).copy(), d
+
+
+def test_oracle_wrap_golden():
+    for case in golden("h2_cases.json")["wrap"]:
+        arena, d = wrap_desc(case)
+        h2, _ = O.h2_serialize_batch(arena, d, case["sid"], case["max_frame"])
+        assert len(h2) == case["h2_len"] and sha(h2) == case["h2_sha256"]
+
+
+def test_oracle_recv_golden():
+    # reference rc 0 on a non-DATA frame is "not DATA" in the batch API
+    for c in golden("h2_cases.json")["recv"]:
+        raw = np.frombuffer(bytes.fromhex(c["raw_hex"]), np.uint8).copy()
+        r = O.h2_deserialize_batch(raw, np.array([0], np.uint64))
+        exp = 3 if (c["rc"] == 0 and c["type"] != 0) else c["rc"]
+        assert r["h2_status"][0] == exp, c["name"]
+        if exp == 0:
+            assert r["pool"][:len(c["payload_hex"]) // 2].tobytes().hex() == c["payload_hex"]
+
+
+def test_oracle_messages_golden():
+    g = golden("h2_cases.json")["messages"][0]
+    stream = np.frombuffer(bytes.fromhex(g["stream_hex"]), np.uint8).copy()
+    r = O.h2_deserialize_batch(stream, O.h2_index(stream), g["max_frame"], align=1)
+    assert r["n_msg"] == len(g["results"])
+    for k, e in enumerate(g["results"]):
+        d = r["msg_desc"][k]
+        assert r["msg_status"][k] == e["rc"]
+        assert (bool(d["fin"]), int(d["opcode"]), int(d["payload_size"])) == \
+            (e["fin"], e["opcode"], e["payload_size"])
+        if e["payload_sha256"]:
+            o = int(d["payload_off"])
+            assert sha(r["payload"][o:o + e["payload_size"]]) == e["payload_sha256"]
+
+
+@pytest.mark.parametrize("idx", [0, 1])
+def test_oracle_h2_digest(idx):
+    g = golden("h2_digests.json")[idx]
+    n, fs = g["n_frames"], g["frame_size"]
+    arena = O.splitmix_words(g["payload_seed"], 0, (n * fs + 7) // 8).view(np.uint8)[:n * fs]
+    d = np.zeros(n, dtype=O.DESC_DTYPE)
+    d["payload_off"] = np.arange(n, dtype=np.uint64) * fs
+    d["payload_size"], d["fin"], d["opcode"], d["mask"] = fs, 1, 2, 1
+    d["mask_key"] = O.keys(g["key_seed"], n)
+    h2, _ = O.h2_serialize_batch(arena, d, g["sid"], g["max_frame"])
+    assert len(h2) == g["h2_len"] and sha(h2) == g["h2_sha256"]
+    r = O.h2_deserialize_batch(h2, O.h2_index(h2), g["max_frame"], align=1,
+                               payload_capacity=n * fs)
+    assert r["n_msg"] == n and (r["msg_status"] == 0).all()
+    assert np.array_equal(r["payload"][:n * fs], arena)
+
+
+# ---- device ---------------------------------------------------------------------
+
+def _gpu():
+    import torch
+    from coldforce_amd import cfws
+    cfws.init()
+    return torch, cfws
+
+
+def gpu_h2_serialize(payload: np.ndarray, desc: np.ndarray, sid=1, S=16384):
+    torch, cfws = _gpu()
+    from coldforce_amd import workloads as W
+    pay = torch.from_numpy(payload if payload.size else np.zeros(16, np.uint8)).cuda()
+    d_t = cfws.desc_to_device(desc)
+    _, wtotal = W.wire_layout(desc)
+    wire = torch.empty(W.round16(wtotal) + 16, dtype=torch.uint8, device="cuda")
+    h2 = torch.full((cfws.h2_wrapped_bound(wire.numel(), len(desc), S),), 0xEE, dtype=torch.uint8,
+                    device="cuda")
+    tot = cfws.h2_serialize(pay, d_t, wire, h2, sid, S)
+    torch.cuda.synchronize()
+    t = int(tot.item())
+    return h2[:t].cpu().numpy(), t
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not gpu_present(), reason="needs the MI355X")
+@pytest.mark.parametrize("S", [16384, 1000, 100, 16])
+def test_gpu_h2_serialize_random(S):
+    rng = random.Random(S)
+    payload = O.fill_splitmix(1 << 20, S, 0)
+    n = 800
+    d = np.zeros(n, dtype=O.DESC_DTYPE)
+    for i in range(n):
+        sz = rng.choice([0, 1, 125, 126, 999, 1000, 16376, 16384, 40000, 70000])
+        d[i] = (rng.randrange(0, (1 << 20) - sz), 0, sz, rng.getrandbits(32), rng.random() < .6,
+                rng.choice([0, 1, 2, 9]), rng.random() < .7, 0)
+    exp, _ = O.h2_serialize_batch(payload, d, 5, S)
+    got, t = gpu_h2_serialize(payload, d, 5, S)
+    assert t == len(exp)
+    bad = np.nonzero(got != exp)[0]
+    assert bad.size == 0, bad[:10]
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not gpu_present(), reason="needs the MI355X")
+def test_gpu_h2_wrap_golden():
+    for case in golden("h2_cases.json")["wrap"]:
+        arena, d = wrap_desc(case)
+        got, t = gpu_h2_serialize(arena, d, case["sid"], case["max_frame"])
+        assert t == case["h2_len"] and sha(got) == case["h2_sha256"]
+
+
+def gpu_h2_deserialize(h2: np.ndarray, index: np.ndarray, S=16384, align=16, pool_cap=None,
+                       payload_cap=None, max_payload=O.DEFAULT_MAX_PAYLOAD):
+    torch, cfws = _gpu()
+    h = torch.from_numpy(np.concatenate([h2, np.zeros(16, np.uint8)])).cuda()
+    idx = torch.from_numpy(index.astype(np.int64)).cuda()
+    pool = torch.empty(max(pool_cap if pool_cap is not None else len(h2), 16), dtype=torch.uint8,
+                       device="cuda")
+    pay = torch.empty(max(payload_cap if payload_cap is not None else len(h2) + 16 * len(index) + 16,
+                          16), dtype=torch.uint8, device="cuda")
+    if pool_cap is not None:
+        pool = pool[:pool_cap] if pool_cap else pool[:0]
+    if payload_cap is not None:
+        pay = pay[:payload_cap]
+    st, md, ms, tot, m = cfws.h2_deserialize(h, len(h2), idx, pool, pay, S, max_payload, align)
+    torch.cuda.synchronize()
+    return dict(h2_status=st.cpu().numpy(), msg_desc=cfws.desc_from_device(md) if m else
+                np.zeros(0, O.DESC_DTYPE), msg_status=ms.cpu().numpy(),
+                payload=pay.cpu().numpy(), total=int(tot.item()), n_msg=m)
+
+
+def check_h2_deserialize(h2, index, **kw):
+    got = gpu_h2_deserialize(h2, index, **kw)
+    exp = O.h2_deserialize_batch(h2, index, kw.get("S", 16384), kw.get("max_payload", O.DEFAULT_MAX_PAYLOAD),
+                                 kw.get("align", 16), kw.get("pool_cap"), kw.get("payload_cap"))
+    assert np.array_equal(got["h2_status"], exp["h2_status"])
+    assert got["n_msg"] == exp["n_msg"] and got["total"] == exp["total"]
+    assert np.array_equal(got["msg_status"], exp["msg_status"])
+    for f in ("payload_off", "wire_off", "payload_size", "mask_key", "fin", "opcode", "mask",
+              "header_size"):
+        assert np.array_equal(got["msg_desc"][f], exp["msg_desc"][f]), f
+    assert np.array_equal(got["payload"][:got["total"]], exp["payload"][:exp["total"]])
+    return got
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not gpu_present(), reason="needs the MI355X")
+def test_gpu_h2_deserialize_golden_messages():
+    g = golden("h2_cases.json")["messages"][0]
+    stream = np.frombuffer(bytes.fromhex(g["stream_hex"]), np.uint8).copy()
+    check_h2_deserialize(stream, O.h2_index(stream), align=1)
+    for c in golden("h2_cases.json")["recv"]:
+        raw = np.frombuffer(bytes.fromhex(c["raw_hex"]), np.uint8).copy()
+        check_h2_deserialize(raw, np.array([0], np.uint64))
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not gpu_present(), reason="needs the MI355X")
+@pytest.mark.parametrize("S", [16384, 100])
+def test_gpu_h2_roundtrip_random(S):
+    rng = random.Random(S + 1)
+    payload = O.fill_splitmix(1 << 20, 3, 0)
+    n = 500
+    d = np.zeros(n, dtype=O.DESC_DTYPE)
+    for i in range(n):
+        sz = rng.choice([0, 5, 126, 999, 16376, 20000, 70000])
+        d[i] = (rng.randrange(0, (1 << 20) - sz), 0, sz, rng.getrandbits(32), 1,
+                rng.choice([1, 2, 9]), rng.random() < .7, 0)
+    h2, _ = O.h2_serialize_batch(payload, d, 1, S)
+    index = O.h2_index(h2)
+    check_h2_deserialize(h2, index, S=S)
+    check_h2_deserialize(h2, index, S=S, align=1, payload_cap=len(h2) // 3)    # OOM tail
+    check_h2_deserialize(h2, index, S=S, pool_cap=len(h2) // 2)                # pool OOM
+    bad = h2.copy()
+    for k in range(3, len(index), 37):                                        # corrupt headers
+        bad[int(index[k]) + 3] = 6 if k % 2 else bad[int(index[k]) + 3]
+        bad[int(index[k])] = 0xFF if not k % 2 else bad[int(index[k])]
+    check_h2_deserialize(bad, index, S=S)
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not gpu_present(), reason="needs the MI355X")
+@pytest.mark.parametrize("idx", [0, 1, 2, 3])
+def test_gpu_config5_digest(idx):
+    """Config 5 batches (16,376 B and 64 KiB frames, 1,024 and 65,536 of
+    them): the DATA-frame stream equals the reference's byte for byte, and
+    unwrap + unmask restores every payload."""
+    torch, cfws = _gpu()
+    from coldforce_amd import workloads as W
+    g = golden("h2_digests.json")[idx]
+    n, fs = g["n_frames"], g["frame_size"]
+    desc = W.uniform_batch(n, fs, g["key_seed"])
+    payload = torch.empty(W.round16(n * fs) + 16, dtype=torch.uint8, device="cuda")
+    cfws.fill_splitmix(payload, g["payload_seed"])
+    offs, wtotal = W.wire_layout(desc)
+    wire = torch.empty(W.round16(wtotal) + 16, dtype=torch.uint8, device="cuda")
+    h2 = torch.empty(cfws.h2_wrapped_bound(wire.numel(), n), dtype=torch.uint8, device="cuda")
+    tot = cfws.h2_serialize(payload, cfws.desc_to_device(desc), wire, h2, g["sid"], g["max_frame"])
+    torch.cuda.synchronize()
+    t = int(tot.item())
+    assert t == g["h2_len"]
+    h = hashlib.sha256()
+    for o in range(0, t, 1 << 28):
+        h.update(h2[o:min(t, o + (1 << 28))].cpu().numpy().tobytes())
+    assert h.hexdigest() == g["h2_sha256"]
+    # DATA frame starts: k = ceil(W / S) frames per WS frame, 9-byte headers
+    S = g["max_frame"]
+    W_ = fs + 14 if fs > 65535 else fs + 8
+    k = -(-W_ // S)
+    starts = np.concatenate([f * (W_ + 9 * k) + np.arange(k) * (S + 9) for f in range(n)]) \
+        if n <= 1024 else None
+    if starts is None:
+        per = (W_ + 9 * k) * np.arange(n, dtype=np.uint64)
+        starts = (per[:, None] + (np.arange(k, dtype=np.uint64) * (S + 9))[None, :]).reshape(-1)
+    idx_t = torch.from_numpy(starts.astype(np.int64)).cuda()
+    pool = torch.empty(t, dtype=torch.uint8, device="cuda")
+    back = torch.empty(n * fs + 64, dtype=torch.uint8, device="cuda")
+    st, md, ms, ptot, m = cfws.h2_deserialize(h2, t, idx_t, pool, back, S, align=1)
+    torch.cuda.synchronize()
+    assert m == n and int(ptot.item()) == n * fs
+    assert bool((st == 0).all()) and bool((ms == 0).all())
+    assert torch.equal(back[:n * fs], payload[:n * fs])
