@@ -478,16 +478,18 @@ uint64_t orc_h2_deserialize_batch(const uint8_t* h2, uint64_t size, const uint64
                 }
             }
         }
-        if (st == 0 && dlen && pooled + dlen > pool_cap) st = ORC_ERROR_OUT_OF_MEMORY;
+        /* the pool layout is fixed by the parse; capacity only marks */
+        uint64_t at = pooled;
+        if (st == 0) pooled += dlen;
+        if (st == 0 && dlen && at + dlen > pool_cap) st = ORC_ERROR_OUT_OF_MEMORY;
         h2_status[i] = st;
         if (st == 0) {
-            memcpy(pool + pooled, h2 + s + hs, (size_t)dlen);
-            pooled += dlen;
+            memcpy(pool + at, h2 + s + hs, (size_t)dlen);
             if (es) {
                 starts[n_msg] = msg_start;
-                ends[n_msg] = pooled;
+                ends[n_msg] = at + dlen;
                 ++n_msg;
-                msg_start = pooled;
+                msg_start = at + dlen;
             }
         }
     }
@@ -495,7 +497,9 @@ uint64_t orc_h2_deserialize_batch(const uint8_t* h2, uint64_t size, const uint64
     uint64_t off = 0, total;
     if (align == 0) align = 1;
     for (uint64_t m = 0; m < n_msg; ++m) {
-        int st = orc_parse_header(pool + starts[m], ends[m] - starts[m], 0, max_payload, &msg_desc[m]);
+        uint64_t end = ends[m] < pool_cap ? ends[m] : pool_cap;   /* pool bytes only */
+        uint64_t avail = end > starts[m] ? end - starts[m] : 0;
+        int st = orc_parse_header(pool + starts[m], avail, 0, max_payload, &msg_desc[m]);
         msg_desc[m].wire_off = starts[m];
         uint64_t len = st == ORC_PARSE_COMPLETE ? msg_desc[m].payload_size : 0;
         uint64_t next = off + (len + align - 1) / align * align;
