@@ -47,9 +47,11 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="target CPU time of the cpu_baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--workload", choices=["config2", "config3"], default="config2",
+    ap.add_argument("--workload", choices=["config2", "config3", "config5"], default="config2",
                     help="config2: uniform 64 KiB frames (the metric's config); config3: Zipf "
-                         "64 B-1 MiB messages in 1-8 continuation fragments, reassembled")
+                         "64 B-1 MiB messages in 1-8 continuation fragments, reassembled; "
+                         "config5: WebSocket over HTTP/2 DATA frames (--frame-size, default "
+                         "16376)")
     return ap.parse_args()
 
 
@@ -95,6 +97,69 @@ def load_traffic(kernel: str):
         return None
 
 
+def bench_h2(args, rank, world, dev):
+    """Config 5, device resident: WS frames -> HTTP/2 DATA frames (send) and
+    DATA frames -> pooled messages -> payloads (receive), per step."""
+    import numpy as np
+    import torch
+
+    from coldforce_amd import cfws, shard
+    from coldforce_amd import workloads as W
+    F = args.frames
+    fs = args.frame_size if args.frame_size != 65536 or "--frame-size" in sys.argv else 16376
+    S = cfws.H2_DEFAULT_MAX_FRAME_SIZE
+    desc_np, byte_base = shard.uniform_shard(F, fs, 5, rank, world)
+    payload = torch.empty(W.round16(F * fs) + 16, dtype=torch.uint8, device=dev)
+    cfws.fill_splitmix(payload, 0x5EED0005, byte_base)
+    offs, wtotal = W.wire_layout(desc_np)
+    wire = torch.empty(W.round16(wtotal) + 16, dtype=torch.uint8, device=dev)
+    h2 = torch.empty(cfws.h2_wrapped_bound(wire.numel(), F, S), dtype=torch.uint8, device=dev)
+    d_t = cfws.desc_to_device(desc_np, dev)
+    ws_s = torch.empty(cfws.lib().cfws_h2_serialize_workspace_size(F, wire.numel(), h2.numel(), S),
+                       dtype=torch.uint8, device=dev)
+    tot = torch.zeros(1, dtype=torch.int64, device=dev)
+    cfws.h2_serialize(payload, d_t, wire, h2, 1, S, ws_s, tot)
+    torch.cuda.synchronize()
+    h2_total = int(tot.item())
+    Wf = int(offs[1] - offs[0]) if F > 1 else wtotal
+    k = -(-Wf // S)
+    per = np.arange(F, dtype=np.uint64) * np.uint64(Wf + 9 * k)
+    starts = (per[:, None] + (np.arange(k, dtype=np.uint64) * np.uint64(S + 9))[None, :]).reshape(-1)
+    idx_t = torch.from_numpy(starts.astype(np.int64)).to(dev)
+    pool = torch.empty(h2_total, dtype=torch.uint8, device=dev)
+    back = torch.empty(F * fs + 64, dtype=torch.uint8, device=dev)
+    ws_d = torch.empty(cfws.lib().cfws_h2_deserialize_workspace_size(len(starts), pool.numel(),
+                                                                      back.numel()),
+                       dtype=torch.uint8, device=dev)
+
+    def step():
+        cfws.h2_serialize(payload, d_t, wire, h2, 1, S, ws_s, tot)
+        return cfws.h2_deserialize(h2, h2_total, idx_t, pool, back, S, align=1, ws_t=ws_d)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        st, md, ms, ptot, m = step()
+    torch.cuda.synchronize()
+    elapsed = shard.max_over_ranks(time.perf_counter() - t0, dev)
+    ok = (m == F and int(ptot.item()) == F * fs and bool((st == 0).all()) and bool((ms == 0).all())
+          and torch.equal(back[:F * fs], payload[:F * fs]))
+    line = {"metric": "WS-over-HTTP/2 payload GiB/s device-resident (config 5)",
+            "value": round(2.0 * F * fs * world * args.steps / elapsed / GIB, 2), "unit": "GiB/s",
+            "n_gpus": world, "steps": args.steps, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "config": {"workload": f"config5: {F} binary frames x {fs} B per GPU, client-mask + "
+                                   f"HTTP/2 DATA wrap (max frame {S}), then DATA unwrap + pool + "
+                                   f"server-unmask", "h2_bytes_per_gpu": h2_total,
+                       "data_frames_per_gpu": len(starts)},
+            "note": "two device passes per direction (WS codec pass + DATA framing pass)",
+            "verified": ok}
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    return 0 if ok else 1
+
+
 def main():
     args = parse()
     import torch
@@ -113,6 +178,11 @@ def main():
     cfws.init()
 
     F, fs = args.frames, args.frame_size
+    if args.workload == "config5":
+        rc = bench_h2(args, rank, world, dev)
+        if world > 1:
+            dist.destroy_process_group()
+        sys.exit(rc)
     flags = 0
     if args.workload == "config3":
         # each rank: its own 4 GiB Zipf batch (independent seed per rank)

@@ -25,9 +25,111 @@ sys.path.insert(0, ROOT)
 GIB = float(1 << 30)
 
 
+def e2e_h2(args):
+    """Config 5 host to host: payload (pinned) -> H2D -> WS serialize + HTTP/2
+    DATA wrap -> D2H DATA stream, and back (H2D -> unwrap + pool + unmask ->
+    D2H), chunks of frames overlapped on `depth` streams."""
+    import numpy as np
+    import torch
+
+    from coldforce_amd import cfws
+    from coldforce_amd import workloads as W
+    F = args.frames
+    fs = 16376 if args.frame_size == 65536 and "--frame-size" not in sys.argv else args.frame_size
+    S = cfws.H2_DEFAULT_MAX_FRAME_SIZE
+    CF = max(1, (args.chunk_mib << 20) // fs)           # frames per chunk
+    desc = W.uniform_batch(F, fs, 5)
+    hs = int(cfws.header_sizes(np.array([fs]), np.array([1]))[0])
+    Wf = fs + hs
+    k = -(-Wf // S)
+    Hf = Wf + 9 * k                                       # DATA-stream bytes per WS frame
+    payload = torch.empty(F * fs, dtype=torch.uint8, pin_memory=True)
+    h2 = torch.empty(F * Hf, dtype=torch.uint8, pin_memory=True)
+    back = torch.empty(F * fs, dtype=torch.uint8, pin_memory=True)
+    dev = torch.empty(F * fs, dtype=torch.uint8, device="cuda")
+    cfws.fill_splitmix(dev, 0x5EED0005)
+    payload.copy_(dev)
+    del dev
+    streams = [torch.cuda.Stream() for _ in range(args.depth)]
+    chunks = [(c0, min(F, c0 + CF)) for c0 in range(0, F, CF)]
+    descs = []
+    for c0, c1 in chunks:
+        d = desc[c0:c1].copy()
+        d["payload_off"] -= np.uint64(c0 * fs)
+        descs.append(cfws.desc_to_device(d))
+    per = np.arange(CF, dtype=np.uint64) * np.uint64(Hf)
+    starts = (per[:, None] + (np.arange(k, dtype=np.uint64) * np.uint64(S + 9))[None, :]).reshape(-1)
+    slot = []
+    for s in range(args.depth):
+        with torch.cuda.stream(streams[s]):
+            pay_d = torch.empty(CF * fs + 16, dtype=torch.uint8, device="cuda")
+            wire_d = torch.empty(CF * Wf + 32, dtype=torch.uint8, device="cuda")
+            h2_d = torch.empty(cfws.h2_wrapped_bound(wire_d.numel(), CF, S), dtype=torch.uint8, device="cuda")
+            pool_d = torch.empty(CF * Wf + 16, dtype=torch.uint8, device="cuda")
+            back_d = torch.empty(CF * fs + 64, dtype=torch.uint8, device="cuda")
+            ws_s = torch.empty(cfws.lib().cfws_h2_serialize_workspace_size(CF, wire_d.numel(), h2_d.numel(), S),
+                               dtype=torch.uint8, device="cuda")
+            ws_d = torch.empty(cfws.lib().cfws_h2_deserialize_workspace_size(CF * k, pool_d.numel(),
+                                                                            back_d.numel()),
+                               dtype=torch.uint8, device="cuda")
+            idx = torch.from_numpy(starts.astype(np.int64)).cuda()
+            tot = torch.zeros(1, dtype=torch.int64, device="cuda")
+        slot.append((pay_d, wire_d, h2_d, pool_d, back_d, ws_s, ws_d, idx, tot))
+    torch.cuda.synchronize()
+
+    def ser():
+        for c, (c0, c1) in enumerate(chunks):
+            s = c % args.depth
+            st = streams[s]
+            pay_d, wire_d, h2_d, _, _, ws_s, _, _, tot = slot[s]
+            with torch.cuda.stream(st):
+                pay_d[:(c1 - c0) * fs].copy_(payload[c0 * fs:c1 * fs], non_blocking=True)
+                cfws.h2_serialize(pay_d, descs[c], wire_d, h2_d, 1, S, ws_s, tot, stream=st)
+                h2[c0 * Hf:c1 * Hf].copy_(h2_d[:(c1 - c0) * Hf], non_blocking=True)
+        torch.cuda.synchronize()
+
+    def de():
+        ok = True
+        for c, (c0, c1) in enumerate(chunks):
+            s = c % args.depth
+            st = streams[s]
+            _, _, h2_d, pool_d, back_d, _, ws_d, idx, _ = slot[s]
+            n = c1 - c0
+            with torch.cuda.stream(st):
+                h2_d[:n * Hf].copy_(h2[c0 * Hf:c1 * Hf], non_blocking=True)
+                hs_, md, ms, ptot, m = cfws.h2_deserialize(h2_d, n * Hf, idx[:n * k], pool_d, back_d,
+                                                           S, align=1, ws_t=ws_d, stream=st)
+                back[c0 * fs:c1 * fs].copy_(back_d[:n * fs], non_blocking=True)
+                ok = ok and m == n
+        torch.cuda.synchronize()
+        return ok
+
+    ser()
+    t0 = time.perf_counter()
+    for _ in range(args.reps):
+        ser()
+    t_ser = (time.perf_counter() - t0) / args.reps
+    de()
+    t0 = time.perf_counter()
+    for _ in range(args.reps):
+        ok = de()
+    t_de = (time.perf_counter() - t0) / args.reps
+    nbytes = F * fs
+    ok = ok and torch.equal(back, payload)
+    line = {"what": "config 5 host-to-host (PCIe-inclusive): WS over HTTP/2 DATA frames",
+            "workload": "config5", "frames": F, "payload_bytes": nbytes, "h2_bytes": F * Hf,
+            "data_frames": F * k, "chunk_frames": CF, "depth": args.depth,
+            "serialize_s": round(t_ser, 4), "deserialize_s": round(t_de, 4),
+            "serialize_GiBps": round(nbytes / t_ser / GIB, 2),
+            "deserialize_GiBps": round(nbytes / t_de / GIB, 2),
+            "round_trip_GiBps": round(2 * nbytes / (t_ser + t_de) / GIB, 2), "verified": ok}
+    print(json.dumps(line), flush=True)
+    return 0 if ok else 1
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--workload", choices=["config2", "config3"], default="config2")
+    ap.add_argument("--workload", choices=["config2", "config3", "config5"], default="config2")
     ap.add_argument("--frames", type=int, default=65536)
     ap.add_argument("--frame-size", type=int, default=65536)
     ap.add_argument("--chunk-mib", type=int, default=64)
@@ -42,6 +144,8 @@ def main():
     from coldforce_amd import workloads as W
 
     cfws.init()
+    if args.workload == "config5":
+        sys.exit(e2e_h2(args))
     if args.workload == "config3":
         c3 = W.CONFIG3
         desc, msgs = W.zipf_batch(c3["target_bytes"], c3["seed"], c3["key_seed"])
