@@ -264,8 +264,8 @@ def main():
     dom_name = "serialize_execute" if ser_ms >= de_ms else "deserialize_execute"
     dom_ms = max(ser_ms, de_ms)
     achieved = alg_bytes / (dom_ms * 1e-3) / 1e9
-    kernel_symbol = ("xform_kernel<true>" if dom_name == "serialize_execute"
-                     else "xform_kernel<false>")
+    kernel_symbol = ("xform_kernel<0>" if dom_name == "serialize_execute"   # kModeSer
+                     else "xform_kernel<1>")                                 # kModeDeser
     total_payload = 2.0 * arena_bytes * world * args.steps
     line = {
         "metric": METRIC,
