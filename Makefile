@@ -7,8 +7,7 @@
 HIPCC    ?= /opt/rocm/bin/hipcc
 ARCH     ?= gfx950
 HIPFLAGS ?= -O3 -std=c++17 -fPIC -Wall -Wno-unused-result
-SRC      := coldforce_amd/csrc/cfws_device.hip coldforce_amd/csrc/cfws_frame.cpp \
-            coldforce_amd/csrc/cfws_pipeline.cpp
+HOSTSRC  := cfws_frame cfws_pipeline cfws_index
 HDR      := include/cfws.h include/cfws_co_ws_frame.h coldforce_amd/csrc/cfws_internal.h
 LIB      := coldforce_amd/libcfws.so
 OBJDIR   := build
@@ -19,15 +18,11 @@ $(OBJDIR)/cfws_device.o: coldforce_amd/csrc/cfws_device.hip $(HDR)
 	@mkdir -p $(OBJDIR)
 	$(HIPCC) --offload-arch=$(ARCH) $(HIPFLAGS) -Iinclude -Icoldforce_amd/csrc -c $< -o $@
 
-$(OBJDIR)/cfws_frame.o: coldforce_amd/csrc/cfws_frame.cpp $(HDR)
+$(OBJDIR)/%.o: coldforce_amd/csrc/%.cpp $(HDR)
 	@mkdir -p $(OBJDIR)
 	$(HIPCC) --offload-arch=$(ARCH) $(HIPFLAGS) -Iinclude -Icoldforce_amd/csrc -c $< -o $@
 
-$(OBJDIR)/cfws_pipeline.o: coldforce_amd/csrc/cfws_pipeline.cpp $(HDR)
-	@mkdir -p $(OBJDIR)
-	$(HIPCC) --offload-arch=$(ARCH) $(HIPFLAGS) -Iinclude -Icoldforce_amd/csrc -c $< -o $@
-
-$(LIB): $(OBJDIR)/cfws_device.o $(OBJDIR)/cfws_frame.o $(OBJDIR)/cfws_pipeline.o
+$(LIB): $(OBJDIR)/cfws_device.o $(addprefix $(OBJDIR)/,$(addsuffix .o,$(HOSTSRC)))
 	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $^
 
 oracle:
@@ -51,8 +46,7 @@ clean:
 variant: $(HDR)
 	@mkdir -p $(OBJDIR)/variants/$(V)
 	$(HIPCC) --offload-arch=$(ARCH) $(HIPFLAGS) $(F) -Iinclude -Icoldforce_amd/csrc -c coldforce_amd/csrc/cfws_device.hip -o $(OBJDIR)/variants/$(V)/cfws_device.o
-	$(HIPCC) --offload-arch=$(ARCH) $(HIPFLAGS) $(F) -Iinclude -Icoldforce_amd/csrc -c coldforce_amd/csrc/cfws_frame.cpp -o $(OBJDIR)/variants/$(V)/cfws_frame.o
-	$(HIPCC) --offload-arch=$(ARCH) $(HIPFLAGS) $(F) -Iinclude -Icoldforce_amd/csrc -c coldforce_amd/csrc/cfws_pipeline.cpp -o $(OBJDIR)/variants/$(V)/cfws_pipeline.o
-	$(HIPCC) --offload-arch=$(ARCH) -shared -o $(OBJDIR)/variants/libcfws_$(V).so $(OBJDIR)/variants/$(V)/cfws_device.o $(OBJDIR)/variants/$(V)/cfws_frame.o $(OBJDIR)/variants/$(V)/cfws_pipeline.o
+	for h in $(HOSTSRC); do $(HIPCC) --offload-arch=$(ARCH) $(HIPFLAGS) $(F) -Iinclude -Icoldforce_amd/csrc -c coldforce_amd/csrc/$$h.cpp -o $(OBJDIR)/variants/$(V)/$$h.o || exit 1; done
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o $(OBJDIR)/variants/libcfws_$(V).so $(OBJDIR)/variants/$(V)/*.o
 
 .PHONY: variant

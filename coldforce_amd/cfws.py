@@ -47,9 +47,10 @@ BATCH_SYMBOLS = (
     "cfws_deserialize_plan", "cfws_deserialize_execute", "cfws_deserialize_batch",
     "cfws_xor_mask", "cfws_draw_mask_keys", "cfws_release_thread_resources",
     "cfws_fill_splitmix", "cfws_pipeline_create", "cfws_pipeline_destroy",
-    "cfws_pipeline_serialize", "cfws_pipeline_deserialize",
+    "cfws_pipeline_serialize", "cfws_pipeline_deserialize", "cfws_pipeline_receive",
     "cfws_h2_serialize_workspace_size", "cfws_h2_serialize_batch",
     "cfws_h2_deserialize_workspace_size", "cfws_h2_deserialize_batch",
+    "cfws_index_frames", "cfws_index_workspace_size", "cfws_index_frames_batch",
 )
 DROPIN_SYMBOLS = (
     "co_ws_frame_serialize", "co_ws_frame_deserialize", "co_ws_frame_create",
@@ -116,11 +117,19 @@ def lib(path: str = LIB_PATH) -> C.CDLL:
         "cfws_h2_deserialize_batch": ([_vp, _u64, _vp, _sz, _u32, _vp, _vp, _u64, _u64, _u32, _vp,
                                        _vp, _vp, _u64, _vp, C.POINTER(_sz), _vp, _sz, _vp],
                                       C.c_int),
+        "cfws_index_frames": ([_vp, _u64, _u64, _u64, _vp, _sz, C.POINTER(_u64),
+                               C.POINTER(C.c_int32)], _sz),
+        "cfws_index_workspace_size": ([_sz], _sz),
+        "cfws_index_frames_batch": ([_vp, _vp, _vp, _sz, _u64, _vp, _u64, _vp, _vp, _vp, _vp, _vp,
+                                     _sz, _vp], C.c_int),
         "cfws_pipeline_create": ([_u64, _sz, C.c_int, C.POINTER(_vp)], C.c_int),
         "cfws_pipeline_destroy": ([_vp], None),
         "cfws_pipeline_serialize": ([_vp, _vp, _vp, _sz, _vp, _u64, C.POINTER(_u64)], C.c_int),
         "cfws_pipeline_deserialize": ([_vp, _vp, _u64, _vp, _sz, _u64, _u32, _u32, _vp, _vp, _vp,
                                        _u64, C.POINTER(_u64)], C.c_int),
+        "cfws_pipeline_receive": ([_vp, _vp, _u64, _u64, _u64, _u32, _vp, _vp, C.POINTER(_sz),
+                                   C.POINTER(_u64), C.POINTER(C.c_int32), _vp, _u64,
+                                   C.POINTER(_u64)], C.c_int),
         "co_ws_frame_serialize": ([C.c_bool, C.c_uint8, C.c_bool, _vp, _sz, C.POINTER(CoArray)],
                                   C.c_bool),
         "co_ws_frame_deserialize": ([C.POINTER(CoWsFrame), _vp, _sz, C.POINTER(C.c_size_t)],
@@ -398,6 +407,49 @@ def h2_deserialize(h2_t, h2_size: int, index_t, pool_t, payload_t, S: int = H2_D
     return h2_status, msg_desc[:m], msg_status[:m], total, m
 
 
+# ---- receive-buffer frame indexing -----------------------------------------
+INDEX_FULL = 2
+
+
+def index_frames(buf: np.ndarray, begin: int = 0, end: int | None = None,
+                 max_payload: int = DEFAULT_MAX_PAYLOAD, max_starts: int | None = None):
+    """Host receive-loop walk of one connection's bytes buf[begin, end)
+    (cfws_index_frames): (starts, consumed, stop)."""
+    end = buf.size if end is None else end
+    cap = max((end - begin) // 2 + 1, 1) if max_starts is None else max_starts
+    starts = np.zeros(max(cap, 1), dtype=np.uint64)
+    b = buf if buf.size else np.zeros(1, np.uint8)
+    consumed, stop = _u64(0), C.c_int32(0)
+    k = lib().cfws_index_frames(b.ctypes.data, begin, end, max_payload, starts.ctypes.data, cap,
+                                C.byref(consumed), C.byref(stop))
+    return starts[:k], int(consumed.value), int(stop.value)
+
+
+def index_frames_batch(buf_t, begin_t, end_t, max_payload: int = DEFAULT_MAX_PAYLOAD,
+                       starts_t=None, ws_t=None, stream=None):
+    """Device receive-loop walk of many connections at once
+    (cfws_index_frames_batch). Returns (starts_t, first_t, consumed_t,
+    stop_t, total) -- total synchronises."""
+    import torch
+    n = begin_t.numel()
+    dev = buf_t.device
+    if starts_t is None:
+        span = int((end_t - begin_t).clamp(min=0).sum().item()) if n else 0
+        starts_t = torch.empty(max(span // 2 + n, 1), dtype=torch.int64, device=dev)
+    first = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
+    consumed = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
+    stop = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+    total = torch.zeros(1, dtype=torch.int64, device=dev)
+    if ws_t is None:
+        ws_t = torch.empty(lib().cfws_index_workspace_size(n), dtype=torch.uint8, device=dev)
+    _check(lib().cfws_index_frames_batch(_p(buf_t), _p(begin_t), _p(end_t), n, max_payload,
+                                         _p(starts_t), starts_t.numel(), _p(first), _p(consumed),
+                                         _p(stop), _p(total), _p(ws_t), ws_t.numel(),
+                                         _stream(stream)),
+           "cfws_index_frames_batch")
+    return starts_t, first[:n], consumed[:n], stop[:n], int(total.item())
+
+
 # ---- host-memory pipeline --------------------------------------------------
 
 class Pipeline:
@@ -442,3 +494,19 @@ class Pipeline:
                                                payload_capacity, C.byref(tot)),
                "cfws_pipeline_deserialize")
         return desc, status, tot.value
+
+    def receive(self, wire_ptr: int, begin: int, end: int, payload_ptr: int, payload_capacity: int,
+                max_frames: int, align: int = 16, max_payload: int = DEFAULT_MAX_PAYLOAD):
+        """The receive loop over host bytes [begin, end): index + deserialize.
+        Returns (desc, status, consumed, stop, total)."""
+        desc = np.zeros(max(max_frames, 1), dtype=DESC_DTYPE)
+        status = np.zeros(max(max_frames, 1), dtype=np.int32)
+        n = C.c_size_t(max_frames)
+        consumed, stop, tot = C.c_uint64(), C.c_int32(), C.c_uint64()
+        _check(lib().cfws_pipeline_receive(self.h, wire_ptr, begin, end, max_payload, align,
+                                           desc.ctypes.data, status.ctypes.data, C.byref(n),
+                                           C.byref(consumed), C.byref(stop), payload_ptr,
+                                           payload_capacity, C.byref(tot)),
+               "cfws_pipeline_receive")
+        k = n.value
+        return desc[:k], status[:k], consumed.value, stop.value, tot.value

@@ -628,10 +628,55 @@ serialize_sizes_kernel(cfws_frame_desc_t* __restrict__ desc, uint64_t* __restric
     vals[f] = hs + len;
 }
 
-// Header decode at index[f] (co_ws_frame.c:131-213), with the callers'
-// two-byte precheck (co_ws_client.c:202-206). Writes the layout sizes of
-// both passes: vals0 = data (or every frame without reassembly), vals1 =
-// control frames when reassembling.
+// WS header at s of data[0, size) (co_ws_frame.c:131-213), with the callers'
+// two-byte precheck (co_ws_client.c:202-206): the reference's decisions in
+// its order (MORE_DATA before DATA_TOO_BIG). d gets what the reference has
+// written into the frame by the time it returns.
+__device__ __forceinline__ int32_t parse_ws_header(const uint8_t* __restrict__ wire, uint64_t size,
+                                                   uint64_t s, uint64_t max_payload,
+                                                   cfws_frame_desc_t& d)
+{
+    d.payload_off = 0;
+    d.wire_off = s;
+    d.payload_size = 0;
+    d.mask_key = 0;
+    d.fin = 0;
+    d.opcode = 0;
+    d.mask = 0;
+    d.header_size = 0;
+    if (s > size || size - s < 2) return CFWS_PARSE_MORE_DATA;
+    const uint32_t b0 = wire[s], b1 = wire[s + 1];
+    d.fin = (uint8_t)(b0 >> 7);
+    d.opcode = (uint8_t)(b0 & 0x7fu);
+    if (d.opcode > 0x0f) return CFWS_ERROR_INVALID_FRAME;
+    d.mask = (uint8_t)(b1 >> 7);
+    const uint32_t l7 = b1 & 0x7fu;
+    uint64_t p = s + 2;
+    if (l7 <= 125) {
+        d.payload_size = l7;
+    } else {
+        const uint32_t ext = (l7 == 126) ? 2u : 8u;
+        if (size - p < ext) return CFWS_PARSE_MORE_DATA;
+        uint64_t len = 0;
+        for (uint32_t i = 0; i < ext; ++i) len = (len << 8) | wire[p + i];
+        d.payload_size = len;
+        p += ext;
+    }
+    if (d.mask) {
+        if (size - p < 4) return CFWS_PARSE_MORE_DATA;
+        d.mask_key = (uint32_t)wire[p] | (uint32_t)wire[p + 1] << 8 |
+                     (uint32_t)wire[p + 2] << 16 | (uint32_t)wire[p + 3] << 24;
+        p += 4;
+    }
+    d.header_size = (uint8_t)(p - s);
+    if (size - p < d.payload_size) return CFWS_PARSE_MORE_DATA;
+    if (d.payload_size > max_payload) return CFWS_ERROR_DATA_TOO_BIG;
+    return CFWS_PARSE_COMPLETE;
+}
+
+// Header decode at index[f]. Writes the layout sizes of both passes:
+// vals0 = data (or every frame without reassembly), vals1 = control frames
+// when reassembling.
 __global__ void __launch_bounds__(kThreads)
 deserialize_parse_kernel(const uint8_t* __restrict__ wire, uint64_t wire_size_all,
                          const uint64_t* __restrict__ index, const uint64_t* __restrict__ ends,
@@ -642,49 +687,11 @@ deserialize_parse_kernel(const uint8_t* __restrict__ wire, uint64_t wire_size_al
 {
     const uint64_t f = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
     if (f >= n) return;
-    const uint64_t s = index[f];
     // data_size of the call: the whole buffer, or this frame's own message
     // (co_http2_stream_receive_ws_frame passes the pooled DATA, :144-146)
     const uint64_t wire_size = ends && ends[f] < wire_size_all ? ends[f] : wire_size_all;
     cfws_frame_desc_t d;
-    d.payload_off = 0;
-    d.wire_off = s;
-    d.payload_size = 0;
-    d.mask_key = 0;
-    d.fin = 0;
-    d.opcode = 0;
-    d.mask = 0;
-    d.header_size = 0;
-    int32_t st = CFWS_PARSE_COMPLETE;
-    do {
-        if (s > wire_size || wire_size - s < 2) { st = CFWS_PARSE_MORE_DATA; break; }
-        const uint32_t b0 = wire[s], b1 = wire[s + 1];
-        d.fin = (uint8_t)(b0 >> 7);
-        d.opcode = (uint8_t)(b0 & 0x7fu);
-        if (d.opcode > 0x0f) { st = CFWS_ERROR_INVALID_FRAME; break; }
-        d.mask = (uint8_t)(b1 >> 7);
-        const uint32_t l7 = b1 & 0x7fu;
-        uint64_t p = s + 2;
-        if (l7 <= 125) {
-            d.payload_size = l7;
-        } else {
-            const uint32_t ext = (l7 == 126) ? 2u : 8u;
-            if (wire_size - p < ext) { st = CFWS_PARSE_MORE_DATA; break; }
-            uint64_t len = 0;
-            for (uint32_t i = 0; i < ext; ++i) len = (len << 8) | wire[p + i];
-            d.payload_size = len;
-            p += ext;
-        }
-        if (d.mask) {
-            if (wire_size - p < 4) { st = CFWS_PARSE_MORE_DATA; break; }
-            d.mask_key = (uint32_t)wire[p] | (uint32_t)wire[p + 1] << 8 |
-                         (uint32_t)wire[p + 2] << 16 | (uint32_t)wire[p + 3] << 24;
-            p += 4;
-        }
-        d.header_size = (uint8_t)(p - s);
-        if (wire_size - p < d.payload_size) { st = CFWS_PARSE_MORE_DATA; break; }
-        if (d.payload_size > max_payload) { st = CFWS_ERROR_DATA_TOO_BIG; break; }
-    } while (0);
+    const int32_t st = parse_ws_header(wire, wire_size, index[f], max_payload, d);
     desc[f] = d;
     status[f] = st;
     const uint64_t len = (st == CFWS_PARSE_COMPLETE) ? d.payload_size : 0;
@@ -1039,6 +1046,45 @@ h2_starts_kernel(const uint64_t* __restrict__ ends, const uint64_t* __restrict__
     const uint64_t m = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
     if (m >= n || m >= *n_msg_p) return;
     starts[m] = m == 0 ? 0 : ends[m - 1];
+}
+
+// ---------------------------------------------------------------------------
+// receive-buffer frame indexing (co_ws_server.c:107-169)
+// ---------------------------------------------------------------------------
+
+// One connection per thread: the receive loop's walk over buf[begin, end).
+// The walk is a chain of dependent header reads, so a connection is one
+// thread and the parallelism is across connections (a server's event loop
+// tick holds the receive buffers of many). Pass 1 (kWrite = false) counts
+// and records consumed / stop; pass 2 walks again and writes the starts at
+// the scanned offsets.
+template <bool kWrite>
+__global__ void __launch_bounds__(kThreads)
+index_walk_kernel(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ begin,
+                  const uint64_t* __restrict__ end, uint64_t n, uint64_t max_payload,
+                  uint64_t* __restrict__ first, uint64_t* __restrict__ consumed,
+                  int32_t* __restrict__ stop, uint64_t* __restrict__ starts, uint64_t cap)
+{
+    const uint64_t c = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
+    if (c >= n) return;
+    const uint64_t e = end[c];
+    uint64_t p = begin[c];
+    uint64_t k = kWrite ? first[c] : 0;
+    int32_t st = CFWS_PARSE_COMPLETE;
+    while (e > p) {
+        if (e - p < 2) { st = CFWS_PARSE_MORE_DATA; break; }
+        cfws_frame_desc_t d;
+        st = parse_ws_header(buf, e, p, max_payload, d);
+        if (st != CFWS_PARSE_COMPLETE) break;
+        if (kWrite && k < cap) starts[k] = p;
+        ++k;
+        p += d.header_size + d.payload_size;
+    }
+    if (!kWrite) {
+        first[c] = k;
+        consumed[c] = p;
+        stop[c] = st;
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1478,6 +1524,38 @@ int cfws_h2_deserialize_batch(const void* d_h2, uint64_t h2_size, const uint64_t
         return rc;
     return cfws_deserialize_execute(d_pool, d_msg_desc, d_msg_status, n_msg, 0, d_payload,
                                     payload_cap, wsd, stream);
+}
+
+size_t cfws_index_workspace_size(size_t n_conns)
+{
+    return 64 + sizeof(uint64_t) * (size_t)grid_for(n_conns, kScanBlock);
+}
+
+int cfws_index_frames_batch(const void* d_buf, const uint64_t* d_begin, const uint64_t* d_end,
+                            size_t n, uint64_t max_payload, uint64_t* d_starts, uint64_t cap,
+                            uint64_t* d_first, uint64_t* d_consumed, int32_t* d_stop,
+                            uint64_t* d_total, void* ws, size_t ws_size, void* stream)
+{
+    if (int rc = check_init()) return rc;
+    if (ws_size < cfws_index_workspace_size(n))
+        return set_err(CFWS_ERROR_WORKSPACE, "index workspace too small", hipSuccess);
+    if ((n && (!d_buf || !d_begin || !d_end || !d_first || !d_consumed || !d_stop)) ||
+        (cap && !d_starts) || !d_total || !ws)
+        return set_err(CFWS_ERROR_INVALID_ARGUMENT, "index: null pointer", hipSuccess);
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    if (n == 0) {
+        (void)hipMemsetAsync(d_total, 0, 8, st);
+        return launch_check("index");
+    }
+    const uint8_t* buf = static_cast<const uint8_t*>(d_buf);
+    uint64_t* partials = ws_ptr<uint64_t>(ws, 64);
+    const uint32_t g = grid_for(n, kThreads);
+    index_walk_kernel<false><<<g, kThreads, 0, st>>>(buf, d_begin, d_end, n, max_payload, d_first,
+                                                     d_consumed, d_stop, nullptr, 0);
+    if (int rc = run_scan(d_first, n, partials, d_total, st)) return rc;
+    index_walk_kernel<true><<<g, kThreads, 0, st>>>(buf, d_begin, d_end, n, max_payload, d_first,
+                                                    nullptr, nullptr, d_starts, cap);
+    return launch_check("index");
 }
 
 int cfws_xor_mask(const void* d_src, void* d_dst, uint64_t n, uint32_t key, uint32_t phase,

@@ -311,4 +311,24 @@ int cfws_pipeline_deserialize(cfws_pipeline_t* p, const void* h_wire, uint64_t w
     return CFWS_OK;
 }
 
+int cfws_pipeline_receive(cfws_pipeline_t* p, const void* h_wire, uint64_t begin, uint64_t end,
+                          uint64_t max_payload, uint32_t align, cfws_frame_desc_t* h_desc,
+                          int32_t* h_status, size_t* n_frames, uint64_t* consumed, int32_t* stop,
+                          void* h_payload, uint64_t payload_capacity, uint64_t* payload_total)
+{
+    if (!p || !n_frames || (end > begin && !h_wire)) return fail("null argument");
+    // the receive loop's walk (co_ws_server.c:107-169) on the host, where the
+    // bytes are; its starts drive the chunked device deserialize
+    std::vector<uint64_t> starts(*n_frames ? *n_frames : 1);
+    uint64_t used = begin;
+    int32_t why = CFWS_PARSE_COMPLETE;
+    const size_t n = cfws_index_frames(h_wire, begin, end, max_payload, starts.data(), *n_frames,
+                                       &used, &why);
+    *n_frames = n;
+    if (consumed) *consumed = used;
+    if (stop) *stop = why;
+    return cfws_pipeline_deserialize(p, h_wire, end, starts.data(), n, max_payload, align, 0,
+                                     h_desc, h_status, h_payload, payload_capacity, payload_total);
+}
+
 }  // extern "C"

@@ -135,6 +135,45 @@ int cfws_deserialize_batch(const void* d_wire, uint64_t wire_size,
                            uint64_t* d_payload_total, void* d_workspace,
                            size_t workspace_size, void* stream);
 
+/* ---- receive-buffer frame indexing --------
+ * The frame walk of the receive loops co_ws_server_on_tcp_receive_ready
+ * (co_ws_server.c:107-169) / co_ws_client_on_tcp_receive_ready
+ * (co_ws_client.c:200-270) over one connection's received bytes
+ * buf[begin, end): from the receive index `begin`, while bytes remain, stop
+ * when fewer than 2 are left or a frame does not parse COMPLETE against
+ * data_size = end (co_ws_frame_deserialize's decisions, co_ws_frame.c
+ * :131-213, with max_payload as co_ws_config_get_max_receive_payload_size).
+ * Per connection it reports the starts of the COMPLETE frames, the receive
+ * index after them (*consumed, where the reference leaves
+ * receive_data.index) and why the walk stopped (*stop):
+ *   CFWS_PARSE_COMPLETE      every byte consumed (the loop clears the buffer)
+ *   CFWS_PARSE_MORE_DATA     under 2 bytes left, or a frame incomplete: wait
+ *   CFWS_ERROR_INVALID_FRAME the frame at *consumed is not WS (HTTP fallback
+ *                            / close 1002, co_ws_client.c:62-71)
+ *   CFWS_ERROR_DATA_TOO_BIG  the frame at *consumed exceeds max_payload
+ *                            (close 1009)
+ *   CFWS_INDEX_FULL          host form only: `starts` is full and another
+ *                            COMPLETE frame follows; resume at *consumed.
+ * The starts feed cfws_deserialize_* (every frame they name is COMPLETE).
+ *
+ * Host form: one connection, on the calling thread (receive buffers in host
+ * memory). Returns the number of starts written. */
+#define CFWS_INDEX_FULL 2
+size_t cfws_index_frames(const void* h_buf, uint64_t begin, uint64_t end, uint64_t max_payload,
+                         uint64_t* starts, size_t max_starts, uint64_t* consumed, int32_t* stop);
+
+/* Device form: n_conns connections of one device arena at once, connection
+ * c = d_buf[d_begin[c], d_end[c]). d_first[c] = index of c's first start in
+ * d_starts (exclusive prefix sum of the per-connection counts), *d_total =
+ * all starts (unclamped); starts at positions >= starts_capacity are not
+ * written. d_consumed / d_stop per connection as above. */
+size_t cfws_index_workspace_size(size_t n_conns);
+int cfws_index_frames_batch(const void* d_buf, const uint64_t* d_begin, const uint64_t* d_end,
+                            size_t n_conns, uint64_t max_payload, uint64_t* d_starts,
+                            uint64_t starts_capacity, uint64_t* d_first, uint64_t* d_consumed,
+                            int32_t* d_stop, uint64_t* d_total, void* d_workspace,
+                            size_t workspace_size, void* stream);
+
 /* ---- WebSocket over HTTP/2 (src/ws_http2) ---------------------------------
  * Send: every WS frame of the batch is serialized (cfws_serialize_batch, into
  * d_wire) and carried in HTTP/2 DATA frames of at most max_frame_size payload
@@ -200,6 +239,16 @@ int cfws_pipeline_deserialize(cfws_pipeline_t* pipeline, const void* h_wire,
                               uint32_t flags, cfws_frame_desc_t* h_desc, int32_t* h_status,
                               void* h_payload, uint64_t payload_capacity,
                               uint64_t* payload_total);
+/* The receive loop over one host buffer h_wire[begin, end): cfws_index_frames
+ * (on the calling thread) then cfws_pipeline_deserialize of the COMPLETE
+ * frames it found. *n_frames: in, the capacity of h_desc / h_status; out,
+ * the frames deserialized. *consumed / *stop as cfws_index_frames reports
+ * them (CFWS_INDEX_FULL: more frames follow; call again from *consumed). */
+int cfws_pipeline_receive(cfws_pipeline_t* pipeline, const void* h_wire, uint64_t begin,
+                          uint64_t end, uint64_t max_payload, uint32_t align,
+                          cfws_frame_desc_t* h_desc, int32_t* h_status, size_t* n_frames,
+                          uint64_t* consumed, int32_t* stop, void* h_payload,
+                          uint64_t payload_capacity, uint64_t* payload_total);
 
 /* ---- single-buffer XOR (used by the per-frame drop-in path) --------------
  * d_dst[i] = d_src[i] ^ key byte (i + key_phase) % 4, i < n. */

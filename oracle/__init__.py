@@ -145,6 +145,22 @@ def index_frames(wire: np.ndarray, max_frames: int, max_payload: int = DEFAULT_M
     return starts[:k], int(consumed.value)
 
 
+def index_stream(buf: np.ndarray, begin: int = 0, end: int | None = None,
+                 max_payload: int = DEFAULT_MAX_PAYLOAD):
+    """One connection's receive loop over buf[begin, end) (orc_index_stream):
+    (starts, consumed, stop)."""
+    end = len(buf) if end is None else end
+    f = lib().orc_index_stream
+    f.argtypes = [_vp, _u64, _u64, _u64, _vp, _sz, C.POINTER(_u64), C.POINTER(C.c_int32)]
+    f.restype = _sz
+    b = buf if buf.size else np.zeros(1, np.uint8)
+    cap = max((end - begin) // 2 + 1, 1)
+    starts = np.zeros(cap, dtype=np.uint64)
+    consumed, stop = _u64(0), C.c_int32(0)
+    k = f(_ptr(b), begin, end, max_payload, _ptr(starts), cap, C.byref(consumed), C.byref(stop))
+    return starts[:k], int(consumed.value), int(stop.value)
+
+
 def fill_splitmix(n_bytes: int, seed: int, byte_base: int = 0) -> np.ndarray:
     out = np.zeros(max(n_bytes, 1), dtype=np.uint8)
     lib().orc_fill_splitmix(_ptr(out), n_bytes, seed, byte_base)
@@ -325,6 +341,22 @@ def ref_h2_send(R, ws: bytes, S: int = 16384, sid: int = 1) -> bytes:
     k = f(_ptr(src), len(ws), S, sid, _ptr(out), out.size)
     assert k >= 0
     return out[:k].tobytes()
+
+
+def ref_index_stream(R, data: bytes, begin: int = 0, max_payload: int = DEFAULT_MAX_PAYLOAD):
+    """The reference's receive loop (co_ws_server.c:107-169) around its own
+    co_ws_frame_deserialize: (starts, consumed, stop)."""
+    f = R.ref_index_stream
+    f.argtypes = [_vp, C.c_ulonglong, C.c_ulonglong, C.c_ulonglong, _vp, C.c_ulonglong,
+                  C.POINTER(C.c_ulonglong), C.POINTER(C.c_int)]
+    f.restype = C.c_longlong
+    src = np.frombuffer(data, dtype=np.uint8) if data else np.zeros(1, np.uint8)
+    cap = len(data) // 2 + 1
+    starts = np.zeros(cap, dtype=np.uint64)
+    consumed, stop = C.c_ulonglong(), C.c_int()
+    k = f(_ptr(src), len(data), begin, max_payload, _ptr(starts), cap, C.byref(consumed),
+          C.byref(stop))
+    return starts[:k], int(consumed.value), int(stop.value)
 
 
 def ref_h2_recv(R, data: bytes, index: int = 0, S: int = 16384):

@@ -311,6 +311,33 @@ uint64_t orc_deserialize_batch(const uint8_t* wire, uint64_t wire_size,
     return total;
 }
 
+/* The receive loop of co_ws_server_on_tcp_receive_ready
+ * (co_ws_server.c:107-169; co_ws_client.c:200-270 is the same walk) over one
+ * connection's received bytes buf[begin, end): stop when under 2 bytes
+ * remain (:109-113) or a frame is not COMPLETE (:144-166); the receive index
+ * advances only over COMPLETE frames (co_ws_frame.c:244). */
+size_t orc_index_stream(const uint8_t* buf, uint64_t begin, uint64_t end, uint64_t max_payload,
+                        uint64_t* starts, size_t max_frames, uint64_t* consumed, int32_t* stop)
+{
+    size_t k = 0;
+    uint64_t p = begin;
+    int32_t st = ORC_PARSE_COMPLETE;
+    orc_desc_t d;
+    while (end > p) {
+        if (end - p < 2) { st = ORC_PARSE_MORE_DATA; break; }
+        /* the frame's data_size is the whole receive buffer: bytes before
+         * `begin` are only ever skipped, so parse the tail from p. */
+        st = orc_parse_header(buf, end, p, max_payload, &d);
+        if (st != ORC_PARSE_COMPLETE) break;
+        if (k < max_frames) starts[k] = p;
+        ++k;
+        p += d.header_size + d.payload_size;
+    }
+    if (consumed) *consumed = p;
+    if (stop) *stop = st;
+    return k;
+}
+
 size_t orc_index_frames(const uint8_t* wire, uint64_t size, uint64_t max_payload,
                         uint64_t* starts, size_t max_frames, uint64_t* consumed)
 {

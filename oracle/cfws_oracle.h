@@ -129,6 +129,14 @@ size_t orc_index_frames(const uint8_t* wire, uint64_t wire_size,
                         uint64_t max_payload, uint64_t* starts,
                         size_t max_frames, uint64_t* consumed);
 
+/* One connection's receive loop over buf[begin, end) (co_ws_server.c:107-169):
+ * returns the number of COMPLETE frames (starts beyond max_frames are not
+ * written), *consumed = receive index after them, *stop = 0 when every byte
+ * was consumed, else the code of the walk's last parse (1 = MORE_DATA, also
+ * under 2 bytes left; -7001 / -7005 errors). */
+size_t orc_index_stream(const uint8_t* buf, uint64_t begin, uint64_t end, uint64_t max_payload,
+                        uint64_t* starts, size_t max_frames, uint64_t* consumed, int32_t* stop);
+
 /* Synthetic payload bytes: byte at global offset o is byte (o % 8) of
  * splitmix64 output number (o / 8) for `seed` (little-endian). */
 void orc_fill_splitmix(uint8_t* out, uint64_t n_bytes, uint64_t seed,

@@ -64,6 +64,35 @@ int ref_deserialize(const unsigned char* data, unsigned long long size,
     return r;
 }
 
+/* The receive loop of co_ws_server_on_tcp_receive_ready (co_ws_server.c
+ * :107-169) around the reference's own co_ws_frame_deserialize, over
+ * data[0, size) from receive index `begin`: the callbacks are replaced by
+ * recording each COMPLETE frame's start. Returns the frame count. */
+long long ref_index_stream(const unsigned char* data, unsigned long long size,
+                           unsigned long long begin, unsigned long long max_payload,
+                           unsigned long long* starts, unsigned long long max_frames,
+                           unsigned long long* consumed, int* stop)
+{
+    co_ws_config_set_max_receive_payload_size((size_t)max_payload);
+    size_t index = (size_t)begin;
+    long long k = 0;
+    int st = CO_WS_PARSE_COMPLETE;
+    while (size > index) {
+        if (size - index < CO_WS_FRAME_HEADER_MIN_SIZE) { st = CO_WS_PARSE_MORE_DATA; break; }
+        co_ws_frame_t* f = co_ws_frame_create();
+        size_t at = index;
+        st = co_ws_frame_deserialize(f, data, (size_t)size, &index);
+        co_ws_frame_destroy(f);
+        if (st != CO_WS_PARSE_COMPLETE) break;
+        if ((unsigned long long)k < max_frames) starts[k] = at;
+        ++k;
+    }
+    *consumed = index;
+    *stop = st;
+    co_ws_config_set_max_receive_payload_size(CO_WS_CONFIG_DEFAULT_MAX_RECEIVE_PAYLOAD_SIZE);
+    return k;
+}
+
 /* ---- HTTP/2 DATA framing through the reference's frame codec ------------
  * co_http2_frame.c (compiled in place) encodes / decodes each frame; the
  * split of one buffer into DATA frames restates co_http2_stream_send_data

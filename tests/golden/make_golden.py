@@ -14,6 +14,9 @@ Fixtures (inputs + expected outputs):
                         size limits, concatenated frames, non-minimal lengths
   keys.json             mask-key stream after srandom(seed)
   batch_digests.json    SHA-256 of whole serialized batches (config 2 full size)
+  index_cases.json      receive-loop frame indexing (co_ws_server.c:107-169 around
+                        the reference's co_ws_frame_deserialize): frame starts,
+                        consumed index, stop code per connection stream
 
 Payload bytes are synthetic: splitmix64 stream (oracle.fill_splitmix).
 Usage: python tests/golden/make_golden.py [--skip-full]
@@ -300,13 +303,70 @@ def h2_digest(R, n_frames, frame_size, payload_seed, key_seed, S=16384, sid=1):
                 key_seed=key_seed, max_frame=S, sid=sid, h2_len=total, h2_sha256=h.hexdigest())
 
 
+def index_cases(R):
+    """Streams of reference-serialized frames, cut and corrupted the ways a
+    receive buffer can be; the reference's loop gives starts/consumed/stop.
+    Each distinct byte string is stored once (`blobs`); a case is a prefix of
+    a blob, a receive index and a payload limit."""
+    import random
+    rng = random.Random(0x1D3)
+    O.srandom(R, 4242)
+    M = O.DEFAULT_MAX_PAYLOAD
+
+    def frames(spec):
+        return [O.ref_serialize(R, fin, op, mask, O.fill_splitmix(n, 0x1D3 + n).tobytes())
+                for (fin, op, mask, n) in spec]
+
+    base = frames([(1, 1, 1, 0), (1, 2, 1, 1), (0, 1, 0, 125), (1, 0, 1, 126), (1, 9, 0, 5),
+                   (1, 2, 1, 65535), (1, 2, 0, 65536), (1, 8, 1, 2), (1, 2, 1, 70000),
+                   (1, 10, 0, 0), (1, 2, 1, 300)])
+    whole = b"".join(base)
+    ends = [int(x) for x in np.cumsum([len(f) for f in base])]
+    blobs = {"whole": whole,
+             "whole+1": whole + b"\x82",
+             "http": b"GET / HTTP/1.1\r\nHost: x\r\n\r\n",
+             "rsv": whole[:ends[2]] + b"\xc2\x00" + whole[ends[2]:ends[4]],
+             "msb64": whole[:ends[0]] + bytes([0x82, 0x7f, 0x80]) + bytes(7),
+             "tiny": b"\x82\x00" * 300 + b"\x81\x01a" * 200}
+    cases = [("empty", "whole", 0, 0, M), ("one byte", "whole", 1, 0, M),
+             ("whole", "whole", len(whole), 0, M), ("trailing byte", "whole+1", len(whole) + 1, 0, M),
+             ("receive index mid-buffer", "whole", len(whole), ends[2], M),
+             ("receive index at end", "whole", len(whole), len(whole), M),
+             ("http request", "http", None, 0, M), ("rsv bit after 3 frames", "rsv", None, 0, M),
+             ("too big complete", "whole", len(whole), 0, 1000),
+             ("too big incomplete (MORE_DATA first)", "whole", ends[4] + 5000, 0, 1000),
+             ("64-bit length msb", "msb64", None, 0, M), ("tiny frames", "tiny", None, 0, M)]
+    for k in (1, 3, 5, 8):
+        for cut in (1, 2, 3, 4, 5, 9, 13, 14, 100):
+            cases.append((f"cut {cut} B into frame {k}", "whole", ends[k - 1] + cut, 0, M))
+    for t in range(24):
+        spec = [(rng.random() < .7, rng.choice([0, 1, 2, 8, 9, 10, 3]), rng.random() < .5,
+                 rng.choice([0, 1, 2, 7, 125, 126, 127, 1000, 4096] + ([65536] if t % 6 == 0 else [])))
+                for _ in range(rng.randrange(1, 40))]
+        w = b"".join(frames(spec))
+        blobs[f"random {t}"] = w
+        cut = len(w) if t % 3 == 0 else rng.randrange(0, len(w) + 1)
+        cases.append((f"random {t}", f"random {t}", cut, 0, M))
+    out = []
+    for name, blob, cut, begin, mp in cases:
+        data = blobs[blob][:cut] if cut is not None else blobs[blob]
+        st, consumed, stop = O.ref_index_stream(R, data, begin, mp)
+        out.append(dict(name=name, blob=blob, size=len(data), begin=begin, max_payload=mp,
+                        starts=[int(x) for x in st], consumed=consumed, stop=stop))
+    return dict(blobs={k: v.hex() for k, v in blobs.items()}, cases=out)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--skip-full", action="store_true", help="skip the 4 GiB config-2 digest")
+    ap.add_argument("--only", help="regenerate one fixture family (e.g. index)")
     a = ap.parse_args()
     O.build(ref=True)
     R = O.ref_lib("O2")
     assert R is not None, "oracle/_ref not built (needs /root/reference)"
+    if a.only == "index":
+        dump("index_cases.json", index_cases(R))
+        return
     dump("rfc6455_kat.json", rfc6455(R))
     dump("serialize_cases.json", serialize_cases(R))
     dump("deserialize_cases.json", deserialize_cases(R))
@@ -325,6 +385,7 @@ def main():
     if not a.skip_full:
         h2d += [h2_digest(R, 65536, 16376, 0x5EED0005, 5), h2_digest(R, 65536, 65536, 0x5EED0005, 5)]
     dump("h2_digests.json", h2d)
+    dump("index_cases.json", index_cases(R))
 
 
 if __name__ == "__main__":

@@ -101,3 +101,34 @@ def test_pipeline_config2_reduced_digest():
     pl.close()
     assert ptot == n * fs and (st == 0).all()
     assert np.array_equal(back, payload)
+
+
+@pytest.mark.parametrize("cut", [None, -1, -70000])
+def test_pipeline_receive_indexes_then_deserializes(cut):
+    """cfws_pipeline_receive: the host receive-loop walk, then the chunked
+    device deserialize -- equal to the oracle's walk + batch deserialize,
+    with a trailing partial frame (MORE_DATA) and an invalid frame (-7001)."""
+    rng = random.Random(99)
+    frames = [O.serialize_keyed(rng.random() < .7, rng.choice([0, 1, 2, 9]), rng.random() < .6,
+                                rng.getrandbits(32),
+                                rng.randbytes(rng.choice([0, 3, 125, 126, 5000, 70000])))
+              for _ in range(600)]
+    raw = b"".join(frames)
+    if cut is not None:
+        raw = raw[:cut]
+    if cut == -70000:
+        raw = raw[:len(raw) // 2] + b"\xf0\x00" + raw[len(raw) // 2:]
+    wire_t, wire = pinned(len(raw))
+    wire[:len(raw)] = np.frombuffer(raw, np.uint8)
+    e_st, e_con, e_stop = O.index_stream(wire[:len(raw)], 0, len(raw))
+    e_out, e_d, e_status, e_tot = O.deserialize_batch(wire[:len(raw)], e_st, align=16)
+    out_t, out = pinned(e_tot + 64)
+    pl = cfws.Pipeline(chunk_bytes=1 << 20, max_frames=256, depth=3)
+    desc, st, consumed, stop, tot = pl.receive(wire_t.data_ptr(), 0, len(raw), out_t.data_ptr(),
+                                               out.size, max_frames=1000)
+    pl.close()
+    assert (consumed, stop) == (e_con, e_stop)
+    assert len(desc) == len(e_st) and np.array_equal(desc["wire_off"], e_st)
+    assert tot == e_tot and (st == 0).all()
+    assert np.array_equal(desc["payload_off"], e_d["payload_off"])
+    assert np.array_equal(out[:tot], e_out[:tot])

@@ -173,3 +173,20 @@ def test_batch_deserialize_errors_and_capacity():
     # capacity 100: the 200-byte payload does not fit
     out, desc, st, total = O.deserialize_batch(wire, starts[:1], align=16, capacity=100)
     assert st[0] == O.ERROR_OUT_OF_MEMORY and total == 100 and not out[:100].any()
+
+
+def _index_cases():
+    g = golden("index_cases.json")
+    blobs = {k: bytes.fromhex(v) for k, v in g["blobs"].items()}
+    return [(c, blobs[c["blob"]][:c["size"]]) for c in g["cases"]]
+
+
+@pytest.mark.parametrize("i", range(len(golden("index_cases.json")["cases"])))
+def test_index_stream_matches_reference_receive_loop(i):
+    """orc_index_stream == the reference's receive loop (co_ws_server.c:107-169
+    around its own co_ws_frame_deserialize) on the committed streams."""
+    c, data = _index_cases()[i]
+    st, consumed, stop = O.index_stream(np.frombuffer(data, np.uint8), c["begin"], len(data),
+                                        c["max_payload"])
+    assert [int(x) for x in st] == c["starts"], c["name"]
+    assert consumed == c["consumed"] and stop == c["stop"], c["name"]
