@@ -214,15 +214,16 @@ int cfws_pipeline_deserialize(cfws_pipeline_t* p, const void* h_wire, uint64_t w
     const uint8_t* src = static_cast<const uint8_t*>(h_wire);
     uint8_t* dst = static_cast<uint8_t*>(h_payload);
 
-    struct Chunk { size_t i, j; int slot; uint64_t wire_lo; };
-    std::vector<Chunk> pend;         // chunks whose layout total is not consumed yet
+    struct Chunk { size_t i, j; int slot; uint64_t wire_lo, base; };
+    std::vector<Chunk> pend;         // launched; layout total not read yet
+    std::vector<Chunk> landing;      // D2H enqueued; descriptors not rebased yet
     uint64_t base = 0;               // payload bytes laid out by earlier chunks
     uint64_t out_slot = p->chunk + 64;
 
-    // Finish chunk k: its layout total is known -> D2H payload, descriptors
-    // and status, then rebase on the host once they land.
-    std::vector<Chunk> done;
-    auto drain = [&](const Chunk& k) -> int {
+    // Chunk k's layout total is known: enqueue the D2H of its payload,
+    // descriptors and status, and move the payload base on. Does not wait
+    // for the copies, so the next chunk's kernels overlap them.
+    auto settle = [&](Chunk k) -> int {
         Slot& S = p->slot[k.slot];
         CFWS_HIP(hipEventSynchronize(S.ev_total));
         const uint64_t tot = *S.h_total;          // unclamped chunk layout bytes
@@ -237,14 +238,29 @@ int cfws_pipeline_deserialize(cfws_pipeline_t* p, const void* h_wire, uint64_t w
         CFWS_HIP(hipMemcpyAsync(sstat, S.d_status, (k.j - k.i) * sizeof(int32_t),
                                 hipMemcpyDeviceToHost, S.st));
         CFWS_HIP(hipEventRecord(S.ev_done, S.st));
+        k.base = base;
+        base += tot;
+        landing.push_back(k);
+        return CFWS_OK;
+    };
+    // Chunk k's copies have landed: rebase its descriptors into the caller's.
+    auto finish = [&](const Chunk& k) -> int {
+        Slot& S = p->slot[k.slot];
         CFWS_HIP(hipEventSynchronize(S.ev_done));
+        const auto* sdesc = static_cast<const cfws_frame_desc_t*>(S.h_stage);
+        const auto* sstat = reinterpret_cast<const int32_t*>(sdesc + p->max_frames);
         for (size_t f = k.i; f < k.j; ++f) {
             h_desc[f] = sdesc[f - k.i];
             h_desc[f].wire_off += k.wire_lo;
-            h_desc[f].payload_off += base;
+            h_desc[f].payload_off += k.base;
             h_status[f] = sstat[f - k.i];
         }
-        base += tot;
+        return CFWS_OK;
+    };
+    auto settle_all = [&]() -> int {
+        for (const Chunk& k : pend)
+            if (int rc = settle(k)) return rc;
+        pend.clear();
         return CFWS_OK;
     };
 
@@ -266,15 +282,17 @@ int cfws_pipeline_deserialize(cfws_pipeline_t* p, const void* h_wire, uint64_t w
             return fail("a frame is larger than the pipeline chunk");
         const int s = c % p->depth;
         Slot& S = p->slot[s];
-        // slot reuse: its previous chunk must be fully drained first
+        // slot reuse: its previous chunk must have landed (staging reused)
         for (size_t q = 0; q < pend.size(); ++q)
             if (pend[q].slot == s) {
-                while (!pend.empty() && pend.front().slot != s) {
-                    if (int rc = drain(pend.front())) return rc;
-                    pend.erase(pend.begin());
-                }
-                if (int rc = drain(pend.front())) return rc;
-                pend.erase(pend.begin());
+                if (int rc = settle_all()) return rc;
+                break;
+            }
+        for (size_t q = 0; q < landing.size(); ++q)
+            if (landing[q].slot == s) {
+                for (size_t r = 0; r <= q; ++r)
+                    if (int rc = finish(landing[r])) return rc;
+                landing.erase(landing.begin(), landing.begin() + q + 1);
                 break;
             }
         auto* sidx = static_cast<uint64_t*>(S.h_stage);
@@ -282,11 +300,8 @@ int cfws_pipeline_deserialize(cfws_pipeline_t* p, const void* h_wire, uint64_t w
         CFWS_HIP(hipMemcpyAsync(S.d_in, src + wire_lo, hi - wire_lo, hipMemcpyHostToDevice, S.st));
         CFWS_HIP(hipMemcpyAsync(S.d_index, sidx, (j - i) * sizeof(uint64_t), hipMemcpyHostToDevice, S.st));
         // The capacity rule needs this chunk's payload base: everything laid
-        // out before it must be known (drain all pending chunks first).
-        while (!pend.empty()) {
-            if (int rc = drain(pend.front())) return rc;
-            pend.erase(pend.begin());
-        }
+        // out before it must be known (settle all pending chunks first).
+        if (int rc = settle_all()) return rc;
         const uint64_t cap = base >= payload_capacity ? 0 : std::min(out_slot, payload_capacity - base);
         // cap == 0 (capacity exhausted): the plan marks every non-empty
         // COMPLETE frame OUT_OF_MEMORY, exactly the batch rule.
@@ -299,14 +314,13 @@ int cfws_pipeline_deserialize(cfws_pipeline_t* p, const void* h_wire, uint64_t w
                                 static_cast<char*>(S.d_ws) + cfws_internal_grand_total_offset(), 8,
                                 hipMemcpyDeviceToHost, S.st));
         CFWS_HIP(hipEventRecord(S.ev_total, S.st));
-        pend.push_back(Chunk{i, j, s, wire_lo});
+        pend.push_back(Chunk{i, j, s, wire_lo, 0});
         i = j;
         ++c;
     }
-    while (!pend.empty()) {
-        if (int rc = drain(pend.front())) return rc;
-        pend.erase(pend.begin());
-    }
+    if (int rc = settle_all()) return rc;
+    for (const Chunk& k : landing)
+        if (int rc = finish(k)) return rc;
     if (payload_total) *payload_total = std::min(base, payload_capacity);
     return CFWS_OK;
 }

@@ -107,3 +107,18 @@ def test_no_cpu_fallback():
     assert not ok
     w = O.serialize_keyed(True, 2, True, 0x11223344, b"x" * 100)
     assert cfws.frame_deserialize(w)["rc"] == -7006
+
+
+def test_link_level_dropin_fails_loudly_without_device():
+    """The C harness built against coldforce's own headers (oracle/_ref/
+    dropin_link, linked to libcfws.so): with no GPU its first masked
+    non-empty frame fails -- serialize returns false and says why."""
+    import os
+    import subprocess
+    exe = os.path.join(O.HERE, "_ref", "dropin_link")
+    if not os.path.exists(exe):
+        pytest.skip("oracle/_ref/dropin_link not built (needs /root/reference)")
+    r = subprocess.run([exe, "77"], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 2
+    assert "serialize failed size=1 mask=1" in r.stdout
+    assert "no HIP device" in r.stderr or "gfx950" in r.stderr

@@ -109,3 +109,40 @@ def test_frame_object_api():
     assert L.co_ws_frame_get_opcode(f) == 0xFF and not L.co_ws_frame_get_fin(f)
     assert L.co_ws_frame_get_payload_size(f) == 0 and not L.co_ws_frame_get_payload_data(f)
     L.co_ws_frame_destroy(f)
+
+
+def _fnv1a(b: bytes) -> int:
+    h = 0xcbf29ce484222325
+    for x in b:
+        h = ((h ^ x) * 0x100000001b3) & 0xFFFFFFFFFFFFFFFF
+    return h
+
+
+def test_link_level_dropin_harness():
+    """oracle/_ref/dropin_link: a C program built against coldforce's own
+    headers (co_ws_frame.h, co_ws_config.h, co_byte_array.h) and the
+    reference's co_array.c, linked to libcfws.so in place of co_ws_frame.c.
+    Its wire equals the oracle's for the same random() stream, every frame
+    decodes back, and the error codes are the reference's."""
+    import os
+    import subprocess
+    exe = os.path.join(O.HERE, "_ref", "dropin_link")
+    if not os.path.exists(exe):
+        pytest.skip("oracle/_ref/dropin_link not built (built where /root/reference exists)")
+    r = subprocess.run([exe, "77"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    lines = r.stdout.split("\n")
+    L = O.lib()
+    O.srandom(L, 77)
+    wire = b""
+    sizes = [0, 1, 125, 126, 1000, 65535, 65536, 70000]
+    for n in sizes:
+        data = bytes((i * 131 + n) & 0xff for i in range(n))
+        for mask in (False, True):
+            wire += O.ref_serialize(L, True, 2, mask, data)
+    assert lines[0] == f"wire {len(wire)} {_fnv1a(wire):016x}"
+    assert lines[1] == f"frames {2 * len(sizes)} ok"
+    at = 0
+    for n in sizes[:4]:
+        at += 2 * n + O.header_size(n, False) + O.header_size(n, True)
+    assert lines[2] == f"codes 1 -7001 -7005 index {at}"
