@@ -134,7 +134,7 @@ def main():
     ap.add_argument("--frame-size", type=int, default=65536)
     ap.add_argument("--chunk-mib", type=int, default=64)
     ap.add_argument("--depth", type=int, default=3)
-    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--reps", type=int, default=7)
     args = ap.parse_args()
 
     import numpy as np
@@ -177,20 +177,33 @@ def main():
     pl = cfws.Pipeline(chunk_bytes=args.chunk_mib << 20, max_frames=1 << 16, depth=args.depth)
     d = desc.copy()
     pl.serialize(payload.data_ptr(), d, wire.data_ptr(), wire.numel())          # warm-up
-    t0 = time.perf_counter()
+    ts = []
     for _ in range(args.reps):
         d = desc.copy()
+        t0 = time.perf_counter()
         tot = pl.serialize(payload.data_ptr(), d, wire.data_ptr(), wire.numel())
-    t_ser = (time.perf_counter() - t0) / args.reps
+        ts.append(time.perf_counter() - t0)
+    t_ser = float(np.median(ts))
     pl.deserialize(wire.data_ptr(), tot, offs, back.data_ptr(), back.numel(), align=1)
-    t0 = time.perf_counter()
+    ts = []
     for _ in range(args.reps):
+        t0 = time.perf_counter()
         dd, st, ptot = pl.deserialize(wire.data_ptr(), tot, offs, back.data_ptr(), back.numel(),
                                       align=1)
-    t_de = (time.perf_counter() - t0) / args.reps
-    pl.close()
+        ts.append(time.perf_counter() - t0)
+    t_de = float(np.median(ts))
     ok = (tot == wire_total and ptot == nbytes and bool((st == 0).all())
           and torch.equal(back[:nbytes], payload))
+    # the receive loop: host frame walk (cfws_index_frames) + the same pipeline
+    ts = []
+    for _ in range(args.reps):
+        t0 = time.perf_counter()
+        dr, sr, consumed, stop, rtot = pl.receive(wire.data_ptr(), 0, tot, back.data_ptr(),
+                                                  back.numel(), max_frames=len(desc), align=1)
+        ts.append(time.perf_counter() - t0)
+    t_rx = float(np.median(ts))
+    ok = ok and consumed == tot and stop == 0 and rtot == nbytes and len(dr) == len(desc)
+    pl.close()
     line = {
         "what": "host-to-host (PCIe-inclusive) codec rate through cfws_pipeline_*",
         "workload": args.workload, "frames": len(desc), "payload_bytes": nbytes,
@@ -199,6 +212,8 @@ def main():
         "serialize_GiBps": round(nbytes / t_ser / GIB, 2),
         "deserialize_GiBps": round(nbytes / t_de / GIB, 2),
         "round_trip_GiBps": round(2 * nbytes / (t_ser + t_de) / GIB, 2),
+        "receive_s": round(t_rx, 4), "receive_GiBps": round(nbytes / t_rx / GIB, 2),
+        "timing": f"median of {args.reps} reps after one warm-up",
         "pinned_h2d_GBps": round(h2d, 1), "pinned_d2h_GBps": round(d2h, 1),
         "verified": ok,
     }

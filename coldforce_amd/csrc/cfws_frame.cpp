@@ -57,9 +57,27 @@ bool device_stage(size_t n)
     return true;
 }
 
+// The mask keys are the process's random() stream (co_random.c:32-35), so
+// the device work of a frame must not consume it: the HIP/HSA runtime may
+// call rand()/random() (glibc: one shared state) while it initialises.
+// While the guard lives, random() runs on a private state; the caller's
+// state is left exactly where the reference leaves it.
+class RandomStateGuard {
+public:
+    RandomStateGuard() : saved_(initstate(0x5eedu, scratch_, sizeof scratch_)) {}
+    ~RandomStateGuard() { setstate(saved_); }
+    RandomStateGuard(const RandomStateGuard&) = delete;
+    RandomStateGuard& operator=(const RandomStateGuard&) = delete;
+
+private:
+    char scratch_[128];
+    char* saved_;
+};
+
 // dst[i] = src[i] ^ key[i % 4] for a host buffer, through the device.
 bool device_xor(const uint8_t* src, uint8_t* dst, size_t n, uint32_t key)
 {
+    RandomStateGuard keep_random_stream;
     if (!device_stage(n)) return false;
     hipStream_t st = t_dev.stream;
     if (hipMemcpyAsync(t_dev.buf, src, n, hipMemcpyHostToDevice, st) != hipSuccess) return false;

@@ -341,7 +341,9 @@ int cfws_pipeline_receive(cfws_pipeline_t* p, const void* h_wire, uint64_t begin
     *n_frames = n;
     if (consumed) *consumed = used;
     if (stop) *stop = why;
-    return cfws_pipeline_deserialize(p, h_wire, end, starts.data(), n, max_payload, align, 0,
+    // every indexed frame is COMPLETE inside [begin, used): bytes past `used`
+    // (an incomplete or invalid frame) are not staged
+    return cfws_pipeline_deserialize(p, h_wire, used, starts.data(), n, max_payload, align, 0,
                                      h_desc, h_status, h_payload, payload_capacity, payload_total);
 }
 

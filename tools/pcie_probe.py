@@ -1,6 +1,9 @@
-"""PCIe probe for the host-memory path: DMA copies one way and both ways at
-once, and kernels that read / write pinned host memory directly (zero-copy,
-cfws_xor_mask on mapped host pointers). Prints one JSON line.
+"""PCIe probe for the host-memory path: DMA copies of pinned host memory one
+way and both ways at once. Prints one JSON line.
+
+(Kernels must not dereference torch's pinned host pointers directly: a
+first zero-copy attempt faulted the GPU -- torch's pinned allocations are
+not guaranteed to be mapped at the same address for the device.)
 
 usage: python tools/pcie_probe.py [MiB]
 """
@@ -53,28 +56,6 @@ def main():
     res["h2d_GBps"] = n / timed(h2d) / 1e9
     res["d2h_GBps"] = n / timed(d2h) / 1e9
     res["bidir_GBps_each"] = n / timed(both) / 1e9
-    # zero-copy kernels (mapped pinned host memory)
-    L = cfws.lib()
-    st = torch.cuda.current_stream().cuda_stream
-
-    def k_h2d():
-        assert L.cfws_xor_mask(h_a.data_ptr(), d_a.data_ptr(), n, 0x01020304, 0, st) == 0
-
-    def k_d2h():
-        assert L.cfws_xor_mask(d_a.data_ptr(), h_b.data_ptr(), n, 0x01020304, 0, st) == 0
-
-    def k_h2h():
-        assert L.cfws_xor_mask(h_a.data_ptr(), h_b.data_ptr(), n, 0x01020304, 0, st) == 0
-
-    for name, fn in (("kernel_read_host_GBps", k_h2d), ("kernel_write_host_GBps", k_d2h),
-                     ("kernel_host_to_host_GBps_each", k_h2h)):
-        try:
-            res[name] = n / timed(fn) / 1e9
-        except Exception as e:  # noqa: BLE001
-            res[name] = f"error: {e}"
-    torch.cuda.synchronize()
-    ok = bool((h_b[:4096].cpu() == (h_a[:4096] ^ torch.tensor([4, 3, 2, 1], dtype=torch.uint8).repeat(1024))).all())
-    res["kernel_h2h_verified"] = ok
     print(json.dumps({k: (round(v, 2) if isinstance(v, float) else v) for k, v in res.items()}))
 
 
