@@ -283,20 +283,10 @@ __device__ __forceinline__ uint4 body_chunk(const uint8_t* __restrict__ src, con
     return o;
 }
 
-// Byte idx (0..31) of the 32-byte window {A, B}, without dynamic register
-// indexing (which would go to scratch).
-__device__ __forceinline__ uint32_t window_byte(const uint4& A, const uint4& B, uint32_t idx)
-{
-    const bool q1 = (idx & 4u) != 0, q2 = (idx & 8u) != 0;
-    const uint32_t a = q2 ? (q1 ? A.w : A.z) : (q1 ? A.y : A.x);
-    const uint32_t b = q2 ? (q1 ? B.w : B.z) : (q1 ? B.y : B.x);
-    return (((idx & 16u) ? b : a) >> (8 * (idx & 3u))) & 0xffu;
-}
-
 // Slow fallback: byte by byte, walking frames forward from f (chunks that
 // hold more than two frames: runs of frames shorter than ~14 bytes).
 template <int kMode>
-__device__ __noinline__ uint4 edge_chunk_bytes(const Pass P, uint32_t f, uint64_t D)
+__device__ __forceinline__ uint4 edge_chunk_bytes(const Pass& P, uint32_t f, uint64_t D)
 {
     FrameView v = frame_view<kMode>(P, f);
     uint64_t next = (f + 1 < P.n_frames) ? P.offs[f + 1] : ~uint64_t(0);
@@ -328,37 +318,54 @@ __device__ __noinline__ uint4 edge_chunk_bytes(const Pass P, uint32_t f, uint64_
     return make_uint4(w0, w1, w2, w3);
 }
 
-// Where frame v's body overlaps [D, lim): the aligned source block holding
-// the first overlapping byte (and the next one when the overlap spans two).
-// Only blocks that hold a valid source byte are read.
-__device__ __forceinline__ void edge_blocks(const uint8_t* __restrict__ src, const FrameView& v,
-                                            uint64_t D, uint64_t lim, uint4& A, uint4& B,
-                                            uint64_t& abase)
+// Frame v's (masked) body bytes lined up with the output chunk at D: byte j
+// of the result is the body byte at output position D + j, for every j
+// whose position lies inside v's body (other bytes are don't-care). One or
+// two aligned source blocks are read -- only blocks that hold a body byte
+// of the chunk -- and shifted once with funnel16; the per-byte assembly in
+// edge_chunk then indexes registers statically (a dynamic byte index into
+// {A, B} is lowered through scratch memory).
+__device__ __forceinline__ uint4 edge_body(const uint8_t* __restrict__ src, const FrameView& v,
+                                           uint64_t D, uint64_t lim)
 {
     const uint64_t be = v.body_start + v.body_len;
     const uint64_t lo = D > v.body_start ? D : v.body_start;
     const uint64_t hi = lim < be ? lim : be;
-    abase = 0;
+    uint4 W = make_uint4(0, 0, 0, 0);
     if (hi > lo) {
         const uint64_t s_first = v.src_off + (lo - v.body_start);
         const uint64_t s_last = v.src_off + (hi - 1 - v.body_start);
-        abase = s_first & ~uint64_t(15);
-        A = ld16(src + abase);
-        B = ((s_last & ~uint64_t(15)) != abase) ? ld16(src + abase + 16) : A;
+        const uint64_t abase = s_first & ~uint64_t(15);
+        const uint4 A = ld16(src + abase);
+        const uint4 B = ((s_last & ~uint64_t(15)) != abase) ? ld16(src + abase + 16) : A;
+        // window byte ph holds the body byte at output position lo
+        const uint32_t ph = (uint32_t)(s_first - abase);
+        const uint32_t j0 = (uint32_t)(lo - D);                   // 0..15
+        if (ph >= j0) {
+            W = funnel16(A, B, ph - j0);
+        } else {                                                   // body starts mid-chunk
+            W = funnel16(make_uint4(0, 0, 0, 0), A, 16u - (j0 - ph));
+        }
+        xor4(W, rotr8(v.key, (uint32_t)(D - v.body_start) & 3u));
     }
+    return W;
 }
 
-// Byte at output position pos of frame v (pos inside v's output range).
+__device__ __forceinline__ uint32_t u4_byte(const uint4& w, int j)
+{
+    const uint32_t d = j < 4 ? w.x : (j < 8 ? w.y : (j < 12 ? w.z : w.w));
+    return (d >> (8 * (j & 3))) & 0xffu;
+}
+
+// Byte at output position pos of frame v (pos inside v's output range),
+// given v's body bytes lined up with the chunk (edge_body).
 template <int kMode>
 __device__ __forceinline__ uint32_t edge_byte(const Pass& P, const FrameView& v, uint64_t pos,
-                                              const uint4& A, const uint4& B, uint64_t abase)
+                                              const uint4& W, int j)
 {
     const uint64_t r = pos - v.out_off;
     if (r < v.pre) return header_byte_of<kMode>(P, v, (uint32_t)r);
-    const uint64_t k = r - v.pre;
-    if (k >= v.body_len) return 0;
-    const uint32_t idx = (uint32_t)(v.src_off + k - abase);
-    return (window_byte(A, B, idx) ^ (v.key >> (8 * (k & 3u)))) & 0xffu;
+    return (r - v.pre < v.body_len) ? u4_byte(W, j) : 0u;
 }
 
 // A chunk that crosses a header, a frame boundary, padding or the end of
@@ -366,7 +373,7 @@ __device__ __forceinline__ uint32_t edge_byte(const Pass& P, const FrameView& v,
 // than the chunk) all source blocks are loaded up front and the bytes are
 // assembled in registers: one memory round trip instead of sixteen.
 template <int kMode>
-__device__ __noinline__ uint4 edge_chunk(const Pass P, uint32_t f, uint64_t D)
+__device__ __forceinline__ uint4 edge_chunk(const Pass& P, uint32_t f, uint64_t D)
 {
     const uint64_t lim = D + 16 < P.total ? D + 16 : P.total;
     const uint64_t o1 = (f + 1 < P.n_frames) ? P.offs[f + 1] : ~uint64_t(0);
@@ -376,18 +383,16 @@ __device__ __noinline__ uint4 edge_chunk(const Pass P, uint32_t f, uint64_t D)
     const bool two = o1 < lim;
     FrameView vb = va;
     if (two) vb = frame_view<kMode>(P, f + 1);
-    uint4 Aa = make_uint4(0, 0, 0, 0), Ba = Aa, Ab = Aa, Bb = Aa;
-    uint64_t ba = 0, bb = 0;
-    edge_blocks(P.src, va, D, lim, Aa, Ba, ba);
-    if (two) edge_blocks(P.src, vb, D, lim, Ab, Bb, bb);
+    const uint4 Wa = edge_body(P.src, va, D, lim);
+    const uint4 Wb = two ? edge_body(P.src, vb, D, lim) : Wa;
     uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
         const uint64_t pos = D + j;
         uint32_t b = 0;
         if (pos < lim)
-            b = (two && pos >= o1) ? edge_byte<kMode>(P, vb, pos, Ab, Bb, bb)
-                                   : edge_byte<kMode>(P, va, pos, Aa, Ba, ba);
+            b = (two && pos >= o1) ? edge_byte<kMode>(P, vb, pos, Wb, j)
+                                   : edge_byte<kMode>(P, va, pos, Wa, j);
         const uint32_t sh = 8 * (j & 3);
         if (j < 4) w0 |= b << sh;
         else if (j < 8) w1 |= b << sh;
@@ -402,8 +407,10 @@ __device__ __forceinline__ void store_chunk(const Pass& P, uint64_t D, uint4 o)
     if (D + 16 <= P.capacity) {
         st16(P.dst + D, o);
     } else {
-        const uint32_t w[4] = {o.x, o.y, o.z, o.w};
-        for (uint32_t j = 0; D + j < P.capacity; ++j) P.dst[D + j] = (uint8_t)(w[j >> 2] >> (8 * (j & 3)));
+        for (uint32_t j = 0; D + j < P.capacity; ++j) {
+            const uint32_t w = j < 4 ? o.x : (j < 8 ? o.y : (j < 12 ? o.z : o.w));
+            P.dst[D + j] = (uint8_t)(w >> (8 * (j & 3)));
+        }
     }
 }
 
@@ -567,18 +574,25 @@ xform_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
     }
 }
 
-// One thread per frame: the 16-byte chunks that START inside the frame's
-// output range and do not lie entirely inside its body -- header chunks,
-// the chunk that crosses into the next frame, padding, the pass end.
+// Two threads per frame (part 0: the chunks before the body -- headers;
+// part 1: the chunks reaching past the body end -- the boundary into the
+// next frame, padding, the pass end): the 16-byte chunks that START inside
+// the frame's output range and do not lie entirely inside its body. The
+// kernel is latency-bound (descriptor -> offsets -> source blocks -> store),
+// so the work is spread thin: 64-thread blocks, edge_chunk inlined.
+constexpr uint32_t kEdgeThreads = 64;
+
 template <int kMode>
-__global__ void __launch_bounds__(kThreads)
+__global__ void __launch_bounds__(kEdgeThreads)
 edge_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
             const cfws_frame_desc_t* __restrict__ desc, const int32_t* __restrict__ status,
             const uint64_t* __restrict__ offs, const uint64_t* __restrict__ total_p,
             const uint64_t* __restrict__ base_p, uint64_t capacity, uint32_t n_frames,
             uint32_t klass, uint32_t sid)
 {
-    const uint64_t f = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
+    const uint64_t t = uint64_t(blockIdx.x) * kEdgeThreads + threadIdx.x;
+    const uint64_t f = t >> 1;
+    const uint32_t part = (uint32_t)(t & 1u);
     if (f >= n_frames) return;
     const uint64_t out_base = base_p ? *base_p : 0;
     Pass P;
@@ -599,14 +613,17 @@ edge_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
     const FrameView v = frame_view<kMode>(P, (uint32_t)f);
     const uint64_t be = v.body_start + v.body_len;
     const uint64_t first = (lo + 15) & ~uint64_t(15);
-    // chunks before the body (headers): D < body_start
-    for (uint64_t D = first; D < hi && D < v.body_start; D += 16)
-        store_chunk(P, D, edge_chunk<kMode>(P, (uint32_t)f, D));
+    if (part == 0) {
+        // chunks before the body (headers): D < body_start
+        for (uint64_t D = first; D < hi && D < v.body_start; D += 16)
+            store_chunk(P, D, edge_chunk<kMode>(P, (uint32_t)f, D));
+        return;
+    }
     // chunks reaching past the body end (boundary, padding, pass end)
-    uint64_t t = be >= 15 ? ((be - 15 + 15) & ~uint64_t(15)) : 0;   // first D with D + 16 > be
-    if (t < first) t = first;
-    if (t < v.body_start) t = (v.body_start + 15) & ~uint64_t(15);  // header chunks done above
-    for (uint64_t D = t; D < hi; D += 16) {
+    uint64_t d0 = be >= 15 ? ((be - 15 + 15) & ~uint64_t(15)) : 0;  // first D with D + 16 > be
+    if (d0 < first) d0 = first;
+    if (d0 < v.body_start) d0 = (v.body_start + 15) & ~uint64_t(15);  // header chunks: part 0
+    for (uint64_t D = d0; D < hi; D += 16) {
         if (D >= be && D + 16 <= hi)          // pure alignment padding / OOM body
             store_chunk(P, D, make_uint4(0, 0, 0, 0));
         else
@@ -1208,7 +1225,7 @@ void launch_streaming(const void* src, void* dst, const cfws_frame_desc_t* desc,
     xform_kernel<kMode><<<stream_grid(regions), kThreads, xform_lds_bytes(), st>>>(
         static_cast<const uint8_t*>(src), static_cast<uint8_t*>(dst), desc, status, offs, map,
         total_p, base_p, cap, (uint32_t)n, klass, sid);
-    edge_kernel<kMode><<<grid_for(n, kThreads), kThreads, 0, st>>>(
+    edge_kernel<kMode><<<grid_for(2 * (uint64_t)n, kEdgeThreads), kEdgeThreads, 0, st>>>(
         static_cast<const uint8_t*>(src), static_cast<uint8_t*>(dst), desc, status, offs,
         total_p, base_p, cap, (uint32_t)n, klass, sid);
 }
