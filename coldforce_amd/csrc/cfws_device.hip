@@ -58,7 +58,11 @@ enum : uint32_t { kClassAll = 0, kClassData = 1, kClassControl = 2 };
 //                                   "strip a prefix, copy the body" pass:
 //                                   HTTP/2 DATA unwrap uses it too)
 //   kModeH2Wrap: HTTP/2 DATA wrap -- 9-byte DATA header + a slice of WS wire
-enum : int { kModeSer = 0, kModeDeser = 1, kModeH2Wrap = 2 };
+//   kModeH2Ser:  WS serialize straight into HTTP/2 DATA frames -- per DATA
+//                frame: 9-byte DATA header, the WS header when the slice
+//                starts the WS frame, then the masked payload slice (one
+//                pass: the WS wire bytes are never materialised)
+enum : int { kModeSer = 0, kModeDeser = 1, kModeH2Wrap = 2, kModeH2Ser = 3 };
 __host__ __device__ constexpr bool is_ser(int mode) { return mode != kModeDeser; }
 
 // ---------------------------------------------------------------------------
@@ -139,7 +143,8 @@ struct Pass {
     uint64_t capacity;            // writable bytes from dst
     uint32_t n_frames;
     uint32_t klass;
-    uint32_t sid;                 // HTTP/2 stream id (kModeH2Wrap)
+    uint32_t sid;                 // HTTP/2 stream id (kModeH2Wrap, kModeH2Ser)
+    const cfws_frame_desc_t* parent;   // kModeH2Ser: the WS frames
 };
 
 // What one frame contributes to a pass's output.
@@ -153,7 +158,9 @@ struct FrameView {
     uint64_t src_off;
     uint32_t key;   // 0 when the frame is not masked: XOR becomes a copy
     uint32_t pre;
-    uint32_t hb;    // serialize: header byte 0 | mask bit << 8
+    uint32_t hb;    // serialize: header byte 0 | mask bit << 8; DATA: flags
+    uint32_t aux;   // kModeH2Ser: the parent WS frame
+    uint32_t s0;    // kModeH2Ser: the slice's first byte within the WS frame
 };
 
 // Byte r < pre of a serialize frame's header, from its view (co_ws_frame.c:34-91).
@@ -177,7 +184,25 @@ __device__ __forceinline__ FrameView frame_view(const Pass& P, uint32_t f)
     v.key = d.mask() ? d.key() : 0u;
     v.out_off = P.offs[f];
     v.hb = 0;
-    if (is_ser(kMode)) {
+    v.aux = 0;
+    v.s0 = 0;
+    if (kMode == kModeH2Ser) {
+        // d: one DATA frame = a slice [payload_off, + payload_size) of the
+        // virtual WS wire arena; key field = its WS frame w
+        const uint32_t wf = d.key();
+        const DescWords w = load_desc(P.parent, wf);
+        const uint64_t s0 = d.payload_off - w.wire_off;
+        const uint64_t hs = w.header_size();
+        const uint64_t h_in = s0 < hs ? (hs - s0 < d.payload_size ? hs - s0 : d.payload_size) : 0;
+        const uint64_t q = s0 + h_in - hs;             // payload index of the body start
+        v.pre = d.payload_size ? 9u + (uint32_t)h_in : 0u;   // unused slots: empty
+        v.body_len = d.payload_size - h_in;
+        v.src_off = w.payload_off + q;
+        v.key = w.mask() ? rotr8(w.key(), (uint32_t)(q & 3u)) : 0u;
+        v.hb = d.fin() ? 0x1u : 0u;                      // DATA flags: END_STREAM
+        v.aux = wf;
+        v.s0 = (uint32_t)s0;                           // only read when h_in > 0 (s0 < 14)
+    } else if (is_ser(kMode)) {
         v.pre = d.header_size();
         v.body_len = d.payload_size;
         v.src_off = d.payload_off;
@@ -249,22 +274,33 @@ __device__ __forceinline__ void xor4(uint4& o, uint32_t k)
 
 // Byte r of an HTTP/2 DATA frame header (co_http2_frame.c:33-72: 24-bit BE
 // length, type 0, flags, 31-bit BE stream id).
-__device__ __forceinline__ uint32_t h2_header_byte(const FrameView& v, uint32_t sid, uint32_t r)
+__device__ __forceinline__ uint32_t h2_header_byte(uint32_t len, uint32_t flags, uint32_t sid,
+                                                   uint32_t r)
 {
-    const uint32_t len = (uint32_t)v.body_len;
     const uint32_t sidm = sid & 0x7fffffffu;
     return r == 0 ? (len >> 16) & 0xffu
          : r == 1 ? (len >> 8) & 0xffu
          : r == 2 ? len & 0xffu
          : r == 3 ? 0u
-         : r == 4 ? (v.hb & 0xffu)
+         : r == 4 ? (flags & 0xffu)
          : (sidm >> (8 * (8 - r))) & 0xffu;
 }
 
 template <int kMode>
 __device__ __forceinline__ uint32_t header_byte_of(const Pass& P, const FrameView& v, uint32_t r)
 {
-    return kMode == kModeH2Wrap ? h2_header_byte(v, P.sid, r) : view_header_byte(v, r);
+    if (kMode == kModeH2Wrap) return h2_header_byte((uint32_t)v.body_len, v.hb, P.sid, r);
+    if (kMode == kModeH2Ser) {
+        if (r < 9) return h2_header_byte(v.pre - 9u + (uint32_t)v.body_len, v.hb, P.sid, r);
+        // the WS frame's header (co_ws_frame.c:34-91), from its descriptor
+        const DescWords w = load_desc(P.parent, v.aux);
+        FrameView wv;
+        wv.body_len = w.payload_size;
+        wv.key = w.mask() ? w.key() : 0u;
+        wv.hb = ((w.opcode() | (w.fin() ? 0x80u : 0u)) & 0xffu) | (w.mask() ? 0x100u : 0u);
+        return view_header_byte(wv, r - 9u + v.s0);
+    }
+    return view_header_byte(v, r);
 }
 
 // One chunk entirely inside v's body.
@@ -529,7 +565,8 @@ xform_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
              const cfws_frame_desc_t* __restrict__ desc, const int32_t* __restrict__ status,
              const uint64_t* __restrict__ offs, const uint32_t* __restrict__ region_map,
              const uint64_t* __restrict__ total_p, const uint64_t* __restrict__ base_p,
-             uint64_t capacity, uint32_t n_frames, uint32_t klass, uint32_t sid)
+             uint64_t capacity, uint32_t n_frames, uint32_t klass, uint32_t sid,
+             const cfws_frame_desc_t* __restrict__ parent)
 {
     const uint64_t out_base = base_p ? *base_p : 0;
     Pass P;
@@ -543,6 +580,7 @@ xform_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
     P.n_frames = n_frames;
     P.klass = klass;
     P.sid = sid;
+    P.parent = parent;
     const uint64_t n_regions = (P.total + kRegion - 1) / kRegion;
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -588,7 +626,7 @@ edge_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
             const cfws_frame_desc_t* __restrict__ desc, const int32_t* __restrict__ status,
             const uint64_t* __restrict__ offs, const uint64_t* __restrict__ total_p,
             const uint64_t* __restrict__ base_p, uint64_t capacity, uint32_t n_frames,
-            uint32_t klass, uint32_t sid)
+            uint32_t klass, uint32_t sid, const cfws_frame_desc_t* __restrict__ parent)
 {
     const uint64_t t = uint64_t(blockIdx.x) * kEdgeThreads + threadIdx.x;
     const uint64_t f = t >> 1;
@@ -606,6 +644,7 @@ edge_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
     P.n_frames = n_frames;
     P.klass = klass;
     P.sid = sid;
+    P.parent = parent;
     const uint64_t lo = offs[f];
     uint64_t hi = (f + 1 < n_frames) ? offs[f + 1] : P.total;
     if (hi > P.total) hi = P.total;
@@ -949,7 +988,7 @@ h2_expand_kernel(const cfws_frame_desc_t* __restrict__ desc, const uint64_t* __r
         e.payload_off = w0 + j * S;
         e.wire_off = 9 * d + e.payload_off;
         e.payload_size = (j + 1 < k) ? S : W - j * S;
-        e.mask_key = 0;
+        e.mask_key = (uint32_t)f;                    // the WS frame (kModeH2Ser)
         e.fin = (j + 1 == k) ? 1 : 0;
         e.opcode = 0;
         e.mask = 0;
@@ -1220,14 +1259,15 @@ template <int kMode>
 void launch_streaming(const void* src, void* dst, const cfws_frame_desc_t* desc,
                       const int32_t* status, const uint64_t* offs, const uint32_t* map,
                       const uint64_t* total_p, const uint64_t* base_p, uint64_t regions,
-                      uint64_t cap, size_t n, uint32_t klass, uint32_t sid, hipStream_t st)
+                      uint64_t cap, size_t n, uint32_t klass, uint32_t sid, hipStream_t st,
+                      const cfws_frame_desc_t* parent = nullptr)
 {
     xform_kernel<kMode><<<stream_grid(regions), kThreads, xform_lds_bytes(), st>>>(
         static_cast<const uint8_t*>(src), static_cast<uint8_t*>(dst), desc, status, offs, map,
-        total_p, base_p, cap, (uint32_t)n, klass, sid);
+        total_p, base_p, cap, (uint32_t)n, klass, sid, parent);
     edge_kernel<kMode><<<grid_for(2 * (uint64_t)n, kEdgeThreads), kEdgeThreads, 0, st>>>(
         static_cast<const uint8_t*>(src), static_cast<uint8_t*>(dst), desc, status, offs,
-        total_p, base_p, cap, (uint32_t)n, klass, sid);
+        total_p, base_p, cap, (uint32_t)n, klass, sid, parent);
 }
 
 template <int kMode>
@@ -1461,10 +1501,19 @@ int cfws_h2_serialize_batch(const void* d_payload, cfws_frame_desc_t* d_desc, si
         if (d_h2_total) (void)hipMemsetAsync(d_h2_total, 0, 8, st);
         return launch_check("h2_serialize(empty)");
     }
-    // 1. the WS frames, exactly as cfws_serialize_batch writes them
+    // 1. the WS frames' layout, exactly as cfws_serialize_batch lays them
+    //    out (header sizes, wire offsets into d_desc). With max_frame_size
+    //    >= 64 every WS header lies in its first DATA frame and the WS bytes
+    //    go straight into the DATA frames (kModeH2Ser, one streaming pass);
+    //    smaller limits write the WS wire first and wrap it (two passes).
+    const bool fused = S >= 64;
     const WsLayout WL = ws_layout(n, wire_cap);
-    if (int rc = cfws_serialize_batch(d_payload, d_desc, n, d_wire, wire_cap, nullptr, ws, WL.bytes, stream))
+    if (fused) {
+        if (int rc = cfws_serialize_plan(d_desc, n, wire_cap, nullptr, ws, WL.bytes, stream)) return rc;
+    } else if (int rc = cfws_serialize_batch(d_payload, d_desc, n, d_wire, wire_cap, nullptr, ws,
+                                             WL.bytes, stream)) {
         return rc;
+    }
     // 2. their DATA frames
     uint64_t* hdr = ws_ptr<uint64_t>(ws, L.hdr);
     uint64_t* vals = ws_ptr<uint64_t>(ws, L.vals);
@@ -1477,8 +1526,11 @@ int cfws_h2_serialize_batch(const void* d_payload, cfws_frame_desc_t* d_desc, si
     h2_finalize_kernel<<<grid_for(L.n_max, kThreads), kThreads, 0, st>>>(
         ddesc, doffs, L.n_max, hdr + 3, ws_ptr<const uint64_t>(ws, WL.hdr + 24), h2_cap, map, hdr,
         d_h2_total);
-    // 3. wrap: 9-byte DATA header + slice, one streaming pass
-    if (h2_cap)
+    // 3. the DATA frames: 9-byte header + slice, one streaming pass
+    if (h2_cap && fused)
+        launch_streaming<kModeH2Ser>(d_payload, d_h2, ddesc, nullptr, doffs, map, hdr, nullptr,
+                                     L.regions, h2_cap, L.n_max, kClassAll, stream_id, st, d_desc);
+    else if (h2_cap)
         launch_streaming<kModeH2Wrap>(d_wire, d_h2, ddesc, nullptr, doffs, map, hdr, nullptr,
                                       L.regions, h2_cap, L.n_max, kClassAll, stream_id, st);
     return launch_check("h2_serialize");

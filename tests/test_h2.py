@@ -108,7 +108,7 @@ def gpu_h2_serialize(payload: np.ndarray, desc: np.ndarray, sid=1, S=16384):
 
 @pytest.mark.gpu
 @pytest.mark.skipif(not gpu_present(), reason="needs the MI355X")
-@pytest.mark.parametrize("S", [16384, 1000, 100, 16])
+@pytest.mark.parametrize("S", [16384, 1000, 100, 64, 63, 16])
 def test_gpu_h2_serialize_random(S):
     rng = random.Random(S)
     payload = O.fill_splitmix(1 << 20, S, 0)
