@@ -153,7 +153,7 @@ def bench_h2(args, rank, world, dev):
                                    f"HTTP/2 DATA wrap (max frame {S}), then DATA unwrap + pool + "
                                    f"server-unmask", "h2_bytes_per_gpu": h2_total,
                        "data_frames_per_gpu": len(starts)},
-            "note": "send: one fused pass (WS frame straight into DATA frames); receive: DATA unwrap pass + WS deserialize pass",
+            "note": "one fused streaming pass per direction: WS frames straight into DATA frames (send), WS payload slices straight out of DATA frames (receive)",
             "verified": ok}
     if rank == 0:
         print(json.dumps(line), flush=True)

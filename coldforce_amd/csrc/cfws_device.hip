@@ -1104,6 +1104,112 @@ h2_starts_kernel(const uint64_t* __restrict__ ends, const uint64_t* __restrict__
     starts[m] = m == 0 ? 0 : ends[m - 1];
 }
 
+// ---- fused receive: WS frames read straight out of the DATA frames --------
+// With every DATA payload inside the pool capacity the pool is only a
+// concatenation: pool byte p lives in the DATA frame d with
+// poff[d] <= p < poff[d] + len[d]. The message plan gathers each message's
+// 2-14 WS header bytes through that map, and the payload pass copies +
+// unmasks each DATA frame's slice of its message's WS payload directly from
+// the HTTP/2 arena (one streaming pass instead of pool + deserialize).
+
+// DATA frame holding pool byte p (p < pool total): the last d with poff[d] <= p.
+__device__ __forceinline__ uint64_t pool_frame(const uint64_t* __restrict__ poff, uint64_t n, uint64_t p)
+{
+    uint64_t lo = 0, hi = n;             // first d with poff[d] > p, minus one
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if (poff[mid] <= p) lo = mid + 1; else hi = mid;
+    }
+    return lo - 1;
+}
+
+// co_ws_frame_deserialize on each pooled message [starts[m], ends[m])
+// (co_ws_http2_extension.c:134-164), header bytes gathered from the DATA
+// frames; same outputs as deserialize_parse_kernel on the pool.
+__global__ void __launch_bounds__(kThreads)
+h2_msg_parse_kernel(const uint8_t* __restrict__ h2, const cfws_frame_desc_t* __restrict__ pdesc,
+                    const int32_t* __restrict__ h2_status, const uint64_t* __restrict__ poff,
+                    uint64_t n_h2, const uint64_t* __restrict__ starts,
+                    const uint64_t* __restrict__ ends, uint64_t n_msg, uint64_t max_payload,
+                    uint64_t align, cfws_frame_desc_t* __restrict__ mdesc,
+                    int32_t* __restrict__ mstatus, uint64_t* __restrict__ vals)
+{
+    const uint64_t m = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
+    if (m >= n_msg) return;
+    const uint64_t s = starts[m], len = ends[m] - s;
+    uint8_t hb[16];
+    const uint32_t k = len < 14 ? (uint32_t)len : 14u;
+    uint64_t d = k ? pool_frame(poff, n_h2, s) : 0;
+    for (uint32_t i = 0; i < k; ++i) {
+        const uint64_t p = s + i;
+        while (p >= poff[d] + (h2_status[d] == CFWS_H2_PARSE_COMPLETE ? pdesc[d].payload_size : 0)) ++d;
+        hb[i] = h2[pdesc[d].wire_off + pdesc[d].header_size + (p - poff[d])];
+    }
+    cfws_frame_desc_t dd;
+    const int32_t st = parse_ws_header(hb, len, 0, max_payload, dd);
+    dd.wire_off = s;
+    mdesc[m] = dd;
+    mstatus[m] = st;
+    const uint64_t pl = st == CFWS_PARSE_COMPLETE ? dd.payload_size : 0;
+    vals[m] = (pl + align - 1) & ~(align - 1);
+}
+
+// One unit per DATA frame: the part of its pooled bytes that is WS payload
+// of its message's frame, as a deserialize-mode frame of the payload pass
+// (source = that slice in the HTTP/2 arena, key rotated to the slice's
+// payload index, output = message payload offset + index). Frames outside
+// any message, or of a message whose frame did not parse COMPLETE, are
+// empty units at the matching layout position (offsets stay monotone and
+// the pass zero-fills what the layout does not cover).
+__global__ void __launch_bounds__(kThreads)
+h2_units_kernel(const cfws_frame_desc_t* __restrict__ pdesc, const int32_t* __restrict__ h2_status,
+                const uint64_t* __restrict__ poff, const uint64_t* __restrict__ msg_id, uint64_t n,
+                uint64_t n_msg, const uint64_t* __restrict__ starts,
+                const cfws_frame_desc_t* __restrict__ mdesc, const int32_t* __restrict__ mstatus,
+                const uint64_t* __restrict__ hdr, cfws_frame_desc_t* __restrict__ udesc,
+                int32_t* __restrict__ ustatus, uint64_t* __restrict__ uoffs)
+{
+    const uint64_t d = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
+    if (d >= n) return;
+    const uint64_t m = msg_id[d];
+    cfws_frame_desc_t u = {};
+    uint64_t out = hdr[3];                             // past the last message
+    if (m < n_msg) {
+        const cfws_frame_desc_t M = mdesc[m];
+        const int32_t ms = mstatus[m];
+        const uint64_t hs = M.header_size;
+        // the message's layout span: payload_size when it parsed (an OOM
+        // frame keeps its layout), else nothing
+        const uint64_t span = (ms == CFWS_PARSE_COMPLETE || ms == CFWS_ERROR_OUT_OF_MEMORY)
+                                  ? M.payload_size : 0;
+        const uint64_t a = poff[d] - starts[m];
+        const uint64_t dl = h2_status[d] == CFWS_H2_PARSE_COMPLETE ? pdesc[d].payload_size : 0;
+        const uint64_t b = a + dl;
+        const uint64_t qa = a > hs ? (a - hs < span ? a - hs : span) : 0;
+        const uint64_t qb = b > hs ? (b - hs < span ? b - hs : span) : 0;
+        out = M.payload_off + qa;
+        if (ms == CFWS_PARSE_COMPLETE && qb > qa) {
+            u.wire_off = pdesc[d].wire_off + pdesc[d].header_size + (hs + qa - a);
+            u.payload_size = qb - qa;
+            u.mask = M.mask;
+            u.mask_key = M.mask ? __builtin_amdgcn_alignbyte(M.mask_key, M.mask_key,
+                                                             (uint32_t)(qa & 3u)) : 0u;
+        }
+    }
+    udesc[d] = u;
+    ustatus[d] = CFWS_PARSE_COMPLETE;
+    uoffs[d] = out;
+}
+
+__global__ void __launch_bounds__(kThreads)
+h2_unit_map_kernel(const uint64_t* __restrict__ uoffs, uint64_t n, const uint64_t* __restrict__ hdr,
+                   uint32_t* __restrict__ map)
+{
+    const uint64_t d = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
+    if (d >= n) return;
+    map_regions(uoffs, d, n, hdr[3], hdr[0], map);
+}
+
 // ---------------------------------------------------------------------------
 // receive-buffer frame indexing (co_ws_server.c:107-169)
 // ---------------------------------------------------------------------------
@@ -1455,6 +1561,8 @@ struct H2DeLayout {
     uint64_t es_total;   // u64: message count
     uint64_t starts, ends;   // u64[n_h2]
     uint64_t wsd;        // WS deserialize workspace
+    uint64_t udesc;      // cfws_frame_desc_t[n_h2]: fused payload-pass units
+    uint64_t ustatus;    // int32[n_h2]
     uint64_t bytes;
 };
 
@@ -1470,6 +1578,8 @@ H2DeLayout h2_de_layout(uint64_t n, uint64_t pool_cap, uint64_t payload_cap)
     L.starts = at; at = align_up(at + 8 * n, 256);
     L.ends = at; at = align_up(at + 8 * n, 256);
     L.wsd = at; at = align_up(at + ws_layout(n, payload_cap).bytes, 256);
+    L.udesc = at; at = align_up(at + sizeof(cfws_frame_desc_t) * n, 256);
+    L.ustatus = at; at = align_up(at + 4 * n, 256);
     L.bytes = at;
     return L;
 }
@@ -1567,8 +1677,6 @@ int cfws_h2_deserialize_batch(const void* d_h2, uint64_t h2_size, const uint64_t
     deserialize_finalize_kernel<<<grid_for(n, kThreads), kThreads, 0, st>>>(
         pdesc, d_h2_status, poffs, poffs, phdr, n, pool_cap, 0, ws_ptr<uint32_t>(pws, PL.map[0]),
         ws_ptr<uint32_t>(pws, PL.map[1]), nullptr);
-    if (pool_cap)
-        launch_pass<kModeDeser>(PL, 0, d_h2, d_pool, pdesc, d_h2_status, pws, pool_cap, n, kClassAll, st);
     // 2. messages: END_STREAM closes one (co_http2_stream.c:550-608)
     uint64_t* es = ws_ptr<uint64_t>(ws, L.es);
     uint64_t* n_msg_d = ws_ptr<uint64_t>(ws, L.es_total);
@@ -1578,21 +1686,55 @@ int cfws_h2_deserialize_batch(const void* d_h2, uint64_t h2_size, const uint64_t
     if (int rc = run_scan(es, n, ws_ptr<uint64_t>(ws, L.es_part), n_msg_d, st)) return rc;
     h2_messages_kernel<<<grid_for(n, kThreads), kThreads, 0, st>>>(pdesc, d_h2_status, es, n, ends);
     h2_starts_kernel<<<grid_for(n, kThreads), kThreads, 0, st>>>(ends, n_msg_d, n, starts);
-    uint64_t n_msg = 0;
-    hipError_t e = hipMemcpyAsync(&n_msg, n_msg_d, 8, hipMemcpyDeviceToHost, st);
+    uint64_t counts[2] = {0, 0};       // messages, pooled bytes
+    hipError_t e = hipMemcpyAsync(&counts[0], n_msg_d, 8, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipMemcpyAsync(&counts[1], phdr + 3, 8, hipMemcpyDeviceToHost, st);
     if (e == hipSuccess) e = hipStreamSynchronize(st);
     if (e != hipSuccess) return set_err(CFWS_ERROR_HIP, "h2_deserialize message count", e);
+    const uint64_t n_msg = counts[0];
     if (n_messages) *n_messages = (size_t)n_msg;
+    void* wsd = ws_ptr<void>(ws, L.wsd);
+    const WsLayout WL = ws_layout(n, payload_cap);
     // 3. each pooled message through co_ws_frame_deserialize, against its
     //    own size (co_ws_http2_extension.c:134-164)
-    void* wsd = ws_ptr<void>(ws, L.wsd);
-    const size_t wsd_size = ws_layout(n, payload_cap).bytes;
-    if (int rc = deserialize_plan_impl(d_pool, pool_cap, starts, ends, n_msg, max_payload, align, 0,
-                                       d_msg_desc, d_msg_status, payload_cap, d_payload_total, wsd,
-                                       wsd_size, stream))
-        return rc;
-    return cfws_deserialize_execute(d_pool, d_msg_desc, d_msg_status, n_msg, 0, d_payload,
-                                    payload_cap, wsd, stream);
+    if (counts[1] > pool_cap) {
+        // the pool capacity cuts DATA payloads: materialise the pool
+        // (layout-first OOM rule) and deserialize from it
+        if (pool_cap)
+            launch_pass<kModeDeser>(PL, 0, d_h2, d_pool, pdesc, d_h2_status, pws, pool_cap, n,
+                                    kClassAll, st);
+        if (int rc = deserialize_plan_impl(d_pool, pool_cap, starts, ends, n_msg, max_payload, align,
+                                           0, d_msg_desc, d_msg_status, payload_cap,
+                                           d_payload_total, wsd, WL.bytes, stream))
+            return rc;
+        return cfws_deserialize_execute(d_pool, d_msg_desc, d_msg_status, n_msg, 0, d_payload,
+                                        payload_cap, wsd, stream);
+    }
+    // fused: the pool is never written
+    if (align == 0 || (align & (align - 1)) || align > 4096)
+        return set_err(CFWS_ERROR_INVALID_ARGUMENT, "align must be a power of two <= 4096", hipSuccess);
+    uint64_t* hdr = ws_ptr<uint64_t>(wsd, WL.hdr);
+    if (n_msg == 0) return zero_totals(WL, wsd, d_payload_total, st);
+    uint64_t* offs0 = ws_ptr<uint64_t>(wsd, WL.offs[0]);
+    h2_msg_parse_kernel<<<grid_for(n_msg, kThreads), kThreads, 0, st>>>(
+        static_cast<const uint8_t*>(d_h2), pdesc, d_h2_status, poffs, n, starts, ends, n_msg,
+        max_payload, align, d_msg_desc, d_msg_status, offs0);
+    if (int rc = run_scan(offs0, n_msg, ws_ptr<uint64_t>(wsd, WL.partials[0]), hdr + 3, st)) return rc;
+    deserialize_finalize_kernel<<<grid_for(n_msg, kThreads), kThreads, 0, st>>>(
+        d_msg_desc, d_msg_status, offs0, offs0, hdr, n_msg, payload_cap, 0,
+        ws_ptr<uint32_t>(wsd, WL.map[0]), ws_ptr<uint32_t>(wsd, WL.map[1]), d_payload_total);
+    cfws_frame_desc_t* udesc = ws_ptr<cfws_frame_desc_t>(ws, L.udesc);
+    int32_t* ustatus = ws_ptr<int32_t>(ws, L.ustatus);
+    uint64_t* uoffs = ws_ptr<uint64_t>(wsd, WL.offs[1]);
+    uint32_t* umap = ws_ptr<uint32_t>(wsd, WL.map[1]);
+    h2_units_kernel<<<grid_for(n, kThreads), kThreads, 0, st>>>(
+        pdesc, d_h2_status, poffs, es, n, n_msg, starts, d_msg_desc, d_msg_status, hdr, udesc,
+        ustatus, uoffs);
+    h2_unit_map_kernel<<<grid_for(n, kThreads), kThreads, 0, st>>>(uoffs, n, hdr, umap);
+    if (payload_cap)
+        launch_streaming<kModeDeser>(d_h2, d_payload, udesc, ustatus, uoffs, umap, hdr, nullptr,
+                                     WL.regions, payload_cap, n, kClassAll, 0, st);
+    return launch_check("h2_deserialize");
 }
 
 size_t cfws_index_workspace_size(size_t n_conns)

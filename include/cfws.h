@@ -190,7 +190,11 @@ int cfws_index_frames_batch(const void* d_buf, const uint64_t* d_begin, const ui
  * own size (co_ws_http2_extension.c:134-164): d_msg_desc / d_msg_status get
  * one entry per message (room for n_h2 entries), payloads land in d_payload
  * as cfws_deserialize_batch lays them out (flags = 0). Synchronises the
- * stream to return *n_messages. */
+ * stream to return *n_messages. When every DATA payload fits pool_capacity
+ * the pool is virtual: WS headers are gathered and payload slices copied +
+ * unmasked straight out of the DATA frames in one pass, and d_pool is not
+ * written; otherwise the pool is materialised first (the capacity rule
+ * needs it). */
 #define CFWS_H2_DEFAULT_MAX_FRAME_SIZE 16384u
 #define CFWS_H2_PARSE_COMPLETE    0     /* co_http.h:40-42 */
 #define CFWS_H2_PARSE_MORE_DATA   1

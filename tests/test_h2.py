@@ -205,6 +205,40 @@ def test_gpu_h2_roundtrip_random(S):
 
 @pytest.mark.gpu
 @pytest.mark.skipif(not gpu_present(), reason="needs the MI355X")
+@pytest.mark.parametrize("S", [5, 13, 64])
+def test_gpu_h2_deserialize_headers_across_data_frames(S):
+    """DATA frames smaller than the WS header (max_frame_size 5 / 13) put a
+    WS header across several DATA frames; the fused receive gathers it.
+    Messages with trailing bytes after their WS frame, empty DATA frames
+    and a stream cut mid-message are mixed in."""
+    rng = random.Random(S * 7)
+    payload = O.fill_splitmix(1 << 16, 11, 0)
+    n = 60
+    d = np.zeros(n, dtype=O.DESC_DTYPE)
+    for i in range(n):
+        sz = rng.choice([0, 1, 7, 125, 126, 300, 2000])
+        d[i] = (rng.randrange(0, (1 << 16) - sz), 0, sz, rng.getrandbits(32), 1,
+                rng.choice([1, 2, 9]), rng.random() < .7, 0)
+    h2, _ = O.h2_serialize_batch(payload, d, 1, S)
+    # an extra DATA frame (no END_STREAM) of junk in front of message 3's
+    # END_STREAM frame: that message then carries bytes after its WS frame
+    index = O.h2_index(h2)
+    cut = int(index[len(index) // 2])
+    tail = h2[cut:]
+    junk = np.array([0, 0, 3, 0, 0, 0, 0, 0, 1, 0xAA, 0xBB, 0xCC], np.uint8)
+    empty = np.array([0, 0, 0, 0, 0, 0, 0, 0, 1], np.uint8)
+    h2 = np.concatenate([h2[:cut], empty, tail[:-4]])
+    index = O.h2_index(h2)
+    check_h2_deserialize(h2, index, S=S)
+    check_h2_deserialize(h2, index, S=S, align=1, payload_cap=len(h2) // 4)
+    # trailing junk inside a message: insert before a final DATA frame
+    k = int(index[5])
+    h2b = np.concatenate([h2[:k], junk, h2[k:]])
+    check_h2_deserialize(h2b, O.h2_index(h2b), S=S)
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not gpu_present(), reason="needs the MI355X")
 @pytest.mark.parametrize("idx", [0, 1, 2, 3])
 def test_gpu_config5_digest(idx):
     """Config 5 batches (16,376 B and 64 KiB frames, 1,024 and 65,536 of
