@@ -35,6 +35,7 @@ GIB = float(1 << 30)
 METRIC = "WS payload mask/unmask GiB/s device-resident, 64KiB frames, 1/2/4/8 GPUs"
 PAYLOAD_SEED = 0x5EED0002
 KEY_SEED = 2
+CONFIG4 = dict(frames_total=8 << 20, shards=8, payload_seed=0x5EED0004, key_seed=4)
 
 
 def parse():
@@ -47,9 +48,12 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="target CPU time of the cpu_baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--workload", choices=["config2", "config3", "config5"], default="config2",
+    ap.add_argument("--workload", choices=["config2", "config3", "config4", "config5"],
+                    default="config2",
                     help="config2: uniform 64 KiB frames (the metric's config); config3: Zipf "
                          "64 B-1 MiB messages in 1-8 continuation fragments, reassembled; "
+                         "config4: the 8 M x 64 KiB batch cut in 8 shards, rank r runs shard r "
+                         "(1,048,576 frames = 64 GiB per GPU); "
                          "config5: WebSocket over HTTP/2 DATA frames (--frame-size, default "
                          "16376)")
     return ap.parse_args()
@@ -193,6 +197,17 @@ def main():
         cfws.fill_splitmix(payload, c3["seed"] + rank)
         flags = cfws.DESERIALIZE_REASSEMBLE
         F = len(desc_np)
+    elif args.workload == "config4":
+        # one 8-way shard of the 8 M-frame batch per GPU (64 GiB payload +
+        # 64 GiB wire + 64 GiB unmasked copy resident in HBM)
+        c4 = CONFIG4
+        if world > c4["shards"]:
+            sys.exit("bench.py: config4 has 8 shards")
+        F = c4["frames_total"] // c4["shards"]
+        desc_np, byte_base = shard.uniform_shard(F, fs, c4["key_seed"], rank, c4["shards"])
+        arena_bytes = F * fs
+        payload = torch.empty(arena_bytes, dtype=torch.uint8, device=dev)
+        cfws.fill_splitmix(payload, c4["payload_seed"], byte_base)
     else:
         desc_np, byte_base = shard.uniform_shard(F, fs, KEY_SEED, rank, world)
         arena_bytes = F * fs
@@ -284,6 +299,9 @@ def main():
             "workload": (f"config2: {F} binary frames x {fs // 1024} KiB per GPU, client-mask "
                          f"(serialize) then server-unmask (deserialize), device resident"
                          if args.workload == "config2" else
+                         f"config4: shard {rank} of 8 of the 8 M x 64 KiB batch ({F} frames, "
+                         f"64 GiB per GPU), client-mask then server-unmask, device resident"
+                         if args.workload == "config4" else
                          f"config3: {F} frames / {len(msgs['len'])} Zipf messages (64 B-1 MiB, "
                          f"1-8 fragments) per GPU, client-mask then server-unmask with "
                          f"continuation reassembly, device resident"),
@@ -299,7 +317,7 @@ def main():
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": load_traffic(kernel_symbol),
+            "traffic": load_traffic(kernel_symbol) if args.workload == "config2" else None,
             "algorithmic_bytes_per_launch": alg_bytes,
             "avg_launch_ms": round(dom_ms, 4),
         },
