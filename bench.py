@@ -75,6 +75,19 @@ def cpu_baseline(frame_size: int, seconds: float):
     if iters > 1:
         ms, us = oracle.cpu_bench(n, frame_size, threads, iters, kind)
     payload = n * frame_size * iters
+
+    def one_thread(k):
+        """1-thread rate of `k` over ~2 s (the survey's 1-thread / N-thread pair)."""
+        m1, u1 = oracle.cpu_bench(64, frame_size, 1, 1, k)
+        it = max(1, int(math.ceil(2.0 / max(m1 + u1, 1e-3))))
+        m1, u1 = oracle.cpu_bench(64, frame_size, 1, it, k)
+        return round(2 * 64 * frame_size * it / (m1 + u1) / GIB, 3)
+
+    single = {}
+    if kind == "reference":
+        single = {"reference_O2": one_thread("reference"),
+                  "reference_O0_as_shipped": one_thread("reference_O0")}
+    single["port_O2"] = one_thread("port")
     return {
         "value": round(2 * payload / (ms + us) / GIB, 3),
         "unit": "GiB/s",
@@ -87,6 +100,7 @@ def cpu_baseline(frame_size: int, seconds: float):
         "mask_gibs": round(payload / ms / GIB, 3),
         "unmask_gibs": round(payload / us / GIB, 3),
         "seconds": round(ms + us, 2),
+        "single_thread_gibs": single,
     }
 
 

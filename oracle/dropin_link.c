@@ -39,8 +39,55 @@ static void fill(uint8_t* d, size_t n)
     for (size_t i = 0; i < n; ++i) d[i] = (uint8_t)(i * 131u + n);
 }
 
+#include <time.h>
+
+static double now(void)
+{
+    struct timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return t.tv_sec + 1e-9 * t.tv_nsec;
+}
+
+/* `dropin_link bench SIZE N`: per-frame latency of the drop-in, as a
+ * receive/send loop sees it -- N x (co_ws_frame_serialize(mask) into a
+ * cleared byte array + co_ws_frame_deserialize + co_ws_frame_destroy). */
+static int bench(size_t size, long n)
+{
+    uint8_t* data = malloc(size + 1);
+    fill(data, size);
+    co_byte_array_t* b = co_byte_array_create();
+    srandom(1);
+    for (int warm = 0; warm < 2; ++warm) {
+        co_byte_array_clear(b);
+        if (!co_ws_frame_serialize(true, CO_WS_OPCODE_BINARY, true, data, size, b)) return 2;
+    }
+    double ts = 0, td = 0;
+    for (long i = 0; i < n; ++i) {
+        co_byte_array_clear(b);
+        const double t0 = now();
+        if (!co_ws_frame_serialize(true, CO_WS_OPCODE_BINARY, true, data, size, b)) return 2;
+        const double t1 = now();
+        co_ws_frame_t* f = co_ws_frame_create();
+        size_t index = 0;
+        const int r = co_ws_frame_deserialize(f, co_byte_array_get_ptr(b, 0), co_byte_array_get_count(b),
+                                              &index);
+        const double t2 = now();
+        if (r != CO_WS_PARSE_COMPLETE || memcmp(co_ws_frame_get_payload_data(f), data, size) != 0) return 3;
+        co_ws_frame_destroy(f);
+        ts += t1 - t0;
+        td += t2 - t1;
+    }
+    printf("{\"frame_bytes\": %zu, \"frames\": %ld, \"serialize_us\": %.2f, \"deserialize_us\": %.2f}\n",
+           size, n, 1e6 * ts / n, 1e6 * td / n);
+    co_byte_array_destroy(b);
+    free(data);
+    return 0;
+}
+
 int main(int argc, char** argv)
 {
+    if (argc > 3 && strcmp(argv[1], "bench") == 0)
+        return bench((size_t)strtoull(argv[2], NULL, 10), strtol(argv[3], NULL, 10));
     const unsigned seed = argc > 1 ? (unsigned)strtoul(argv[1], NULL, 10) : 1u;
     static const size_t sizes[] = {0, 1, 125, 126, 1000, 65535, 65536, 70000};
     const size_t ns = sizeof sizes / sizeof sizes[0];
