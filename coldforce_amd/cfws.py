@@ -51,6 +51,7 @@ BATCH_SYMBOLS = (
     "cfws_h2_serialize_workspace_size", "cfws_h2_serialize_batch",
     "cfws_h2_deserialize_workspace_size", "cfws_h2_deserialize_batch",
     "cfws_index_frames", "cfws_index_workspace_size", "cfws_index_frames_batch",
+    "cfws_ws_accept_keys_batch",
 )
 DROPIN_SYMBOLS = (
     "co_ws_frame_serialize", "co_ws_frame_deserialize", "co_ws_frame_create",
@@ -122,6 +123,7 @@ def lib(path: str = LIB_PATH) -> C.CDLL:
         "cfws_index_workspace_size": ([_sz], _sz),
         "cfws_index_frames_batch": ([_vp, _vp, _vp, _sz, _u64, _vp, _u64, _vp, _vp, _vp, _vp, _vp,
                                      _sz, _vp], C.c_int),
+        "cfws_ws_accept_keys_batch": ([_vp, _vp, _sz, _vp, _vp], C.c_int),
         "cfws_pipeline_create": ([_u64, _sz, C.c_int, C.POINTER(_vp)], C.c_int),
         "cfws_pipeline_destroy": ([_vp], None),
         "cfws_pipeline_serialize": ([_vp, _vp, _vp, _sz, _vp, _u64, C.POINTER(_u64)], C.c_int),
@@ -448,6 +450,26 @@ def index_frames_batch(buf_t, begin_t, end_t, max_payload: int = DEFAULT_MAX_PAY
                                          _stream(stream)),
            "cfws_index_frames_batch")
     return starts_t, first[:n], consumed[:n], stop[:n], int(total.item())
+
+
+# ---- handshake accept keys ---------------------------------------------------
+WS_ACCEPT_SLOT = 32
+
+
+def ws_accept_keys(keys, device="cuda", stream=None) -> list[str]:
+    """Sec-WebSocket-Accept of every key (bytes) through
+    cfws_ws_accept_keys_batch."""
+    import torch
+    off = np.zeros(len(keys) + 1, dtype=np.int64)
+    off[1:] = np.cumsum([len(k) for k in keys])
+    raw = np.frombuffer(b"".join(keys) or b"\0", np.uint8).copy()
+    d_keys = torch.from_numpy(raw).to(device)
+    d_off = torch.from_numpy(off).to(device)
+    out = torch.zeros(max(len(keys), 1) * WS_ACCEPT_SLOT, dtype=torch.uint8, device=device)
+    _check(lib().cfws_ws_accept_keys_batch(_p(d_keys), _p(d_off), len(keys), _p(out),
+                                           _stream(stream)), "cfws_ws_accept_keys_batch")
+    h = out.cpu().numpy().reshape(-1, WS_ACCEPT_SLOT)
+    return [bytes(h[i, :28]).decode() for i in range(len(keys))]
 
 
 # ---- host-memory pipeline --------------------------------------------------

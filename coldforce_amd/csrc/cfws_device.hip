@@ -1211,6 +1211,81 @@ h2_unit_map_kernel(const uint64_t* __restrict__ uoffs, uint64_t n, const uint64_
 }
 
 // ---------------------------------------------------------------------------
+// handshake accept keys (co_ws_create_base64_accept_key,
+// co_ws_http_extension.c:26-57): base64(SHA-1(key || GUID))
+// ---------------------------------------------------------------------------
+__constant__ char kWsGuid[37] = "258EAFA5-E914-47DA-95CA-C5AB0DC85B11";
+__constant__ char kB64[65] = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789+/";
+
+// Byte i of the SHA-1 input key || GUID || 0x80 || 0... || bit length (BE64)
+// over `blocks` 64-byte blocks.
+__device__ __forceinline__ uint32_t accept_msg_byte(const uint8_t* __restrict__ key, uint64_t L,
+                                                    uint64_t blocks, uint64_t i)
+{
+    const uint64_t m = L + 36;
+    if (i < L) return key[i];
+    if (i < m) return (uint8_t)kWsGuid[i - L];
+    if (i == m) return 0x80u;
+    const uint64_t end = blocks * 64;
+    if (i >= end - 8) return (uint32_t)((m * 8) >> (8 * (end - 1 - i))) & 0xffu;
+    return 0;
+}
+
+__device__ __forceinline__ uint32_t rol32(uint32_t v, int b) { return (v << b) | (v >> (32 - b)); }
+
+// One thread per connection: a connection storm's accept keys at once.
+__global__ void __launch_bounds__(kThreads)
+ws_accept_kernel(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ key_off, uint64_t n,
+                 char* __restrict__ out)
+{
+    const uint64_t c = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
+    if (c >= n) return;
+    const uint8_t* key = keys + key_off[c];
+    const uint64_t L = key_off[c + 1] - key_off[c];
+    const uint64_t blocks = (L + 36 + 9 + 63) / 64;
+    uint32_t st[5] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u, 0xc3d2e1f0u};
+    for (uint64_t b = 0; b < blocks; ++b) {
+        uint32_t w[16];
+#pragma unroll
+        for (int t = 0; t < 16; ++t) {
+            const uint64_t i = b * 64 + 4 * t;
+            w[t] = accept_msg_byte(key, L, blocks, i) << 24 | accept_msg_byte(key, L, blocks, i + 1) << 16 |
+                   accept_msg_byte(key, L, blocks, i + 2) << 8 | accept_msg_byte(key, L, blocks, i + 3);
+        }
+        uint32_t a = st[0], bb = st[1], cc = st[2], d = st[3], e = st[4];
+#pragma unroll
+        for (int r = 0; r < 80; ++r) {
+            if (r >= 16)
+                w[r & 15] = rol32(w[(r + 13) & 15] ^ w[(r + 8) & 15] ^ w[(r + 2) & 15] ^ w[r & 15], 1);
+            const uint32_t f = r < 20 ? ((bb & cc) | (~bb & d))
+                             : r < 40 ? (bb ^ cc ^ d)
+                             : r < 60 ? ((bb & cc) | (bb & d) | (cc & d)) : (bb ^ cc ^ d);
+            const uint32_t k = r < 20 ? 0x5a827999u : r < 40 ? 0x6ed9eba1u : r < 60 ? 0x8f1bbcdcu : 0xca62c1d6u;
+            const uint32_t t = rol32(a, 5) + f + e + k + w[r & 15];
+            e = d; d = cc; cc = rol32(bb, 30); bb = a; a = t;
+        }
+        st[0] += a; st[1] += bb; st[2] += cc; st[3] += d; st[4] += e;
+    }
+    // base64 of the 20 hash bytes: 6 full groups + 2 bytes -> 3 chars + '='
+    char* o = out + CFWS_WS_ACCEPT_SLOT * c;
+#pragma unroll
+    for (int g = 0; g < 7; ++g) {
+        uint32_t v = 0;
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            const int idx = 3 * g + j;
+            const uint32_t byte = idx < 20 ? (st[idx >> 2] >> (8 * (3 - (idx & 3)))) & 0xffu : 0u;
+            v = v << 8 | byte;
+        }
+        o[4 * g] = kB64[(v >> 18) & 63];
+        o[4 * g + 1] = kB64[(v >> 12) & 63];
+        o[4 * g + 2] = kB64[(v >> 6) & 63];
+        o[4 * g + 3] = g < 6 ? kB64[v & 63] : '=';
+    }
+    o[28] = 0;
+}
+
+// ---------------------------------------------------------------------------
 // receive-buffer frame indexing (co_ws_server.c:107-169)
 // ---------------------------------------------------------------------------
 
@@ -1767,6 +1842,18 @@ int cfws_index_frames_batch(const void* d_buf, const uint64_t* d_begin, const ui
     index_walk_kernel<true><<<g, kThreads, 0, st>>>(buf, d_begin, d_end, n, max_payload, d_first,
                                                     nullptr, nullptr, d_starts, cap);
     return launch_check("index");
+}
+
+int cfws_ws_accept_keys_batch(const void* d_keys, const uint64_t* d_key_off, size_t n,
+                              char* d_accept, void* stream)
+{
+    if (int rc = check_init()) return rc;
+    if (n == 0) return CFWS_OK;
+    if (!d_keys || !d_key_off || !d_accept)
+        return set_err(CFWS_ERROR_INVALID_ARGUMENT, "accept keys: null pointer", hipSuccess);
+    ws_accept_kernel<<<grid_for(n, kThreads), kThreads, 0, static_cast<hipStream_t>(stream)>>>(
+        static_cast<const uint8_t*>(d_keys), d_key_off, n, d_accept);
+    return launch_check("ws_accept_keys");
 }
 
 int cfws_xor_mask(const void* d_src, void* d_dst, uint64_t n, uint32_t key, uint32_t phase,

@@ -174,6 +174,18 @@ int cfws_index_frames_batch(const void* d_buf, const uint64_t* d_begin, const ui
                             int32_t* d_stop, uint64_t* d_total, void* d_workspace,
                             size_t workspace_size, void* stream);
 
+/* ---- handshake accept keys ----------------
+ * Sec-WebSocket-Accept for n connections at once, as
+ * co_ws_create_base64_accept_key computes it for one
+ * (co_ws_http_extension.c:26-57; used by the server's upgrade response :342
+ * and the client's check :245): base64(SHA-1(key || "258EAFA5-E914-47DA-
+ * 95CA-C5AB0DC85B11")) with '=' padding. Key c is the bytes
+ * d_keys[d_key_off[c], d_key_off[c + 1]) (n + 1 offsets, any length); its
+ * 28-character accept value + NUL goes to d_accept + CFWS_WS_ACCEPT_SLOT * c. */
+#define CFWS_WS_ACCEPT_SLOT 32
+int cfws_ws_accept_keys_batch(const void* d_keys, const uint64_t* d_key_off, size_t n,
+                              char* d_accept, void* stream);
+
 /* ---- WebSocket over HTTP/2 (src/ws_http2) ---------------------------------
  * Send: every WS frame of the batch is serialized (cfws_serialize_batch, into
  * d_wire) and carried in HTTP/2 DATA frames of at most max_frame_size payload

@@ -161,6 +161,16 @@ def index_stream(buf: np.ndarray, begin: int = 0, end: int | None = None,
     return starts[:k], int(consumed.value), int(stop.value)
 
 
+def ws_accept_key(key: bytes) -> str:
+    """base64(SHA-1(key || GUID)) -- co_ws_create_base64_accept_key."""
+    f = lib().orc_ws_accept_key
+    f.argtypes = [C.c_char_p, _u64, C.c_char_p]
+    f.restype = None
+    out = C.create_string_buffer(29)
+    f(key, len(key), out)
+    return out.value.decode()
+
+
 def fill_splitmix(n_bytes: int, seed: int, byte_base: int = 0) -> np.ndarray:
     out = np.zeros(max(n_bytes, 1), dtype=np.uint8)
     lib().orc_fill_splitmix(_ptr(out), n_bytes, seed, byte_base)
@@ -357,6 +367,16 @@ def ref_index_stream(R, data: bytes, begin: int = 0, max_payload: int = DEFAULT_
     k = f(_ptr(src), len(data), begin, max_payload, _ptr(starts), cap, C.byref(consumed),
           C.byref(stop))
     return starts[:k], int(consumed.value), int(stop.value)
+
+
+def ref_ws_accept_key(R, key: bytes) -> str:
+    """The reference's co_sha1 + co_base64_encode on key || GUID."""
+    f = R.ref_ws_accept_key
+    f.argtypes = [C.c_char_p, C.c_ulonglong, C.c_char_p, C.c_ulonglong]
+    f.restype = C.c_int
+    out = C.create_string_buffer(64)
+    assert f(key, len(key), out, 64) == 28
+    return out.value.decode()
 
 
 def ref_h2_recv(R, data: bytes, index: int = 0, S: int = 16384):

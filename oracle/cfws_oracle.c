@@ -551,3 +551,76 @@ uint64_t orc_h2_deserialize_batch(const uint8_t* h2, uint64_t size, const uint64
     if (n_msg_out) *n_msg_out = n_msg;
     return total;
 }
+
+/* ---- handshake accept key ----------------------------
+ * co_ws_create_base64_accept_key (co_ws_http_extension.c:26-57):
+ * base64(SHA-1(key || GUID)) with '=' padding. SHA-1 as FIPS 180-4 (the
+ * reference's co_sha1.c:55-283 is the classic public-domain transform);
+ * base64 with the standard alphabet (co_base64.c:17-91). */
+static uint32_t orc_rol(uint32_t v, int b) { return (v << b) | (v >> (32 - b)); }
+
+static void orc_sha1_block(uint32_t st[5], const uint8_t* p)
+{
+    uint32_t w[80];
+    for (int i = 0; i < 16; ++i)
+        w[i] = (uint32_t)p[4 * i] << 24 | (uint32_t)p[4 * i + 1] << 16 | (uint32_t)p[4 * i + 2] << 8 | p[4 * i + 3];
+    for (int i = 16; i < 80; ++i) w[i] = orc_rol(w[i - 3] ^ w[i - 8] ^ w[i - 14] ^ w[i - 16], 1);
+    uint32_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4];
+    for (int i = 0; i < 80; ++i) {
+        uint32_t f, k;
+        if (i < 20) { f = (b & c) | (~b & d); k = 0x5a827999u; }
+        else if (i < 40) { f = b ^ c ^ d; k = 0x6ed9eba1u; }
+        else if (i < 60) { f = (b & c) | (b & d) | (c & d); k = 0x8f1bbcdcu; }
+        else { f = b ^ c ^ d; k = 0xca62c1d6u; }
+        const uint32_t t = orc_rol(a, 5) + f + e + k + w[i];
+        e = d; d = c; c = orc_rol(b, 30); b = a; a = t;
+    }
+    st[0] += a; st[1] += b; st[2] += c; st[3] += d; st[4] += e;
+}
+
+void orc_sha1(const void* data, uint64_t n, uint8_t out[20])
+{
+    uint32_t st[5] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u, 0xc3d2e1f0u};
+    const uint8_t* p = (const uint8_t*)data;
+    uint64_t i = 0;
+    for (; i + 64 <= n; i += 64) orc_sha1_block(st, p + i);
+    uint8_t tail[128];
+    memset(tail, 0, sizeof tail);
+    const uint64_t r = n - i;
+    if (r) memcpy(tail, p + i, (size_t)r);
+    tail[r] = 0x80;
+    const uint64_t tl = r + 9 <= 64 ? 64 : 128;
+    const uint64_t bits = n * 8;
+    for (int j = 0; j < 8; ++j) tail[tl - 1 - j] = (uint8_t)(bits >> (8 * j));
+    orc_sha1_block(st, tail);
+    if (tl == 128) orc_sha1_block(st, tail + 64);
+    for (int j = 0; j < 20; ++j) out[j] = (uint8_t)(st[j >> 2] >> (8 * (3 - (j & 3))));
+}
+
+uint64_t orc_base64(const uint8_t* src, uint64_t n, char* out)
+{
+    static const char tab[] = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789+/";
+    uint64_t o = 0;
+    for (uint64_t i = 0; i < n; i += 3) {
+        const uint32_t b0 = src[i], b1 = i + 1 < n ? src[i + 1] : 0, b2 = i + 2 < n ? src[i + 2] : 0;
+        const uint32_t v = b0 << 16 | b1 << 8 | b2;
+        out[o++] = tab[(v >> 18) & 63];
+        out[o++] = tab[(v >> 12) & 63];
+        out[o++] = i + 1 < n ? tab[(v >> 6) & 63] : '=';
+        out[o++] = i + 2 < n ? tab[v & 63] : '=';
+    }
+    out[o] = 0;
+    return o;
+}
+
+void orc_ws_accept_key(const char* key, uint64_t key_len, char out[29])
+{
+    static const char guid[] = "258EAFA5-E914-47DA-95CA-C5AB0DC85B11";
+    uint8_t* buf = (uint8_t*)malloc((size_t)key_len + 36 + 1);
+    memcpy(buf, key, (size_t)key_len);
+    memcpy(buf + key_len, guid, 36);
+    uint8_t h[20];
+    orc_sha1(buf, key_len + 36, h);
+    free(buf);
+    orc_base64(h, 20, out);
+}

@@ -148,8 +148,16 @@ void orc_fill_splitmix(uint8_t* out, uint64_t n_bytes, uint64_t seed,
 int orc_cpu_bench(uint64_t n_frames, uint64_t frame_size, int threads,
                   int iters, double* mask_seconds, double* unmask_seconds);
 
+/* Handshake accept key, co_ws_create_base64_accept_key
+ * (co_ws_http_extension.c:26-57): out = base64(SHA-1(key || GUID)), 28
+ * characters + NUL. */
+void orc_sha1(const void* data, uint64_t n, uint8_t out[20]);
+uint64_t orc_base64(const uint8_t* src, uint64_t n, char* out);
+void orc_ws_accept_key(const char* key, uint64_t key_len, char out[29]);
+
 #ifdef __cplusplus
 }
 #endif
 
 #endif
+

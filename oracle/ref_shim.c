@@ -160,3 +160,28 @@ int ref_h2_recv(const unsigned char* data, unsigned long long size, unsigned lon
     co_byte_array_destroy(b);
     return r;
 }
+
+/* ---- handshake accept key through the reference's co_sha1.c + co_base64.c
+ * (compiled in place): the body of the static co_ws_create_base64_accept_key
+ * (co_ws_http_extension.c:26-57), whose file needs the whole HTTP stack. */
+#include <coldforce/http/co_base64.h>
+#include <coldforce/http/co_sha1.h>
+
+int ref_ws_accept_key(const char* key, unsigned long long key_len, char* out, unsigned long long cap)
+{
+    size_t key_data_size = (size_t)key_len + 36;
+    char* key_data = malloc(key_data_size + 1);
+    memcpy(key_data, key, (size_t)key_len);
+    memcpy(key_data + key_len, "258EAFA5-E914-47DA-95CA-C5AB0DC85B11", 37);
+    uint8_t sha1_hash[CO_SHA1_HASH_SIZE];
+    co_sha1(key_data, (uint32_t)key_data_size, sha1_hash);
+    free(key_data);
+    char* b64;
+    size_t b64_len;
+    co_base64_encode(sha1_hash, sizeof(sha1_hash), &b64, &b64_len, true);
+    int r = (int)b64_len;
+    if (b64_len + 1 <= cap) memcpy(out, b64, b64_len + 1);
+    else r = -1;
+    free(b64);
+    return r;
+}

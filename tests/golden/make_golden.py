@@ -14,6 +14,7 @@ Fixtures (inputs + expected outputs):
                         size limits, concatenated frames, non-minimal lengths
   keys.json             mask-key stream after srandom(seed)
   batch_digests.json    SHA-256 of whole serialized batches (config 2 full size)
+  handshake_cases.json  Sec-WebSocket-Accept keys (co_sha1.c + co_base64.c)
   index_cases.json      receive-loop frame indexing (co_ws_server.c:107-169 around
                         the reference's co_ws_frame_deserialize): frame starts,
                         consumed index, stop code per connection stream
@@ -356,6 +357,21 @@ def index_cases(R):
     return dict(blobs={k: v.hex() for k, v in blobs.items()}, cases=out)
 
 
+def handshake_cases(R):
+    """Sec-WebSocket-Accept for keys of every shape through the reference's
+    co_sha1.c + co_base64.c (lengths 0-300 cross SHA-1's one/two/three
+    block padding boundaries: 55/56 and 119/120 bytes with the 36-byte GUID)."""
+    import random
+    rng = random.Random(0xACCE)
+    keys = [b"dGhlIHNhbXBsZSBub25jZQ==", b""]                 # RFC 6455 1.3 example
+    for n in [1, 2, 3, 16, 18, 19, 20, 24, 27, 28, 63, 64, 83, 84, 85, 100, 147, 148, 200, 300]:
+        keys.append(bytes(rng.randrange(33, 127) for _ in range(n)))
+    for _ in range(40):                                           # real-shaped nonces
+        import base64
+        keys.append(base64.b64encode(rng.randbytes(16)))
+    return [dict(key_hex=k.hex(), accept=O.ref_ws_accept_key(R, k)) for k in keys]
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--skip-full", action="store_true", help="skip the 4 GiB config-2 digest")
@@ -366,6 +382,9 @@ def main():
     assert R is not None, "oracle/_ref not built (needs /root/reference)"
     if a.only == "index":
         dump("index_cases.json", index_cases(R))
+        return
+    if a.only == "handshake":
+        dump("handshake_cases.json", handshake_cases(R))
         return
     dump("rfc6455_kat.json", rfc6455(R))
     dump("serialize_cases.json", serialize_cases(R))
@@ -386,6 +405,7 @@ def main():
         h2d += [h2_digest(R, 65536, 16376, 0x5EED0005, 5), h2_digest(R, 65536, 65536, 0x5EED0005, 5)]
     dump("h2_digests.json", h2d)
     dump("index_cases.json", index_cases(R))
+    dump("handshake_cases.json", handshake_cases(R))
 
 
 if __name__ == "__main__":

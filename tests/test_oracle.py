@@ -190,3 +190,13 @@ def test_index_stream_matches_reference_receive_loop(i):
                                         c["max_payload"])
     assert [int(x) for x in st] == c["starts"], c["name"]
     assert consumed == c["consumed"] and stop == c["stop"], c["name"]
+
+
+def test_ws_accept_key_rfc6455_example():
+    """RFC 6455 section 1.3: the example nonce's Sec-WebSocket-Accept."""
+    assert O.ws_accept_key(b"dGhlIHNhbXBsZSBub25jZQ==") == "s3pPLMBiTxaQ9kYGzzhZRbK+xOo="
+
+
+def test_ws_accept_key_matches_reference_fixtures():
+    for c in golden("handshake_cases.json"):
+        assert O.ws_accept_key(bytes.fromhex(c["key_hex"])) == c["accept"], c["key_hex"]
