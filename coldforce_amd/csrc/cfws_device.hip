@@ -48,6 +48,11 @@ constexpr uint64_t kSlice = 64 * kChunk;                     // one wave-instruc
 constexpr uint64_t kRegion = kSlice * kUnroll;               // one wave's region: 4 KiB
 constexpr int kScanItems = 8;
 constexpr uint64_t kScanBlock = uint64_t(kThreads) * kScanItems;
+// Plan kernels: one frame per thread. Their per-frame work is a chain of
+// dependent loads (descriptor or header bytes), so parallelism beats items
+// per thread: 2,048-frame blocks left 224 of 256 CUs idle at 65,536 frames.
+constexpr int kPlanItems = 1;
+constexpr uint64_t kPlanBlock = uint64_t(kThreads) * kPlanItems;
 
 // Frame classes a pass copies (deserialize): all, data only, control only.
 enum : uint32_t { kClassAll = 0, kClassData = 1, kClassControl = 2 };
@@ -86,7 +91,7 @@ WsLayout ws_layout(uint64_t n, uint64_t capacity)
 {
     WsLayout L;
     L.regions = (capacity + kRegion - 1) / kRegion;
-    L.scan_blocks = (n + kScanBlock - 1) / kScanBlock;
+    L.scan_blocks = (n + kPlanBlock - 1) / kPlanBlock;     // >= any run_scan's blocks
     uint64_t at = 0;
     L.hdr = at;
     at += 256;
@@ -673,17 +678,6 @@ edge_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
 // ---------------------------------------------------------------------------
 // plan kernels
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(kThreads)
-serialize_sizes_kernel(cfws_frame_desc_t* __restrict__ desc, uint64_t* __restrict__ vals, uint64_t n)
-{
-    const uint64_t f = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
-    if (f >= n) return;
-    const uint64_t len = desc[f].payload_size;
-    const uint32_t hs = header_size_of(len, desc[f].mask != 0);
-    desc[f].header_size = (uint8_t)hs;
-    vals[f] = hs + len;
-}
-
 // WS header at s of data[0, size) (co_ws_frame.c:131-213), with the callers'
 // two-byte precheck (co_ws_client.c:202-206): the reference's decisions in
 // its order (MORE_DATA before DATA_TOO_BIG). d gets what the reference has
@@ -728,36 +722,6 @@ __device__ __forceinline__ int32_t parse_ws_header(const uint8_t* __restrict__ w
     if (size - p < d.payload_size) return CFWS_PARSE_MORE_DATA;
     if (d.payload_size > max_payload) return CFWS_ERROR_DATA_TOO_BIG;
     return CFWS_PARSE_COMPLETE;
-}
-
-// Header decode at index[f]. Writes the layout sizes of both passes:
-// vals0 = data (or every frame without reassembly), vals1 = control frames
-// when reassembling.
-__global__ void __launch_bounds__(kThreads)
-deserialize_parse_kernel(const uint8_t* __restrict__ wire, uint64_t wire_size_all,
-                         const uint64_t* __restrict__ index, const uint64_t* __restrict__ ends,
-                         uint64_t n, uint64_t max_payload,
-                         uint64_t align, uint32_t reassemble, cfws_frame_desc_t* __restrict__ desc,
-                         int32_t* __restrict__ status, uint64_t* __restrict__ vals0,
-                         uint64_t* __restrict__ vals1)
-{
-    const uint64_t f = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
-    if (f >= n) return;
-    // data_size of the call: the whole buffer, or this frame's own message
-    // (co_http2_stream_receive_ws_frame passes the pooled DATA, :144-146)
-    const uint64_t wire_size = ends && ends[f] < wire_size_all ? ends[f] : wire_size_all;
-    cfws_frame_desc_t d;
-    const int32_t st = parse_ws_header(wire, wire_size, index[f], max_payload, d);
-    desc[f] = d;
-    status[f] = st;
-    const uint64_t len = (st == CFWS_PARSE_COMPLETE) ? d.payload_size : 0;
-    if (reassemble) {
-        const bool ctl = is_control(d.opcode);
-        vals0[f] = ctl ? 0 : len;
-        vals1[f] = ctl ? len : 0;
-    } else {
-        vals0[f] = (len + align - 1) & ~(align - 1);
-    }
 }
 
 // Exclusive block scan of one value per thread; *block_total gets the sum.
@@ -816,6 +780,25 @@ scan_partials_kernel(uint64_t* __restrict__ partials, uint64_t nb, uint64_t* __r
     if (threadIdx.x == 0) *grand = carry;
 }
 
+// scan_partials_kernel for up to two passes in one launch (block p: pass p).
+__global__ void __launch_bounds__(kThreads)
+scan_partials2_kernel(uint64_t* __restrict__ partials0, uint64_t* __restrict__ partials1, uint64_t nb,
+                      uint64_t* __restrict__ grand0, uint64_t* __restrict__ grand1)
+{
+    __shared__ uint64_t s_wave[kWaves];
+    uint64_t* partials = blockIdx.x ? partials1 : partials0;
+    uint64_t carry = 0;
+    for (uint64_t b = 0; b < nb; b += kThreads) {
+        const uint64_t i = b + threadIdx.x;
+        const uint64_t x = i < nb ? partials[i] : 0;
+        uint64_t tot;
+        const uint64_t ex = block_exclusive_scan(x, s_wave, &tot);
+        if (i < nb) partials[i] = carry + ex;
+        carry += tot;
+    }
+    if (threadIdx.x == 0) *(blockIdx.x ? grand1 : grand0) = carry;
+}
+
 __global__ void __launch_bounds__(kThreads)
 scan_apply_kernel(uint64_t* __restrict__ vals, uint64_t n, const uint64_t* __restrict__ partials)
 {
@@ -852,20 +835,189 @@ __device__ __forceinline__ void map_regions(const uint64_t* __restrict__ offs, u
     if (f == n - 1) map[(total + kRegion - 1) / kRegion] = (uint32_t)(n - 1);
 }
 
-__global__ void __launch_bounds__(kThreads)
-serialize_finalize_kernel(cfws_frame_desc_t* __restrict__ desc, const uint64_t* __restrict__ offs,
-                          uint64_t* __restrict__ hdr, uint64_t n, uint64_t capacity,
-                          uint32_t* __restrict__ map, uint64_t* __restrict__ user_total)
+// Region-map entries of one frame's output bytes [lo, hi) of a pass over
+// [0, total): every region whose first byte lies inside gets the frame.
+__device__ __forceinline__ void map_range(uint64_t lo, uint64_t hi, uint64_t f, uint64_t total,
+                                          uint32_t* __restrict__ map)
 {
-    const uint64_t f = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
-    if (f >= n) return;
+    const uint64_t a = lo < total ? lo : total;
+    const uint64_t b = hi < total ? hi : total;
+    if (b > a) {
+        const uint64_t r1 = (b + kRegion - 1) / kRegion;
+        for (uint64_t r = (a + kRegion - 1) / kRegion; r < r1; ++r) map[r] = (uint32_t)f;
+    }
+}
+
+// ---- plans: three launches each -------------------------------------------
+// 1. per frame: sizes (serialize: header size, co_ws_frame.c:41-91;
+//    deserialize: the header decode) + the block's sum;
+// 2. scan_partials_kernel: the block sums (one block per pass);
+// 3. per block: exclusive offsets of its 2,048 frames, then everything the
+//    offsets decide (descriptor offsets, capacity rule, region maps, totals).
+
+__global__ void __launch_bounds__(kThreads)
+serialize_plan_reduce_kernel(cfws_frame_desc_t* __restrict__ desc, uint64_t* __restrict__ vals,
+                             uint64_t n, uint64_t* __restrict__ partials)
+{
+    __shared__ uint64_t s_wave[kWaves];
+    const uint64_t b0 = uint64_t(blockIdx.x) * kPlanBlock;
+    uint64_t sum = 0;
+#pragma unroll
+    for (int k = 0; k < kPlanItems; ++k) {
+        const uint64_t f = b0 + uint64_t(k) * kThreads + threadIdx.x;
+        if (f < n) {
+            const uint64_t len = desc[f].payload_size;
+            const uint32_t hs = header_size_of(len, desc[f].mask != 0);
+            desc[f].header_size = (uint8_t)hs;
+            vals[f] = hs + len;
+            sum += hs + len;
+        }
+    }
+    uint64_t total;
+    block_exclusive_scan(sum, s_wave, &total);
+    if (threadIdx.x == 0) partials[blockIdx.x] = total;
+}
+
+__global__ void __launch_bounds__(kThreads)
+serialize_plan_apply_kernel(cfws_frame_desc_t* __restrict__ desc, uint64_t* __restrict__ vals,
+                            uint64_t n, const uint64_t* __restrict__ partials,
+                            uint64_t* __restrict__ hdr, uint64_t capacity,
+                            uint32_t* __restrict__ map, uint64_t* __restrict__ user_total)
+{
+    __shared__ uint64_t s_wave[kWaves];
     const uint64_t g = hdr[3];
     const uint64_t total = g < capacity ? g : capacity;
-    desc[f].wire_off = offs[f];
-    map_regions(offs, f, n, g, total, map);
-    if (f == n - 1) {
-        hdr[0] = total;
-        if (user_total) *user_total = g;
+    const uint64_t i0 = uint64_t(blockIdx.x) * kPlanBlock + uint64_t(threadIdx.x) * kPlanItems;
+    uint64_t v[kPlanItems];
+    uint64_t sum = 0;
+#pragma unroll
+    for (int k = 0; k < kPlanItems; ++k) {
+        v[k] = (i0 + k < n) ? vals[i0 + k] : 0;
+        sum += v[k];
+    }
+    uint64_t tot;
+    uint64_t run = block_exclusive_scan(sum, s_wave, &tot) + partials[blockIdx.x];
+#pragma unroll
+    for (int k = 0; k < kPlanItems; ++k) {
+        const uint64_t f = i0 + k;
+        if (f < n) {
+            vals[f] = run;
+            desc[f].wire_off = run;
+            map_range(run, run + v[k], f, total, map);
+            if (f == n - 1) {
+                map[(total + kRegion - 1) / kRegion] = (uint32_t)f;
+                hdr[0] = total;
+                if (user_total) *user_total = g;
+            }
+        }
+        run += v[k];
+    }
+}
+
+// Header decode at index[f] against its data size (the whole buffer, or the
+// frame's own message: co_http2_stream_receive_ws_frame passes the pooled
+// DATA, co_ws_http2_extension.c:144-146). Layout sizes: vals0 = data (or
+// every frame without reassembly), vals1 = control frames when reassembling.
+__global__ void __launch_bounds__(kThreads)
+deserialize_plan_reduce_kernel(const uint8_t* __restrict__ wire, uint64_t wire_size_all,
+                               const uint64_t* __restrict__ index, const uint64_t* __restrict__ ends,
+                               uint64_t n, uint64_t max_payload, uint64_t align, uint32_t reassemble,
+                               cfws_frame_desc_t* __restrict__ desc, int32_t* __restrict__ status,
+                               uint64_t* __restrict__ vals0, uint64_t* __restrict__ vals1,
+                               uint64_t* __restrict__ partials0, uint64_t* __restrict__ partials1)
+{
+    __shared__ uint64_t s_wave[kWaves];
+    const uint64_t b0 = uint64_t(blockIdx.x) * kPlanBlock;
+    uint64_t sum0 = 0, sum1 = 0;
+#pragma unroll
+    for (int k = 0; k < kPlanItems; ++k) {
+        const uint64_t f = b0 + uint64_t(k) * kThreads + threadIdx.x;
+        if (f >= n) continue;
+        const uint64_t wire_size = ends && ends[f] < wire_size_all ? ends[f] : wire_size_all;
+        cfws_frame_desc_t d;
+        const int32_t st = parse_ws_header(wire, wire_size, index[f], max_payload, d);
+        desc[f] = d;
+        status[f] = st;
+        const uint64_t len = (st == CFWS_PARSE_COMPLETE) ? d.payload_size : 0;
+        if (reassemble) {
+            const bool ctl = is_control(d.opcode);
+            vals0[f] = ctl ? 0 : len;
+            vals1[f] = ctl ? len : 0;
+            sum0 += ctl ? 0 : len;
+            sum1 += ctl ? len : 0;
+        } else {
+            const uint64_t v = (len + align - 1) & ~(align - 1);
+            vals0[f] = v;
+            sum0 += v;
+        }
+    }
+    uint64_t total;
+    block_exclusive_scan(sum0, s_wave, &total);
+    if (threadIdx.x == 0) partials0[blockIdx.x] = total;
+    if (reassemble) {
+        block_exclusive_scan(sum1, s_wave, &total);
+        if (threadIdx.x == 0) partials1[blockIdx.x] = total;
+    }
+}
+
+// Offsets into the descriptors, the capacity rule (a COMPLETE frame with a
+// payload that does not fit gets CFWS_ERROR_OUT_OF_MEMORY, like the
+// reference's failed malloc, co_ws_frame.c:216-223), region maps, totals.
+__global__ void __launch_bounds__(kThreads)
+deserialize_plan_apply_kernel(cfws_frame_desc_t* __restrict__ desc, int32_t* __restrict__ status,
+                              uint64_t* __restrict__ vals0, uint64_t* __restrict__ vals1, uint64_t n,
+                              const uint64_t* __restrict__ partials0,
+                              const uint64_t* __restrict__ partials1, uint64_t* __restrict__ hdr,
+                              uint64_t capacity, uint32_t reassemble, uint32_t* __restrict__ map0,
+                              uint32_t* __restrict__ map1, uint64_t* __restrict__ user_total)
+{
+    __shared__ uint64_t s_wave[kWaves];
+    const uint64_t g0 = hdr[3];
+    const uint64_t g1 = reassemble ? hdr[4] : 0;
+    const uint64_t t0 = g0 < capacity ? g0 : capacity;
+    const uint64_t room1 = capacity - t0;
+    const uint64_t t1 = g1 < room1 ? g1 : room1;
+    const uint64_t i0 = uint64_t(blockIdx.x) * kPlanBlock + uint64_t(threadIdx.x) * kPlanItems;
+    uint64_t v0[kPlanItems], v1[kPlanItems];
+    uint64_t s0 = 0, s1 = 0;
+#pragma unroll
+    for (int k = 0; k < kPlanItems; ++k) {
+        v0[k] = (i0 + k < n) ? vals0[i0 + k] : 0;
+        v1[k] = (reassemble && i0 + k < n) ? vals1[i0 + k] : 0;
+        s0 += v0[k];
+        s1 += v1[k];
+    }
+    uint64_t tot;
+    uint64_t run0 = block_exclusive_scan(s0, s_wave, &tot) + partials0[blockIdx.x];
+    uint64_t run1 = 0;
+    if (reassemble) run1 = block_exclusive_scan(s1, s_wave, &tot) + partials1[blockIdx.x];
+#pragma unroll
+    for (int k = 0; k < kPlanItems; ++k) {
+        const uint64_t f = i0 + k;
+        if (f < n) {
+            vals0[f] = run0;
+            const bool ctl = reassemble && is_control(desc[f].opcode);
+            const uint64_t off = ctl ? g0 + run1 : run0;
+            desc[f].payload_off = off;
+            const uint64_t len = desc[f].payload_size;
+            if (status[f] == CFWS_PARSE_COMPLETE && len > 0 && off + len > capacity)
+                status[f] = CFWS_ERROR_OUT_OF_MEMORY;
+            map_range(run0, run0 + v0[k], f, t0, map0);
+            if (reassemble) {
+                vals1[f] = run1;
+                map_range(run1, run1 + v1[k], f, t1, map1);
+            }
+            if (f == n - 1) {
+                map0[(t0 + kRegion - 1) / kRegion] = (uint32_t)f;
+                if (reassemble) map1[(t1 + kRegion - 1) / kRegion] = (uint32_t)f;
+                hdr[0] = t0;
+                hdr[1] = t1;
+                hdr[2] = t0;
+                if (user_total) *user_total = t0 + t1;
+            }
+        }
+        run0 += v0[k];
+        run1 += v1[k];
     }
 }
 
@@ -1492,10 +1644,12 @@ int cfws_serialize_plan(cfws_frame_desc_t* d_desc, size_t n, uint64_t cap, uint6
     if (!d_desc) return set_err(CFWS_ERROR_INVALID_ARGUMENT, "null descriptor table", hipSuccess);
     uint64_t* hdr = ws_ptr<uint64_t>(ws, L.hdr);
     uint64_t* offs = ws_ptr<uint64_t>(ws, L.offs[0]);
-    serialize_sizes_kernel<<<grid_for(n, kThreads), kThreads, 0, st>>>(d_desc, offs, n);
-    if (int rc = run_scan(offs, n, ws_ptr<uint64_t>(ws, L.partials[0]), hdr + 3, st)) return rc;
-    serialize_finalize_kernel<<<grid_for(n, kThreads), kThreads, 0, st>>>(
-        d_desc, offs, hdr, n, cap, ws_ptr<uint32_t>(ws, L.map[0]), d_total);
+    uint64_t* partials = ws_ptr<uint64_t>(ws, L.partials[0]);
+    const uint32_t nb = grid_for(n, kPlanBlock);
+    serialize_plan_reduce_kernel<<<nb, kThreads, 0, st>>>(d_desc, offs, n, partials);
+    scan_partials_kernel<<<1, kThreads, 0, st>>>(partials, nb, hdr + 3);
+    serialize_plan_apply_kernel<<<nb, kThreads, 0, st>>>(d_desc, offs, n, partials, hdr, cap,
+                                                        ws_ptr<uint32_t>(ws, L.map[0]), d_total);
     return launch_check("serialize_plan");
 }
 
@@ -1542,15 +1696,16 @@ static int deserialize_plan_impl(const void* d_wire, uint64_t wire_size, const u
     uint64_t* hdr = ws_ptr<uint64_t>(ws, L.hdr);
     uint64_t* offs0 = ws_ptr<uint64_t>(ws, L.offs[0]);
     uint64_t* offs1 = ws_ptr<uint64_t>(ws, L.offs[1]);
-    deserialize_parse_kernel<<<grid_for(n, kThreads), kThreads, 0, st>>>(
+    uint64_t* part0 = ws_ptr<uint64_t>(ws, L.partials[0]);
+    uint64_t* part1 = ws_ptr<uint64_t>(ws, L.partials[1]);
+    const uint32_t nb = grid_for(n, kPlanBlock);
+    deserialize_plan_reduce_kernel<<<nb, kThreads, 0, st>>>(
         static_cast<const uint8_t*>(d_wire), wire_size, d_index, d_ends, n, max_payload, align, reasm,
-        d_desc, d_status, offs0, offs1);
-    if (int rc = run_scan(offs0, n, ws_ptr<uint64_t>(ws, L.partials[0]), hdr + 3, st)) return rc;
-    if (reasm)
-        if (int rc = run_scan(offs1, n, ws_ptr<uint64_t>(ws, L.partials[1]), hdr + 4, st)) return rc;
-    deserialize_finalize_kernel<<<grid_for(n, kThreads), kThreads, 0, st>>>(
-        d_desc, d_status, offs0, offs1, hdr, n, cap, reasm, ws_ptr<uint32_t>(ws, L.map[0]),
-        ws_ptr<uint32_t>(ws, L.map[1]), d_total);
+        d_desc, d_status, offs0, offs1, part0, part1);
+    scan_partials2_kernel<<<reasm ? 2 : 1, kThreads, 0, st>>>(part0, part1, nb, hdr + 3, hdr + 4);
+    deserialize_plan_apply_kernel<<<nb, kThreads, 0, st>>>(
+        d_desc, d_status, offs0, offs1, n, part0, part1, hdr, cap, reasm,
+        ws_ptr<uint32_t>(ws, L.map[0]), ws_ptr<uint32_t>(ws, L.map[1]), d_total);
     return launch_check("deserialize_plan");
 }
 
