@@ -166,6 +166,9 @@ struct FrameView {
     uint32_t hb;    // serialize: header byte 0 | mask bit << 8; DATA: flags
     uint32_t aux;   // kModeH2Ser: the parent WS frame
     uint32_t s0;    // kModeH2Ser: the slice's first byte within the WS frame
+    uint64_t ws_len;  // kModeH2Ser: the WS frame's payload size, key and
+    uint32_t ws_key;  //   header byte 0 | mask bit << 8 (its header bytes
+    uint32_t ws_hb;   //   are generated from these)
 };
 
 // Byte r < pre of a serialize frame's header, from its view (co_ws_frame.c:34-91).
@@ -190,6 +193,9 @@ __device__ __forceinline__ FrameView frame_view(const Pass& P, uint32_t f)
     v.out_off = P.offs[f];
     v.hb = 0;
     v.aux = 0;
+    v.ws_len = 0;
+    v.ws_key = 0;
+    v.ws_hb = 0;
     v.s0 = 0;
     if (kMode == kModeH2Ser) {
         // d: one DATA frame = a slice [payload_off, + payload_size) of the
@@ -207,6 +213,9 @@ __device__ __forceinline__ FrameView frame_view(const Pass& P, uint32_t f)
         v.hb = d.fin() ? 0x1u : 0u;                      // DATA flags: END_STREAM
         v.aux = wf;
         v.s0 = (uint32_t)s0;                           // only read when h_in > 0 (s0 < 14)
+        v.ws_len = w.payload_size;
+        v.ws_key = w.mask() ? w.key() : 0u;
+        v.ws_hb = ((w.opcode() | (w.fin() ? 0x80u : 0u)) & 0xffu) | (w.mask() ? 0x100u : 0u);
     } else if (is_ser(kMode)) {
         v.pre = d.header_size();
         v.body_len = d.payload_size;
@@ -297,12 +306,11 @@ __device__ __forceinline__ uint32_t header_byte_of(const Pass& P, const FrameVie
     if (kMode == kModeH2Wrap) return h2_header_byte((uint32_t)v.body_len, v.hb, P.sid, r);
     if (kMode == kModeH2Ser) {
         if (r < 9) return h2_header_byte(v.pre - 9u + (uint32_t)v.body_len, v.hb, P.sid, r);
-        // the WS frame's header (co_ws_frame.c:34-91), from its descriptor
-        const DescWords w = load_desc(P.parent, v.aux);
+        // the WS frame's header (co_ws_frame.c:34-91)
         FrameView wv;
-        wv.body_len = w.payload_size;
-        wv.key = w.mask() ? w.key() : 0u;
-        wv.hb = ((w.opcode() | (w.fin() ? 0x80u : 0u)) & 0xffu) | (w.mask() ? 0x100u : 0u);
+        wv.body_len = v.ws_len;
+        wv.key = v.ws_key;
+        wv.hb = v.ws_hb;
         return view_header_byte(wv, r - 9u + v.s0);
     }
     return view_header_byte(v, r);
@@ -324,8 +332,10 @@ __device__ __forceinline__ uint4 body_chunk(const uint8_t* __restrict__ src, con
     return o;
 }
 
-// Slow fallback: byte by byte, walking frames forward from f (chunks that
-// hold more than two frames: runs of frames shorter than ~14 bytes).
+// Chunks that hold more than two frames (runs of frames shorter than ~14
+// bytes): byte by byte, walking frames forward from f. (Loading the views of
+// four bytes at a time measured 30 % slower on config 3: the register cost
+// dropped the edge kernels' occupancy more than the shorter chains saved.)
 template <int kMode>
 __device__ __forceinline__ uint4 edge_chunk_bytes(const Pass& P, uint32_t f, uint64_t D)
 {
@@ -414,16 +424,13 @@ __device__ __forceinline__ uint32_t edge_byte(const Pass& P, const FrameView& v,
 // than the chunk) all source blocks are loaded up front and the bytes are
 // assembled in registers: one memory round trip instead of sixteen.
 template <int kMode>
-__device__ __forceinline__ uint4 edge_chunk(const Pass& P, uint32_t f, uint64_t D)
+__device__ __forceinline__ uint4 edge_chunk(const Pass& P, uint32_t f, uint64_t D,
+                                            const FrameView& va, const FrameView& vb, uint64_t o1,
+                                            uint64_t o2)
 {
     const uint64_t lim = D + 16 < P.total ? D + 16 : P.total;
-    const uint64_t o1 = (f + 1 < P.n_frames) ? P.offs[f + 1] : ~uint64_t(0);
-    const uint64_t o2 = (f + 2 < P.n_frames) ? P.offs[f + 2] : ~uint64_t(0);
     if (o2 < lim) return edge_chunk_bytes<kMode>(P, f, D);
-    const FrameView va = frame_view<kMode>(P, f);
     const bool two = o1 < lim;
-    FrameView vb = va;
-    if (two) vb = frame_view<kMode>(P, f + 1);
     const uint4 Wa = edge_body(P.src, va, D, lim);
     const uint4 Wb = two ? edge_body(P.src, vb, D, lim) : Wa;
     uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;
@@ -623,7 +630,49 @@ xform_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
 // the frame's output range and do not lie entirely inside its body. The
 // kernel is latency-bound (descriptor -> offsets -> source blocks -> store),
 // so the work is spread thin: 64-thread blocks, edge_chunk inlined.
-constexpr uint32_t kEdgeThreads = 64;
+#ifndef CFWS_EDGE_THREADS
+#define CFWS_EDGE_THREADS 64
+#endif
+constexpr uint32_t kEdgeThreads = CFWS_EDGE_THREADS;
+
+// The edge chunks of frame f in pass P (part 0: before the body; part 1:
+// reaching past the body end).
+template <int kMode>
+__device__ __forceinline__ void edge_frame(const Pass& P, uint64_t f, uint32_t part)
+{
+    // Everything the chunks need that depends on f alone is loaded up front
+    // (frame f and f + 1's descriptors, statuses, offsets): one memory round
+    // trip before the source blocks instead of a chain of six.
+    const uint32_t n = P.n_frames;
+    const uint32_t fa = (uint32_t)f, fb = fa + 1 < n ? fa + 1 : fa;
+    const FrameView va = frame_view<kMode>(P, fa);
+    const FrameView vb = frame_view<kMode>(P, fb);
+    const uint64_t o2 = fa + 2 < n ? P.offs[fa + 2] : ~uint64_t(0);
+    const uint64_t o1 = fa + 1 < n ? vb.out_off : ~uint64_t(0);
+    const uint64_t lo = va.out_off;
+    uint64_t hi = fa + 1 < n ? vb.out_off : P.total;
+    if (hi > P.total) hi = P.total;
+    if (lo >= hi) return;
+    const FrameView& v = va;
+    const uint64_t be = v.body_start + v.body_len;
+    const uint64_t first = (lo + 15) & ~uint64_t(15);
+    if (part == 0) {
+        // chunks before the body (headers): D < body_start
+        for (uint64_t D = first; D < hi && D < v.body_start; D += 16)
+            store_chunk(P, D, edge_chunk<kMode>(P, fa, D, va, vb, o1, o2));
+        return;
+    }
+    // chunks reaching past the body end (boundary, padding, pass end)
+    uint64_t d0 = be >= 15 ? ((be - 15 + 15) & ~uint64_t(15)) : 0;  // first D with D + 16 > be
+    if (d0 < first) d0 = first;
+    if (d0 < v.body_start) d0 = (v.body_start + 15) & ~uint64_t(15);  // header chunks: part 0
+    for (uint64_t D = d0; D < hi; D += 16) {
+        if (D >= be && D + 16 <= hi)          // pure alignment padding / OOM body
+            store_chunk(P, D, make_uint4(0, 0, 0, 0));
+        else
+            store_chunk(P, D, edge_chunk<kMode>(P, fa, D, va, vb, o1, o2));
+    }
+}
 
 template <int kMode>
 __global__ void __launch_bounds__(kEdgeThreads)
@@ -635,7 +684,6 @@ edge_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
 {
     const uint64_t t = uint64_t(blockIdx.x) * kEdgeThreads + threadIdx.x;
     const uint64_t f = t >> 1;
-    const uint32_t part = (uint32_t)(t & 1u);
     if (f >= n_frames) return;
     const uint64_t out_base = base_p ? *base_p : 0;
     Pass P;
@@ -650,29 +698,38 @@ edge_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
     P.klass = klass;
     P.sid = sid;
     P.parent = parent;
-    const uint64_t lo = offs[f];
-    uint64_t hi = (f + 1 < n_frames) ? offs[f + 1] : P.total;
-    if (hi > P.total) hi = P.total;
-    if (lo >= hi) return;
-    const FrameView v = frame_view<kMode>(P, (uint32_t)f);
-    const uint64_t be = v.body_start + v.body_len;
-    const uint64_t first = (lo + 15) & ~uint64_t(15);
-    if (part == 0) {
-        // chunks before the body (headers): D < body_start
-        for (uint64_t D = first; D < hi && D < v.body_start; D += 16)
-            store_chunk(P, D, edge_chunk<kMode>(P, (uint32_t)f, D));
-        return;
-    }
-    // chunks reaching past the body end (boundary, padding, pass end)
-    uint64_t d0 = be >= 15 ? ((be - 15 + 15) & ~uint64_t(15)) : 0;  // first D with D + 16 > be
-    if (d0 < first) d0 = first;
-    if (d0 < v.body_start) d0 = (v.body_start + 15) & ~uint64_t(15);  // header chunks: part 0
-    for (uint64_t D = d0; D < hi; D += 16) {
-        if (D >= be && D + 16 <= hi)          // pure alignment padding / OOM body
-            store_chunk(P, D, make_uint4(0, 0, 0, 0));
-        else
-            store_chunk(P, D, edge_chunk<kMode>(P, (uint32_t)f, D));
-    }
+    edge_frame<kMode>(P, f, (uint32_t)(t & 1u));
+}
+
+// Both reassembly passes in one launch: a frame has bytes in exactly one of
+// them (data frames in pass 0, control frames in pass 1), so each thread
+// serves its frame's pass only.
+__global__ void __launch_bounds__(kEdgeThreads)
+edge_reasm_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                  const cfws_frame_desc_t* __restrict__ desc, const int32_t* __restrict__ status,
+                  const uint64_t* __restrict__ offs0, const uint64_t* __restrict__ offs1,
+                  const uint64_t* __restrict__ hdr, uint64_t capacity, uint32_t n_frames)
+{
+    const uint64_t t = uint64_t(blockIdx.x) * kEdgeThreads + threadIdx.x;
+    const uint64_t f = t >> 1;
+    if (f >= n_frames) return;
+    const uint32_t p = is_control(desc[f].opcode) ? 1u : 0u;
+    const uint64_t out_base = p ? hdr[2] : 0;
+    Pass P;
+    P.src = src;
+    P.dst = dst + out_base;
+    P.desc = desc;
+    P.status = status;
+    P.offs = p ? offs1 : offs0;
+    P.total = hdr[p];
+    // pass 0's last chunk must not write past the data bytes: pass 1 starts
+    // there (at an unaligned address) and runs concurrently in this launch
+    P.capacity = p ? capacity - out_base : (hdr[0] < capacity ? hdr[0] : capacity);
+    P.n_frames = n_frames;
+    P.klass = p ? kClassControl : kClassData;
+    P.sid = 0;
+    P.parent = nullptr;
+    edge_frame<kModeDeser>(P, f, (uint32_t)(t & 1u));
 }
 
 // ---------------------------------------------------------------------------
@@ -1593,12 +1650,12 @@ void launch_streaming(const void* src, void* dst, const cfws_frame_desc_t* desc,
                       const int32_t* status, const uint64_t* offs, const uint32_t* map,
                       const uint64_t* total_p, const uint64_t* base_p, uint64_t regions,
                       uint64_t cap, size_t n, uint32_t klass, uint32_t sid, hipStream_t st,
-                      const cfws_frame_desc_t* parent = nullptr)
+                      const cfws_frame_desc_t* parent = nullptr, bool edges = true)
 {
     xform_kernel<kMode><<<stream_grid(regions), kThreads, xform_lds_bytes(), st>>>(
         static_cast<const uint8_t*>(src), static_cast<uint8_t*>(dst), desc, status, offs, map,
         total_p, base_p, cap, (uint32_t)n, klass, sid, parent);
-    edge_kernel<kMode><<<grid_for(2 * (uint64_t)n, kEdgeThreads), kEdgeThreads, 0, st>>>(
+    if (edges) edge_kernel<kMode><<<grid_for(2 * (uint64_t)n, kEdgeThreads), kEdgeThreads, 0, st>>>(
         static_cast<const uint8_t*>(src), static_cast<uint8_t*>(dst), desc, status, offs,
         total_p, base_p, cap, (uint32_t)n, klass, sid, parent);
 }
@@ -1606,12 +1663,18 @@ void launch_streaming(const void* src, void* dst, const cfws_frame_desc_t* desc,
 template <int kMode>
 void launch_pass(const WsLayout& L, int p, const void* src, void* dst, const cfws_frame_desc_t* desc,
                  const int32_t* status, const void* ws, uint64_t cap, size_t n, uint32_t klass,
-                 hipStream_t st, uint32_t sid = 0)
+                 hipStream_t st, uint32_t sid = 0, bool edges = true)
 {
     const uint64_t* hdr = ws_ptr<const uint64_t>(ws, L.hdr);
+    // Pass 1 (reassembly: control frames, <= 125-byte payloads each) is
+    // usually tiny or empty, and its size is only known on the device: a
+    // capped grid (the kernel strides over the regions) instead of one
+    // workgroup per 16 KiB of capacity, which cost ~20 us of empty dispatch.
+    const uint64_t regions = p == 1 ? (L.regions < 4096 ? L.regions : 4096) : L.regions;
     launch_streaming<kMode>(src, dst, desc, status, ws_ptr<const uint64_t>(ws, L.offs[p]),
                             ws_ptr<const uint32_t>(ws, L.map[p]), hdr + p,
-                            p == 1 ? hdr + 2 : nullptr, L.regions, cap, n, klass, sid, st);
+                            p == 1 ? hdr + 2 : nullptr, regions, cap, n, klass, sid, st, nullptr,
+                            edges);
 }
 
 }  // namespace
@@ -1731,8 +1794,14 @@ int cfws_deserialize_execute(const void* d_wire, const cfws_frame_desc_t* d_desc
     const WsLayout L = ws_layout(n, cap);
     hipStream_t st = static_cast<hipStream_t>(stream);
     if (flags & CFWS_DESERIALIZE_REASSEMBLE) {
-        launch_pass<kModeDeser>(L, 0, d_wire, d_payload, d_desc, d_status, ws, cap, n, kClassData, st);
-        launch_pass<kModeDeser>(L, 1, d_wire, d_payload, d_desc, d_status, ws, cap, n, kClassControl, st);
+        launch_pass<kModeDeser>(L, 0, d_wire, d_payload, d_desc, d_status, ws, cap, n, kClassData, st,
+                                0, false);
+        launch_pass<kModeDeser>(L, 1, d_wire, d_payload, d_desc, d_status, ws, cap, n, kClassControl,
+                                st, 0, false);
+        edge_reasm_kernel<<<grid_for(2 * (uint64_t)n, kEdgeThreads), kEdgeThreads, 0, st>>>(
+            static_cast<const uint8_t*>(d_wire), static_cast<uint8_t*>(d_payload), d_desc, d_status,
+            ws_ptr<const uint64_t>(ws, L.offs[0]), ws_ptr<const uint64_t>(ws, L.offs[1]),
+            ws_ptr<const uint64_t>(ws, L.hdr), cap, (uint32_t)n);
     } else {
         launch_pass<kModeDeser>(L, 0, d_wire, d_payload, d_desc, d_status, ws, cap, n, kClassAll, st);
     }
