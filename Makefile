@@ -12,7 +12,16 @@ HDR      := include/cfws.h include/cfws_co_ws_frame.h coldforce_amd/csrc/cfws_in
 LIB      := coldforce_amd/libcfws.so
 OBJDIR   := build
 
-all: $(LIB) oracle
+all: $(LIB) oracle examples
+
+# C users of the ABI (no Python): built against include/, linked to libcfws.so
+examples: build/examples/batch_roundtrip
+
+build/examples/batch_roundtrip: examples/batch_roundtrip.c $(LIB) $(HDR)
+	@mkdir -p build/examples
+	$(CC) -O2 -std=gnu11 -Wall -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include -Iinclude -o $@ $< \
+	    -Lcoldforce_amd -lcfws -L/opt/rocm/lib -lamdhip64 \
+	    -Wl,-rpath,'$$ORIGIN/../../coldforce_amd' -Wl,-rpath,/opt/rocm/lib
 
 $(OBJDIR)/cfws_device.o: coldforce_amd/csrc/cfws_device.hip $(HDR)
 	@mkdir -p $(OBJDIR)
@@ -40,7 +49,7 @@ clean:
 	rm -rf $(OBJDIR) $(LIB)
 	$(MAKE) -s -C oracle clean
 
-.PHONY: all oracle ref asm clean
+.PHONY: all oracle ref asm clean examples
 
 # A/B build variants (kept out of git under build/): make variant V=nt F="-DCFWS_NT_STORE"
 variant: $(HDR)

@@ -1,0 +1,149 @@
+/*
+ * batch_roundtrip.c -- the batch C ABI (include/cfws.h) from plain C, the way
+ * a coldforce send/receive loop would drive it: no Python, no torch.
+ *
+ *   client side:  payloads (pinned host) -> H2D -> cfws_serialize_batch
+ *                 (mask keys drawn like co_ws_frame_serialize draws them)
+ *   server side:  cfws_index_frames_batch over the wire as one connection's
+ *                 receive buffer -> cfws_deserialize_batch -> D2H payloads
+ *
+ * Checks that every payload comes back and that the wire equals what
+ * sequential co_ws_frame_serialize calls (the drop-in, same library) append
+ * to one co_byte_array_t for the same random() stream.
+ *
+ * build: make examples   ->  build/examples/batch_roundtrip
+ * run:   build/examples/batch_roundtrip [n_frames] [max_payload]
+ */
+#include <hip/hip_runtime_api.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "cfws.h"
+#include "cfws_co_ws_frame.h"
+
+#define CHECK(x)                                                                    \
+    do {                                                                            \
+        int rc_ = (x);                                                              \
+        if (rc_ != 0) {                                                             \
+            fprintf(stderr, "%s:%d: %s -> %d (%s)\n", __FILE__, __LINE__, #x, rc_,  \
+                    cfws_last_error());                                             \
+            return 1;                                                               \
+        }                                                                           \
+    } while (0)
+
+int main(int argc, char** argv)
+{
+    const size_t n = argc > 1 ? strtoull(argv[1], NULL, 10) : 4096;
+    const size_t max_len = argc > 2 ? strtoull(argv[2], NULL, 10) : 70000;
+    CHECK(cfws_init());
+
+    /* frames: sizes across every header form, payloads back to back */
+    cfws_frame_desc_t* desc = calloc(n, sizeof *desc);
+    uint8_t* mask = malloc(n);
+    uint64_t arena = 0;
+    srandom(12345);
+    for (size_t i = 0; i < n; ++i) {
+        const size_t pick[] = {0, 1, 125, 126, 1000, 65535, 65536, max_len};
+        desc[i].payload_size = pick[random() % 8] % (max_len + 1);
+        desc[i].payload_off = arena;
+        desc[i].fin = 1;
+        desc[i].opcode = (i % 5 == 0) ? 1 : 2;
+        desc[i].mask = mask[i] = (i % 3) != 0;
+        arena += desc[i].payload_size;
+    }
+    uint8_t* payload;
+    CHECK(hipHostMalloc((void**)&payload, arena + 16, 0));
+    for (uint64_t k = 0; k < arena; ++k) payload[k] = (uint8_t)(k * 2654435761u >> 13);
+
+    /* keys exactly as n co_ws_frame_serialize calls would draw them */
+    uint32_t* keys = malloc(n * sizeof *keys);
+    srandom(777);
+    cfws_draw_mask_keys(n, mask, keys);
+    for (size_t i = 0; i < n; ++i) desc[i].mask_key = keys[i];
+
+    /* the drop-in's wire for the same stream, for comparison */
+    co_byte_array_t ref = {0};
+    ref.element_size = 1;
+    ref.capacity = 8;
+    ref.buffer = malloc(8);
+    srandom(777);
+    for (size_t i = 0; i < n; ++i)
+        if (!co_ws_frame_serialize(true, desc[i].opcode, desc[i].mask != 0,
+                                   payload + desc[i].payload_off, desc[i].payload_size, &ref)) {
+            fprintf(stderr, "drop-in serialize failed\n");
+            return 1;
+        }
+
+    /* device arenas */
+    const uint64_t wire_cap = arena + 14 * n + 64, back_cap = arena + 16 * n + 64;
+    void *d_payload, *d_wire, *d_back, *d_ws_s, *d_ws_d, *d_ws_i;
+    cfws_frame_desc_t *d_desc, *d_desc2;
+    int32_t *d_status, *d_stop;
+    uint64_t *d_total, *d_starts, *d_first, *d_consumed, *d_begin, *d_end, *d_ntot;
+    const size_t ws_s = cfws_workspace_size(n, wire_cap), ws_d = cfws_workspace_size(n, back_cap);
+    const size_t ws_i = cfws_index_workspace_size(1);
+    CHECK(hipMalloc(&d_payload, arena + 16));
+    CHECK(hipMalloc(&d_wire, wire_cap));
+    CHECK(hipMalloc(&d_back, back_cap));
+    CHECK(hipMalloc((void**)&d_desc, n * sizeof *d_desc));
+    CHECK(hipMalloc((void**)&d_desc2, n * sizeof *d_desc2));
+    CHECK(hipMalloc((void**)&d_status, n * sizeof *d_status));
+    CHECK(hipMalloc((void**)&d_total, 8));
+    CHECK(hipMalloc((void**)&d_starts, (n + 1) * 8));
+    CHECK(hipMalloc((void**)&d_first, 8));
+    CHECK(hipMalloc((void**)&d_consumed, 8));
+    CHECK(hipMalloc((void**)&d_stop, 4));
+    CHECK(hipMalloc((void**)&d_begin, 8));
+    CHECK(hipMalloc((void**)&d_end, 8));
+    CHECK(hipMalloc((void**)&d_ntot, 8));
+    CHECK(hipMalloc(&d_ws_s, ws_s));
+    CHECK(hipMalloc(&d_ws_d, ws_d));
+    CHECK(hipMalloc(&d_ws_i, ws_i));
+    hipStream_t st;
+    CHECK(hipStreamCreate(&st));
+
+    /* client: serialize */
+    CHECK(hipMemcpyAsync(d_payload, payload, arena, hipMemcpyHostToDevice, st));
+    CHECK(hipMemcpyAsync(d_desc, desc, n * sizeof *desc, hipMemcpyHostToDevice, st));
+    CHECK(cfws_serialize_batch(d_payload, d_desc, n, d_wire, wire_cap, d_total, d_ws_s, ws_s, st));
+    uint64_t wire_total = 0;
+    CHECK(hipMemcpyAsync(&wire_total, d_total, 8, hipMemcpyDeviceToHost, st));
+    CHECK(hipStreamSynchronize(st));
+    uint8_t* wire = malloc(wire_total + 1);
+    CHECK(hipMemcpy(wire, d_wire, wire_total, hipMemcpyDeviceToHost));
+    const int same = wire_total == ref.count && memcmp(wire, ref.buffer, wire_total) == 0;
+
+    /* server: the wire as one connection's receive buffer */
+    const uint64_t begin = 0;
+    CHECK(hipMemcpyAsync(d_begin, &begin, 8, hipMemcpyHostToDevice, st));
+    CHECK(hipMemcpyAsync(d_end, &wire_total, 8, hipMemcpyHostToDevice, st));
+    CHECK(cfws_index_frames_batch(d_wire, d_begin, d_end, 1, CFWS_DEFAULT_MAX_RECEIVE_PAYLOAD_SIZE,
+                                  d_starts, n + 1, d_first, d_consumed, d_stop, d_ntot, d_ws_i, ws_i,
+                                  st));
+    uint64_t n_found = 0, consumed = 0;
+    int32_t stop = -1;
+    CHECK(hipMemcpyAsync(&n_found, d_ntot, 8, hipMemcpyDeviceToHost, st));
+    CHECK(hipMemcpyAsync(&consumed, d_consumed, 8, hipMemcpyDeviceToHost, st));
+    CHECK(hipMemcpyAsync(&stop, d_stop, 4, hipMemcpyDeviceToHost, st));
+    CHECK(hipStreamSynchronize(st));
+    CHECK(cfws_deserialize_batch(d_wire, wire_total, d_starts, n_found,
+                                 CFWS_DEFAULT_MAX_RECEIVE_PAYLOAD_SIZE, 1, 0, d_desc2, d_status,
+                                 d_back, back_cap, d_total, d_ws_d, ws_d, st));
+    uint64_t back_total = 0;
+    CHECK(hipMemcpyAsync(&back_total, d_total, 8, hipMemcpyDeviceToHost, st));
+    CHECK(hipStreamSynchronize(st));
+    uint8_t* back = malloc(back_total + 1);
+    int32_t* status = malloc(n * sizeof *status);
+    CHECK(hipMemcpy(back, d_back, back_total, hipMemcpyDeviceToHost));
+    CHECK(hipMemcpy(status, d_status, n * sizeof *status, hipMemcpyDeviceToHost));
+    int ok = same && n_found == n && consumed == wire_total && stop == CFWS_PARSE_COMPLETE &&
+             back_total == arena && memcmp(back, payload, arena) == 0;
+    for (size_t i = 0; ok && i < n; ++i) ok = status[i] == CFWS_PARSE_COMPLETE;
+    printf("{\"frames\": %zu, \"payload_bytes\": %llu, \"wire_bytes\": %llu, "
+           "\"wire_equals_dropin\": %s, \"indexed\": %llu, \"roundtrip\": %s}\n",
+           n, (unsigned long long)arena, (unsigned long long)wire_total, same ? "true" : "false",
+           (unsigned long long)n_found, ok ? "true" : "false");
+    return ok ? 0 : 2;
+}
