@@ -21,6 +21,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("CFWS_LIB") or os.path.join(HERE, "libcfws.so")   # CFWS_LIB: A/B builds
 
 OK = 0
+ERROR_INVALID_ARGUMENT, ERROR_WORKSPACE, ERROR_HIP, ERROR_NO_DEVICE = -1, -2, -3, -4   # cfws.h
 PARSE_COMPLETE = 0
 PARSE_MORE_DATA = 1
 ERROR_INVALID_FRAME = -7001
