@@ -253,6 +253,33 @@ __device__ __forceinline__ uint4 ld16(const uint8_t* p)
     return make_uint4(v.x, v.y, v.z, v.w);
 }
 
+// The streaming kernel's body loads. Every source byte is read by exactly one
+// lane, once, yet `nt` measured slower here (config 2: 6.37/6.49 TB/s plain
+// vs 5.97/6.29 nt, profiles/r01_ab_dpp.json), although the bare copy probe
+// (tools/copy_probe.hip) gains from it; -DCFWS_STREAM_NT turns it on.
+__device__ __forceinline__ uint4 ld16_stream(const uint8_t* p)
+{
+#ifdef CFWS_STREAM_NT
+    const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+    return make_uint4(v.x, v.y, v.z, v.w);
+#else
+    return ld16(p);
+#endif
+}
+
+// Lane i receives lane i + 1's `v` (DPP wave_shl:1); lane 63, which has no
+// right neighbour, keeps `last`.
+__device__ __forceinline__ uint32_t from_next_lane(uint32_t v, uint32_t last)
+{
+    return __builtin_amdgcn_update_dpp(last, v, 0x130, 0xf, 0xf, false);
+}
+
+__device__ __forceinline__ uint4 from_next_lane(const uint4& v, const uint4& last)
+{
+    return make_uint4(from_next_lane(v.x, last.x), from_next_lane(v.y, last.y),
+                      from_next_lane(v.z, last.z), from_next_lane(v.w, last.w));
+}
+
 __device__ __forceinline__ void st16(uint8_t* p, uint4 o)
 {
     const u32x4 v = {o.x, o.y, o.z, o.w};
@@ -467,8 +494,11 @@ __device__ __forceinline__ void store_chunk(const Pass& P, uint64_t D, uint4 o)
 // ---------------------------------------------------------------------------
 
 // A region inside one frame's body: frame, source phase and rotated key are
-// wave-uniform (SGPRs); all kUnroll x {A, B} loads are in flight before the
-// first store.
+// wave-uniform (SGPRs); all kUnroll loads are in flight before the first
+// store. Each lane loads the one aligned source block A that holds its
+// chunk's first byte; when the source is misaligned against the output
+// (phase != 0) the block B after it is the next lane's A, taken over DPP, so
+// every source byte is loaded once (lane 63 loads its B itself).
 __device__ __forceinline__ void fast_region(const Pass& P, const FrameView& v, uint64_t base,
                                             uint32_t lane)
 {
@@ -477,25 +507,28 @@ __device__ __forceinline__ void fast_region(const Pass& P, const FrameView& v, u
     const uint32_t kr = rotr8(v.key, (uint32_t)((0 - v.body_start) & 3u));
     const uint8_t* s0 = P.src + ((base + delta) & ~uint64_t(15)) + lane * kChunk;
     uint8_t* d0 = P.dst + base + lane * kChunk;
-    if (ph == 0) {
-        uint4 a[kUnroll];
+    uint4 a[kUnroll];
 #pragma unroll
-        for (int u = 0; u < kUnroll; ++u) a[u] = ld16(s0 + u * kSlice);
+    for (int u = 0; u < kUnroll; ++u) a[u] = ld16_stream(s0 + u * kSlice);
+    if (ph == 0) {
 #pragma unroll
         for (int u = 0; u < kUnroll; ++u) {
             xor4(a[u], kr);
             st16(d0 + u * kSlice, a[u]);
         }
     } else {
-        uint4 a[kUnroll], b[kUnroll];
+        // lane 63's B is the block after its A: it holds the chunk's last
+        // byte, a body byte, so it lies inside the source allocation.
+        uint4 e[kUnroll];
 #pragma unroll
-        for (int u = 0; u < kUnroll; ++u) {
-            a[u] = ld16(s0 + u * kSlice);
-            b[u] = ld16(s0 + u * kSlice + 16);
+        for (int u = 0; u < kUnroll; ++u) e[u] = make_uint4(0, 0, 0, 0);
+        if (lane == 63) {
+#pragma unroll
+            for (int u = 0; u < kUnroll; ++u) e[u] = ld16(s0 + u * kSlice + 16);
         }
 #pragma unroll
         for (int u = 0; u < kUnroll; ++u) {
-            uint4 o = funnel16(a[u], b[u], ph);
+            uint4 o = funnel16(a[u], from_next_lane(a[u], e[u]), ph);
             xor4(o, kr);
             st16(d0 + u * kSlice, o);
         }
@@ -563,64 +596,6 @@ __device__ __forceinline__ void general_region(const Pass& P, uint32_t f0, uint3
         const FrameView v = frame_view<kMode>(P, fr[u]);
         if (D >= v.body_start && D + kChunk <= v.body_start + v.body_len)
             st16(P.dst + D, body_chunk(P.src, v, D));
-    }
-}
-
-// The streaming kernel: serialize (kSer) = header + (masked) payload into
-// the wire arena; deserialize = copy + unmask into the payload arena. It
-// writes every 16-byte chunk that lies inside one frame's body; the chunks
-// holding headers, boundaries, padding or the pass end belong to
-// edge_kernel. Both read the same plan; their chunk sets are disjoint.
-template <int kMode>
-__global__ void __launch_bounds__(kThreads)
-xform_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
-             const cfws_frame_desc_t* __restrict__ desc, const int32_t* __restrict__ status,
-             const uint64_t* __restrict__ offs, const uint32_t* __restrict__ region_map,
-             const uint64_t* __restrict__ total_p, const uint64_t* __restrict__ base_p,
-             uint64_t capacity, uint32_t n_frames, uint32_t klass, uint32_t sid,
-             const cfws_frame_desc_t* __restrict__ parent)
-{
-    const uint64_t out_base = base_p ? *base_p : 0;
-    Pass P;
-    P.src = src;
-    P.dst = dst + out_base;
-    P.desc = desc;
-    P.status = status;
-    P.offs = offs;
-    P.total = *total_p;                              // clamped by the plan
-    P.capacity = capacity - out_base;
-    P.n_frames = n_frames;
-    P.klass = klass;
-    P.sid = sid;
-    P.parent = parent;
-    const uint64_t n_regions = (P.total + kRegion - 1) / kRegion;
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint64_t stride = uint64_t(gridDim.x) * kWaves;
-
-    for (uint64_t r = uint64_t(blockIdx.x) * kWaves + wave; r < n_regions; r += stride) {
-        const uint64_t base = r * kRegion;
-        const uint64_t end = base + kRegion;
-        // The plan writes every entry in [0, n_regions]; the clamps only keep
-        // a corrupted workspace from turning into an out-of-bounds read.
-        uint32_t f0 = region_map[r];
-        uint32_t f1 = region_map[r + 1];
-        if (f1 >= n_frames) f1 = n_frames - 1;
-        if (f0 > f1) f0 = f1;
-        // region_map[r + 1] holds the NEXT region's first byte; frames that
-        // start at or after this region's end do not touch it.
-        if (f1 > f0 && offs[f0 + 1] >= end) f1 = f0;
-        const FrameView va = frame_view<kMode>(P, f0);
-        if (f0 == f1) {
-            if (base >= va.body_start && end <= va.body_start + va.body_len)
-                fast_region(P, va, base, lane);
-            else
-                two_frame_region<kMode>(P, va, va, base, lane);   // partial body, one frame
-        } else if (f1 == f0 + 1 || offs[f0 + 2] >= end) {
-            two_frame_region<kMode>(P, va, frame_view<kMode>(P, f0 + 1), base, lane);
-        } else {
-            general_region<kMode>(P, f0, f1, base, lane);
-        }
     }
 }
 
@@ -699,6 +674,83 @@ edge_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
     P.sid = sid;
     P.parent = parent;
     edge_frame<kMode>(P, f, (uint32_t)(t & 1u));
+}
+
+// WS serialize / deserialize carry their edge chunks in the streaming
+// launch; the HTTP/2 modes keep a separate edge launch (their edge code
+// needs more registers than the merged kernel's 5-waves-per-EU budget).
+__host__ __device__ constexpr bool has_edge_blocks(int mode)
+{
+    return mode == kModeSer || mode == kModeDeser;
+}
+
+// The streaming kernel: serialize (kSer) = header + (masked) payload into
+// the wire arena; deserialize = copy + unmask into the payload arena.
+// The first `edge_blocks` workgroups write the edge chunks (edge_frame: two
+// threads per frame); the rest stream the regions, writing every 16-byte
+// chunk that lies inside one frame's body. The two chunk sets are disjoint.
+// Edge workgroups are dispatched first, so their latency-bound chains run
+// under the stream instead of as a launch of their own after it (which cost
+// 17 us serialize / 4 us deserialize on config 2, plus a kernel boundary).
+// The wave-per-EU floor keeps the merged kernel at <= 102 VGPRs, so the
+// 5 workgroups per CU the LDS reservation allows stay resident.
+template <int kMode>
+__global__ void __launch_bounds__(kThreads, 5)
+xform_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+             const cfws_frame_desc_t* __restrict__ desc, const int32_t* __restrict__ status,
+             const uint64_t* __restrict__ offs, const uint32_t* __restrict__ region_map,
+             const uint64_t* __restrict__ total_p, const uint64_t* __restrict__ base_p,
+             uint64_t capacity, uint32_t n_frames, uint32_t klass, uint32_t sid,
+             const cfws_frame_desc_t* __restrict__ parent, uint32_t edge_blocks)
+{
+    const uint64_t out_base = base_p ? *base_p : 0;
+    Pass P;
+    P.src = src;
+    P.dst = dst + out_base;
+    P.desc = desc;
+    P.status = status;
+    P.offs = offs;
+    P.total = *total_p;                              // clamped by the plan
+    P.capacity = capacity - out_base;
+    P.n_frames = n_frames;
+    P.klass = klass;
+    P.sid = sid;
+    P.parent = parent;
+    if (has_edge_blocks(kMode) && blockIdx.x < edge_blocks) {
+        const uint64_t t = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
+        if ((t >> 1) < n_frames) edge_frame<kMode>(P, t >> 1, (uint32_t)(t & 1u));
+        return;
+    }
+    const uint64_t n_regions = (P.total + kRegion - 1) / kRegion;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t stride = uint64_t(gridDim.x - edge_blocks) * kWaves;
+
+    for (uint64_t r = uint64_t(blockIdx.x - edge_blocks) * kWaves + wave; r < n_regions;
+         r += stride) {
+        const uint64_t base = r * kRegion;
+        const uint64_t end = base + kRegion;
+        // The plan writes every entry in [0, n_regions]; the clamps only keep
+        // a corrupted workspace from turning into an out-of-bounds read.
+        uint32_t f0 = region_map[r];
+        uint32_t f1 = region_map[r + 1];
+        if (f1 >= n_frames) f1 = n_frames - 1;
+        if (f0 > f1) f0 = f1;
+        // region_map[r + 1] holds the NEXT region's first byte; frames that
+        // start at or after this region's end do not touch it.
+        if (f1 > f0 && offs[f0 + 1] >= end) f1 = f0;
+        const FrameView va = frame_view<kMode>(P, f0);
+        if (f0 == f1) {
+            if (base >= va.body_start && end <= va.body_start + va.body_len)
+                fast_region(P, va, base, lane);
+            else
+                two_frame_region<kMode>(P, va, va, base, lane);   // partial body, one frame
+        } else if (f1 == f0 + 1 || offs[f0 + 2] >= end) {
+            two_frame_region<kMode>(P, va, frame_view<kMode>(P, f0 + 1), base, lane);
+        } else {
+            general_region<kMode>(P, f0, f1, base, lane);
+        }
+    }
 }
 
 // Both reassembly passes in one launch: a frame has bytes in exactly one of
@@ -1627,11 +1679,12 @@ int zero_totals(const WsLayout& L, void* ws, uint64_t* d_total, hipStream_t st)
 }
 
 // Dynamic LDS the streaming kernel reserves per workgroup. It is never
-// touched: it only caps residency at 6 workgroups (24 waves) per CU. At the
-// register-limited 8 workgroups per CU the kernel ran 8-12 % slower (more
-// streams contending for HBM pages); 6 measured best on config 2 and 3
-// (sweep 3..8 per CU, tools/envab.sh). CFWS_XFORM_LDS overrides (0 = none).
-constexpr uint32_t kXformLdsDefault = 27000;     // 53 x 512 B granules; 6 x fits 160 KiB
+// touched: it only caps residency at 5 workgroups (20 waves) per CU. More
+// resident streams contend for HBM pages: at the register-limited 8 per CU
+// the kernel ran 8-12 % slower, at 7 6 % slower; 5 measured best with the
+// DPP body path (config 2: 6.44/6.46 TB/s vs 6.44/6.40 at 6 and 6.41/6.42 at
+// 4; profiles/r01_ab_dpp.json, tools/ab.sh). CFWS_XFORM_LDS overrides (0 = none).
+constexpr uint32_t kXformLdsDefault = 32000;     // 5 x fits 160 KiB, 6 x does not
 
 uint32_t xform_lds_bytes()
 {
@@ -1644,7 +1697,19 @@ uint32_t xform_lds_bytes()
     return (uint32_t)v;
 }
 
-// The streaming kernel plus the edge kernel of one pass.
+// One pass: the streaming kernel with its edge workgroups in front
+// (CFWS_EDGE_SPLIT=1: the edge chunks as a launch of their own after it, the
+// previous layout, kept for A/B).
+bool edge_split()
+{
+    static int v = -1;
+    if (v < 0) {
+        const char* s = getenv("CFWS_EDGE_SPLIT");
+        v = (s && *s == '1') ? 1 : 0;
+    }
+    return v == 1;
+}
+
 template <int kMode>
 void launch_streaming(const void* src, void* dst, const cfws_frame_desc_t* desc,
                       const int32_t* status, const uint64_t* offs, const uint32_t* map,
@@ -1652,10 +1717,12 @@ void launch_streaming(const void* src, void* dst, const cfws_frame_desc_t* desc,
                       uint64_t cap, size_t n, uint32_t klass, uint32_t sid, hipStream_t st,
                       const cfws_frame_desc_t* parent = nullptr, bool edges = true)
 {
-    xform_kernel<kMode><<<stream_grid(regions), kThreads, xform_lds_bytes(), st>>>(
+    const bool split = edges && (edge_split() || !has_edge_blocks(kMode));
+    const uint32_t eb = (edges && !split) ? grid_for(2 * (uint64_t)n, kThreads) : 0;
+    xform_kernel<kMode><<<eb + stream_grid(regions), kThreads, xform_lds_bytes(), st>>>(
         static_cast<const uint8_t*>(src), static_cast<uint8_t*>(dst), desc, status, offs, map,
-        total_p, base_p, cap, (uint32_t)n, klass, sid, parent);
-    if (edges) edge_kernel<kMode><<<grid_for(2 * (uint64_t)n, kEdgeThreads), kEdgeThreads, 0, st>>>(
+        total_p, base_p, cap, (uint32_t)n, klass, sid, parent, eb);
+    if (split) edge_kernel<kMode><<<grid_for(2 * (uint64_t)n, kEdgeThreads), kEdgeThreads, 0, st>>>(
         static_cast<const uint8_t*>(src), static_cast<uint8_t*>(dst), desc, status, offs,
         total_p, base_p, cap, (uint32_t)n, klass, sid, parent);
 }

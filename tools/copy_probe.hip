@@ -1,0 +1,329 @@
+// HBM streaming ceiling probe for gfx950: what a read+write stream (the
+// shape of xform_kernel), a read-only stream and a write-only stream reach on
+// this part, by cache policy, bytes per wave and occupancy. Standalone, not
+// part of libcfws; used to decide whether the codec's 6.3 TB/s has headroom.
+//
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/copy_probe.hip -o build/copy_probe
+//   build/copy_probe [GiB]
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+#include <cstdint>
+#include <vector>
+#include <algorithm>
+
+#define CHECK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { \
+    fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); exit(1); } } while (0)
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+// aux cache-policy bits (gfx940+): sc0 = 1, nt = 2, sc1 = 16
+template <int kLoadAux, int kStoreAux, int kU, bool kMisaligned>
+__global__ void __launch_bounds__(256) copy_kernel(const uint8_t* __restrict__ src,
+                                                   uint8_t* __restrict__ dst, uint32_t key)
+{
+    extern __shared__ uint8_t lds_pad[];
+    (void)lds_pad;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t region = (uint64_t(blockIdx.x) * 4 + wave) * (uint64_t(kU) * 1024);
+    auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)(src + region), 0, kU * 1024 + 16, 0x00020000);
+    auto rd = __builtin_amdgcn_make_buffer_rsrc((void*)(dst + region), 0, kU * 1024, 0x00020000);
+    u32x4 a[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u)
+        a[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, u * 1024 + lane * 16, 0, kLoadAux);
+    if (kMisaligned) {
+        u32x4 b[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u)
+            b[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, u * 1024 + lane * 16 + 16, 0, kLoadAux);
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            a[u].x = __builtin_amdgcn_alignbyte(a[u].y, a[u].x, 2);
+            a[u].y = __builtin_amdgcn_alignbyte(a[u].z, a[u].y, 2);
+            a[u].z = __builtin_amdgcn_alignbyte(a[u].w, a[u].z, 2);
+            a[u].w = __builtin_amdgcn_alignbyte(b[u].x, a[u].w, 2);
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+        a[u] ^= key;
+        __builtin_amdgcn_raw_buffer_store_b128(a[u], rd, u * 1024 + lane * 16, 0, kStoreAux);
+    }
+}
+
+// Misaligned source via a DPP wave shift: each lane loads ONE block and takes
+// its neighbour's (lane + 1) over DPP; lane 63 loads the extra block itself.
+template <int kLoadAux, int kStoreAux, int kU>
+__global__ void __launch_bounds__(256) copy_dpp_kernel(const uint8_t* __restrict__ src,
+                                                       uint8_t* __restrict__ dst, uint32_t key)
+{
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t region = (uint64_t(blockIdx.x) * 4 + wave) * (uint64_t(kU) * 1024);
+    auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)(src + region), 0, kU * 1024 + 16, 0x00020000);
+    auto rd = __builtin_amdgcn_make_buffer_rsrc((void*)(dst + region), 0, kU * 1024, 0x00020000);
+    u32x4 a[kU];
+    u32x4 e[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+        a[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, u * 1024 + lane * 16, 0, kLoadAux);
+    }
+    if (lane == 63) {
+#pragma unroll
+        for (int u = 0; u < kU; ++u)
+            e[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, u * 1024 + 1024, 0, kLoadAux);
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+        // wave_shl:1 (0x130): lane i reads lane i + 1
+        uint32_t nx = __builtin_amdgcn_update_dpp(0u, a[u].x, 0x130, 0xf, 0xf, false);
+        if (lane == 63) nx = e[u].x;
+        u32x4 o;
+        o.x = __builtin_amdgcn_alignbyte(a[u].y, a[u].x, 2);
+        o.y = __builtin_amdgcn_alignbyte(a[u].z, a[u].y, 2);
+        o.z = __builtin_amdgcn_alignbyte(a[u].w, a[u].z, 2);
+        o.w = __builtin_amdgcn_alignbyte(nx, a[u].w, 2);
+        o ^= key;
+        __builtin_amdgcn_raw_buffer_store_b128(o, rd, u * 1024 + lane * 16, 0, kStoreAux);
+    }
+}
+
+template <int kLoadAux, int kU>
+__global__ void __launch_bounds__(256) read_kernel(const uint8_t* __restrict__ src, uint32_t* out)
+{
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t region = (uint64_t(blockIdx.x) * 4 + wave) * (uint64_t(kU) * 1024);
+    auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)(src + region), 0, kU * 1024, 0x00020000);
+    u32x4 acc = {0, 0, 0, 0};
+#pragma unroll
+    for (int u = 0; u < kU; ++u)
+        acc ^= __builtin_amdgcn_raw_buffer_load_b128(rs, u * 1024 + lane * 16, 0, kLoadAux);
+    const uint32_t x = acc.x ^ acc.y ^ acc.z ^ acc.w;
+    if (x == 0x12345678u) out[0] = x;   // practically never; keeps the loads live
+}
+
+template <int kStoreAux, int kU>
+__global__ void __launch_bounds__(256) write_kernel(uint8_t* __restrict__ dst, uint32_t key)
+{
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t region = (uint64_t(blockIdx.x) * 4 + wave) * (uint64_t(kU) * 1024);
+    auto rd = __builtin_amdgcn_make_buffer_rsrc((void*)(dst + region), 0, kU * 1024, 0x00020000);
+    u32x4 v = {key ^ lane, key, key + lane, key};
+#pragma unroll
+    for (int u = 0; u < kU; ++u)
+        __builtin_amdgcn_raw_buffer_store_b128(v, rd, u * 1024 + lane * 16, 0, kStoreAux);
+}
+
+struct Result { const char* name; int lds; double tbps; };
+
+static uint8_t *g_src, *g_dst;
+static uint32_t* g_out;
+static uint64_t g_bytes;
+
+template <typename F>
+static double time_it(F launch, double bytes_moved)
+{
+    hipEvent_t a, b;
+    CHECK(hipEventCreate(&a));
+    CHECK(hipEventCreate(&b));
+    for (int i = 0; i < 3; ++i) launch();
+    CHECK(hipDeviceSynchronize());
+    std::vector<float> ms;
+    for (int i = 0; i < 15; ++i) {
+        CHECK(hipEventRecord(a, 0));
+        launch();
+        CHECK(hipEventRecord(b, 0));
+        CHECK(hipEventSynchronize(b));
+        float t;
+        CHECK(hipEventElapsedTime(&t, a, b));
+        ms.push_back(t);
+    }
+    CHECK(hipGetLastError());
+    std::sort(ms.begin(), ms.end());
+    CHECK(hipEventDestroy(a));
+    CHECK(hipEventDestroy(b));
+    return bytes_moved / (ms[ms.size() / 2] * 1e-3) / 1e12;
+}
+
+template <int L, int S, int U, bool M>
+static void run_copy(const char* name, int lds)
+{
+    const uint64_t per_block = uint64_t(U) * 4096;
+    const uint32_t blocks = (uint32_t)(g_bytes / per_block);
+    auto k = copy_kernel<L, S, U, M>;
+    CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    const double t = time_it([&] { k<<<blocks, 256, lds>>>(g_src, g_dst, 0x9e3779b9u); },
+                             2.0 * double(blocks) * per_block);
+    printf("{\"kind\": \"copy\", \"variant\": \"%s\", \"load_aux\": %d, \"store_aux\": %d, \"kib_per_wave\": %d, "
+           "\"misaligned\": %d, \"lds\": %d, \"TBps\": %.3f}\n", name, L, S, U, (int)M, lds, t);
+    fflush(stdout);
+}
+
+template <int L, int S, int U>
+static void run_dpp(int lds)
+{
+    const uint64_t per_block = uint64_t(U) * 4096;
+    const uint32_t blocks = (uint32_t)(g_bytes / per_block);
+    auto k = copy_dpp_kernel<L, S, U>;
+    CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    const double t = time_it([&] { k<<<blocks, 256, lds>>>(g_src, g_dst, 0x9e3779b9u); },
+                             2.0 * double(blocks) * per_block);
+    printf("{\"kind\": \"copy_dpp\", \"load_aux\": %d, \"store_aux\": %d, \"kib_per_wave\": %d, \"lds\": %d, \"TBps\": %.3f}\n",
+           L, S, U, lds, t);
+    fflush(stdout);
+}
+
+template <int L, int U>
+static void run_read(int lds)
+{
+    const uint64_t per_block = uint64_t(U) * 4096;
+    const uint32_t blocks = (uint32_t)(g_bytes / per_block);
+    auto k = read_kernel<L, U>;
+    CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    const double t = time_it([&] { k<<<blocks, 256, lds>>>(g_src, g_out); }, double(blocks) * per_block);
+    printf("{\"kind\": \"read\", \"load_aux\": %d, \"kib_per_wave\": %d, \"lds\": %d, \"TBps\": %.3f}\n",
+           L, U, lds, t);
+    fflush(stdout);
+}
+
+template <int S, int U>
+static void run_write(int lds)
+{
+    const uint64_t per_block = uint64_t(U) * 4096;
+    const uint32_t blocks = (uint32_t)(g_bytes / per_block);
+    auto k = write_kernel<S, U>;
+    CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    const double t = time_it([&] { k<<<blocks, 256, lds>>>(g_dst, 7u); }, double(blocks) * per_block);
+    printf("{\"kind\": \"write\", \"store_aux\": %d, \"kib_per_wave\": %d, \"lds\": %d, \"TBps\": %.3f}\n",
+           S, U, lds, t);
+    fflush(stdout);
+}
+
+
+// The same streams through global_load/global_store (the codec's form):
+// kMode 0 aligned, 1 misaligned with two loads per chunk (the codec's
+// funnel), 2 misaligned with one load + DPP neighbour exchange.
+template <bool kNtLoad, int kMode, int kU>
+__global__ void __launch_bounds__(256) gcopy_kernel(const uint8_t* __restrict__ src,
+                                                    uint8_t* __restrict__ dst, uint32_t key)
+{
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t region = (uint64_t(blockIdx.x) * 4 + wave) * (uint64_t(kU) * 1024);
+    const u32x4* s = reinterpret_cast<const u32x4*>(src + region) + lane;
+    u32x4* d = reinterpret_cast<u32x4*>(dst + region) + lane;
+    auto ld = [](const u32x4* p) {
+        if (kNtLoad) return __builtin_nontemporal_load(p);
+        return *p;
+    };
+    u32x4 a[kU], b[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) a[u] = ld(s + u * 64);
+    if (kMode == 1) {
+#pragma unroll
+        for (int u = 0; u < kU; ++u) b[u] = ld(s + u * 64 + 1);
+    } else if (kMode == 2) {
+        if (lane == 63) {
+#pragma unroll
+            for (int u = 0; u < kU; ++u) b[u] = ld(s + u * 64 + 1);
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+        u32x4 o = a[u];
+        if (kMode != 0) {
+            uint32_t nx = b[u].x;
+            if (kMode == 2) {
+                const uint32_t sh = __builtin_amdgcn_update_dpp(0u, a[u].x, 0x130, 0xf, 0xf, false);
+                nx = lane == 63 ? b[u].x : sh;
+            }
+            o.x = __builtin_amdgcn_alignbyte(a[u].y, a[u].x, 2);
+            o.y = __builtin_amdgcn_alignbyte(a[u].z, a[u].y, 2);
+            o.z = __builtin_amdgcn_alignbyte(a[u].w, a[u].z, 2);
+            o.w = __builtin_amdgcn_alignbyte(nx, a[u].w, 2);
+        }
+        o ^= key;
+        __builtin_nontemporal_store(o, d + u * 64);
+    }
+}
+
+template <bool NL, int M, int U>
+static void run_gcopy(int lds)
+{
+    const uint64_t per_block = uint64_t(U) * 4096;
+    const uint32_t blocks = (uint32_t)(g_bytes / per_block);
+    auto k = gcopy_kernel<NL, M, U>;
+    CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    const double t = time_it([&] { k<<<blocks, 256, lds>>>(g_src, g_dst, 0x9e3779b9u); },
+                             2.0 * double(blocks) * per_block);
+    printf("{\"kind\": \"gcopy\", \"nt_load\": %d, \"mode\": %d, \"kib_per_wave\": %d, \"lds\": %d, \"TBps\": %.3f}\n",
+           (int)NL, M, U, lds, t);
+    fflush(stdout);
+}
+
+int main(int argc, char** argv)
+{
+    const double gib = argc > 1 ? atof(argv[1]) : 4.0;
+    g_bytes = uint64_t(gib * double(1ull << 30));
+    g_bytes -= g_bytes % (64 * 4096);
+    CHECK(hipMalloc(&g_src, g_bytes + 4096));
+    CHECK(hipMalloc(&g_dst, g_bytes + 4096));
+    CHECK(hipMalloc(&g_out, 64));
+    CHECK(hipMemset(g_src, 0x5a, g_bytes + 4096));
+    CHECK(hipMemset(g_dst, 0, g_bytes + 4096));
+    // LDS pads: 0 (VGPR-bound), 27000 (6 WG/CU), 40000 (4), 54000 (3), 80000 (2)
+    const int sweep = argc > 2 ? atoi(argv[2]) : 1;
+    if (sweep == 0) {
+        for (int lds : {0, 27000, 54000}) {
+            run_copy<0, 0, 4, false>("plain", lds);
+            run_copy<0, 2, 4, false>("nt_store", lds);
+            run_copy<0, 2, 4, true>("nt_store_misaligned", lds);
+            run_copy<0, 16, 4, false>("sc1_store", lds);
+            run_copy<0, 19, 4, false>("sc0sc1nt_store", lds);
+            run_copy<16, 2, 4, false>("sc1_load_nt_store", lds);
+            run_copy<0, 2, 8, false>("nt_store_8k", lds);
+            run_copy<0, 2, 16, false>("nt_store_16k", lds);
+            run_read<0, 4>(lds);
+            run_read<0, 16>(lds);
+            run_write<0, 4>(lds);
+            run_write<19, 4>(lds);
+        }
+    }
+    if (sweep == 2) {
+        for (int rep = 0; rep < 2; ++rep)
+            for (int lds : {0, 27000, 40000, 54000}) {
+                run_gcopy<false, 0, 4>(lds);
+                run_gcopy<true, 0, 4>(lds);
+                run_gcopy<false, 1, 4>(lds);
+                run_gcopy<true, 1, 4>(lds);
+                run_gcopy<false, 2, 4>(lds);
+                run_gcopy<true, 2, 4>(lds);
+                run_gcopy<true, 0, 2>(lds);
+                run_gcopy<true, 2, 2>(lds);
+                run_gcopy<false, 1, 2>(lds);
+            }
+        return 0;
+    }
+    for (int rep = 0; rep < 2; ++rep) {
+        for (int lds : {27000, 40000, 54000, 80000}) {
+            run_copy<0, 2, 4, false>("nt_store", lds);
+            run_copy<2, 2, 4, false>("nt_load_nt_store", lds);
+            run_copy<2, 2, 4, true>("nt_load_nt_store_misaligned", lds);
+            run_copy<2, 2, 2, false>("nt_load_nt_store_2k", lds);
+            run_copy<2, 0, 4, false>("nt_load_plain_store", lds);
+            run_dpp<0, 2, 4>(lds);
+            run_dpp<2, 2, 4>(lds);
+            run_dpp<2, 2, 2>(lds);
+            run_dpp<2, 0, 4>(lds);
+            run_read<2, 4>(lds);
+            run_write<2, 4>(lds);
+        }
+    }
+    CHECK(hipFree(g_src));
+    CHECK(hipFree(g_dst));
+    return 0;
+}

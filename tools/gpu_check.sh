@@ -8,7 +8,7 @@ OUT=gpurun_out/${TAG:-run}
 mkdir -p "$OUT"
 rocm-smi --showproductname > "$OUT/smi.txt" 2>&1 || true
 nproc > "$OUT/nproc.txt"
-timeout -k 10 900 python -m pytest tests -x -q -m gpu > "$OUT/pytest_gpu.txt" 2>&1 &&
+timeout -k 10 900 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread > "$OUT/pytest_gpu.txt" 2>&1 &&
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.txt" 2>&1 &&
 timeout -k 10 600 python bench.py ${BENCH_ARGS:-} > "$OUT/bench.json" 2> "$OUT/bench.err" &&
 ( cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/$OUT/prof" -o run -- \

@@ -8,7 +8,7 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 OUT=gpurun_out/${TAG:-round}
 mkdir -p "$OUT"
-timeout -k 10 900 python -m pytest tests -x -q -m gpu > "$OUT/pytest_gpu.txt" 2>&1 &&
+timeout -k 10 900 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread > "$OUT/pytest_gpu.txt" 2>&1 &&
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > "$OUT/smoke.txt" 2>&1 &&
 timeout -k 10 600 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" &&
 timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 \
