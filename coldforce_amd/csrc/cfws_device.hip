@@ -957,11 +957,32 @@ __device__ __forceinline__ void map_range(uint64_t lo, uint64_t hi, uint64_t f, 
     }
 }
 
-// ---- plans: three launches each -------------------------------------------
+// This block's exclusive prefix and the grand total, straight from the
+// per-block sums the reduce kernel wrote (plans of up to kSelfScanBlocks
+// blocks: every apply block reads them all, <= 8 KiB from L2, instead of
+// a scan launch between the two).
+constexpr uint64_t kSelfScanBlocks = 1024;
+
+__device__ __forceinline__ void prefix_from_partials(const uint64_t* __restrict__ partials, uint64_t nb,
+                                                     uint64_t b, uint64_t* s_wave, uint64_t& before,
+                                                     uint64_t& all)
+{
+    uint64_t xb = 0, xa = 0;
+    for (uint64_t i = threadIdx.x; i < nb; i += kThreads) {
+        const uint64_t v = partials[i];
+        xa += v;
+        if (i < b) xb += v;
+    }
+    block_exclusive_scan(xb, s_wave, &before);
+    block_exclusive_scan(xa, s_wave, &all);
+}
+
+// ---- plans: two launches each (three above kSelfScanBlocks blocks) ---------
 // 1. per frame: sizes (serialize: header size, co_ws_frame.c:41-91;
 //    deserialize: the header decode) + the block's sum;
-// 2. scan_partials_kernel: the block sums (one block per pass);
-// 3. per block: exclusive offsets of its 2,048 frames, then everything the
+// (2. scan_partials_kernel: the block sums, one block per pass -- only when
+//    there are more than kSelfScanBlocks blocks; otherwise step 3 sums them);
+// 3. per block: exclusive offsets of its frames, then everything the
 //    offsets decide (descriptor offsets, capacity rule, region maps, totals).
 
 __global__ void __launch_bounds__(kThreads)
@@ -989,12 +1010,18 @@ serialize_plan_reduce_kernel(cfws_frame_desc_t* __restrict__ desc, uint64_t* __r
 
 __global__ void __launch_bounds__(kThreads)
 serialize_plan_apply_kernel(cfws_frame_desc_t* __restrict__ desc, uint64_t* __restrict__ vals,
-                            uint64_t n, const uint64_t* __restrict__ partials,
-                            uint64_t* __restrict__ hdr, uint64_t capacity,
+                            uint64_t n, const uint64_t* __restrict__ partials, uint64_t nb,
+                            uint32_t self_scan, uint64_t* __restrict__ hdr, uint64_t capacity,
                             uint32_t* __restrict__ map, uint64_t* __restrict__ user_total)
 {
     __shared__ uint64_t s_wave[kWaves];
-    const uint64_t g = hdr[3];
+    uint64_t prefix, g;
+    if (self_scan) {
+        prefix_from_partials(partials, nb, blockIdx.x, s_wave, prefix, g);
+    } else {
+        prefix = partials[blockIdx.x];
+        g = hdr[3];
+    }
     const uint64_t total = g < capacity ? g : capacity;
     const uint64_t i0 = uint64_t(blockIdx.x) * kPlanBlock + uint64_t(threadIdx.x) * kPlanItems;
     uint64_t v[kPlanItems];
@@ -1005,7 +1032,7 @@ serialize_plan_apply_kernel(cfws_frame_desc_t* __restrict__ desc, uint64_t* __re
         sum += v[k];
     }
     uint64_t tot;
-    uint64_t run = block_exclusive_scan(sum, s_wave, &tot) + partials[blockIdx.x];
+    uint64_t run = block_exclusive_scan(sum, s_wave, &tot) + prefix;
 #pragma unroll
     for (int k = 0; k < kPlanItems; ++k) {
         const uint64_t f = i0 + k;
@@ -1016,6 +1043,7 @@ serialize_plan_apply_kernel(cfws_frame_desc_t* __restrict__ desc, uint64_t* __re
             if (f == n - 1) {
                 map[(total + kRegion - 1) / kRegion] = (uint32_t)f;
                 hdr[0] = total;
+                if (self_scan) hdr[3] = g;
                 if (user_total) *user_total = g;
             }
         }
@@ -1076,13 +1104,24 @@ __global__ void __launch_bounds__(kThreads)
 deserialize_plan_apply_kernel(cfws_frame_desc_t* __restrict__ desc, int32_t* __restrict__ status,
                               uint64_t* __restrict__ vals0, uint64_t* __restrict__ vals1, uint64_t n,
                               const uint64_t* __restrict__ partials0,
-                              const uint64_t* __restrict__ partials1, uint64_t* __restrict__ hdr,
+                              const uint64_t* __restrict__ partials1, uint64_t nb,
+                              uint32_t self_scan, uint64_t* __restrict__ hdr,
                               uint64_t capacity, uint32_t reassemble, uint32_t* __restrict__ map0,
                               uint32_t* __restrict__ map1, uint64_t* __restrict__ user_total)
 {
     __shared__ uint64_t s_wave[kWaves];
-    const uint64_t g0 = hdr[3];
-    const uint64_t g1 = reassemble ? hdr[4] : 0;
+    uint64_t pre0, pre1 = 0, g0, g1 = 0;
+    if (self_scan) {
+        prefix_from_partials(partials0, nb, blockIdx.x, s_wave, pre0, g0);
+        if (reassemble) prefix_from_partials(partials1, nb, blockIdx.x, s_wave, pre1, g1);
+    } else {
+        pre0 = partials0[blockIdx.x];
+        g0 = hdr[3];
+        if (reassemble) {
+            pre1 = partials1[blockIdx.x];
+            g1 = hdr[4];
+        }
+    }
     const uint64_t t0 = g0 < capacity ? g0 : capacity;
     const uint64_t room1 = capacity - t0;
     const uint64_t t1 = g1 < room1 ? g1 : room1;
@@ -1097,9 +1136,9 @@ deserialize_plan_apply_kernel(cfws_frame_desc_t* __restrict__ desc, int32_t* __r
         s1 += v1[k];
     }
     uint64_t tot;
-    uint64_t run0 = block_exclusive_scan(s0, s_wave, &tot) + partials0[blockIdx.x];
+    uint64_t run0 = block_exclusive_scan(s0, s_wave, &tot) + pre0;
     uint64_t run1 = 0;
-    if (reassemble) run1 = block_exclusive_scan(s1, s_wave, &tot) + partials1[blockIdx.x];
+    if (reassemble) run1 = block_exclusive_scan(s1, s_wave, &tot) + pre1;
 #pragma unroll
     for (int k = 0; k < kPlanItems; ++k) {
         const uint64_t f = i0 + k;
@@ -1122,6 +1161,10 @@ deserialize_plan_apply_kernel(cfws_frame_desc_t* __restrict__ desc, int32_t* __r
                 hdr[0] = t0;
                 hdr[1] = t1;
                 hdr[2] = t0;
+                if (self_scan) {
+                    hdr[3] = g0;
+                    if (reassemble) hdr[4] = g1;
+                }
                 if (user_total) *user_total = t0 + t1;
             }
         }
@@ -1776,10 +1819,12 @@ int cfws_serialize_plan(cfws_frame_desc_t* d_desc, size_t n, uint64_t cap, uint6
     uint64_t* offs = ws_ptr<uint64_t>(ws, L.offs[0]);
     uint64_t* partials = ws_ptr<uint64_t>(ws, L.partials[0]);
     const uint32_t nb = grid_for(n, kPlanBlock);
+    const uint32_t self_scan = nb <= kSelfScanBlocks ? 1u : 0u;
     serialize_plan_reduce_kernel<<<nb, kThreads, 0, st>>>(d_desc, offs, n, partials);
-    scan_partials_kernel<<<1, kThreads, 0, st>>>(partials, nb, hdr + 3);
-    serialize_plan_apply_kernel<<<nb, kThreads, 0, st>>>(d_desc, offs, n, partials, hdr, cap,
-                                                        ws_ptr<uint32_t>(ws, L.map[0]), d_total);
+    if (!self_scan) scan_partials_kernel<<<1, kThreads, 0, st>>>(partials, nb, hdr + 3);
+    serialize_plan_apply_kernel<<<nb, kThreads, 0, st>>>(d_desc, offs, n, partials, nb, self_scan,
+                                                        hdr, cap, ws_ptr<uint32_t>(ws, L.map[0]),
+                                                        d_total);
     return launch_check("serialize_plan");
 }
 
@@ -1832,9 +1877,11 @@ static int deserialize_plan_impl(const void* d_wire, uint64_t wire_size, const u
     deserialize_plan_reduce_kernel<<<nb, kThreads, 0, st>>>(
         static_cast<const uint8_t*>(d_wire), wire_size, d_index, d_ends, n, max_payload, align, reasm,
         d_desc, d_status, offs0, offs1, part0, part1);
-    scan_partials2_kernel<<<reasm ? 2 : 1, kThreads, 0, st>>>(part0, part1, nb, hdr + 3, hdr + 4);
+    const uint32_t self_scan = nb <= kSelfScanBlocks ? 1u : 0u;
+    if (!self_scan)
+        scan_partials2_kernel<<<reasm ? 2 : 1, kThreads, 0, st>>>(part0, part1, nb, hdr + 3, hdr + 4);
     deserialize_plan_apply_kernel<<<nb, kThreads, 0, st>>>(
-        d_desc, d_status, offs0, offs1, n, part0, part1, hdr, cap, reasm,
+        d_desc, d_status, offs0, offs1, n, part0, part1, nb, self_scan, hdr, cap, reasm,
         ws_ptr<uint32_t>(ws, L.map[0]), ws_ptr<uint32_t>(ws, L.map[1]), d_total);
     return launch_check("deserialize_plan");
 }

@@ -25,16 +25,37 @@ namespace {
 // co_ws_config.c:12-15 -- one process-wide, unsynchronised setting.
 size_t g_max_receive_payload_size = 32u * 1024u * 1024u;
 
-// Per calling thread: one stream and one device staging buffer, reused
+// Per calling thread: one stream, a pinned host staging buffer the device
+// reads and writes in place (mapped into the GPU's address space), and a
+// device staging buffer for frames above the zero-copy limit; all reused
 // across frames (coldforce runs each connection on one co_thread).
 struct ThreadDevice {
     hipStream_t stream = nullptr;
-    void* buf = nullptr;
+    void* buf = nullptr;           // device memory (DMA path)
     size_t cap = 0;
+    uint8_t* host = nullptr;       // pinned host memory (zero-copy path)
+    void* host_dev = nullptr;      // its device-side address
+    size_t host_cap = 0;
 };
 thread_local ThreadDevice t_dev;
 
-bool device_stage(size_t n)
+// Frames up to this size take the zero-copy path: the payload is copied into
+// the pinned buffer and the XOR kernel reads and writes it over PCIe, so a
+// frame costs one launch + one synchronize instead of H2D + launch + D2H
+// (profiles/r01_dropin_latency_*.json). Larger frames take the DMA path, whose
+// copy engines move bulk bytes faster than a kernel's PCIe accesses.
+// CFWS_DROPIN_ZC_MAX overrides (bytes; 0 = DMA path always).
+size_t zero_copy_max()
+{
+    static size_t v = static_cast<size_t>(-1);
+    if (v == static_cast<size_t>(-1)) {
+        const char* s = getenv("CFWS_DROPIN_ZC_MAX");
+        v = s ? static_cast<size_t>(strtoull(s, nullptr, 10)) : (size_t(1) << 20);
+    }
+    return v;
+}
+
+bool stream_ready()
 {
     if (cfws_init() != CFWS_OK) return false;
     if (!t_dev.stream && hipStreamCreateWithFlags(&t_dev.stream, hipStreamNonBlocking) != hipSuccess) {
@@ -42,6 +63,12 @@ bool device_stage(size_t n)
         t_dev.stream = nullptr;
         return false;
     }
+    return true;
+}
+
+bool device_stage(size_t n)
+{
+    if (!stream_ready()) return false;
     if (t_dev.cap < n) {
         size_t cap = 1u << 16;
         while (cap < n) cap <<= 1;
@@ -53,6 +80,34 @@ bool device_stage(size_t n)
             return false;
         }
         t_dev.cap = cap;
+    }
+    return true;
+}
+
+bool host_stage(size_t n)
+{
+    if (!stream_ready()) return false;
+    if (t_dev.host_cap < n) {
+        size_t cap = 1u << 16;
+        while (cap < n) cap <<= 1;
+        if (t_dev.host) (void)hipHostFree(t_dev.host);
+        t_dev.host = nullptr;
+        t_dev.host_dev = nullptr;
+        t_dev.host_cap = 0;
+        void* h = nullptr;
+        if (hipHostMalloc(&h, cap, hipHostMallocMapped) != hipSuccess) {
+            fprintf(stderr, "cfws: hipHostMalloc(%zu) failed\n", cap);
+            return false;
+        }
+        void* d = nullptr;
+        if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess || !d) {
+            fprintf(stderr, "cfws: hipHostGetDevicePointer failed\n");
+            (void)hipHostFree(h);
+            return false;
+        }
+        t_dev.host = static_cast<uint8_t*>(h);
+        t_dev.host_dev = d;
+        t_dev.host_cap = cap;
     }
     return true;
 }
@@ -78,16 +133,23 @@ private:
 bool device_xor(const uint8_t* src, uint8_t* dst, size_t n, uint32_t key)
 {
     RandomStateGuard keep_random_stream;
-    if (!device_stage(n)) return false;
+    const bool zero_copy = n <= zero_copy_max();
+    if (zero_copy ? !host_stage(n) : !device_stage(n)) return false;
     hipStream_t st = t_dev.stream;
-    if (hipMemcpyAsync(t_dev.buf, src, n, hipMemcpyHostToDevice, st) != hipSuccess) return false;
-    if (cfws_xor_mask(t_dev.buf, t_dev.buf, n, key, 0, st) != CFWS_OK) return false;
-    if (hipMemcpyAsync(dst, t_dev.buf, n, hipMemcpyDeviceToHost, st) != hipSuccess) return false;
+    if (zero_copy) {
+        memcpy(t_dev.host, src, n);
+        if (cfws_xor_mask(t_dev.host_dev, t_dev.host_dev, n, key, 0, st) != CFWS_OK) return false;
+    } else {
+        if (hipMemcpyAsync(t_dev.buf, src, n, hipMemcpyHostToDevice, st) != hipSuccess) return false;
+        if (cfws_xor_mask(t_dev.buf, t_dev.buf, n, key, 0, st) != CFWS_OK) return false;
+        if (hipMemcpyAsync(dst, t_dev.buf, n, hipMemcpyDeviceToHost, st) != hipSuccess) return false;
+    }
     hipError_t e = hipStreamSynchronize(st);
     if (e != hipSuccess) {
         fprintf(stderr, "cfws: device XOR failed: %s\n", hipGetErrorString(e));
         return false;
     }
+    if (zero_copy) memcpy(dst, t_dev.host, n);
     return true;
 }
 
@@ -251,6 +313,7 @@ void cfws_draw_mask_keys(size_t n, const uint8_t* mask_flags, uint32_t* keys)
 void cfws_release_thread_resources(void)
 {
     if (t_dev.buf) (void)hipFree(t_dev.buf);
+    if (t_dev.host) (void)hipHostFree(t_dev.host);
     if (t_dev.stream) (void)hipStreamDestroy(t_dev.stream);
     t_dev = ThreadDevice{};
 }

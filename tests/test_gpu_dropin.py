@@ -93,7 +93,9 @@ def test_random_roundtrip_vs_oracle():
     rng = random.Random(4)
     L = O.lib()
     for trial in range(60):
-        n = rng.choice([1, 2, 125, 126, 65535, 65536, 65537, rng.randrange(300000)])
+        # up to 1 MiB: zero-copy path; above: the DMA path (cfws_frame.cpp)
+        n = rng.choice([1, 2, 125, 126, 65535, 65536, 65537, rng.randrange(300000),
+                        (1 << 20) + rng.randrange(1, 3 << 20)])
         data = rng.randbytes(n)
         libc.srandom(trial)
         ok, w = cfws.frame_serialize(rng.random() < .5, rng.randrange(16), True, data)
@@ -118,18 +120,25 @@ def _fnv1a(b: bytes) -> int:
     return h
 
 
-def test_link_level_dropin_harness():
+@pytest.mark.parametrize("zc_max", [None, "0", "1000"])
+def test_link_level_dropin_harness(zc_max):
     """oracle/_ref/dropin_link: a C program built against coldforce's own
     headers (co_ws_frame.h, co_ws_config.h, co_byte_array.h) and the
     reference's co_array.c, linked to libcfws.so in place of co_ws_frame.c.
     Its wire equals the oracle's for the same random() stream, every frame
-    decodes back, and the error codes are the reference's."""
+    decodes back, and the error codes are the reference's -- on the
+    zero-copy path (default), the DMA path (CFWS_DROPIN_ZC_MAX=0) and both
+    mixed (frames over 1,000 B by DMA)."""
     import os
     import subprocess
     exe = os.path.join(O.HERE, "_ref", "dropin_link")
     if not os.path.exists(exe):
         pytest.skip("oracle/_ref/dropin_link not built (built where /root/reference exists)")
-    r = subprocess.run([exe, "77"], capture_output=True, text=True, timeout=120)
+    env = dict(os.environ)
+    env.pop("CFWS_DROPIN_ZC_MAX", None)
+    if zc_max is not None:
+        env["CFWS_DROPIN_ZC_MAX"] = zc_max
+    r = subprocess.run([exe, "77"], capture_output=True, text=True, timeout=120, env=env)
     assert r.returncode == 0, r.stdout + r.stderr
     lines = r.stdout.split("\n")
     L = O.lib()

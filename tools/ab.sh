@@ -10,8 +10,9 @@ mkdir -p "$OUT"
 for round in 1 2; do
   for v in ${VARIANTS:-base}; do
     if [ "$v" = base ]; then lib=coldforce_amd/libcfws.so; else lib=build/variants/libcfws_$v.so; fi
-    for lds in ${LDS:-27000}; do
-      CFWS_LIB=$PWD/$lib CFWS_XFORM_LDS=$lds timeout -k 10 300 python bench.py --steps 20 --warmup 3 \
+    for lds in ${LDS:-default}; do
+      if [ "$lds" = default ]; then unset CFWS_XFORM_LDS; else export CFWS_XFORM_LDS=$lds; fi
+      CFWS_LIB=$PWD/$lib timeout -k 10 300 python bench.py --steps 20 --warmup 3 \
           --no-cpu-baseline --workload ${WL:-config2} \
           > "$OUT/${v}_lds${lds}_r$round.json" 2> "$OUT/${v}_lds${lds}_r$round.err" || { echo "variant $v lds $lds failed"; exit 1; }
     done
