@@ -538,13 +538,16 @@ __device__ __forceinline__ void fast_region(const Pass& P, const FrameView& v, u
 // A region crossed by exactly one frame boundary (the boundary case of large
 // frames): both views are wave-uniform, each lane picks one by comparing its
 // chunk with the boundary. Chunks not entirely inside a body are left to
-// edge_kernel.
+// edge_kernel. As in fast_region, a lane's block B comes from the next lane
+// over DPP when that lane loads it (same frame, chunk inside the body);
+// otherwise (lane 63, the last chunk before a body end) the lane loads it.
 template <int kMode>
 __device__ __forceinline__ void two_frame_region(const Pass& P, const FrameView& va,
                                                  const FrameView& vb, uint64_t base, uint32_t lane)
 {
-    uint4 a[kUnroll], b[kUnroll];
+    uint4 a[kUnroll], e[kUnroll];
     bool fast[kUnroll];
+    uint32_t own_b = 0;
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u) {
         const uint64_t D = base + u * kSlice + lane * kChunk;
@@ -554,19 +557,29 @@ __device__ __forceinline__ void two_frame_region(const Pass& P, const FrameView&
         const uint64_t s = (hi ? vb.src_off : va.src_off) + (D - bs);
         const uint8_t* sp = P.src + (s & ~uint64_t(15));
         fast[u] = D >= bs && D + kChunk <= be;
+        a[u] = make_uint4(0, 0, 0, 0);
+        e[u] = make_uint4(0, 0, 0, 0);
         if (fast[u]) {
-            a[u] = ld16(sp);
-            if (s & 15u) b[u] = ld16(sp + 16);
+            a[u] = ld16_stream(sp);
+            // the next lane's chunk D + 16 loads block sp + 16 iff it is in
+            // the same frame and inside the body
+            const bool next_loads = lane != 63 && (D + kChunk >= vb.out_off) == hi &&
+                                    D + 2 * kChunk <= be;
+            if ((s & 15u) && !next_loads) {
+                e[u] = ld16(sp + 16);
+                own_b |= 1u << u;
+            }
         }
     }
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u) {
+        const uint4 nb = from_next_lane(a[u], e[u]);     // every lane: DPP needs the full wave
         if (!fast[u]) continue;
         const uint64_t D = base + u * kSlice + lane * kChunk;
         const bool hi = D >= vb.out_off;
         const uint64_t k0 = D - (hi ? vb.body_start : va.body_start);
         const uint32_t ph = (uint32_t)(((hi ? vb.src_off : va.src_off) + k0) & 15u);
-        uint4 o = ph ? funnel16(a[u], b[u], ph) : a[u];
+        uint4 o = ph ? funnel16(a[u], (own_b >> u) & 1u ? e[u] : nb, ph) : a[u];
         xor4(o, rotr8(hi ? vb.key : va.key, (uint32_t)(k0 & 3u)));
         st16(P.dst + D, o);
     }
