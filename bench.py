@@ -48,14 +48,15 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="target CPU time of the cpu_baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--workload", choices=["config2", "config3", "config4", "config5"],
+    ap.add_argument("--workload", choices=["config2", "config3", "config4", "config5", "split"],
                     default="config2",
                     help="config2: uniform 64 KiB frames (the metric's config); config3: Zipf "
                          "64 B-1 MiB messages in 1-8 continuation fragments, reassembled; "
                          "config4: the 8 M x 64 KiB batch cut in 8 shards, rank r runs shard r "
                          "(1,048,576 frames = 64 GiB per GPU); "
                          "config5: WebSocket over HTTP/2 DATA frames (--frame-size, default "
-                         "16376)")
+                         "16376); split: config 2 through the split ops (encode_headers + "
+                         "mask_batch, parse_headers + unmask_batch)")
     return ap.parse_args()
 
 
@@ -178,6 +179,57 @@ def bench_h2(args, rank, world, dev):
     return 0 if ok else 1
 
 
+def bench_split(args, rank, world, dev):
+    """Config 2 through the split ops of include/cfws.h: cfws_encode_headers
+    + cfws_mask_batch (send), cfws_parse_headers + cfws_unmask_batch
+    (receive), per step; wire offsets laid out by the host."""
+    import numpy as np
+    import torch
+
+    from coldforce_amd import cfws, shard
+    from coldforce_amd import workloads as W
+    F, fs = args.frames, args.frame_size
+    desc_np, byte_base = shard.uniform_shard(F, fs, KEY_SEED, rank, world)
+    offs, wire_total = W.wire_layout(desc_np)
+    desc_np["wire_off"] = offs
+    payload = torch.empty(F * fs, dtype=torch.uint8, device=dev)
+    cfws.fill_splitmix(payload, PAYLOAD_SEED, byte_base)
+    wire = torch.empty(W.round16(wire_total), dtype=torch.uint8, device=dev)
+    back = torch.empty(F * fs, dtype=torch.uint8, device=dev)
+    d_t = cfws.desc_to_device(desc_np, dev)
+    idx = torch.from_numpy(offs.astype(np.int64)).to(dev)
+    pd_t = torch.empty((F, 32), dtype=torch.uint8, device=dev)
+    st_t = torch.empty(F, dtype=torch.int32, device=dev)
+    # the receive side's payload layout: the frame index x frame size
+    pay_off = torch.from_numpy((np.arange(F, dtype=np.uint64) * np.uint64(fs)).view(np.int64)).to(dev)
+
+    def step():
+        cfws.encode_headers(d_t, wire)
+        cfws.mask_batch(payload, d_t, wire, fs)
+        cfws.parse_headers(wire, wire_total, idx, pd_t, st_t)
+        pd_t.view(torch.int64)[:, 0] = pay_off
+        cfws.unmask_batch(wire, pd_t, st_t, back, fs)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    elapsed = shard.max_over_ranks(time.perf_counter() - t0, dev)
+    ok = bool((st_t == 0).all()) and torch.equal(back, payload)
+    line = {"metric": "WS payload mask/unmask GiB/s device-resident, split ops (config 2 layout)",
+            "value": round(2.0 * F * fs * world * args.steps / elapsed / GIB, 2), "unit": "GiB/s",
+            "n_gpus": world, "steps": args.steps, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "config": {"workload": f"split: {F} binary frames x {fs} B per GPU: encode_headers + "
+                                   f"mask_batch, then parse_headers + unmask_batch"},
+            "verified": ok}
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    return 0 if ok else 1
+
+
 def main():
     args = parse()
     import torch
@@ -196,8 +248,8 @@ def main():
     cfws.init()
 
     F, fs = args.frames, args.frame_size
-    if args.workload == "config5":
-        rc = bench_h2(args, rank, world, dev)
+    if args.workload in ("config5", "split"):
+        rc = (bench_h2 if args.workload == "config5" else bench_split)(args, rank, world, dev)
         if world > 1:
             dist.destroy_process_group()
         sys.exit(rc)

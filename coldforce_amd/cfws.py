@@ -52,7 +52,8 @@ BATCH_SYMBOLS = (
     "cfws_h2_serialize_workspace_size", "cfws_h2_serialize_batch",
     "cfws_h2_deserialize_workspace_size", "cfws_h2_deserialize_batch",
     "cfws_index_frames", "cfws_index_workspace_size", "cfws_index_frames_batch",
-    "cfws_ws_accept_keys_batch",
+    "cfws_ws_accept_keys_batch", "cfws_encode_headers", "cfws_parse_headers",
+    "cfws_mask_batch", "cfws_unmask_batch",
 )
 DROPIN_SYMBOLS = (
     "co_ws_frame_serialize", "co_ws_frame_deserialize", "co_ws_frame_create",
@@ -108,6 +109,10 @@ def lib(path: str = LIB_PATH) -> C.CDLL:
         "cfws_deserialize_execute": ([_vp, _vp, _vp, _sz, _u32, _vp, _u64, _vp, _vp], C.c_int),
         "cfws_deserialize_batch": ([_vp, _u64, _vp, _sz, _u64, _u32, _u32, _vp, _vp, _vp, _u64,
                                     _vp, _vp, _sz, _vp], C.c_int),
+        "cfws_encode_headers": ([_vp, _sz, _vp, _u64, _vp], C.c_int),
+        "cfws_parse_headers": ([_vp, _u64, _vp, _sz, _u64, _vp, _vp, _vp], C.c_int),
+        "cfws_mask_batch": ([_vp, _vp, _sz, _u64, _vp, _u64, _vp], C.c_int),
+        "cfws_unmask_batch": ([_vp, _vp, _vp, _sz, _u64, _vp, _u64, _vp], C.c_int),
         "cfws_xor_mask": ([_vp, _vp, _u64, _u32, _u32, _vp], C.c_int),
         "cfws_draw_mask_keys": ([_sz, _vp, _vp], None),
         "cfws_release_thread_resources": ([], None),
@@ -280,6 +285,36 @@ def deserialize(wire_t, wire_size: int, index_t, payload_t, desc_t=None, status_
                                         _stream(stream)),
            "cfws_deserialize_batch")
     return desc_t, status_t, total_t
+
+
+# ---- split ops (headers and payload XOR as separate passes) -----------------
+
+def encode_headers(desc_t, wire_t, wire_capacity: int | None = None, stream=None) -> None:
+    cap = wire_t.numel() if wire_capacity is None else wire_capacity
+    _check(lib().cfws_encode_headers(_p(desc_t), desc_t.shape[0], _p(wire_t), cap,
+                                     _stream(stream)), "cfws_encode_headers")
+
+
+def parse_headers(wire_t, wire_size: int, index_t, desc_t, status_t,
+                  max_payload: int = DEFAULT_MAX_PAYLOAD, stream=None) -> None:
+    _check(lib().cfws_parse_headers(_p(wire_t), wire_size, _p(index_t), index_t.numel(),
+                                    max_payload, _p(desc_t), _p(status_t), _stream(stream)),
+           "cfws_parse_headers")
+
+
+def mask_batch(payload_t, desc_t, wire_t, max_payload_size: int, wire_capacity: int | None = None,
+               stream=None) -> None:
+    cap = wire_t.numel() if wire_capacity is None else wire_capacity
+    _check(lib().cfws_mask_batch(_p(payload_t), _p(desc_t), desc_t.shape[0], max_payload_size,
+                                 _p(wire_t), cap, _stream(stream)), "cfws_mask_batch")
+
+
+def unmask_batch(wire_t, desc_t, status_t, payload_t, max_payload_size: int,
+                 payload_capacity: int | None = None, stream=None) -> None:
+    cap = payload_t.numel() if payload_capacity is None else payload_capacity
+    _check(lib().cfws_unmask_batch(_p(wire_t), _p(desc_t), _p(status_t), desc_t.shape[0],
+                                   max_payload_size, _p(payload_t), cap, _stream(stream)),
+           "cfws_unmask_batch")
 
 
 def xor_mask(src_t, dst_t, n: int, key: int, phase: int = 0, stream=None) -> None:

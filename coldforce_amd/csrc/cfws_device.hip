@@ -972,9 +972,9 @@ __device__ __forceinline__ void map_range(uint64_t lo, uint64_t hi, uint64_t f, 
 
 // This block's exclusive prefix and the grand total, straight from the
 // per-block sums the reduce kernel wrote (plans of up to kSelfScanBlocks
-// blocks: every apply block reads them all, <= 8 KiB from L2, instead of
+// blocks: every apply block reads them all, <= 16 KiB from L2, instead of
 // a scan launch between the two).
-constexpr uint64_t kSelfScanBlocks = 1024;
+constexpr uint64_t kSelfScanBlocks = 2048;
 
 __device__ __forceinline__ void prefix_from_partials(const uint64_t* __restrict__ partials, uint64_t nb,
                                                      uint64_t b, uint64_t* s_wave, uint64_t& before,
@@ -1216,6 +1216,108 @@ deserialize_finalize_kernel(cfws_frame_desc_t* __restrict__ desc, int32_t* __res
         hdr[1] = t1;
         hdr[2] = t0;
         if (user_total) *user_total = t0 + t1;
+    }
+}
+
+// ---- split ops: header and payload passes over caller-laid-out frames -----
+
+// co_ws_frame.c:34-91 for every frame: its 2-14 header bytes at wire_off,
+// one thread per frame; bytes at or past cap are not written.
+__global__ void __launch_bounds__(kThreads)
+encode_headers_kernel(cfws_frame_desc_t* __restrict__ desc, uint64_t n, uint8_t* __restrict__ wire,
+                      uint64_t cap)
+{
+    const uint64_t f = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
+    if (f >= n) return;
+    const DescWords d = load_desc(desc, (uint32_t)f);
+    const uint32_t hs = header_size_of(d.payload_size, d.mask() != 0);
+    FrameView v;
+    v.body_len = d.payload_size;
+    v.key = d.mask() ? d.key() : 0u;
+    v.hb = ((d.opcode() | (d.fin() ? 0x80u : 0u)) & 0xffu) | (d.mask() ? 0x100u : 0u);
+#pragma unroll
+    for (uint32_t r = 0; r < 14; ++r)
+        if (r < hs && d.wire_off + r < cap) wire[d.wire_off + r] = (uint8_t)view_header_byte(v, r);
+    desc[f].header_size = (uint8_t)hs;
+}
+
+// co_ws_frame.c:131-213 (+ the callers' 2-byte precheck) at every frame
+// start, one thread per frame: cfws_deserialize_plan's decode without the
+// payload layout.
+__global__ void __launch_bounds__(kThreads)
+parse_headers_kernel(const uint8_t* __restrict__ wire, uint64_t size, const uint64_t* __restrict__ index,
+                     uint64_t n, uint64_t max_payload, cfws_frame_desc_t* __restrict__ desc,
+                     int32_t* __restrict__ status)
+{
+    const uint64_t f = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
+    if (f >= n) return;
+    cfws_frame_desc_t d;
+    status[f] = parse_ws_header(wire, size, index[f], max_payload, d);
+    desc[f] = d;
+}
+
+// The payload loops (mask: co_ws_frame.c:93-97, unmask: :232-242) of every
+// frame, each frame from its own source to its own destination. Work unit
+// (frame, piece): a workgroup writes the 16-byte destination chunks of one
+// frame, 1,024 per pass (4 per lane, loads in flight before the stores),
+// striding by `pieces` passes. Chunks inside the frame are one 16-byte store
+// (source funnel-shifted into place); the frame's first and last chunk, which
+// it may share with its neighbours, are written byte by byte.
+constexpr uint32_t kPieceChunks = 4 * kThreads;
+
+template <bool kUnmask>
+__global__ void __launch_bounds__(kThreads)
+payload_xor_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                   const cfws_frame_desc_t* __restrict__ desc, const int32_t* __restrict__ status,
+                   uint64_t n, uint32_t pieces, uint64_t cap)
+{
+    const uint64_t f = blockIdx.x / pieces;
+    const uint32_t p = blockIdx.x % pieces;
+    if (f >= n) return;
+    if (kUnmask && status && status[f] != CFWS_PARSE_COMPLETE) return;
+    const DescWords d = load_desc(desc, (uint32_t)f);
+    const uint64_t len = d.payload_size;
+    const uint64_t so = kUnmask ? d.wire_off + d.header_size() : d.payload_off;
+    const uint64_t dof = kUnmask ? d.payload_off : d.wire_off + header_size_of(len, d.mask() != 0);
+    const uint32_t key = d.mask() ? d.key() : 0u;
+    if (len == 0 || dof >= cap) return;
+    const uint64_t dend = len < cap - dof ? dof + len : cap;
+    const uint64_t c0 = dof & ~uint64_t(15);
+    const uint64_t nchunks = (dend - c0 + 15) >> 4;
+    for (uint64_t base = uint64_t(p) * kPieceChunks; base < nchunks;
+         base += uint64_t(pieces) * kPieceChunks) {
+        uint4 o[4];
+        bool full[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint64_t A = c0 + 16 * (base + uint64_t(k) * kThreads + threadIdx.x);
+            full[k] = A >= dof && A + 16 <= dend;
+            if (full[k]) {
+                const uint64_t kk = A - dof;
+                const uint64_t s = so + kk;
+                const uint8_t* sp = src + (s & ~uint64_t(15));
+                const uint32_t ph = (uint32_t)(s & 15u);
+                o[k] = ld16(sp);
+                // the block holding the chunk's last source byte: a payload byte
+                if (ph) o[k] = funnel16(o[k], ld16(sp + 16), ph);
+                xor4(o[k], rotr8(key, (uint32_t)(kk & 3u)));
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint64_t c = base + uint64_t(k) * kThreads + threadIdx.x;
+            const uint64_t A = c0 + 16 * c;
+            if (full[k]) {
+                st16(dst + A, o[k]);
+            } else if (c < nchunks) {
+                for (uint32_t j = 0; j < 16; ++j) {
+                    const uint64_t x = A + j;
+                    if (x < dof || x >= dend) continue;
+                    const uint64_t kk = x - dof;
+                    dst[x] = (uint8_t)(src[so + kk] ^ (key >> (8 * (kk & 3u))));
+                }
+            }
+        }
     }
 }
 
@@ -2205,6 +2307,83 @@ int cfws_ws_accept_keys_batch(const void* d_keys, const uint64_t* d_key_off, siz
     ws_accept_kernel<<<grid_for(n, kThreads), kThreads, 0, static_cast<hipStream_t>(stream)>>>(
         static_cast<const uint8_t*>(d_keys), d_key_off, n, d_accept);
     return launch_check("ws_accept_keys");
+}
+
+int cfws_encode_headers(cfws_frame_desc_t* d_desc, size_t n, void* d_wire, uint64_t wire_capacity,
+                        void* stream)
+{
+    if (int rc = check_init()) return rc;
+    if (n == 0) return CFWS_OK;
+    if (!d_desc || !d_wire) return set_err(CFWS_ERROR_INVALID_ARGUMENT, "null pointer", hipSuccess);
+    if (n > 0xffffffffull) return set_err(CFWS_ERROR_INVALID_ARGUMENT, "too many frames", hipSuccess);
+    encode_headers_kernel<<<grid_for(n, kThreads), kThreads, 0, static_cast<hipStream_t>(stream)>>>(
+        d_desc, n, static_cast<uint8_t*>(d_wire), wire_capacity);
+    return launch_check("encode_headers");
+}
+
+int cfws_parse_headers(const void* d_wire, uint64_t wire_size, const uint64_t* d_frame_index, size_t n,
+                       uint64_t max_payload, cfws_frame_desc_t* d_desc, int32_t* d_status,
+                       void* stream)
+{
+    if (int rc = check_init()) return rc;
+    if (n == 0) return CFWS_OK;
+    if (!d_wire || !d_frame_index || !d_desc || !d_status)
+        return set_err(CFWS_ERROR_INVALID_ARGUMENT, "null pointer", hipSuccess);
+    parse_headers_kernel<<<grid_for(n, kThreads), kThreads, 0, static_cast<hipStream_t>(stream)>>>(
+        static_cast<const uint8_t*>(d_wire), wire_size, d_frame_index, n, max_payload, d_desc,
+        d_status);
+    return launch_check("parse_headers");
+}
+
+}  // extern "C"
+
+namespace {
+
+// Pieces per frame for the split payload ops: enough workgroups to cover the
+// largest frame in one pass, capped so the grid stays under 2^31 blocks.
+uint32_t payload_pieces(size_t n, uint64_t max_payload_size)
+{
+    const uint64_t chunks = max_payload_size / 16 + 2;
+    uint64_t pieces = (chunks + kPieceChunks - 1) / kPieceChunks;
+    if (pieces > 65536) pieces = 65536;
+    while (pieces > 1 && pieces * n > 0x7fffffffull) pieces >>= 1;
+    return (uint32_t)pieces;
+}
+
+template <bool kUnmask>
+int launch_payload_xor(const void* src, void* dst, const cfws_frame_desc_t* d_desc,
+                       const int32_t* d_status, size_t n, uint64_t max_payload_size, uint64_t cap,
+                       void* stream, const char* what)
+{
+    if (int rc = check_init()) return rc;
+    if (n == 0 || cap == 0) return CFWS_OK;
+    if (!src || !dst || !d_desc) return set_err(CFWS_ERROR_INVALID_ARGUMENT, "null pointer", hipSuccess);
+    if (misaligned(src, dst))
+        return set_err(CFWS_ERROR_INVALID_ARGUMENT, "arenas must be 16-byte aligned", hipSuccess);
+    if (n > 0x7fffffffull) return set_err(CFWS_ERROR_INVALID_ARGUMENT, "too many frames", hipSuccess);
+    const uint32_t pieces = payload_pieces(n, max_payload_size);
+    payload_xor_kernel<kUnmask><<<(uint32_t)(n * pieces), kThreads, 0, static_cast<hipStream_t>(stream)>>>(
+        static_cast<const uint8_t*>(src), static_cast<uint8_t*>(dst), d_desc, d_status, n, pieces, cap);
+    return launch_check(what);
+}
+
+}  // namespace
+
+extern "C" {
+
+int cfws_mask_batch(const void* d_payload, const cfws_frame_desc_t* d_desc, size_t n,
+                    uint64_t max_payload_size, void* d_wire, uint64_t wire_capacity, void* stream)
+{
+    return launch_payload_xor<false>(d_payload, d_wire, d_desc, nullptr, n, max_payload_size,
+                                     wire_capacity, stream, "mask_batch");
+}
+
+int cfws_unmask_batch(const void* d_wire, const cfws_frame_desc_t* d_desc, const int32_t* d_status,
+                      size_t n, uint64_t max_payload_size, void* d_payload,
+                      uint64_t payload_capacity, void* stream)
+{
+    return launch_payload_xor<true>(d_wire, d_payload, d_desc, d_status, n, max_payload_size,
+                                    payload_capacity, stream, "unmask_batch");
 }
 
 int cfws_xor_mask(const void* d_src, void* d_dst, uint64_t n, uint32_t key, uint32_t phase,

@@ -135,6 +135,44 @@ int cfws_deserialize_batch(const void* d_wire, uint64_t wire_size,
                            uint64_t* d_payload_total, void* d_workspace,
                            size_t workspace_size, void* stream);
 
+/* ---- split ops: headers and payload XOR as separate passes ---------------
+ * The two halves of the codec over frames the caller lays out itself (a send
+ * path that gathers headers and payloads into iovecs, a receive path that
+ * places payloads in its own buffers): every descriptor names its own source
+ * and destination, nothing is packed and no workspace is needed.
+ *   cfws_encode_headers: frame i's header (co_ws_frame.c:34-91: b0 = opcode
+ *     | fin << 7, minimal 7/16/64-bit length, the 4 key bytes when mask) at
+ *     d_wire + wire_off; sets header_size (2..14).
+ *   cfws_parse_headers: co_ws_frame_deserialize's header decisions
+ *     (co_ws_frame.c:131-213, with the callers' 2-byte precheck,
+ *     co_ws_client.c:202-206) at d_frame_index[i] against wire_size: d_desc[i]
+ *     (wire_off = the start, payload_off = 0) and d_status[i] -- the decode of
+ *     cfws_deserialize_plan without its payload layout.
+ *   cfws_mask_batch: the serialize payload loop (co_ws_frame.c:93-97):
+ *     d_wire[wire_off + h + k] = d_payload[payload_off + k] ^ key[k % 4],
+ *     k < payload_size, h = the header size of (payload_size, mask); a copy
+ *     when mask == 0. Header bytes are not touched.
+ *   cfws_unmask_batch: the deserialize payload loop (co_ws_frame.c:232-242):
+ *     d_payload[payload_off + k] = d_wire[wire_off + header_size + k] ^
+ *     key[k % 4] for every frame whose d_status is CFWS_PARSE_COMPLETE
+ *     (d_status NULL: every frame); a copy when mask == 0.
+ * Destination bytes at or past the capacity are not written. Destination
+ * ranges of different frames must not overlap; sources may. max_payload_size
+ * is an upper bound of payload_size over the batch: it sizes the grid (a
+ * larger frame is still processed, by fewer workgroups). Arenas 16-byte
+ * aligned. */
+int cfws_encode_headers(cfws_frame_desc_t* d_desc, size_t n_frames, void* d_wire,
+                        uint64_t wire_capacity, void* stream);
+int cfws_parse_headers(const void* d_wire, uint64_t wire_size, const uint64_t* d_frame_index,
+                       size_t n_frames, uint64_t max_payload, cfws_frame_desc_t* d_desc,
+                       int32_t* d_status, void* stream);
+int cfws_mask_batch(const void* d_payload, const cfws_frame_desc_t* d_desc, size_t n_frames,
+                    uint64_t max_payload_size, void* d_wire, uint64_t wire_capacity,
+                    void* stream);
+int cfws_unmask_batch(const void* d_wire, const cfws_frame_desc_t* d_desc, const int32_t* d_status,
+                      size_t n_frames, uint64_t max_payload_size, void* d_payload,
+                      uint64_t payload_capacity, void* stream);
+
 /* ---- receive-buffer frame indexing --------
  * The frame walk of the receive loops co_ws_server_on_tcp_receive_ready
  * (co_ws_server.c:107-169) / co_ws_client_on_tcp_receive_ready

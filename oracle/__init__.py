@@ -71,6 +71,10 @@ def lib() -> C.CDLL:
         L.orc_deserialize_batch.argtypes = [_vp, _u64, _vp, _sz, _u64, C.c_uint32, C.c_uint32,
                                             _vp, _vp, _vp, _u64]
         L.orc_deserialize_batch.restype = _u64
+        L.orc_encode_headers.argtypes = [_vp, _sz, _vp, _u64]
+        L.orc_parse_headers.argtypes = [_vp, _u64, _vp, _sz, _u64, _vp, _vp]
+        L.orc_mask_batch.argtypes = [_vp, _vp, _sz, _vp, _u64]
+        L.orc_unmask_batch.argtypes = [_vp, _vp, _vp, _sz, _vp, _u64]
         L.orc_index_frames.argtypes = [_vp, _u64, _u64, _vp, _sz, C.POINTER(_u64)]
         L.orc_index_frames.restype = _sz
         L.orc_fill_splitmix.argtypes = [_vp, _u64, _u64, _u64]
@@ -134,6 +138,44 @@ def deserialize_batch(wire: np.ndarray, starts: np.ndarray, align: int = 16,
                                         align, flags, _ptr(desc), _ptr(status), _ptr(out),
                                         capacity)
     return out, desc, status, int(total)
+
+
+def encode_headers(desc: np.ndarray, wire: np.ndarray, capacity: int | None = None) -> np.ndarray:
+    """Split op (include/cfws.h): headers at wire_off, in place in `wire`;
+    returns desc with header_size set."""
+    desc = desc.copy()
+    cap = len(wire) if capacity is None else capacity
+    lib().orc_encode_headers(_ptr(desc), len(desc), _ptr(wire), cap)
+    return desc
+
+
+def parse_headers(wire: np.ndarray, starts: np.ndarray, max_payload: int = DEFAULT_MAX_PAYLOAD,
+                  wire_size: int | None = None):
+    starts = np.ascontiguousarray(starts, dtype=np.uint64)
+    desc = np.zeros(len(starts), dtype=DESC_DTYPE)
+    status = np.zeros(len(starts), dtype=np.int32)
+    size = len(wire) if wire_size is None else wire_size
+    w = wire if wire.size else np.zeros(1, np.uint8)
+    lib().orc_parse_headers(_ptr(w), size, _ptr(starts), len(starts), max_payload, _ptr(desc),
+                            _ptr(status))
+    return desc, status
+
+
+def mask_batch(payload: np.ndarray, desc: np.ndarray, wire: np.ndarray,
+               capacity: int | None = None) -> None:
+    """Split op: masked payloads into `wire` in place (headers untouched)."""
+    cap = len(wire) if capacity is None else capacity
+    pl = payload if payload.size else np.zeros(1, np.uint8)
+    lib().orc_mask_batch(_ptr(pl), _ptr(np.ascontiguousarray(desc)), len(desc), _ptr(wire), cap)
+
+
+def unmask_batch(wire: np.ndarray, desc: np.ndarray, status, payload: np.ndarray,
+                 capacity: int | None = None) -> None:
+    """Split op: unmasked payloads into `payload` in place."""
+    cap = len(payload) if capacity is None else capacity
+    st = None if status is None else np.ascontiguousarray(status, dtype=np.int32)
+    lib().orc_unmask_batch(_ptr(wire), _ptr(np.ascontiguousarray(desc)), _ptr(st), len(desc),
+                           _ptr(payload), cap)
 
 
 def index_frames(wire: np.ndarray, max_frames: int, max_payload: int = DEFAULT_MAX_PAYLOAD):

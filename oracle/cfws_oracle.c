@@ -311,6 +311,57 @@ uint64_t orc_deserialize_batch(const uint8_t* wire, uint64_t wire_size,
     return total;
 }
 
+/* ---- split ops: the header and payload passes of co_ws_frame.c ------- */
+
+/* Copies src[0, n) ^ key[k % 4] (mask) or src (no mask) to dst, keeping only
+ * the destination bytes below `lim` (dst_off = dst's offset in its arena). */
+static void orc_put_payload(uint8_t* arena, uint64_t dst_off, uint64_t lim, const uint8_t* src,
+                            uint64_t n, bool mask, uint32_t key)
+{
+    if (dst_off >= lim) return;
+    if (n > lim - dst_off) n = lim - dst_off;
+    if (mask) orc_xor_bytes(arena + dst_off, src, n, key);
+    else if (n) memcpy(arena + dst_off, src, (size_t)n);
+}
+
+void orc_encode_headers(orc_desc_t* d, size_t n, uint8_t* wire, uint64_t cap)
+{   /* co_ws_frame.c:34-91 */
+    for (size_t i = 0; i < n; ++i) {
+        uint8_t h[16];
+        uint32_t hs = orc_encode_header(d[i].fin != 0, d[i].opcode, d[i].mask != 0, d[i].mask_key,
+                                        d[i].payload_size, h);
+        d[i].header_size = (uint8_t)hs;
+        for (uint32_t k = 0; k < hs; ++k)
+            if (d[i].wire_off + k < cap) wire[d[i].wire_off + k] = h[k];
+    }
+}
+
+void orc_parse_headers(const uint8_t* wire, uint64_t size, const uint64_t* starts, size_t n,
+                       uint64_t max_payload, orc_desc_t* d, int32_t* status)
+{   /* co_ws_frame.c:131-213 */
+    for (size_t i = 0; i < n; ++i)
+        status[i] = orc_parse_header(wire, size, starts[i], max_payload, &d[i]);
+}
+
+void orc_mask_batch(const uint8_t* payload, const orc_desc_t* d, size_t n, uint8_t* wire,
+                    uint64_t cap)
+{   /* co_ws_frame.c:93-97 */
+    for (size_t i = 0; i < n; ++i)
+        orc_put_payload(wire, d[i].wire_off + orc_header_size(d[i].payload_size, d[i].mask != 0),
+                        cap, payload + d[i].payload_off, d[i].payload_size, d[i].mask != 0,
+                        d[i].mask_key);
+}
+
+void orc_unmask_batch(const uint8_t* wire, const orc_desc_t* d, const int32_t* status, size_t n,
+                      uint8_t* payload, uint64_t cap)
+{   /* co_ws_frame.c:232-242 */
+    for (size_t i = 0; i < n; ++i) {
+        if (status && status[i] != ORC_PARSE_COMPLETE) continue;
+        orc_put_payload(payload, d[i].payload_off, cap, wire + d[i].wire_off + d[i].header_size,
+                        d[i].payload_size, d[i].mask != 0, d[i].mask_key);
+    }
+}
+
 /* The receive loop of co_ws_server_on_tcp_receive_ready
  * (co_ws_server.c:107-169; co_ws_client.c:200-270 is the same walk) over one
  * connection's received bytes buf[begin, end): stop when under 2 bytes

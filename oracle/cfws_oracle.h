@@ -111,6 +111,27 @@ uint64_t orc_deserialize_batch(const uint8_t* wire, uint64_t wire_size,
                                orc_desc_t* desc, int32_t* status,
                                uint8_t* payload, uint64_t payload_capacity);
 
+/* Split ops (cfws.h "split ops"): headers and payload loops of the codec as
+ * separate passes over caller-laid-out frames. Bytes at or past the
+ * destination capacity are not written.
+ *   orc_encode_headers: co_ws_frame.c:34-91 at wire + desc[i].wire_off; sets
+ *     header_size.
+ *   orc_parse_headers:  co_ws_frame.c:131-213 (+ the callers' 2-byte
+ *     precheck) at starts[i]: desc[i] (payload_off 0), status[i].
+ *   orc_mask_batch:     co_ws_frame.c:93-97: wire[wire_off + header size of
+ *     (payload_size, mask) + k] = payload[payload_off + k] ^ key[k % 4] (a copy
+ *     when mask == 0).
+ *   orc_unmask_batch:   co_ws_frame.c:232-242 for every frame whose status is
+ *     COMPLETE (status NULL: every frame): payload[payload_off + k] =
+ *     wire[wire_off + header_size + k] ^ key[k % 4] (a copy when mask == 0). */
+void orc_encode_headers(orc_desc_t* desc, size_t n, uint8_t* wire, uint64_t wire_capacity);
+void orc_parse_headers(const uint8_t* wire, uint64_t wire_size, const uint64_t* starts, size_t n,
+                       uint64_t max_payload, orc_desc_t* desc, int32_t* status);
+void orc_mask_batch(const uint8_t* payload, const orc_desc_t* desc, size_t n, uint8_t* wire,
+                    uint64_t wire_capacity);
+void orc_unmask_batch(const uint8_t* wire, const orc_desc_t* desc, const int32_t* status, size_t n,
+                      uint8_t* payload, uint64_t payload_capacity);
+
 /* WebSocket over HTTP/2 (src/ws_http2): see cfws_oracle.c. */
 uint64_t orc_h2_send(const uint8_t* ws, uint64_t len, uint32_t max_frame, uint32_t sid,
                      uint8_t* out);

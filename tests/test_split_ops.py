@@ -1,0 +1,278 @@
+"""The split ops of include/cfws.h -- cfws_encode_headers, cfws_parse_headers,
+cfws_mask_batch, cfws_unmask_batch: the header and payload passes of
+co_ws_frame.c (:34-91, :93-97, :131-213, :232-242) over caller-laid-out
+frames.
+
+CPU: the oracle's split restatements compose back to the oracle's serialize
+/ deserialize (which the reference's own vectors pin, test_oracle.py).
+GPU: the device ops equal the oracle byte for byte on packed and scattered
+layouts, with gaps left untouched, capacity cuts, non-COMPLETE frames
+skipped, and the config-2 batch at full size equal to the reference digest.
+"""
+import hashlib
+import random
+
+import numpy as np
+import pytest
+
+import oracle as O
+from conftest import golden
+
+
+def random_frames(rng, n, payload_len, sizes=None):
+    d = np.zeros(n, dtype=O.DESC_DTYPE)
+    for i in range(n):
+        sz = min(rng.choice(sizes) if sizes else rng.randrange(0, 3000), payload_len)
+        d[i]["payload_off"] = rng.randrange(0, payload_len - sz + 1)
+        d[i]["payload_size"] = sz
+        d[i]["fin"] = rng.random() < 0.7
+        d[i]["opcode"] = rng.randrange(256) if rng.random() < 0.1 else rng.choice([0, 1, 2, 8, 9])
+        d[i]["mask"] = rng.random() < 0.6
+        d[i]["mask_key"] = rng.getrandbits(32) if d[i]["mask"] else 0
+    return d
+
+
+def scattered_wire_offsets(rng, desc, max_gap=40):
+    """Frames placed in order with random gaps (any alignment): no overlap."""
+    off = rng.randrange(0, 16)
+    out = np.zeros(len(desc), dtype=np.uint64)
+    for i, d in enumerate(desc):
+        out[i] = off
+        off += O.header_size(int(d["payload_size"]), bool(d["mask"])) + int(d["payload_size"])
+        off += rng.randrange(0, max_gap)
+    return out, off
+
+
+# ---- CPU: the oracle's split ops against its pinned serialize / deserialize ----
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_oracle_split_composes_to_serialize(seed):
+    rng = random.Random(seed)
+    payload = O.fill_splitmix(200000, 0x5EED + seed)
+    desc = random_frames(rng, 300, len(payload), sizes=[0, 1, 125, 126, 127, 4096, 65535,
+                                                         65536, 65537, rng.randrange(70000)])
+    wire, d_exp = O.serialize_batch(payload, desc)
+    d = desc.copy()
+    d["wire_off"] = d_exp["wire_off"]
+    w2 = np.zeros(len(wire), np.uint8)
+    d2 = O.encode_headers(d, w2)
+    O.mask_batch(payload, d2, w2)
+    assert np.array_equal(w2, wire)
+    assert np.array_equal(d2["header_size"], d_exp["header_size"])
+    pd, st = O.parse_headers(wire, d_exp["wire_off"])
+    _, dd, st_d, _ = O.deserialize_batch(wire, d_exp["wire_off"], align=1)
+    assert np.array_equal(st, st_d)          # opcode bytes > 0x0f (RSV bits) -> -7001
+    for f in ("payload_size", "mask_key", "fin", "opcode", "mask", "header_size"):
+        assert np.array_equal(pd[f], dd[f]), f
+    ok = st == 0
+    # (fin / opcode: b0 = opcode | fin << 7 verbatim, so opcode bit 7 reads back as fin)
+    for f in ("payload_size", "mask_key", "mask", "header_size"):
+        assert np.array_equal(pd[f][ok], d_exp[f][ok]), f
+    out = np.zeros(len(payload), np.uint8)
+    pd["payload_off"] = desc["payload_off"]
+    O.unmask_batch(wire, pd, st, out)
+    for d0, good in zip(desc, ok):
+        a, n = int(d0["payload_off"]), int(d0["payload_size"])
+        if good:
+            assert np.array_equal(out[a:a + n], payload[a:a + n])
+
+
+def test_oracle_parse_headers_golden():
+    for c in golden("deserialize_cases.json"):
+        if c["wire_hex"] is None:
+            continue
+        raw = np.frombuffer(bytes.fromhex(c["wire_hex"]), dtype=np.uint8).copy()
+        d, st = O.parse_headers(raw, np.array([c["index"]], np.uint64), c["max_payload"])
+        exp = O.PARSE_MORE_DATA if len(raw) - c["index"] < 2 else c["rc"]
+        assert st[0] == exp, c["name"]
+        if exp == 0:
+            assert int(d["payload_size"][0]) == c["payload_size"]
+
+
+# ---- GPU -------------------------------------------------------------------
+
+def _torch():
+    return pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def dev():
+    torch = _torch()
+    from coldforce_amd import cfws
+    cfws.init()
+    return torch.device("cuda", 0)
+
+
+def gpu_encode_mask(payload, desc, wire_len, fill=0xA5, capacity=None, max_payload=None,
+                    headers=True):
+    torch = _torch()
+    from coldforce_amd import cfws
+    pay = torch.from_numpy(payload).cuda()
+    d_t = cfws.desc_to_device(desc.view(cfws.DESC_DTYPE))
+    wire = torch.full((wire_len,), fill, dtype=torch.uint8, device="cuda")
+    cap = wire_len if capacity is None else capacity
+    if headers:
+        cfws.encode_headers(d_t, wire, cap)
+    mp = int(desc["payload_size"].max()) if max_payload is None else max_payload
+    cfws.mask_batch(pay, d_t, wire, mp, cap)
+    torch.cuda.synchronize()
+    return wire.cpu().numpy(), cfws.desc_from_device(d_t)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", [3, 4, 5])
+def test_encode_mask_scattered(dev, seed):
+    rng = random.Random(seed)
+    payload = O.fill_splitmix(300000, seed)
+    desc = random_frames(rng, 500, len(payload), sizes=[0, 1, 2, 3, 15, 16, 17, 125, 126, 1000,
+                                                         4096, 65535, 65536, 70000])
+    desc["wire_off"], total = scattered_wire_offsets(rng, desc)
+    wlen = total + 64
+    got, d_got = gpu_encode_mask(payload, desc, wlen)
+    exp = np.full(wlen, 0xA5, np.uint8)
+    d_exp = O.encode_headers(desc, exp)
+    O.mask_batch(payload, d_exp, exp)
+    bad = np.nonzero(got != exp)[0]
+    assert bad.size == 0, f"{bad.size} bytes differ, first at {bad[:8]}"
+    assert np.array_equal(d_got["header_size"], d_exp["header_size"])
+
+
+@pytest.mark.gpu
+def test_encode_mask_packed_equals_serialize(dev):
+    rng = random.Random(11)
+    payload = O.fill_splitmix(1 << 20, 11)
+    desc = random_frames(rng, 2000, len(payload))
+    wire, d_exp = O.serialize_batch(payload, desc)
+    d = desc.copy()
+    d["wire_off"] = d_exp["wire_off"]
+    got, _ = gpu_encode_mask(payload, d, len(wire) + 16)
+    assert np.array_equal(got[:len(wire)], wire)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("max_payload", [0, 1000, 1 << 20])
+def test_mask_grid_hint(dev, max_payload):
+    # the max_payload_size hint only sizes the grid: any value gives the same bytes
+    rng = random.Random(21)
+    payload = O.fill_splitmix(3 << 20, 21)
+    desc = random_frames(rng, 40, len(payload), sizes=[70000, 1 << 20, (2 << 20) + 5, 3])
+    desc["wire_off"], total = scattered_wire_offsets(rng, desc)
+    got, _ = gpu_encode_mask(payload, desc, total + 32, max_payload=max_payload)
+    exp = np.full(total + 32, 0xA5, np.uint8)
+    O.mask_batch(payload, O.encode_headers(desc, exp), exp)
+    assert np.array_equal(got, exp)
+
+
+@pytest.mark.gpu
+def test_mask_capacity_cut(dev):
+    rng = random.Random(31)
+    payload = O.fill_splitmix(100000, 31)
+    desc = random_frames(rng, 60, len(payload))
+    desc["wire_off"], total = scattered_wire_offsets(rng, desc)
+    for cap in (0, 1, 17, total // 3 + 5, total - 1):
+        got, _ = gpu_encode_mask(payload, desc, total + 16, capacity=cap)
+        exp = np.full(total + 16, 0xA5, np.uint8)
+        O.mask_batch(payload, O.encode_headers(desc, exp, cap), exp, cap)
+        assert np.array_equal(got, exp), cap
+
+
+@pytest.mark.gpu
+def test_parse_headers_matches_oracle(dev):
+    torch = _torch()
+    from coldforce_amd import cfws
+    rng = random.Random(41)
+    payload = O.fill_splitmix(400000, 41)
+    desc = random_frames(rng, 700, len(payload), sizes=[0, 1, 125, 126, 127, 65535, 65536, 70000])
+    wire, d_exp = O.serialize_batch(payload, desc)
+    wire = wire.copy()
+    starts = d_exp["wire_off"].astype(np.uint64)
+    for i in rng.sample(range(len(desc)), 20):
+        wire[int(starts[i])] |= 0x20                       # RSV3 -> INVALID_FRAME
+    extra = np.array([len(wire) - 1, len(wire), len(wire) + 9, int(starts[7]) + 1], np.uint64)
+    starts = np.concatenate([starts, extra])
+    for max_payload in (O.DEFAULT_MAX_PAYLOAD, 1000):
+        for size in (len(wire), len(wire) - 70001):
+            w_t = torch.from_numpy(wire).cuda()
+            i_t = torch.from_numpy(starts.astype(np.int64)).cuda()
+            d_t = torch.empty((len(starts), 32), dtype=torch.uint8, device="cuda")
+            s_t = torch.empty(len(starts), dtype=torch.int32, device="cuda")
+            cfws.parse_headers(w_t, size, i_t, d_t, s_t, max_payload)
+            torch.cuda.synchronize()
+            d_got, st_got = cfws.desc_from_device(d_t), s_t.cpu().numpy()
+            d_o, st_o = O.parse_headers(wire, starts, max_payload, wire_size=size)
+            assert np.array_equal(st_got, st_o)
+            for f in ("wire_off", "payload_size", "mask_key", "fin", "opcode", "mask",
+                      "header_size"):
+                assert np.array_equal(d_got[f], d_o[f]), f
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", [51, 52])
+def test_unmask_scattered(dev, seed):
+    torch = _torch()
+    from coldforce_amd import cfws
+    rng = random.Random(seed)
+    payload = O.fill_splitmix(300000, seed)
+    desc = random_frames(rng, 600, len(payload), sizes=[0, 1, 5, 16, 33, 125, 126, 4097, 65536,
+                                                         70000])
+    wire, d_exp = O.serialize_batch(payload, desc)
+    pd, st = O.parse_headers(wire, d_exp["wire_off"])
+    # payloads to scattered destinations, any alignment, with gaps
+    off = rng.randrange(16)
+    for i in range(len(pd)):
+        pd[i]["payload_off"] = off
+        off += int(pd[i]["payload_size"]) + rng.randrange(0, 24)
+    st = st.copy()
+    for i in rng.sample(range(len(st)), 40):
+        st[i] = rng.choice([O.PARSE_MORE_DATA, O.ERROR_INVALID_FRAME, O.ERROR_DATA_TOO_BIG])
+    plen = off + 32
+    for cap in (plen, plen // 2 + 3):
+        w_t = torch.from_numpy(wire).cuda()
+        d_t = cfws.desc_to_device(pd.view(cfws.DESC_DTYPE))
+        s_t = torch.from_numpy(st).cuda()
+        out_t = torch.full((plen,), 0x5C, dtype=torch.uint8, device="cuda")
+        cfws.unmask_batch(w_t, d_t, s_t, out_t, int(pd["payload_size"].max()), cap)
+        torch.cuda.synchronize()
+        exp = np.full(plen, 0x5C, np.uint8)
+        O.unmask_batch(wire, pd, st, exp, cap)
+        got = out_t.cpu().numpy()
+        bad = np.nonzero(got != exp)[0]
+        assert bad.size == 0, f"cap {cap}: {bad.size} bytes differ, first at {bad[:8]}"
+
+
+@pytest.mark.gpu
+def test_split_config2_full_size_digest(dev):
+    """65,536 x 64 KiB through encode_headers + mask_batch: the same wire as
+    the reference's serialize (tests/golden/batch_digests.json), and
+    parse_headers + unmask_batch restore every payload byte."""
+    torch = _torch()
+    from coldforce_amd import cfws
+    from coldforce_amd import workloads as W
+    g = golden("batch_digests.json")[2]
+    n, fs = g["n_frames"], g["frame_size"]
+    desc = W.uniform_batch(n, fs, g["key_seed"])
+    offs, total = W.wire_layout(desc)
+    desc["wire_off"] = offs
+    payload = torch.empty(n * fs, dtype=torch.uint8, device="cuda")
+    cfws.fill_splitmix(payload, g["payload_seed"])
+    d_t = cfws.desc_to_device(desc)
+    wire = torch.empty(W.round16(total), dtype=torch.uint8, device="cuda")
+    cfws.encode_headers(d_t, wire)
+    cfws.mask_batch(payload, d_t, wire, fs)
+    torch.cuda.synchronize()
+    h = hashlib.sha256()
+    step = 1 << 28
+    for o in range(0, total, step):
+        h.update(wire[o:min(total, o + step)].cpu().numpy().tobytes())
+    assert h.hexdigest() == g["wire_sha256"]
+    idx = torch.from_numpy(offs.astype(np.int64)).cuda()
+    pd_t = torch.empty((n, 32), dtype=torch.uint8, device="cuda")
+    st_t = torch.empty(n, dtype=torch.int32, device="cuda")
+    cfws.parse_headers(wire, total, idx, pd_t, st_t)
+    pd = cfws.desc_from_device(pd_t)
+    assert (st_t == 0).all().item()
+    pd["payload_off"] = np.arange(n, dtype=np.uint64) * fs
+    back = torch.empty(n * fs, dtype=torch.uint8, device="cuda")
+    cfws.unmask_batch(wire, cfws.desc_to_device(pd), st_t, back, fs)
+    torch.cuda.synchronize()
+    assert torch.equal(back, payload)
