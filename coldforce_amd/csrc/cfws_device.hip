@@ -1284,31 +1284,41 @@ payload_xor_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
     const uint64_t dend = len < cap - dof ? dof + len : cap;
     const uint64_t c0 = dof & ~uint64_t(15);
     const uint64_t nchunks = (dend - c0 + 15) >> 4;
+    // source phase against the 16-byte destination chunks: one per frame
+    const uint32_t ph = (uint32_t)((so - dof) & 15u);
+    const uint32_t lane = threadIdx.x & 63u;
     for (uint64_t base = uint64_t(p) * kPieceChunks; base < nchunks;
          base += uint64_t(pieces) * kPieceChunks) {
-        uint4 o[4];
+        // a lane's block B is the next lane's A (DPP) when that lane's chunk
+        // is full too; lane 63 and the last full chunk load their own
+        uint4 a[4], e[4];
         bool full[4];
+        uint32_t own_b = 0;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const uint64_t A = c0 + 16 * (base + uint64_t(k) * kThreads + threadIdx.x);
             full[k] = A >= dof && A + 16 <= dend;
+            a[k] = make_uint4(0, 0, 0, 0);
+            e[k] = make_uint4(0, 0, 0, 0);
             if (full[k]) {
-                const uint64_t kk = A - dof;
-                const uint64_t s = so + kk;
-                const uint8_t* sp = src + (s & ~uint64_t(15));
-                const uint32_t ph = (uint32_t)(s & 15u);
-                o[k] = ld16(sp);
+                const uint8_t* sp = src + ((so + (A - dof)) & ~uint64_t(15));
+                a[k] = ld16(sp);
                 // the block holding the chunk's last source byte: a payload byte
-                if (ph) o[k] = funnel16(o[k], ld16(sp + 16), ph);
-                xor4(o[k], rotr8(key, (uint32_t)(kk & 3u)));
+                if (ph && (lane == 63 || A + 32 > dend)) {
+                    e[k] = ld16(sp + 16);
+                    own_b |= 1u << k;
+                }
             }
         }
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
+            const uint4 nb = from_next_lane(a[k], e[k]);     // every lane: DPP needs the full wave
             const uint64_t c = base + uint64_t(k) * kThreads + threadIdx.x;
             const uint64_t A = c0 + 16 * c;
             if (full[k]) {
-                st16(dst + A, o[k]);
+                uint4 o = ph ? funnel16(a[k], (own_b >> k) & 1u ? e[k] : nb, ph) : a[k];
+                xor4(o, rotr8(key, (uint32_t)((A - dof) & 3u)));
+                st16(dst + A, o);
             } else if (c < nchunks) {
                 for (uint32_t j = 0; j < 16; ++j) {
                     const uint64_t x = A + j;
@@ -2362,7 +2372,8 @@ int launch_payload_xor(const void* src, void* dst, const cfws_frame_desc_t* d_de
         return set_err(CFWS_ERROR_INVALID_ARGUMENT, "arenas must be 16-byte aligned", hipSuccess);
     if (n > 0x7fffffffull) return set_err(CFWS_ERROR_INVALID_ARGUMENT, "too many frames", hipSuccess);
     const uint32_t pieces = payload_pieces(n, max_payload_size);
-    payload_xor_kernel<kUnmask><<<(uint32_t)(n * pieces), kThreads, 0, static_cast<hipStream_t>(stream)>>>(
+    payload_xor_kernel<kUnmask><<<(uint32_t)(n * pieces), kThreads, xform_lds_bytes(),
+                                  static_cast<hipStream_t>(stream)>>>(
         static_cast<const uint8_t*>(src), static_cast<uint8_t*>(dst), d_desc, d_status, n, pieces, cap);
     return launch_check(what);
 }
