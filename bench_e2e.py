@@ -25,6 +25,15 @@ sys.path.insert(0, ROOT)
 GIB = float(1 << 30)
 
 
+def host_buffer(args, n):
+    import torch
+
+    from coldforce_amd import cfws
+    if args.host == "mapped":
+        return cfws.mapped_host(n)[:n]
+    return torch.empty(n, dtype=torch.uint8, pin_memory=True)
+
+
 def e2e_h2(args):
     """Config 5 host to host: payload (pinned) -> H2D -> WS serialize + HTTP/2
     DATA wrap -> D2H DATA stream, and back (H2D -> unwrap + pool + unmask ->
@@ -43,9 +52,10 @@ def e2e_h2(args):
     Wf = fs + hs
     k = -(-Wf // S)
     Hf = Wf + 9 * k                                       # DATA-stream bytes per WS frame
-    payload = torch.empty(F * fs, dtype=torch.uint8, pin_memory=True)
-    h2 = torch.empty(F * Hf, dtype=torch.uint8, pin_memory=True)
-    back = torch.empty(F * fs, dtype=torch.uint8, pin_memory=True)
+    payload = host_buffer(args, F * fs)
+    h2 = host_buffer(args, F * Hf)
+    back = host_buffer(args, F * fs)
+    mapped = args.host == "mapped"
     dev = torch.empty(F * fs, dtype=torch.uint8, device="cuda")
     cfws.fill_splitmix(dev, 0x5EED0005)
     payload.copy_(dev)
@@ -85,7 +95,10 @@ def e2e_h2(args):
             with torch.cuda.stream(st):
                 pay_d[:(c1 - c0) * fs].copy_(payload[c0 * fs:c1 * fs], non_blocking=True)
                 cfws.h2_serialize(pay_d, descs[c], wire_d, h2_d, 1, S, ws_s, tot, stream=st)
-                h2[c0 * Hf:c1 * Hf].copy_(h2_d[:(c1 - c0) * Hf], non_blocking=True)
+                if mapped:
+                    cfws.copy_to_host(h2_d, h2[c0 * Hf:].data_ptr(), (c1 - c0) * Hf, stream=st)
+                else:
+                    h2[c0 * Hf:c1 * Hf].copy_(h2_d[:(c1 - c0) * Hf], non_blocking=True)
         torch.cuda.synchronize()
 
     def de():
@@ -99,7 +112,10 @@ def e2e_h2(args):
                 h2_d[:n * Hf].copy_(h2[c0 * Hf:c1 * Hf], non_blocking=True)
                 hs_, md, ms, ptot, m = cfws.h2_deserialize(h2_d, n * Hf, idx[:n * k], pool_d, back_d,
                                                            S, align=1, ws_t=ws_d, stream=st)
-                back[c0 * fs:c1 * fs].copy_(back_d[:n * fs], non_blocking=True)
+                if mapped:
+                    cfws.copy_to_host(back_d, back[c0 * fs:].data_ptr(), n * fs, stream=st)
+                else:
+                    back[c0 * fs:c1 * fs].copy_(back_d[:n * fs], non_blocking=True)
                 ok = ok and m == n
         torch.cuda.synchronize()
         return ok
@@ -122,7 +138,8 @@ def e2e_h2(args):
             "serialize_s": round(t_ser, 4), "deserialize_s": round(t_de, 4),
             "serialize_GiBps": round(nbytes / t_ser / GIB, 2),
             "deserialize_GiBps": round(nbytes / t_de / GIB, 2),
-            "round_trip_GiBps": round(2 * nbytes / (t_ser + t_de) / GIB, 2), "verified": ok}
+            "round_trip_GiBps": round(2 * nbytes / (t_ser + t_de) / GIB, 2), "host": args.host,
+            "verified": ok}
     print(json.dumps(line), flush=True)
     return 0 if ok else 1
 
@@ -135,6 +152,10 @@ def main():
     ap.add_argument("--chunk-mib", type=int, default=64)
     ap.add_argument("--depth", type=int, default=3)
     ap.add_argument("--reps", type=int, default=7)
+    ap.add_argument("--host", choices=["mapped", "torch"], default="mapped",
+                    help="host arenas: mapped pinned memory (hipHostMallocMapped; the D2H leg "
+                         "is a kernel writing it, cfws_copy_to_host) or torch pinned memory "
+                         "(the D2H leg is an SDMA copy)")
     args = ap.parse_args()
 
     import numpy as np
@@ -155,9 +176,9 @@ def main():
         nbytes, seed = args.frames * args.frame_size, 0x5EED0002
     offs, wire_total = W.wire_layout(desc)
 
-    payload = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
-    wire = torch.empty(wire_total + 64, dtype=torch.uint8, pin_memory=True)
-    back = torch.empty(nbytes + 16 * len(desc) + 64, dtype=torch.uint8, pin_memory=True)
+    payload = host_buffer(args, nbytes)
+    wire = host_buffer(args, wire_total + 64)
+    back = host_buffer(args, nbytes + 16 * len(desc) + 64)
     dev = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
     cfws.fill_splitmix(dev, seed)
     torch.cuda.synchronize()
@@ -214,6 +235,7 @@ def main():
         "round_trip_GiBps": round(2 * nbytes / (t_ser + t_de) / GIB, 2),
         "receive_s": round(t_rx, 4), "receive_GiBps": round(nbytes / t_rx / GIB, 2),
         "timing": f"median of {args.reps} reps after one warm-up",
+        "host": args.host,
         "pinned_h2d_GBps": round(h2d, 1), "pinned_d2h_GBps": round(d2h, 1),
         "verified": ok,
     }

@@ -53,7 +53,7 @@ BATCH_SYMBOLS = (
     "cfws_h2_deserialize_workspace_size", "cfws_h2_deserialize_batch",
     "cfws_index_frames", "cfws_index_workspace_size", "cfws_index_frames_batch",
     "cfws_ws_accept_keys_batch", "cfws_encode_headers", "cfws_parse_headers",
-    "cfws_mask_batch", "cfws_unmask_batch",
+    "cfws_mask_batch", "cfws_unmask_batch", "cfws_copy_to_host", "cfws_mapped_device_pointer",
 )
 DROPIN_SYMBOLS = (
     "co_ws_frame_serialize", "co_ws_frame_deserialize", "co_ws_frame_create",
@@ -113,6 +113,8 @@ def lib(path: str = LIB_PATH) -> C.CDLL:
         "cfws_parse_headers": ([_vp, _u64, _vp, _sz, _u64, _vp, _vp, _vp], C.c_int),
         "cfws_mask_batch": ([_vp, _vp, _sz, _u64, _vp, _u64, _vp], C.c_int),
         "cfws_unmask_batch": ([_vp, _vp, _vp, _sz, _u64, _vp, _u64, _vp], C.c_int),
+        "cfws_copy_to_host": ([_vp, _vp, _u64, _vp], C.c_int),
+        "cfws_mapped_device_pointer": ([_vp], _vp),
         "cfws_xor_mask": ([_vp, _vp, _u64, _u32, _u32, _vp], C.c_int),
         "cfws_draw_mask_keys": ([_sz, _vp, _vp], None),
         "cfws_release_thread_resources": ([], None),
@@ -285,6 +287,51 @@ def deserialize(wire_t, wire_size: int, index_t, payload_t, desc_t=None, status_
                                         _stream(stream)),
            "cfws_deserialize_batch")
     return desc_t, status_t, total_t
+
+
+# ---- host memory ---------------------------------------------------------------
+
+_hiprt = None
+
+
+def _hip():
+    global _hiprt
+    if _hiprt is None:
+        lib()                                          # the HIP runtime torch loaded
+        h = C.CDLL("libamdhip64.so")
+        h.hipHostMalloc.argtypes = [C.POINTER(_vp), _sz, C.c_uint]
+        h.hipHostMalloc.restype = C.c_int
+        h.hipHostFree.argtypes = [_vp]
+        h.hipHostFree.restype = C.c_int
+        _hiprt = h
+    return _hiprt
+
+
+HIP_HOST_MALLOC_MAPPED = 0x2
+
+
+def mapped_host(nbytes: int):
+    """A uint8 torch tensor over pinned host memory allocated MAPPED
+    (hipHostMalloc(..., hipHostMallocMapped)): the host pipeline writes such
+    buffers with a kernel instead of an SDMA copy (cfws_copy_to_host). The
+    memory is freed with the tensor."""
+    import weakref
+
+    import numpy as np
+    import torch
+    n = max(int(nbytes), 16)
+    ptr = _vp()
+    rc = _hip().hipHostMalloc(C.byref(ptr), n, HIP_HOST_MALLOC_MAPPED)
+    if rc != 0 or not ptr.value:
+        raise CodecError(f"hipHostMalloc({n}) failed rc={rc}")
+    buf = (C.c_uint8 * n).from_address(ptr.value)
+    weakref.finalize(buf, _hip().hipHostFree, ptr.value)
+    return torch.from_numpy(np.ctypeslib.as_array(buf))
+
+
+def copy_to_host(src_t, h_dst_ptr: int, n: int, stream=None) -> None:
+    """Device -> mapped host copy by a kernel (cfws_copy_to_host)."""
+    _check(lib().cfws_copy_to_host(_p(src_t), h_dst_ptr, n, _stream(stream)), "cfws_copy_to_host")
 
 
 # ---- split ops (headers and payload XOR as separate passes) -----------------

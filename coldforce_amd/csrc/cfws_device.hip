@@ -1331,6 +1331,38 @@ payload_xor_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
     }
 }
 
+// Device -> host copy by a kernel (cfws_copy_to_host): 16-byte stores into
+// device-mapped pinned host memory, any alignment on either side. Running the
+// D2H leg this way beside an SDMA H2D measured 43 GB/s each way against 28
+// for two SDMA copies (tools/pcie_probe2.hip). Each lane writes whole
+// destination-aligned 16-byte chunks (source funnel-shifted into place); the
+// first and last chunk, which the destination may share with other data,
+// byte by byte.
+__global__ void __launch_bounds__(kThreads)
+copy_out_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, uint64_t n)
+{
+    const uintptr_t d0 = reinterpret_cast<uintptr_t>(dst);
+    const uintptr_t c0 = d0 & ~uintptr_t(15);
+    const uint64_t nchunks = (d0 + n - c0 + 15) >> 4;
+    const uint32_t ph = (uint32_t)((reinterpret_cast<uintptr_t>(src) - d0) & 15u);
+    const uint64_t stride = uint64_t(gridDim.x) * kThreads;
+    for (uint64_t c = uint64_t(blockIdx.x) * kThreads + threadIdx.x; c < nchunks; c += stride) {
+        const uintptr_t A = c0 + 16 * c;
+        if (A >= d0 && A + 16 <= d0 + n) {
+            const uint8_t* sp = reinterpret_cast<const uint8_t*>(
+                (reinterpret_cast<uintptr_t>(src) + (A - d0)) & ~uintptr_t(15));
+            uint4 o = ld16(sp);
+            if (ph) o = funnel16(o, ld16(sp + 16), ph);    // holds the chunk's last source byte
+            *reinterpret_cast<u32x4*>(A) = u32x4{o.x, o.y, o.z, o.w};
+        } else {
+            for (uint32_t j = 0; j < 16; ++j) {
+                const uintptr_t x = A + j;
+                if (x >= d0 && x < d0 + n) *reinterpret_cast<uint8_t*>(x) = src[x - d0];
+            }
+        }
+    }
+}
+
 __global__ void __launch_bounds__(kThreads)
 xor_mask_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, uint64_t n,
                 uint32_t key, uint32_t phase)
@@ -1914,6 +1946,17 @@ void launch_pass(const WsLayout& L, int p, const void* src, void* dst, const cfw
 
 }  // namespace
 
+int cfws_internal_copy_out(const void* d_src, void* dev_dst, uint64_t n, void* stream)
+{
+    if (n == 0) return CFWS_OK;
+    const uint64_t chunks = n / 16 + 2;
+    const uint64_t blocks = (chunks + kThreads - 1) / kThreads;
+    copy_out_kernel<<<(uint32_t)(blocks < 1024 ? blocks : 1024), kThreads, 0,
+                      static_cast<hipStream_t>(stream)>>>(static_cast<const uint8_t*>(d_src),
+                                                          static_cast<uint8_t*>(dev_dst), n);
+    return launch_check("copy_to_host");
+}
+
 uint64_t cfws_internal_grand_total_offset() { return ws_layout(0, 0).hdr + 3 * sizeof(uint64_t); }
 
 // ---------------------------------------------------------------------------
@@ -2317,6 +2360,30 @@ int cfws_ws_accept_keys_batch(const void* d_keys, const uint64_t* d_key_off, siz
     ws_accept_kernel<<<grid_for(n, kThreads), kThreads, 0, static_cast<hipStream_t>(stream)>>>(
         static_cast<const uint8_t*>(d_keys), d_key_off, n, d_accept);
     return launch_check("ws_accept_keys");
+}
+
+void* cfws_mapped_device_pointer(const void* h_ptr)
+{
+    if (check_init() != CFWS_OK || !h_ptr) return nullptr;
+    unsigned flags = 0;
+    void* d = nullptr;
+    if (hipHostGetFlags(&flags, const_cast<void*>(h_ptr)) != hipSuccess || !(flags & hipHostMallocMapped) ||
+        hipHostGetDevicePointer(&d, const_cast<void*>(h_ptr), 0) != hipSuccess) {
+        (void)hipGetLastError();     // not a mapped HIP host allocation: no sticky error
+        return nullptr;
+    }
+    return d;
+}
+
+int cfws_copy_to_host(const void* d_src, void* h_dst, uint64_t n, void* stream)
+{
+    if (int rc = check_init()) return rc;
+    if (n == 0) return CFWS_OK;
+    if (!d_src || !h_dst) return set_err(CFWS_ERROR_INVALID_ARGUMENT, "null pointer", hipSuccess);
+    void* d = cfws_mapped_device_pointer(h_dst);
+    if (!d) return set_err(CFWS_ERROR_INVALID_ARGUMENT, "destination is not mapped pinned host memory",
+                           hipSuccess);
+    return cfws_internal_copy_out(d_src, d, n, stream);
 }
 
 int cfws_encode_headers(cfws_frame_desc_t* d_desc, size_t n, void* d_wire, uint64_t wire_capacity,

@@ -9,4 +9,8 @@
 // layout total of pass 0 (the prefix sum before the capacity clamp).
 uint64_t cfws_internal_grand_total_offset();
 
+// D2H by copy_out_kernel into device-mapped host memory at its DEVICE
+// address dev_dst (cfws_mapped_device_pointer); no mapping check.
+int cfws_internal_copy_out(const void* d_src, void* dev_dst, uint64_t n, void* stream);
+
 #endif

@@ -304,6 +304,16 @@ int cfws_pipeline_receive(cfws_pipeline_t* pipeline, const void* h_wire, uint64_
                           uint64_t* consumed, int32_t* stop, void* h_payload,
                           uint64_t payload_capacity, uint64_t* payload_total);
 
+/* D2H by a kernel: copies d_src[0, n) to h_dst, a host buffer allocated (or
+ * registered) MAPPED (hipHostMalloc(..., hipHostMallocMapped)), by 16-byte
+ * stores over PCIe. Beside an SDMA H2D this direction runs at 43 GB/s where a
+ * second SDMA copy gets 28; the pipeline uses it by itself
+ * when its destination is mapped. CFWS_ERROR_INVALID_ARGUMENT when h_dst is
+ * not mapped memory. cfws_mapped_device_pointer: h_ptr's device address when
+ * it is mapped HIP host memory, else NULL. */
+int cfws_copy_to_host(const void* d_src, void* h_dst, uint64_t n, void* stream);
+void* cfws_mapped_device_pointer(const void* h_ptr);
+
 /* ---- single-buffer XOR (used by the per-frame drop-in path) --------------
  * d_dst[i] = d_src[i] ^ key byte (i + key_phase) % 4, i < n. */
 int cfws_xor_mask(const void* d_src, void* d_dst, uint64_t n, uint32_t mask_key,

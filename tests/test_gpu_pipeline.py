@@ -18,14 +18,48 @@ from coldforce_amd import cfws  # noqa: E402
 from coldforce_amd import workloads as W  # noqa: E402
 
 
+HOST = {"kind": "torch"}
+
+
 def pinned(n: int):
-    t = torch.zeros(max(n, 16), dtype=torch.uint8, pin_memory=True)
+    """Host buffer of the kind under test: torch's pinned memory (the
+    pipeline's D2H leg is an SDMA copy) or mapped pinned memory (the D2H leg
+    is copy_out_kernel writing it over PCIe)."""
+    if HOST["kind"] == "mapped":
+        t = cfws.mapped_host(n)
+        t.zero_()
+    else:
+        t = torch.zeros(max(n, 16), dtype=torch.uint8, pin_memory=True)
     return t, t.numpy()
 
 
 @pytest.fixture(scope="module", autouse=True)
 def device():
     cfws.init()
+
+
+@pytest.fixture(autouse=True, params=["torch", "mapped"])
+def host_kind(request):
+    HOST["kind"] = request.param
+    yield request.param
+    HOST["kind"] = "torch"
+
+
+def test_copy_to_host_any_alignment():
+    src = torch.from_numpy(O.fill_splitmix(1 << 20, 5)).cuda()
+    out_t, out = pinned((1 << 20) + 64)
+    if HOST["kind"] == "torch":
+        # not mapped memory: refused, nothing written
+        with pytest.raises(cfws.CodecError):
+            cfws.copy_to_host(src, out_t.data_ptr(), 100)
+        return
+    exp = out.copy()
+    for so, do, n in [(0, 0, 1 << 20), (3, 5, 1000), (16, 1, 17), (7, 7, 65536 + 9), (1, 0, 15),
+                      (0, 33, 0)]:
+        cfws.copy_to_host(src[so:], out_t.data_ptr() + do, n)
+        torch.cuda.synchronize()
+        exp[do:do + n] = src[so:so + n].cpu().numpy()
+        assert np.array_equal(out, exp), (so, do, n)
 
 
 @pytest.mark.parametrize("chunk,depth", [(69632, 1), (69632, 3), (1 << 20, 2)])
