@@ -13,7 +13,8 @@ server-unmask, device resident. One step =
 value = payload bytes processed by both ops on all ranks / wall time of the
 K timed steps (max over ranks), in GiB/s (2^30). With N GPUs each rank owns
 its own 65,536-frame shard of one global batch (weak scaling, no collective
-on the data path; the only collectives are the timing barrier and max).
+on the data path; the only collectives are the timing barrier and max, and
+a gather of each rank's timings for the line's per_gpu rows).
 
 Usage: python bench.py [--gpus N --steps K --warmup W]
        torchrun --nproc-per-node N bench.py --gpus N ...   (N > 1)
@@ -162,7 +163,9 @@ def bench_h2(args, rank, world, dev):
     for _ in range(args.steps):
         st, md, ms, ptot, m = step()
     torch.cuda.synchronize()
-    elapsed = shard.max_over_ranks(time.perf_counter() - t0, dev)
+    local = time.perf_counter() - t0
+    elapsed = shard.max_over_ranks(local, dev)
+    rows = shard.gather_floats([local, F * fs], dev)
     ok = (m == F and int(ptot.item()) == F * fs and bool((st == 0).all()) and bool((ms == 0).all())
           and torch.equal(back[:F * fs], payload[:F * fs]))
     line = {"metric": "WS-over-HTTP/2 payload GiB/s device-resident (config 5)",
@@ -173,7 +176,7 @@ def bench_h2(args, rank, world, dev):
                                    f"server-unmask", "h2_bytes_per_gpu": h2_total,
                        "data_frames_per_gpu": len(starts)},
             "note": "one fused streaming pass per direction: WS frames straight into DATA frames (send), WS payload slices straight out of DATA frames (receive)",
-            "verified": ok}
+            "per_gpu": per_gpu_rows(rows, args.steps), "verified": ok}
     if rank == 0:
         print(json.dumps(line), flush=True)
     return 0 if ok else 1
@@ -217,17 +220,36 @@ def bench_split(args, rank, world, dev):
     for _ in range(args.steps):
         step()
     torch.cuda.synchronize()
-    elapsed = shard.max_over_ranks(time.perf_counter() - t0, dev)
+    local = time.perf_counter() - t0
+    elapsed = shard.max_over_ranks(local, dev)
+    rows = shard.gather_floats([local, F * fs], dev)
     ok = bool((st_t == 0).all()) and torch.equal(back, payload)
     line = {"metric": "WS payload mask/unmask GiB/s device-resident, split ops (config 2 layout)",
             "value": round(2.0 * F * fs * world * args.steps / elapsed / GIB, 2), "unit": "GiB/s",
             "n_gpus": world, "steps": args.steps, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "config": {"workload": f"split: {F} binary frames x {fs} B per GPU: encode_headers + "
                                    f"mask_batch, then parse_headers + unmask_batch"},
-            "verified": ok}
+            "per_gpu": per_gpu_rows(rows, args.steps), "verified": ok}
     if rank == 0:
         print(json.dumps(line), flush=True)
     return 0 if ok else 1
+
+
+def per_gpu_rows(rows, steps: int):
+    """Per-rank rates from shard.gather_floats rows [elapsed_s, payload bytes,
+    serialize execute ms, deserialize execute ms, algorithmic bytes per
+    launch]: each GPU's own payload GiB/s over its own timed span and its
+    slower execute against the HBM roofline."""
+    out = []
+    for r, row in enumerate(rows):
+        el, nbytes = row[0], row[1]
+        o = {"rank": r, "GiBps": round(2.0 * nbytes * steps / el / GIB, 2), "payload_bytes": int(nbytes)}
+        if len(row) == 5:
+            ms, alg = max(row[2], row[3]), row[4]
+            o["execute_GBps"] = round(alg / (ms * 1e-3) / 1e9, 1)
+            o["frac"] = round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+        out.append(o)
+    return out
 
 
 def main():
@@ -255,12 +277,15 @@ def main():
         sys.exit(rc)
     flags = 0
     if args.workload == "config3":
-        # each rank: its own 4 GiB Zipf batch (independent seed per rank)
+        # each rank: its byte-balanced share (cut on message boundaries) of
+        # one global Zipf batch of 4 GiB x world; world 1 is
+        # config 3 itself
         c3 = W.CONFIG3
-        desc_np, msgs = W.zipf_batch(c3["target_bytes"], c3["seed"] + rank, c3["key_seed"] + rank)
+        desc_np, msgs, byte_base = shard.zipf_shard(c3["target_bytes"], rank, world, c3["seed"],
+                                                    c3["key_seed"])
         arena_bytes = int(msgs["arena_bytes"])
         payload = torch.empty(W.round16(arena_bytes), dtype=torch.uint8, device=dev)
-        cfws.fill_splitmix(payload, c3["seed"] + rank)
+        cfws.fill_splitmix(payload, c3["seed"], byte_base)
         flags = cfws.DESERIALIZE_REASSEMBLE
         F = len(desc_np)
     elif args.workload == "config4":
@@ -314,7 +339,8 @@ def main():
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    elapsed = shard.max_over_ranks(time.perf_counter() - t0, dev)
+    local = time.perf_counter() - t0
+    elapsed = shard.max_over_ranks(local, dev)
 
     # correctness of what was timed: unmask(mask(P)) == P, every frame COMPLETE
     verified = (int(tot_ser.item()) == wire_total and int(tot_de.item()) == arena_bytes
@@ -347,7 +373,8 @@ def main():
     achieved = alg_bytes / (dom_ms * 1e-3) / 1e9
     kernel_symbol = ("xform_kernel<0>" if dom_name == "serialize_execute"   # kModeSer
                      else "xform_kernel<1>")                                 # kModeDeser
-    total_payload = 2.0 * arena_bytes * world * args.steps
+    rows = shard.gather_floats([local, arena_bytes, ser_ms, de_ms, alg_bytes], dev)
+    total_payload = 2.0 * sum(r[1] for r in rows) * args.steps
     line = {
         "metric": METRIC,
         "value": round(total_payload / elapsed / GIB, 2),
@@ -369,8 +396,9 @@ def main():
                          f"64 GiB per GPU), client-mask then server-unmask, device resident"
                          if args.workload == "config4" else
                          f"config3: {F} frames / {len(msgs['len'])} Zipf messages (64 B-1 MiB, "
-                         f"1-8 fragments) per GPU, client-mask then server-unmask with "
-                         f"continuation reassembly, device resident"),
+                         f"1-8 fragments) on rank 0, its byte-balanced share of a 4 GiB x "
+                         f"{world} batch, client-mask then server-unmask with continuation "
+                         f"reassembly, device resident"),
             "frames_per_gpu": F,
             "payload_bytes_per_gpu": arena_bytes,
             "wire_bytes_per_gpu": wire_total,
@@ -388,6 +416,7 @@ def main():
             "avg_launch_ms": round(dom_ms, 4),
         },
         "kernels": kern,
+        "per_gpu": per_gpu_rows(rows, args.steps),
         "copy_ceiling": {"GBps": round(copy_gbps, 1), "frac_of_copy": round(achieved / copy_gbps, 4),
                          "how": "torch.Tensor.copy_ of the 4 GiB payload arena, device to device"},
         "verified": verified,

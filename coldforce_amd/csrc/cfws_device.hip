@@ -1337,12 +1337,19 @@ payload_xor_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
 // for two SDMA copies (tools/pcie_probe2.hip). Each lane writes whole
 // destination-aligned 16-byte chunks (source funnel-shifted into place); the
 // first and last chunk, which the destination may share with other data,
-// byte by byte.
+// byte by byte. The chunk grid starts on a kCopyOutAlign boundary of the
+// destination, so each wave's 64 x 16 B of stores is one aligned 1 KiB span
+// of PCIe writes wherever the caller's destination starts.
+#ifndef CFWS_COPY_OUT_ALIGN
+#define CFWS_COPY_OUT_ALIGN 1024
+#endif
+constexpr uintptr_t kCopyOutAlign = CFWS_COPY_OUT_ALIGN;
+
 __global__ void __launch_bounds__(kThreads)
 copy_out_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, uint64_t n)
 {
     const uintptr_t d0 = reinterpret_cast<uintptr_t>(dst);
-    const uintptr_t c0 = d0 & ~uintptr_t(15);
+    const uintptr_t c0 = d0 & ~(kCopyOutAlign - 1);
     const uint64_t nchunks = (d0 + n - c0 + 15) >> 4;
     const uint32_t ph = (uint32_t)((reinterpret_cast<uintptr_t>(src) - d0) & 15u);
     const uint64_t stride = uint64_t(gridDim.x) * kThreads;
@@ -1949,7 +1956,7 @@ void launch_pass(const WsLayout& L, int p, const void* src, void* dst, const cfw
 int cfws_internal_copy_out(const void* d_src, void* dev_dst, uint64_t n, void* stream)
 {
     if (n == 0) return CFWS_OK;
-    const uint64_t chunks = n / 16 + 2;
+    const uint64_t chunks = (n + kCopyOutAlign) / 16 + 1;
     const uint64_t blocks = (chunks + kThreads - 1) / kThreads;
     copy_out_kernel<<<(uint32_t)(blocks < 1024 ? blocks : 1024), kThreads, 0,
                       static_cast<hipStream_t>(stream)>>>(static_cast<const uint8_t*>(d_src),

@@ -43,6 +43,56 @@ def uniform_shard(frames_per_rank: int, frame_size: int, key_seed: int, rank: in
     return d, first * frame_size
 
 
+def byte_shard_range(msg_off: np.ndarray, total_bytes: int, rank: int,
+                     world_size: int) -> tuple[int, int]:
+    """Contiguous messages [m0, m1) for `rank` when a batch of messages (their
+    payload offsets msg_off, back to back, total_bytes in all) is split by
+    cumulative payload bytes: rank g owns the
+    messages that start in [g*T/G, (g+1)*T/G). Cuts fall on message
+    boundaries, so every continuation sequence stays on one GPU."""
+    lo = total_bytes * rank // world_size
+    hi = total_bytes * (rank + 1) // world_size
+    m0 = int(np.searchsorted(msg_off, np.uint64(lo), side="left"))
+    m1 = int(np.searchsorted(msg_off, np.uint64(hi), side="left"))
+    return m0, m1
+
+
+def zipf_shard(bytes_per_rank: int, rank: int, world_size: int, seed: int, key_seed: int):
+    """The rank's byte-balanced share of one global config-3 batch of
+    bytes_per_rank x world_size payload bytes. Keys are the global random()
+    stream's slice, payload bytes the global arena's, so the union of the
+    shards is the single-process batch (and world_size 1 is config 3
+    itself). Returns (desc with rank-local payload_off, messages with
+    rank-local offsets and frame numbers, payload byte_base of the shard)."""
+    desc, msgs = W.zipf_batch(bytes_per_rank * world_size, seed, key_seed)
+    m0, m1 = byte_shard_range(msgs["off"], msgs["data_bytes"], rank, world_size)
+    n_msg = len(msgs["off"])
+    f0 = int(msgs["first_frame"][m0]) if m0 < n_msg else len(desc)
+    f1 = int(msgs["first_frame"][m1]) if m1 < n_msg else len(desc)
+    base = int(msgs["off"][m0]) if m0 < n_msg else msgs["data_bytes"]
+    end = int(msgs["off"][m1]) if m1 < n_msg else msgs["data_bytes"]
+    d = desc[f0:f1].copy()
+    d["payload_off"] -= np.uint64(base)
+    local = dict(off=msgs["off"][m0:m1] - np.uint64(base), len=msgs["len"][m0:m1],
+                 opcode=msgs["opcode"][m0:m1], first_frame=msgs["first_frame"][m0:m1] - f0,
+                 n_frames=msgs["n_frames"][m0:m1], arena_bytes=end - base,
+                 data_bytes=end - base, pings=0)
+    return d, local, base
+
+
+def gather_floats(values, device=None) -> list[list[float]]:
+    """Every rank's `values` (a few floats: timings, byte counts), rank order.
+    Bookkeeping only; the data path has no collective."""
+    import torch
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()):
+        return [list(map(float, values))]
+    t = torch.tensor(list(values), dtype=torch.float64, device=device)
+    out = [torch.empty_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(out, t)
+    return [[float(x) for x in o.tolist()] for o in out]
+
+
 def max_over_ranks(value: float, device=None) -> float:
     import torch
     import torch.distributed as dist
@@ -63,4 +113,5 @@ def sum_over_ranks(value: float, device=None) -> float:
     return float(t.item())
 
 
-__all__ = ["world", "shard_range", "uniform_shard", "max_over_ranks", "sum_over_ranks", "W"]
+__all__ = ["world", "shard_range", "uniform_shard", "byte_shard_range", "zipf_shard", "gather_floats",
+           "max_over_ranks", "sum_over_ranks", "W"]
