@@ -55,7 +55,11 @@ def e2e_h2(args):
     payload = host_buffer(args, F * fs)
     h2 = host_buffer(args, F * Hf)
     back = host_buffer(args, F * fs)
-    mapped = args.host == "mapped"
+    # D2H by kernel (cfws_copy_to_host) only into mapped memory and only when
+    # --d2h kernel: this harness enqueues every chunk without host
+    # back-pressure, and there SDMA measured faster both ways (serialize 38
+    # vs 33 GiB/s), so its auto is SDMA (the C pipeline's auto differs)
+    ser_kernel = de_kernel = args.host == "mapped" and args.d2h == "kernel"
     dev = torch.empty(F * fs, dtype=torch.uint8, device="cuda")
     cfws.fill_splitmix(dev, 0x5EED0005)
     payload.copy_(dev)
@@ -87,15 +91,33 @@ def e2e_h2(args):
         slot.append((pay_d, wire_d, h2_d, pool_d, back_d, ws_s, ws_d, idx, tot))
     torch.cuda.synchronize()
 
+    # H2D copies go in chunk order on one copy stream, each waiting only for
+    # its slot's previous kernels (the input staging free), as in
+    # cfws_pipeline_*: behind the slot's D2H on its own stream they would
+    # alternate with the D2H bursts instead of overlapping them.
+    st_in = torch.cuda.Stream()
+    ev_in = [torch.cuda.Event() for _ in range(args.depth)]
+    ev_exec = [torch.cuda.Event() for _ in range(args.depth)]
+    for s in range(args.depth):
+        ev_exec[s].record(streams[s])
+
+    def to_device(dst, src, s):
+        st_in.wait_event(ev_exec[s])
+        with torch.cuda.stream(st_in):
+            dst.copy_(src, non_blocking=True)
+        ev_in[s].record(st_in)
+
     def ser():
         for c, (c0, c1) in enumerate(chunks):
             s = c % args.depth
             st = streams[s]
             pay_d, wire_d, h2_d, _, _, ws_s, _, _, tot = slot[s]
+            to_device(pay_d[:(c1 - c0) * fs], payload[c0 * fs:c1 * fs], s)
+            st.wait_event(ev_in[s])
             with torch.cuda.stream(st):
-                pay_d[:(c1 - c0) * fs].copy_(payload[c0 * fs:c1 * fs], non_blocking=True)
                 cfws.h2_serialize(pay_d, descs[c], wire_d, h2_d, 1, S, ws_s, tot, stream=st)
-                if mapped:
+                ev_exec[s].record(st)
+                if ser_kernel:
                     cfws.copy_to_host(h2_d, h2[c0 * Hf:].data_ptr(), (c1 - c0) * Hf, stream=st)
                 else:
                     h2[c0 * Hf:c1 * Hf].copy_(h2_d[:(c1 - c0) * Hf], non_blocking=True)
@@ -103,16 +125,28 @@ def e2e_h2(args):
 
     def de():
         ok = True
+
+        def fetch(c):
+            c0, c1 = chunks[c]
+            to_device(slot[c % args.depth][2][:(c1 - c0) * Hf], h2[c0 * Hf:c1 * Hf], c % args.depth)
+
+        # h2_deserialize synchronises its stream (message count): the next
+        # depth - 1 chunks' H2D are queued before each call
+        for c in range(min(args.depth - 1, len(chunks))):
+            fetch(c)
         for c, (c0, c1) in enumerate(chunks):
+            if c + args.depth - 1 < len(chunks):
+                fetch(c + args.depth - 1)
             s = c % args.depth
             st = streams[s]
             _, _, h2_d, pool_d, back_d, _, ws_d, idx, _ = slot[s]
             n = c1 - c0
+            st.wait_event(ev_in[s])
             with torch.cuda.stream(st):
-                h2_d[:n * Hf].copy_(h2[c0 * Hf:c1 * Hf], non_blocking=True)
                 hs_, md, ms, ptot, m = cfws.h2_deserialize(h2_d, n * Hf, idx[:n * k], pool_d, back_d,
                                                            S, align=1, ws_t=ws_d, stream=st)
-                if mapped:
+                ev_exec[s].record(st)
+                if de_kernel:
                     cfws.copy_to_host(back_d, back[c0 * fs:].data_ptr(), n * fs, stream=st)
                 else:
                     back[c0 * fs:c1 * fs].copy_(back_d[:n * fs], non_blocking=True)
@@ -138,7 +172,7 @@ def e2e_h2(args):
             "serialize_s": round(t_ser, 4), "deserialize_s": round(t_de, 4),
             "serialize_GiBps": round(nbytes / t_ser / GIB, 2),
             "deserialize_GiBps": round(nbytes / t_de / GIB, 2),
-            "round_trip_GiBps": round(2 * nbytes / (t_ser + t_de) / GIB, 2), "host": args.host,
+            "round_trip_GiBps": round(2 * nbytes / (t_ser + t_de) / GIB, 2), "host": args.host, "d2h": args.d2h,
             "verified": ok}
     print(json.dumps(line), flush=True)
     return 0 if ok else 1
@@ -152,9 +186,12 @@ def main():
     ap.add_argument("--chunk-mib", type=int, default=64)
     ap.add_argument("--depth", type=int, default=3)
     ap.add_argument("--reps", type=int, default=7)
+    ap.add_argument("--d2h", choices=["auto", "dma", "kernel"], default="auto",
+                    help="the pipeline's D2H mode into mapped arenas (cfws_pipeline_set_d2h): "
+                         "auto = kernel for serialize, SDMA for deserialize")
     ap.add_argument("--host", choices=["mapped", "torch"], default="mapped",
                     help="host arenas: mapped pinned memory (hipHostMallocMapped; the D2H leg "
-                         "is a kernel writing it, cfws_copy_to_host) or torch pinned memory "
+                         "may be a kernel writing it, cfws_copy_to_host) or torch pinned memory "
                          "(the D2H leg is an SDMA copy)")
     args = ap.parse_args()
 
@@ -195,7 +232,8 @@ def main():
     torch.cuda.synchronize()
     h2d = args.reps * nbytes / (time.perf_counter() - t0) / 1e9
 
-    pl = cfws.Pipeline(chunk_bytes=args.chunk_mib << 20, max_frames=1 << 16, depth=args.depth)
+    pl = cfws.Pipeline(chunk_bytes=args.chunk_mib << 20, max_frames=1 << 16, depth=args.depth,
+                       d2h=args.d2h)
     d = desc.copy()
     pl.serialize(payload.data_ptr(), d, wire.data_ptr(), wire.numel())          # warm-up
     ts = []
@@ -235,7 +273,7 @@ def main():
         "round_trip_GiBps": round(2 * nbytes / (t_ser + t_de) / GIB, 2),
         "receive_s": round(t_rx, 4), "receive_GiBps": round(nbytes / t_rx / GIB, 2),
         "timing": f"median of {args.reps} reps after one warm-up",
-        "host": args.host,
+        "host": args.host, "d2h": args.d2h,
         "pinned_h2d_GBps": round(h2d, 1), "pinned_d2h_GBps": round(d2h, 1),
         "verified": ok,
     }

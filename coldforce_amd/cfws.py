@@ -54,6 +54,7 @@ BATCH_SYMBOLS = (
     "cfws_index_frames", "cfws_index_workspace_size", "cfws_index_frames_batch",
     "cfws_ws_accept_keys_batch", "cfws_encode_headers", "cfws_parse_headers",
     "cfws_mask_batch", "cfws_unmask_batch", "cfws_copy_to_host", "cfws_mapped_device_pointer",
+    "cfws_pipeline_set_d2h",
 )
 DROPIN_SYMBOLS = (
     "co_ws_frame_serialize", "co_ws_frame_deserialize", "co_ws_frame_create",
@@ -114,6 +115,7 @@ def lib(path: str = LIB_PATH) -> C.CDLL:
         "cfws_mask_batch": ([_vp, _vp, _sz, _u64, _vp, _u64, _vp], C.c_int),
         "cfws_unmask_batch": ([_vp, _vp, _vp, _sz, _u64, _vp, _u64, _vp], C.c_int),
         "cfws_copy_to_host": ([_vp, _vp, _u64, _vp], C.c_int),
+        "cfws_pipeline_set_d2h": ([_vp, C.c_int], C.c_int),
         "cfws_mapped_device_pointer": ([_vp], _vp),
         "cfws_xor_mask": ([_vp, _vp, _u64, _u32, _u32, _vp], C.c_int),
         "cfws_draw_mask_keys": ([_sz, _vp, _vp], None),
@@ -557,15 +559,25 @@ def ws_accept_keys(keys, device="cuda", stream=None) -> list[str]:
 
 # ---- host-memory pipeline --------------------------------------------------
 
+PIPELINE_D2H = {"auto": 0, "dma": 1, "kernel": 2}     # CFWS_PIPELINE_D2H_*
+
+
 class Pipeline:
     """cfws_pipeline_*: the codec over host buffers (pinned numpy/torch
     memory recommended), H2D / kernels / D2H overlapped across `depth` slots."""
 
-    def __init__(self, chunk_bytes: int = 64 << 20, max_frames: int = 1 << 18, depth: int = 3):
+    def __init__(self, chunk_bytes: int = 64 << 20, max_frames: int = 1 << 18, depth: int = 3,
+                 d2h: str | None = None):
         h = C.c_void_p()
         _check(lib().cfws_pipeline_create(chunk_bytes, max_frames, depth, C.byref(h)),
                "cfws_pipeline_create")
         self.h = h
+        if d2h is not None:
+            self.set_d2h(d2h)
+
+    def set_d2h(self, mode: str) -> None:
+        """'auto' | 'dma' | 'kernel': cfws_pipeline_set_d2h."""
+        _check(lib().cfws_pipeline_set_d2h(self.h, PIPELINE_D2H[mode]), "cfws_pipeline_set_d2h")
 
     def close(self):
         if self.h:

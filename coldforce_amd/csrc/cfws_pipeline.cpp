@@ -6,7 +6,13 @@
 // runs the device batch codec over host buffers: the batch is cut into
 // chunks of frames, and `depth` slots, each with its own stream and device
 // staging, overlap H2D copies, the plan + streaming kernels and D2H copies of
-// consecutive chunks (the two DMA directions run concurrently). The host
+// consecutive chunks (the two DMA directions run concurrently). H2D copies go
+// in chunk order on one copy stream of the pipeline's, each waiting only for
+// its slot's previous execute (the input staging free), never for a D2H: on a
+// slot's own stream the next chunk's H2D would queue behind the slot's D2H,
+// and all slots then alternate between an H2D burst and a D2H burst (half
+// duplex). D2H copies stay on the slot streams (one shared
+// in-order D2H stream measured no faster). The host
 // buffers should be pinned (hipHostMalloc / hipHostRegister) for full PCIe
 // rate. All codec decisions (header encode/decode, layout, status codes) are
 // the device plan's; the host only cuts chunks and rebases offsets.
@@ -40,6 +46,8 @@ struct Slot {
     uint64_t* h_total = nullptr;       // pinned
     hipEvent_t ev_done = nullptr;      // slot free again (its last D2H finished)
     hipEvent_t ev_total = nullptr;     // the chunk's layout total is on the host
+    hipEvent_t ev_in = nullptr;        // the chunk's H2D copies landed (host staging free)
+    hipEvent_t ev_exec = nullptr;      // the chunk's kernels finished (d_in / d_index free)
 };
 
 uint32_t hdr_size(uint64_t n, bool mask)
@@ -54,18 +62,26 @@ int fail(const char* what, hipError_t e = hipSuccess)
     return e == hipSuccess ? CFWS_ERROR_INVALID_ARGUMENT : CFWS_ERROR_HIP;
 }
 
-// Device address of the pipeline's host output when the D2H leg can be a
-// kernel (copy_out_kernel writing mapped pinned memory: 43 GB/s beside the
-// SDMA H2D, against 28 GB/s each way for two SDMA copies).
-// NULL: SDMA copies. CFWS_PIPELINE_D2H=dma forces the copies.
-uint8_t* kernel_d2h_target(void* h_out)
+// Device address of the pipeline's host output when its D2H leg is a kernel
+// (copy_out_kernel storing into mapped pinned memory), NULL for an SDMA copy.
+// Measured per direction with the H2D copies on their own stream (config 2,
+// host to host): serialize 40 GiB/s with the kernel against 22
+// with SDMA; deserialize 44 GiB/s with SDMA against 35 with the kernel. So
+// CFWS_PIPELINE_D2H_AUTO takes the kernel for serialize when its wire arena
+// is mapped and always copies for deserialize.
+uint8_t* kernel_d2h_target(int mode, void* h_out, bool serialize)
 {
-    static int force_dma = -1;
-    if (force_dma < 0) {
-        const char* s = getenv("CFWS_PIPELINE_D2H");
-        force_dma = (s && strcmp(s, "dma") == 0) ? 1 : 0;
-    }
-    return force_dma ? nullptr : static_cast<uint8_t*>(cfws_mapped_device_pointer(h_out));
+    if (mode == CFWS_PIPELINE_D2H_DMA || (mode == CFWS_PIPELINE_D2H_AUTO && !serialize)) return nullptr;
+    return static_cast<uint8_t*>(cfws_mapped_device_pointer(h_out));
+}
+
+// The default mode: CFWS_PIPELINE_D2H=dma | kernel | auto (unset: auto).
+int default_d2h_mode()
+{
+    const char* s = getenv("CFWS_PIPELINE_D2H");
+    if (s && strcmp(s, "dma") == 0) return CFWS_PIPELINE_D2H_DMA;
+    if (s && strcmp(s, "kernel") == 0) return CFWS_PIPELINE_D2H_KERNEL;
+    return CFWS_PIPELINE_D2H_AUTO;
 }
 
 #define CFWS_HIP(call)                                   \
@@ -77,6 +93,8 @@ uint8_t* kernel_d2h_target(void* h_out)
 }  // namespace
 
 struct cfws_pipeline {
+    hipStream_t st_in = nullptr;       // every H2D copy, in chunk order
+    int d2h_mode = CFWS_PIPELINE_D2H_AUTO;
     int depth = 0;
     uint64_t chunk = 0;        // staging bytes per slot and direction
     size_t max_frames = 0;     // frames per chunk
@@ -94,9 +112,14 @@ int cfws_pipeline_create(uint64_t chunk_bytes, size_t max_frames, int depth, cfw
     p->depth = depth;
     p->chunk = (chunk_bytes + 255) & ~uint64_t(255);
     p->max_frames = max_frames;
+    p->d2h_mode = default_d2h_mode();
     // The deserialize output of a chunk can exceed its wire bytes only by
     // the alignment padding; reserve one 4 KiB pad per frame at most.
     const uint64_t out_bytes = p->chunk + 64;
+    if (hipStreamCreateWithFlags(&p->st_in, hipStreamNonBlocking) != hipSuccess) {
+        cfws_pipeline_destroy(p);
+        return fail("pipeline allocation failed");
+    }
     for (int s = 0; s < depth; ++s) {
         Slot& S = p->slot[s];
         S.ws_size = cfws_workspace_size(max_frames, out_bytes);
@@ -111,11 +134,15 @@ int cfws_pipeline_create(uint64_t chunk_bytes, size_t max_frames, int depth, cfw
             hipHostMalloc(&S.h_stage, max_frames * (sizeof(cfws_frame_desc_t) + sizeof(int32_t))) != hipSuccess ||
             hipHostMalloc(reinterpret_cast<void**>(&S.h_total), 64) != hipSuccess ||
             hipEventCreateWithFlags(&S.ev_done, hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&S.ev_total, hipEventDisableTiming) != hipSuccess) {
+            hipEventCreateWithFlags(&S.ev_total, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&S.ev_in, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&S.ev_exec, hipEventDisableTiming) != hipSuccess) {
             cfws_pipeline_destroy(p);
             return fail("pipeline allocation failed");
         }
         (void)hipEventRecord(S.ev_done, S.st);
+        (void)hipEventRecord(S.ev_exec, S.st);
+        (void)hipEventRecord(S.ev_in, p->st_in);
     }
     *out = p;
     return CFWS_OK;
@@ -124,6 +151,7 @@ int cfws_pipeline_create(uint64_t chunk_bytes, size_t max_frames, int depth, cfw
 void cfws_pipeline_destroy(cfws_pipeline_t* p)
 {
     if (!p) return;
+    if (p->st_in) (void)hipStreamSynchronize(p->st_in);
     for (int s = 0; s < kMaxDepth; ++s) {
         Slot& S = p->slot[s];
         if (S.st) (void)hipStreamSynchronize(S.st);
@@ -138,9 +166,19 @@ void cfws_pipeline_destroy(cfws_pipeline_t* p)
         if (S.h_total) (void)hipHostFree(S.h_total);
         if (S.ev_done) (void)hipEventDestroy(S.ev_done);
         if (S.ev_total) (void)hipEventDestroy(S.ev_total);
+        if (S.ev_in) (void)hipEventDestroy(S.ev_in);
+        if (S.ev_exec) (void)hipEventDestroy(S.ev_exec);
         if (S.st) (void)hipStreamDestroy(S.st);
     }
+    if (p->st_in) (void)hipStreamDestroy(p->st_in);
     delete p;
+}
+
+int cfws_pipeline_set_d2h(cfws_pipeline_t* p, int mode)
+{
+    if (!p || mode < CFWS_PIPELINE_D2H_AUTO || mode > CFWS_PIPELINE_D2H_KERNEL) return fail("bad D2H mode");
+    p->d2h_mode = mode;
+    return CFWS_OK;
 }
 
 // co_ws_frame_serialize over a host batch: host payload arena -> host wire
@@ -160,7 +198,7 @@ int cfws_pipeline_serialize(cfws_pipeline_t* p, const void* h_payload, cfws_fram
     if (wire_total) *wire_total = off;
     const uint8_t* src = static_cast<const uint8_t*>(h_payload);
     uint8_t* dst = static_cast<uint8_t*>(h_wire);
-    uint8_t* dst_dev = n ? kernel_d2h_target(h_wire) : nullptr;
+    uint8_t* dst_dev = n ? kernel_d2h_target(p->d2h_mode, h_wire, true) : nullptr;
     size_t i = 0;
     int c = 0;
     while (i < n) {
@@ -184,18 +222,22 @@ int cfws_pipeline_serialize(cfws_pipeline_t* p, const void* h_payload, cfws_fram
         if (hi - src_lo > p->chunk || wire_bytes > p->chunk)
             return fail("a frame is larger than the pipeline chunk");
         Slot& S = p->slot[c % p->depth];
-        CFWS_HIP(hipEventSynchronize(S.ev_done));
+        CFWS_HIP(hipEventSynchronize(S.ev_in));       // the slot's last H2D read the staging
         auto* stage = static_cast<cfws_frame_desc_t*>(S.h_stage);
         for (size_t k = i; k < j; ++k) {
             stage[k - i] = h_desc[k];
             stage[k - i].payload_off -= src_lo;
         }
-        CFWS_HIP(hipMemcpyAsync(S.d_in, src + src_lo, hi - src_lo, hipMemcpyHostToDevice, S.st));
+        CFWS_HIP(hipStreamWaitEvent(p->st_in, S.ev_exec, 0));   // d_in, d_desc free
+        CFWS_HIP(hipMemcpyAsync(S.d_in, src + src_lo, hi - src_lo, hipMemcpyHostToDevice, p->st_in));
         CFWS_HIP(hipMemcpyAsync(S.d_desc, stage, (j - i) * sizeof(cfws_frame_desc_t),
-                                hipMemcpyHostToDevice, S.st));
+                                hipMemcpyHostToDevice, p->st_in));
+        CFWS_HIP(hipEventRecord(S.ev_in, p->st_in));
+        CFWS_HIP(hipStreamWaitEvent(S.st, S.ev_in, 0));
         if (int rc = cfws_serialize_batch(S.d_in, S.d_desc, j - i, S.d_out, p->chunk + 64, S.d_total,
                                           S.d_ws, S.ws_size, S.st))
             return rc;
+        CFWS_HIP(hipEventRecord(S.ev_exec, S.st));
         if (wire_lo < wire_capacity) {
             const uint64_t m = std::min(wire_bytes, wire_capacity - wire_lo);
             if (dst_dev) {
@@ -208,6 +250,7 @@ int cfws_pipeline_serialize(cfws_pipeline_t* p, const void* h_payload, cfws_fram
         i = j;
         ++c;
     }
+    CFWS_HIP(hipStreamSynchronize(p->st_in));
     for (int s = 0; s < p->depth; ++s) CFWS_HIP(hipStreamSynchronize(p->slot[s].st));
     return CFWS_OK;
 }
@@ -232,7 +275,7 @@ int cfws_pipeline_deserialize(cfws_pipeline_t* p, const void* h_wire, uint64_t w
         if (h_index[i] < h_index[i - 1]) return fail("frame index must be increasing");
     const uint8_t* src = static_cast<const uint8_t*>(h_wire);
     uint8_t* dst = static_cast<uint8_t*>(h_payload);
-    uint8_t* dst_dev = n ? kernel_d2h_target(h_payload) : nullptr;
+    uint8_t* dst_dev = n ? kernel_d2h_target(p->d2h_mode, h_payload, false) : nullptr;
 
     struct Chunk { size_t i, j; int slot; uint64_t wire_lo, base; };
     std::vector<Chunk> pend;         // launched; layout total not read yet
@@ -319,10 +362,15 @@ int cfws_pipeline_deserialize(cfws_pipeline_t* p, const void* h_wire, uint64_t w
                 landing.erase(landing.begin(), landing.begin() + q + 1);
                 break;
             }
+        // the staging's last reader, this slot's previous chunk, was finished above
         auto* sidx = static_cast<uint64_t*>(S.h_stage);
         for (size_t k = i; k < j; ++k) sidx[k - i] = h_index[k] - wire_lo;
-        CFWS_HIP(hipMemcpyAsync(S.d_in, src + wire_lo, hi - wire_lo, hipMemcpyHostToDevice, S.st));
-        CFWS_HIP(hipMemcpyAsync(S.d_index, sidx, (j - i) * sizeof(uint64_t), hipMemcpyHostToDevice, S.st));
+        CFWS_HIP(hipStreamWaitEvent(p->st_in, S.ev_exec, 0));   // d_in, d_index free
+        CFWS_HIP(hipMemcpyAsync(S.d_in, src + wire_lo, hi - wire_lo, hipMemcpyHostToDevice, p->st_in));
+        CFWS_HIP(hipMemcpyAsync(S.d_index, sidx, (j - i) * sizeof(uint64_t), hipMemcpyHostToDevice,
+                                p->st_in));
+        CFWS_HIP(hipEventRecord(S.ev_in, p->st_in));
+        CFWS_HIP(hipStreamWaitEvent(S.st, S.ev_in, 0));
         // The capacity rule needs this chunk's payload base: everything laid
         // out before it must be known (settle all pending chunks first).
         if (int rc = settle_all()) return rc;
@@ -333,6 +381,7 @@ int cfws_pipeline_deserialize(cfws_pipeline_t* p, const void* h_wire, uint64_t w
                                             align, 0, S.d_desc, S.d_status, S.d_out, cap,
                                             S.d_total, S.d_ws, S.ws_size, S.st))
             return rc;
+        CFWS_HIP(hipEventRecord(S.ev_exec, S.st));
         // the unclamped layout total: offsets keep counting past the capacity
         CFWS_HIP(hipMemcpyAsync(S.h_total,
                                 static_cast<char*>(S.d_ws) + cfws_internal_grand_total_offset(), 8,

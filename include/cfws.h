@@ -304,11 +304,22 @@ int cfws_pipeline_receive(cfws_pipeline_t* pipeline, const void* h_wire, uint64_
                           uint64_t* consumed, int32_t* stop, void* h_payload,
                           uint64_t payload_capacity, uint64_t* payload_total);
 
+/* How the pipeline's D2H leg moves bytes into a MAPPED host output arena
+ * (hipHostMalloc(..., hipHostMallocMapped)); unmapped arenas always take
+ * SDMA. AUTO (the default): a kernel storing into the arena for serialize,
+ * an SDMA copy for deserialize -- each direction's faster choice beside the
+ * in-order H2D copies. DMA: SDMA both ways; KERNEL:
+ * the kernel both ways. The environment variable CFWS_PIPELINE_D2H = auto |
+ * dma | kernel sets the default of new pipelines. */
+#define CFWS_PIPELINE_D2H_AUTO   0
+#define CFWS_PIPELINE_D2H_DMA    1
+#define CFWS_PIPELINE_D2H_KERNEL 2
+int cfws_pipeline_set_d2h(cfws_pipeline_t* pipeline, int mode);
+
 /* D2H by a kernel: copies d_src[0, n) to h_dst, a host buffer allocated (or
  * registered) MAPPED (hipHostMalloc(..., hipHostMallocMapped)), by 16-byte
- * stores over PCIe. Beside an SDMA H2D this direction runs at 43 GB/s where a
- * second SDMA copy gets 28; the pipeline uses it by itself
- * when its destination is mapped. CFWS_ERROR_INVALID_ARGUMENT when h_dst is
+ * stores over PCIe: the pipeline's D2H leg in CFWS_PIPELINE_D2H_KERNEL mode
+ * (and serialize's in AUTO). CFWS_ERROR_INVALID_ARGUMENT when h_dst is
  * not mapped memory. cfws_mapped_device_pointer: h_ptr's device address when
  * it is mapped HIP host memory, else NULL. */
 int cfws_copy_to_host(const void* d_src, void* h_dst, uint64_t n, void* stream);

@@ -18,7 +18,7 @@ from coldforce_amd import cfws  # noqa: E402
 from coldforce_amd import workloads as W  # noqa: E402
 
 
-HOST = {"kind": "torch"}
+HOST = {"kind": "torch", "d2h": None}
 
 
 def pinned(n: int):
@@ -38,11 +38,19 @@ def device():
     cfws.init()
 
 
-@pytest.fixture(autouse=True, params=["torch", "mapped"])
+@pytest.fixture(autouse=True, params=["torch", "mapped", "mapped-kernel", "mapped-dma"])
 def host_kind(request):
-    HOST["kind"] = request.param
-    yield request.param
-    HOST["kind"] = "torch"
+    """Host arenas x the pipeline's D2H mode: torch pinned memory (SDMA
+    whatever the mode), mapped memory with the default mode (serialize by
+    kernel, deserialize by SDMA) and with each direction forced."""
+    kind, _, d2h = request.param.partition("-")
+    HOST["kind"], HOST["d2h"] = kind, d2h or None
+    yield kind
+    HOST["kind"], HOST["d2h"] = "torch", None
+
+
+def make_pipeline(**kw):
+    return cfws.Pipeline(d2h=HOST["d2h"], **kw)
 
 
 def test_copy_to_host_any_alignment():
@@ -79,7 +87,7 @@ def test_pipeline_serialize_matches_oracle(chunk, depth):
         off = min(off + sz, payload.size - 70000)
     exp, exp_d = O.serialize_batch(payload, d.view(O.DESC_DTYPE))
     wire_t, wire = pinned(len(exp) + 64)
-    p = cfws.Pipeline(chunk_bytes=chunk, max_frames=512, depth=depth)
+    p = make_pipeline(chunk_bytes=chunk, max_frames=512, depth=depth)
     tot = p.serialize(payload_t.data_ptr(), d, wire_t.data_ptr(), wire.size)
     p.close()
     assert tot == len(exp)
@@ -100,7 +108,7 @@ def test_pipeline_deserialize_matches_oracle(chunk, depth, align):
     wire[:len(raw)] = np.frombuffer(raw, np.uint8)
     starts, _ = O.index_frames(wire[:len(raw)], 100000)
     starts = np.concatenate([starts, [len(raw) - 1, len(raw)]]).astype(np.uint64)  # truncated tails
-    pl = cfws.Pipeline(chunk_bytes=chunk, max_frames=300, depth=depth)
+    pl = make_pipeline(chunk_bytes=chunk, max_frames=300, depth=depth)
     for cap in (len(raw) + align * len(starts) + 64, len(raw) // 2):
         out_t, out = pinned(cap)
         desc, st, tot = pl.deserialize(wire_t.data_ptr(), len(raw), starts, out_t.data_ptr(), cap,
@@ -125,7 +133,7 @@ def test_pipeline_config2_reduced_digest():
     payload_t, payload = pinned(n * fs)
     payload[:] = O.splitmix_words(g["payload_seed"], 0, n * fs // 8).view(np.uint8)
     wire_t, wire = pinned(g["wire_len"])
-    pl = cfws.Pipeline(chunk_bytes=8 << 20, max_frames=4096, depth=3)
+    pl = make_pipeline(chunk_bytes=8 << 20, max_frames=4096, depth=3)
     tot = pl.serialize(payload_t.data_ptr(), desc, wire_t.data_ptr(), wire.size)
     assert tot == g["wire_len"]
     assert hashlib.sha256(wire[:tot].tobytes()).hexdigest() == g["wire_sha256"]
@@ -157,7 +165,7 @@ def test_pipeline_receive_indexes_then_deserializes(cut):
     e_st, e_con, e_stop = O.index_stream(wire[:len(raw)], 0, len(raw))
     e_out, e_d, e_status, e_tot = O.deserialize_batch(wire[:len(raw)], e_st, align=16)
     out_t, out = pinned(e_tot + 64)
-    pl = cfws.Pipeline(chunk_bytes=1 << 20, max_frames=256, depth=3)
+    pl = make_pipeline(chunk_bytes=1 << 20, max_frames=256, depth=3)
     desc, st, consumed, stop, tot = pl.receive(wire_t.data_ptr(), 0, len(raw), out_t.data_ptr(),
                                                out.size, max_frames=1000)
     pl.close()
