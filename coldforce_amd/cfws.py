@@ -479,7 +479,7 @@ def h2_deserialize(h2_t, h2_size: int, index_t, pool_t, payload_t, S: int = H2_D
     h2_status = torch.empty(n, dtype=torch.int32, device=dev)
     msg_desc = torch.empty((max(n, 1), 32), dtype=torch.uint8, device=dev)
     msg_status = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
-    total = torch.zeros(1, dtype=torch.int64, device=dev)
+    total = torch.empty(1, dtype=torch.int64, device=dev)      # always written by the library
     if ws_t is None:
         ws_t = torch.empty(lib().cfws_h2_deserialize_workspace_size(n, pool_t.numel(), payload_t.numel()),
                            dtype=torch.uint8, device=dev)

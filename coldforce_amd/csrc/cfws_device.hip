@@ -1501,19 +1501,119 @@ h2_finalize_kernel(cfws_frame_desc_t* __restrict__ ddesc, uint64_t* __restrict__
     }
 }
 
+// ---- HTTP/2 send plan in two launches --------------------------------------
+// The WS layout (header sizes, wire offsets: as serialize_plan_*) and the
+// DATA frames each WS frame becomes (co_http2_stream.c:964-1010) from two
+// sums per block, wire bytes W and DATA-frame count K. The apply kernel scans
+// both, writes the WS descriptors' offsets, expands its frames' DATA
+// descriptors, maps their regions and fills the unused descriptor slots: the
+// work of serialize_plan + h2_count + a scan + h2_expand + h2_finalize (seven
+// launches) in two.
+__device__ __forceinline__ uint64_t data_frames_of(uint64_t W, uint64_t S)
+{
+    return W <= S ? 1 : (W + S - 1) / S;
+}
+
+__global__ void __launch_bounds__(kThreads)
+h2_ser_plan_reduce_kernel(cfws_frame_desc_t* __restrict__ desc, uint64_t n, uint64_t S,
+                          uint64_t* __restrict__ partials_w, uint64_t* __restrict__ partials_k)
+{
+    __shared__ uint64_t s_wave[kWaves];
+    const uint64_t f = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
+    uint64_t w = 0, k = 0;
+    if (f < n) {
+        const uint64_t len = desc[f].payload_size;
+        const uint32_t hs = header_size_of(len, desc[f].mask != 0);
+        desc[f].header_size = (uint8_t)hs;
+        w = hs + len;
+        k = data_frames_of(w, S);
+    }
+    uint64_t tw, tk;
+    block_exclusive_scan(w, s_wave, &tw);
+    block_exclusive_scan(k, s_wave, &tk);
+    if (threadIdx.x == 0) {
+        partials_w[blockIdx.x] = tw;
+        partials_k[blockIdx.x] = tk;
+    }
+}
+
+// hdr[0] = DATA-stream bytes clamped by the capacity, hdr[3] = DATA frames;
+// hdr[4] / hdr[5] = the grand sums when a scan launch made them (more than
+// kSelfScanBlocks blocks). DATA frame d of WS frame f: a slice of its wire
+// bytes at 9 d + wire offset (h2_expand_kernel's layout).
+__global__ void __launch_bounds__(kThreads)
+h2_ser_plan_apply_kernel(cfws_frame_desc_t* __restrict__ desc, uint64_t n, uint64_t S,
+                         const uint64_t* __restrict__ partials_w, const uint64_t* __restrict__ partials_k,
+                         uint64_t nb, uint32_t self_scan, uint64_t* __restrict__ hdr, uint64_t capacity,
+                         uint64_t n_max, cfws_frame_desc_t* __restrict__ ddesc,
+                         uint64_t* __restrict__ doffs, uint32_t* __restrict__ map,
+                         uint64_t* __restrict__ user_total)
+{
+    __shared__ uint64_t s_wave[kWaves];
+    uint64_t pre_w, pre_k, gw, gk;
+    if (self_scan) {
+        prefix_from_partials(partials_w, nb, blockIdx.x, s_wave, pre_w, gw);
+        prefix_from_partials(partials_k, nb, blockIdx.x, s_wave, pre_k, gk);
+    } else {
+        pre_w = partials_w[blockIdx.x];
+        pre_k = partials_k[blockIdx.x];
+        gw = hdr[4];
+        gk = hdr[5];
+    }
+    const uint64_t T = gw + 9 * gk;                      // DATA-stream bytes, unclamped
+    const uint64_t total = T < capacity ? T : capacity;
+    const uint64_t f = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
+    uint64_t w = 0, k = 0;
+    if (f < n) {
+        w = desc[f].header_size + desc[f].payload_size;
+        k = data_frames_of(w, S);
+    }
+    uint64_t tot;
+    const uint64_t w0 = block_exclusive_scan(w, s_wave, &tot) + pre_w;
+    const uint64_t d0 = block_exclusive_scan(k, s_wave, &tot) + pre_k;
+    if (f < n) {
+        desc[f].wire_off = w0;
+        for (uint64_t j = 0; j < k; ++j) {
+            const uint64_t d = d0 + j;
+            if (d >= n_max) break;
+            cfws_frame_desc_t e;
+            e.payload_off = w0 + j * S;
+            e.wire_off = 9 * d + e.payload_off;
+            e.payload_size = (j + 1 < k) ? S : w - j * S;
+            e.mask_key = (uint32_t)f;                    // the WS frame (kModeH2Ser)
+            e.fin = (j + 1 == k) ? 1 : 0;
+            e.opcode = 0;
+            e.mask = 0;
+            e.header_size = 9;
+            ddesc[d] = e;
+            doffs[d] = e.wire_off;
+            // DATA frames lie back to back: this one ends where d + 1 starts
+            map_range(e.wire_off, e.wire_off + 9 + e.payload_size, d, total, map);
+        }
+    }
+    // descriptor slots past the DATA frames: empty frames at the end
+    for (uint64_t d = gk + f; d < n_max; d += uint64_t(gridDim.x) * kThreads) {
+        cfws_frame_desc_t e = {};
+        e.wire_off = T;
+        ddesc[d] = e;
+        doffs[d] = T;
+    }
+    if (f == 0) {
+        map[(total + kRegion - 1) / kRegion] = (uint32_t)(n_max - 1);
+        hdr[0] = total;
+        hdr[3] = gk;
+        if (user_total) *user_total = T;
+    }
+}
+
 // HTTP/2 frame header at index[i] (co_http2_frame.c:211-300): MORE_DATA under
 // 9 bytes, PARSE_ERROR when length > max_frame_size, MORE_DATA when the
 // payload is incomplete; DATA payload after the optional pad length byte and
 // without the padding. Non-DATA frames are CFWS_H2_NOT_DATA (no bytes).
-__global__ void __launch_bounds__(kThreads)
-h2_parse_kernel(const uint8_t* __restrict__ h2, uint64_t size, const uint64_t* __restrict__ index,
-                uint64_t n, uint64_t max_frame, cfws_frame_desc_t* __restrict__ desc,
-                int32_t* __restrict__ status, uint64_t* __restrict__ vals)
+__device__ __forceinline__ int32_t parse_h2_frame(const uint8_t* __restrict__ h2, uint64_t size,
+                                                  uint64_t s, uint64_t max_frame, cfws_frame_desc_t& d)
 {
-    const uint64_t i = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
-    if (i >= n) return;
-    const uint64_t s = index[i];
-    cfws_frame_desc_t d = {};
+    d = {};
     d.wire_off = s;
     int32_t st = CFWS_H2_PARSE_COMPLETE;
     do {
@@ -1535,9 +1635,95 @@ h2_parse_kernel(const uint8_t* __restrict__ h2, uint64_t size, const uint64_t* _
         d.header_size = (uint8_t)hs;
         d.payload_size = len - (hs - 9) - pad;
     } while (0);
-    desc[i] = d;
-    status[i] = st;
-    vals[i] = st == CFWS_H2_PARSE_COMPLETE ? d.payload_size : 0;
+    return st;
+}
+
+// ---- HTTP/2 receive plan, fast form: two launches --------------------------
+// Valid when the pool capacity holds every DATA payload (then no frame is
+// OUT_OF_MEMORY and every COMPLETE END_STREAM frame closes a message); the
+// host checks the pooled total afterwards and otherwise runs the general
+// form (h2_parse + scans + finalize + message kernels). Reduce: the DATA
+// headers (co_http2_frame.c:211-300) and per-block sums of pooled bytes and
+// END_STREAM frames.
+__global__ void __launch_bounds__(kThreads)
+h2_de_plan_reduce_kernel(const uint8_t* __restrict__ h2, uint64_t size, const uint64_t* __restrict__ index,
+                         uint64_t n, uint64_t max_frame, cfws_frame_desc_t* __restrict__ desc,
+                         int32_t* __restrict__ status, uint64_t* __restrict__ partials_p,
+                         uint64_t* __restrict__ partials_e)
+{
+    __shared__ uint64_t s_wave[kWaves];
+    const uint64_t i = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
+    uint64_t v = 0, e = 0;
+    if (i < n) {
+        cfws_frame_desc_t d;
+        const int32_t st = parse_h2_frame(h2, size, index[i], max_frame, d);
+        desc[i] = d;
+        status[i] = st;
+        if (st == CFWS_H2_PARSE_COMPLETE) {
+            v = d.payload_size;
+            e = d.fin;
+        }
+    }
+    uint64_t tp, te;
+    block_exclusive_scan(v, s_wave, &tp);
+    block_exclusive_scan(e, s_wave, &te);
+    if (threadIdx.x == 0) {
+        partials_p[blockIdx.x] = tp;
+        partials_e[blockIdx.x] = te;
+    }
+}
+
+// Apply: pool offsets (poffs, desc payload_off), message ids (END_STREAM
+// frames before, co_http2_stream.c:550-608), and per message its pooled
+// span [starts, ends) and first DATA frame. phdr[3] = pooled bytes,
+// *n_msg_p = messages (made by scan_partials2_kernel above kSelfScanBlocks).
+__global__ void __launch_bounds__(kThreads)
+h2_de_plan_apply_kernel(cfws_frame_desc_t* __restrict__ desc, const int32_t* __restrict__ status,
+                        uint64_t n, const uint64_t* __restrict__ partials_p,
+                        const uint64_t* __restrict__ partials_e, uint64_t nb, uint32_t self_scan,
+                        uint64_t* __restrict__ phdr, uint64_t* __restrict__ poffs,
+                        uint64_t* __restrict__ msg_id, uint64_t* __restrict__ n_msg_p,
+                        uint64_t* __restrict__ starts, uint64_t* __restrict__ ends,
+                        uint64_t* __restrict__ first)
+{
+    __shared__ uint64_t s_wave[kWaves];
+    uint64_t pre_p, pre_e, gp, ge;
+    if (self_scan) {
+        prefix_from_partials(partials_p, nb, blockIdx.x, s_wave, pre_p, gp);
+        prefix_from_partials(partials_e, nb, blockIdx.x, s_wave, pre_e, ge);
+    } else {
+        pre_p = partials_p[blockIdx.x];
+        pre_e = partials_e[blockIdx.x];
+        gp = phdr[3];
+        ge = *n_msg_p;
+    }
+    const uint64_t i = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
+    uint64_t v = 0, e = 0;
+    if (i < n && status[i] == CFWS_H2_PARSE_COMPLETE) {
+        v = desc[i].payload_size;
+        e = desc[i].fin;
+    }
+    uint64_t tot;
+    const uint64_t off = block_exclusive_scan(v, s_wave, &tot) + pre_p;
+    const uint64_t m = block_exclusive_scan(e, s_wave, &tot) + pre_e;
+    if (i < n) {
+        poffs[i] = off;
+        desc[i].payload_off = off;
+        msg_id[i] = m;
+        if (e) {                      // closes message m; m + 1 starts after it
+            ends[m] = off + v;
+            if (m + 1 < n) {
+                starts[m + 1] = off + v;
+                first[m + 1] = i + 1;
+            }
+        }
+    }
+    if (i == 0) {
+        starts[0] = 0;
+        first[0] = 0;
+        phdr[3] = gp;
+        *n_msg_p = ge;
+    }
 }
 
 // A WS message = the pooled payloads of DATA frames up to and including one
@@ -1580,46 +1766,55 @@ h2_starts_kernel(const uint64_t* __restrict__ ends, const uint64_t* __restrict__
 // unmasks each DATA frame's slice of its message's WS payload directly from
 // the HTTP/2 arena (one streaming pass instead of pool + deserialize).
 
-// DATA frame holding pool byte p (p < pool total): the last d with poff[d] <= p.
-__device__ __forceinline__ uint64_t pool_frame(const uint64_t* __restrict__ poff, uint64_t n, uint64_t p)
-{
-    uint64_t lo = 0, hi = n;             // first d with poff[d] > p, minus one
-    while (lo < hi) {
-        const uint64_t mid = (lo + hi) >> 1;
-        if (poff[mid] <= p) lo = mid + 1; else hi = mid;
-    }
-    return lo - 1;
-}
-
 // co_ws_frame_deserialize on each pooled message [starts[m], ends[m])
 // (co_ws_http2_extension.c:134-164), header bytes gathered from the DATA
 // frames; same outputs as deserialize_parse_kernel on the pool.
+// first[m]: message m's first DATA frame (h2_de_plan_apply_kernel: the
+// frame after the previous END_STREAM). partials: per-block sums of vals for
+// deserialize_plan_apply_kernel (plan blocks).
 __global__ void __launch_bounds__(kThreads)
 h2_msg_parse_kernel(const uint8_t* __restrict__ h2, const cfws_frame_desc_t* __restrict__ pdesc,
                     const int32_t* __restrict__ h2_status, const uint64_t* __restrict__ poff,
                     uint64_t n_h2, const uint64_t* __restrict__ starts,
                     const uint64_t* __restrict__ ends, uint64_t n_msg, uint64_t max_payload,
                     uint64_t align, cfws_frame_desc_t* __restrict__ mdesc,
-                    int32_t* __restrict__ mstatus, uint64_t* __restrict__ vals)
+                    int32_t* __restrict__ mstatus, uint64_t* __restrict__ vals,
+                    const uint64_t* __restrict__ first, uint64_t* __restrict__ partials)
 {
+    __shared__ uint64_t s_wave[kWaves];
     const uint64_t m = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
-    if (m >= n_msg) return;
-    const uint64_t s = starts[m], len = ends[m] - s;
-    uint8_t hb[16];
-    const uint32_t k = len < 14 ? (uint32_t)len : 14u;
-    uint64_t d = k ? pool_frame(poff, n_h2, s) : 0;
-    for (uint32_t i = 0; i < k; ++i) {
-        const uint64_t p = s + i;
-        while (p >= poff[d] + (h2_status[d] == CFWS_H2_PARSE_COMPLETE ? pdesc[d].payload_size : 0)) ++d;
-        hb[i] = h2[pdesc[d].wire_off + pdesc[d].header_size + (p - poff[d])];
+    uint64_t v = 0;
+    if (m < n_msg) {
+        const uint64_t s = starts[m], len = ends[m] - s;
+        uint8_t hb[16];
+        const uint32_t k = len < 14 ? (uint32_t)len : 14u;
+        uint64_t d = first[m];
+        const uint64_t l0 = h2_status[d] == CFWS_H2_PARSE_COMPLETE ? pdesc[d].payload_size : 0;
+        if (s + k <= poff[d] + l0) {
+            // the whole header in the first DATA frame (every frame of >= 14
+            // bytes): one base, independent byte loads
+            const uint8_t* b = h2 + pdesc[d].wire_off + pdesc[d].header_size + (s - poff[d]);
+            for (uint32_t i = 0; i < k; ++i) hb[i] = b[i];
+        } else {
+            for (uint32_t i = 0; i < k; ++i) {
+                const uint64_t p = s + i;
+                while (p >= poff[d] + (h2_status[d] == CFWS_H2_PARSE_COMPLETE ? pdesc[d].payload_size : 0))
+                    ++d;
+                hb[i] = h2[pdesc[d].wire_off + pdesc[d].header_size + (p - poff[d])];
+            }
+        }
+        cfws_frame_desc_t dd;
+        const int32_t st = parse_ws_header(hb, len, 0, max_payload, dd);
+        dd.wire_off = s;
+        mdesc[m] = dd;
+        mstatus[m] = st;
+        const uint64_t pl = st == CFWS_PARSE_COMPLETE ? dd.payload_size : 0;
+        v = (pl + align - 1) & ~(align - 1);
+        vals[m] = v;
     }
-    cfws_frame_desc_t dd;
-    const int32_t st = parse_ws_header(hb, len, 0, max_payload, dd);
-    dd.wire_off = s;
-    mdesc[m] = dd;
-    mstatus[m] = st;
-    const uint64_t pl = st == CFWS_PARSE_COMPLETE ? dd.payload_size : 0;
-    vals[m] = (pl + align - 1) & ~(align - 1);
+    uint64_t tot;
+    block_exclusive_scan(v, s_wave, &tot);
+    if (threadIdx.x == 0) partials[blockIdx.x] = tot;
 }
 
 // One unit per DATA frame: the part of its pooled bytes that is WS payload
@@ -1629,18 +1824,17 @@ h2_msg_parse_kernel(const uint8_t* __restrict__ h2, const cfws_frame_desc_t* __r
 // any message, or of a message whose frame did not parse COMPLETE, are
 // empty units at the matching layout position (offsets stay monotone and
 // the pass zero-fills what the layout does not cover).
-__global__ void __launch_bounds__(kThreads)
-h2_units_kernel(const cfws_frame_desc_t* __restrict__ pdesc, const int32_t* __restrict__ h2_status,
-                const uint64_t* __restrict__ poff, const uint64_t* __restrict__ msg_id, uint64_t n,
-                uint64_t n_msg, const uint64_t* __restrict__ starts,
-                const cfws_frame_desc_t* __restrict__ mdesc, const int32_t* __restrict__ mstatus,
-                const uint64_t* __restrict__ hdr, cfws_frame_desc_t* __restrict__ udesc,
-                int32_t* __restrict__ ustatus, uint64_t* __restrict__ uoffs)
+__device__ __forceinline__ uint64_t h2_unit(const cfws_frame_desc_t* __restrict__ pdesc,
+                                            const int32_t* __restrict__ h2_status,
+                                            const uint64_t* __restrict__ poff,
+                                            const uint64_t* __restrict__ msg_id, uint64_t d,
+                                            uint64_t n_msg, const uint64_t* __restrict__ starts,
+                                            const cfws_frame_desc_t* __restrict__ mdesc,
+                                            const int32_t* __restrict__ mstatus,
+                                            const uint64_t* __restrict__ hdr, cfws_frame_desc_t& u)
 {
-    const uint64_t d = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
-    if (d >= n) return;
     const uint64_t m = msg_id[d];
-    cfws_frame_desc_t u = {};
+    u = {};
     uint64_t out = hdr[3];                             // past the last message
     if (m < n_msg) {
         const cfws_frame_desc_t M = mdesc[m];
@@ -1664,19 +1858,35 @@ h2_units_kernel(const cfws_frame_desc_t* __restrict__ pdesc, const int32_t* __re
                                                              (uint32_t)(qa & 3u)) : 0u;
         }
     }
-    udesc[d] = u;
-    ustatus[d] = CFWS_PARSE_COMPLETE;
-    uoffs[d] = out;
+    return out;
 }
 
+// One thread per DATA frame: its unit, and the region map of the payload
+// pass (a unit ends where unit d + 1 starts, computed here too, so no
+// second launch reads uoffs).
 __global__ void __launch_bounds__(kThreads)
-h2_unit_map_kernel(const uint64_t* __restrict__ uoffs, uint64_t n, const uint64_t* __restrict__ hdr,
-                   uint32_t* __restrict__ map)
+h2_units_kernel(const cfws_frame_desc_t* __restrict__ pdesc, const int32_t* __restrict__ h2_status,
+                const uint64_t* __restrict__ poff, const uint64_t* __restrict__ msg_id, uint64_t n,
+                uint64_t n_msg, const uint64_t* __restrict__ starts,
+                const cfws_frame_desc_t* __restrict__ mdesc, const int32_t* __restrict__ mstatus,
+                const uint64_t* __restrict__ hdr, cfws_frame_desc_t* __restrict__ udesc,
+                int32_t* __restrict__ ustatus, uint64_t* __restrict__ uoffs, uint32_t* __restrict__ map)
 {
     const uint64_t d = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
     if (d >= n) return;
-    map_regions(uoffs, d, n, hdr[3], hdr[0], map);
+    cfws_frame_desc_t u, u1;
+    const uint64_t lo = h2_unit(pdesc, h2_status, poff, msg_id, d, n_msg, starts, mdesc, mstatus, hdr, u);
+    const uint64_t hi = d + 1 < n ? h2_unit(pdesc, h2_status, poff, msg_id, d + 1, n_msg, starts, mdesc,
+                                            mstatus, hdr, u1)
+                                  : hdr[3];
+    udesc[d] = u;
+    ustatus[d] = CFWS_PARSE_COMPLETE;
+    uoffs[d] = lo;
+    const uint64_t total = hdr[0];
+    map_range(lo, hi, d, total, map);
+    if (d == n - 1) map[(total + kRegion - 1) / kRegion] = (uint32_t)(n - 1);
 }
+
 
 // ---------------------------------------------------------------------------
 // handshake accept keys (co_ws_create_base64_accept_key,
@@ -1929,6 +2139,9 @@ void launch_streaming(const void* src, void* dst, const cfws_frame_desc_t* desc,
     xform_kernel<kMode><<<eb + stream_grid(regions), kThreads, xform_lds_bytes(), st>>>(
         static_cast<const uint8_t*>(src), static_cast<uint8_t*>(dst), desc, status, offs, map,
         total_p, base_p, cap, (uint32_t)n, klass, sid, parent, eb);
+    // (a separate edge launch on a second stream, overlapping the streaming
+    // kernel, measured no faster on config 5: the stream slowed by what the
+    // overlap saved)
     if (split) edge_kernel<kMode><<<grid_for(2 * (uint64_t)n, kEdgeThreads), kEdgeThreads, 0, st>>>(
         static_cast<const uint8_t*>(src), static_cast<uint8_t*>(dst), desc, status, offs,
         total_p, base_p, cap, (uint32_t)n, klass, sid, parent);
@@ -2148,6 +2361,7 @@ struct H2DeLayout {
     uint64_t es_part;
     uint64_t es_total;   // u64: message count
     uint64_t starts, ends;   // u64[n_h2]
+    uint64_t first;      // u64[n_h2]: a message's first DATA frame
     uint64_t wsd;        // WS deserialize workspace
     uint64_t udesc;      // cfws_frame_desc_t[n_h2]: fused payload-pass units
     uint64_t ustatus;    // int32[n_h2]
@@ -2165,6 +2379,7 @@ H2DeLayout h2_de_layout(uint64_t n, uint64_t pool_cap, uint64_t payload_cap)
     L.es_total = at; at += 256;
     L.starts = at; at = align_up(at + 8 * n, 256);
     L.ends = at; at = align_up(at + 8 * n, 256);
+    L.first = at; at = align_up(at + 8 * n, 256);
     L.wsd = at; at = align_up(at + ws_layout(n, payload_cap).bytes, 256);
     L.udesc = at; at = align_up(at + sizeof(cfws_frame_desc_t) * n, 256);
     L.ustatus = at; at = align_up(at + 4 * n, 256);
@@ -2206,24 +2421,35 @@ int cfws_h2_serialize_batch(const void* d_payload, cfws_frame_desc_t* d_desc, si
     //    smaller limits write the WS wire first and wrap it (two passes).
     const bool fused = S >= 64;
     const WsLayout WL = ws_layout(n, wire_cap);
-    if (fused) {
-        if (int rc = cfws_serialize_plan(d_desc, n, wire_cap, nullptr, ws, WL.bytes, stream)) return rc;
-    } else if (int rc = cfws_serialize_batch(d_payload, d_desc, n, d_wire, wire_cap, nullptr, ws,
-                                             WL.bytes, stream)) {
-        return rc;
-    }
-    // 2. their DATA frames
     uint64_t* hdr = ws_ptr<uint64_t>(ws, L.hdr);
-    uint64_t* vals = ws_ptr<uint64_t>(ws, L.vals);
     cfws_frame_desc_t* ddesc = ws_ptr<cfws_frame_desc_t>(ws, L.ddesc);
     uint64_t* doffs = ws_ptr<uint64_t>(ws, L.doffs);
     uint32_t* map = ws_ptr<uint32_t>(ws, L.map);
-    h2_count_kernel<<<grid_for(n, kThreads), kThreads, 0, st>>>(d_desc, n, S, vals);
-    if (int rc = run_scan(vals, n, ws_ptr<uint64_t>(ws, L.partials), hdr + 3, st)) return rc;
-    h2_expand_kernel<<<grid_for(n, kThreads), kThreads, 0, st>>>(d_desc, vals, n, S, L.n_max, ddesc, doffs);
-    h2_finalize_kernel<<<grid_for(L.n_max, kThreads), kThreads, 0, st>>>(
-        ddesc, doffs, L.n_max, hdr + 3, ws_ptr<const uint64_t>(ws, WL.hdr + 24), h2_cap, map, hdr,
-        d_h2_total);
+    if (fused) {
+        // WS layout + DATA frames + region map in two launches (three above
+        // kSelfScanBlocks blocks)
+        const uint32_t nb = grid_for(n, kPlanBlock);
+        const uint32_t self_scan = nb <= kSelfScanBlocks ? 1u : 0u;
+        uint64_t* pw = ws_ptr<uint64_t>(ws, WL.partials[0]);
+        uint64_t* pk = ws_ptr<uint64_t>(ws, WL.partials[1]);
+        h2_ser_plan_reduce_kernel<<<nb, kThreads, 0, st>>>(d_desc, n, S, pw, pk);
+        if (!self_scan) scan_partials2_kernel<<<2, kThreads, 0, st>>>(pw, pk, nb, hdr + 4, hdr + 5);
+        h2_ser_plan_apply_kernel<<<nb, kThreads, 0, st>>>(d_desc, n, S, pw, pk, nb, self_scan, hdr,
+                                                         h2_cap, L.n_max, ddesc, doffs, map, d_h2_total);
+    } else {
+        if (int rc = cfws_serialize_batch(d_payload, d_desc, n, d_wire, wire_cap, nullptr, ws, WL.bytes,
+                                          stream))
+            return rc;
+        // 2. their DATA frames
+        uint64_t* vals = ws_ptr<uint64_t>(ws, L.vals);
+        h2_count_kernel<<<grid_for(n, kThreads), kThreads, 0, st>>>(d_desc, n, S, vals);
+        if (int rc = run_scan(vals, n, ws_ptr<uint64_t>(ws, L.partials), hdr + 3, st)) return rc;
+        h2_expand_kernel<<<grid_for(n, kThreads), kThreads, 0, st>>>(d_desc, vals, n, S, L.n_max, ddesc,
+                                                                      doffs);
+        h2_finalize_kernel<<<grid_for(L.n_max, kThreads), kThreads, 0, st>>>(
+            ddesc, doffs, L.n_max, hdr + 3, ws_ptr<const uint64_t>(ws, WL.hdr + 24), h2_cap, map, hdr,
+            d_h2_total);
+    }
     // 3. the DATA frames: 9-byte header + slice, one streaming pass
     if (h2_cap && fused)
         launch_streaming<kModeH2Ser>(d_payload, d_h2, ddesc, nullptr, doffs, map, hdr, nullptr,
@@ -2253,72 +2479,97 @@ int cfws_h2_deserialize_batch(const void* d_h2, uint64_t h2_size, const uint64_t
     }
     if (!d_h2 || !d_h2_index || !d_h2_status || !d_pool || !d_msg_desc || !d_msg_status || !d_payload)
         return set_err(CFWS_ERROR_INVALID_ARGUMENT, "null pointer", hipSuccess);
-    // 1. unwrap: DATA payloads pooled back to back (a prefix-strip pass)
+    // 1. unwrap: DATA payloads pooled back to back (a prefix-strip pass).
+    //    The plan's fast form assumes the pool capacity holds them all.
     const WsLayout PL = ws_layout(n, pool_cap);
     void* pws = ws_ptr<void>(ws, L.pool);
     uint64_t* phdr = ws_ptr<uint64_t>(pws, PL.hdr);
     uint64_t* poffs = ws_ptr<uint64_t>(pws, PL.offs[0]);
     cfws_frame_desc_t* pdesc = ws_ptr<cfws_frame_desc_t>(ws, L.pdesc);
-    h2_parse_kernel<<<grid_for(n, kThreads), kThreads, 0, st>>>(
-        static_cast<const uint8_t*>(d_h2), h2_size, d_h2_index, n, S, pdesc, d_h2_status, poffs);
-    if (int rc = run_scan(poffs, n, ws_ptr<uint64_t>(pws, PL.partials[0]), phdr + 3, st)) return rc;
-    deserialize_finalize_kernel<<<grid_for(n, kThreads), kThreads, 0, st>>>(
-        pdesc, d_h2_status, poffs, poffs, phdr, n, pool_cap, 0, ws_ptr<uint32_t>(pws, PL.map[0]),
-        ws_ptr<uint32_t>(pws, PL.map[1]), nullptr);
-    // 2. messages: END_STREAM closes one (co_http2_stream.c:550-608)
     uint64_t* es = ws_ptr<uint64_t>(ws, L.es);
     uint64_t* n_msg_d = ws_ptr<uint64_t>(ws, L.es_total);
     uint64_t* starts = ws_ptr<uint64_t>(ws, L.starts);
     uint64_t* ends = ws_ptr<uint64_t>(ws, L.ends);
-    h2_end_flags_kernel<<<grid_for(n, kThreads), kThreads, 0, st>>>(pdesc, d_h2_status, n, es);
-    if (int rc = run_scan(es, n, ws_ptr<uint64_t>(ws, L.es_part), n_msg_d, st)) return rc;
-    h2_messages_kernel<<<grid_for(n, kThreads), kThreads, 0, st>>>(pdesc, d_h2_status, es, n, ends);
-    h2_starts_kernel<<<grid_for(n, kThreads), kThreads, 0, st>>>(ends, n_msg_d, n, starts);
+    uint64_t* first = ws_ptr<uint64_t>(ws, L.first);
+    const uint8_t* h2 = static_cast<const uint8_t*>(d_h2);
+    {
+        const uint32_t nb = grid_for(n, kPlanBlock);
+        const uint32_t self_scan = nb <= kSelfScanBlocks ? 1u : 0u;
+        uint64_t* pp = ws_ptr<uint64_t>(pws, PL.partials[0]);
+        uint64_t* pe = ws_ptr<uint64_t>(pws, PL.partials[1]);
+        h2_de_plan_reduce_kernel<<<nb, kThreads, 0, st>>>(h2, h2_size, d_h2_index, n, S, pdesc,
+                                                          d_h2_status, pp, pe);
+        if (!self_scan) scan_partials2_kernel<<<2, kThreads, 0, st>>>(pp, pe, nb, phdr + 3, n_msg_d);
+        h2_de_plan_apply_kernel<<<nb, kThreads, 0, st>>>(pdesc, d_h2_status, n, pp, pe, nb, self_scan,
+                                                         phdr, poffs, es, n_msg_d, starts, ends, first);
+    }
     uint64_t counts[2] = {0, 0};       // messages, pooled bytes
-    hipError_t e = hipMemcpyAsync(&counts[0], n_msg_d, 8, hipMemcpyDeviceToHost, st);
-    if (e == hipSuccess) e = hipMemcpyAsync(&counts[1], phdr + 3, 8, hipMemcpyDeviceToHost, st);
-    if (e == hipSuccess) e = hipStreamSynchronize(st);
-    if (e != hipSuccess) return set_err(CFWS_ERROR_HIP, "h2_deserialize message count", e);
-    const uint64_t n_msg = counts[0];
-    if (n_messages) *n_messages = (size_t)n_msg;
+    auto read_counts = [&]() -> int {
+        hipError_t e = hipMemcpyAsync(&counts[0], n_msg_d, 8, hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess) e = hipMemcpyAsync(&counts[1], phdr + 3, 8, hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess) e = hipStreamSynchronize(st);
+        if (e != hipSuccess) return set_err(CFWS_ERROR_HIP, "h2_deserialize message count", e);
+        return CFWS_OK;
+    };
+    if (int rc = read_counts()) return rc;
     void* wsd = ws_ptr<void>(ws, L.wsd);
     const WsLayout WL = ws_layout(n, payload_cap);
-    // 3. each pooled message through co_ws_frame_deserialize, against its
-    //    own size (co_ws_http2_extension.c:134-164)
     if (counts[1] > pool_cap) {
-        // the pool capacity cuts DATA payloads: materialise the pool
-        // (layout-first OOM rule) and deserialize from it
+        // 2'. general form: the pool capacity cuts DATA payloads, and a frame
+        //     past it is OUT_OF_MEMORY and closes no message. Pool offsets
+        //     and the grand total stand; the capacity rule, END_STREAM flags
+        //     and messages are redone (co_http2_stream.c:550-608).
+        deserialize_finalize_kernel<<<grid_for(n, kThreads), kThreads, 0, st>>>(
+            pdesc, d_h2_status, poffs, poffs, phdr, n, pool_cap, 0, ws_ptr<uint32_t>(pws, PL.map[0]),
+            ws_ptr<uint32_t>(pws, PL.map[1]), nullptr);
+        h2_end_flags_kernel<<<grid_for(n, kThreads), kThreads, 0, st>>>(pdesc, d_h2_status, n, es);
+        if (int rc = run_scan(es, n, ws_ptr<uint64_t>(ws, L.es_part), n_msg_d, st)) return rc;
+        h2_messages_kernel<<<grid_for(n, kThreads), kThreads, 0, st>>>(pdesc, d_h2_status, es, n, ends);
+        h2_starts_kernel<<<grid_for(n, kThreads), kThreads, 0, st>>>(ends, n_msg_d, n, starts);
+        if (int rc = read_counts()) return rc;
+        if (n_messages) *n_messages = (size_t)counts[0];
+        // 3'. each pooled message through co_ws_frame_deserialize against
+        //     its own size (co_ws_http2_extension.c:134-164), from the
+        //     materialised pool (layout-first OOM rule)
         if (pool_cap)
             launch_pass<kModeDeser>(PL, 0, d_h2, d_pool, pdesc, d_h2_status, pws, pool_cap, n,
                                     kClassAll, st);
-        if (int rc = deserialize_plan_impl(d_pool, pool_cap, starts, ends, n_msg, max_payload, align,
+        if (int rc = deserialize_plan_impl(d_pool, pool_cap, starts, ends, counts[0], max_payload, align,
                                            0, d_msg_desc, d_msg_status, payload_cap,
                                            d_payload_total, wsd, WL.bytes, stream))
             return rc;
-        return cfws_deserialize_execute(d_pool, d_msg_desc, d_msg_status, n_msg, 0, d_payload,
+        return cfws_deserialize_execute(d_pool, d_msg_desc, d_msg_status, counts[0], 0, d_payload,
                                         payload_cap, wsd, stream);
     }
-    // fused: the pool is never written
+    const uint64_t n_msg = counts[0];
+    if (n_messages) *n_messages = (size_t)n_msg;
+    // 2. fused: the pool is never written. Each message's WS header is
+    //    gathered from its DATA frames and parsed against the message's own
+    //    size (co_ws_http2_extension.c:134-164); then its layout.
     if (align == 0 || (align & (align - 1)) || align > 4096)
         return set_err(CFWS_ERROR_INVALID_ARGUMENT, "align must be a power of two <= 4096", hipSuccess);
     uint64_t* hdr = ws_ptr<uint64_t>(wsd, WL.hdr);
     if (n_msg == 0) return zero_totals(WL, wsd, d_payload_total, st);
     uint64_t* offs0 = ws_ptr<uint64_t>(wsd, WL.offs[0]);
-    h2_msg_parse_kernel<<<grid_for(n_msg, kThreads), kThreads, 0, st>>>(
-        static_cast<const uint8_t*>(d_h2), pdesc, d_h2_status, poffs, n, starts, ends, n_msg,
-        max_payload, align, d_msg_desc, d_msg_status, offs0);
-    if (int rc = run_scan(offs0, n_msg, ws_ptr<uint64_t>(wsd, WL.partials[0]), hdr + 3, st)) return rc;
-    deserialize_finalize_kernel<<<grid_for(n_msg, kThreads), kThreads, 0, st>>>(
-        d_msg_desc, d_msg_status, offs0, offs0, hdr, n_msg, payload_cap, 0,
+    uint64_t* part0 = ws_ptr<uint64_t>(wsd, WL.partials[0]);
+    const uint32_t mb = grid_for(n_msg, kPlanBlock);
+    const uint32_t m_self = mb <= kSelfScanBlocks ? 1u : 0u;
+    h2_msg_parse_kernel<<<mb, kThreads, 0, st>>>(h2, pdesc, d_h2_status, poffs, n, starts, ends, n_msg,
+                                                max_payload, align, d_msg_desc, d_msg_status, offs0,
+                                                first, part0);
+    if (!m_self) scan_partials_kernel<<<1, kThreads, 0, st>>>(part0, mb, hdr + 3);
+    deserialize_plan_apply_kernel<<<mb, kThreads, 0, st>>>(
+        d_msg_desc, d_msg_status, offs0, ws_ptr<uint64_t>(wsd, WL.offs[1]), n_msg, part0,
+        ws_ptr<uint64_t>(wsd, WL.partials[1]), mb, m_self, hdr, payload_cap, 0,
         ws_ptr<uint32_t>(wsd, WL.map[0]), ws_ptr<uint32_t>(wsd, WL.map[1]), d_payload_total);
+    // 3. one payload-pass unit per DATA frame, and the pass's region map
     cfws_frame_desc_t* udesc = ws_ptr<cfws_frame_desc_t>(ws, L.udesc);
     int32_t* ustatus = ws_ptr<int32_t>(ws, L.ustatus);
     uint64_t* uoffs = ws_ptr<uint64_t>(wsd, WL.offs[1]);
     uint32_t* umap = ws_ptr<uint32_t>(wsd, WL.map[1]);
     h2_units_kernel<<<grid_for(n, kThreads), kThreads, 0, st>>>(
         pdesc, d_h2_status, poffs, es, n, n_msg, starts, d_msg_desc, d_msg_status, hdr, udesc,
-        ustatus, uoffs);
-    h2_unit_map_kernel<<<grid_for(n, kThreads), kThreads, 0, st>>>(uoffs, n, hdr, umap);
+        ustatus, uoffs, umap);
     if (payload_cap)
         launch_streaming<kModeDeser>(d_h2, d_payload, udesc, ustatus, uoffs, umap, hdr, nullptr,
                                      WL.regions, payload_cap, n, kClassAll, 0, st);

@@ -279,3 +279,26 @@ def test_gpu_config5_digest(idx):
     assert m == n and int(ptot.item()) == n * fs
     assert bool((st == 0).all()) and bool((ms == 0).all())
     assert torch.equal(back[:n * fs], payload[:n * fs])
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not gpu_present(), reason="needs the MI355X")
+def test_gpu_h2_roundtrip_600k_frames():
+    """600,000 small WS frames, one DATA frame each: both plans run with more
+    than 2,048 blocks (the block sums take a scan launch of their own instead
+    of the apply kernel's self-scan). Send and receive vs the oracle."""
+    rng = np.random.default_rng(600)
+    n = 600_000
+    payload = O.fill_splitmix(1 << 20, 600, 0)
+    d = np.zeros(n, dtype=O.DESC_DTYPE)
+    sz = rng.choice(np.array([0, 1, 7, 60, 125, 126, 200], np.uint64), n)
+    d["payload_off"] = rng.integers(0, (1 << 20) - 256, n).astype(np.uint64)
+    d["payload_size"] = sz
+    d["mask_key"] = rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32)
+    d["fin"], d["opcode"], d["mask"] = 1, 2, (rng.random(n) < .7).astype(np.uint8)
+    exp, _ = O.h2_serialize_batch(payload, d, 3, 16384)
+    got, t = gpu_h2_serialize(payload, d, 3, 16384)
+    assert t == len(exp) and np.array_equal(got, exp)
+    index = O.h2_index(exp)
+    assert len(index) == n
+    check_h2_deserialize(exp, index, align=1)
