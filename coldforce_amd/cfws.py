@@ -54,7 +54,8 @@ BATCH_SYMBOLS = (
     "cfws_index_frames", "cfws_index_workspace_size", "cfws_index_frames_batch",
     "cfws_ws_accept_keys_batch", "cfws_encode_headers", "cfws_parse_headers",
     "cfws_mask_batch", "cfws_unmask_batch", "cfws_copy_to_host", "cfws_mapped_device_pointer",
-    "cfws_pipeline_set_d2h",
+    "cfws_pipeline_set_d2h", "cfws_graph_serialize", "cfws_graph_deserialize", "cfws_graph_launch",
+    "cfws_graph_destroy",
 )
 DROPIN_SYMBOLS = (
     "co_ws_frame_serialize", "co_ws_frame_deserialize", "co_ws_frame_create",
@@ -116,6 +117,11 @@ def lib(path: str = LIB_PATH) -> C.CDLL:
         "cfws_unmask_batch": ([_vp, _vp, _vp, _sz, _u64, _vp, _u64, _vp], C.c_int),
         "cfws_copy_to_host": ([_vp, _vp, _u64, _vp], C.c_int),
         "cfws_pipeline_set_d2h": ([_vp, C.c_int], C.c_int),
+        "cfws_graph_serialize": ([_vp, _vp, _sz, _vp, _u64, _vp, _vp, _sz, _vp], C.c_int),
+        "cfws_graph_deserialize": ([_vp, _u64, _vp, _sz, _u64, _u32, _u32, _vp, _vp, _vp, _u64, _vp,
+                                    _vp, _sz, _vp], C.c_int),
+        "cfws_graph_launch": ([_vp, _vp], C.c_int),
+        "cfws_graph_destroy": ([_vp], None),
         "cfws_mapped_device_pointer": ([_vp], _vp),
         "cfws_xor_mask": ([_vp, _vp, _u64, _u32, _u32, _vp], C.c_int),
         "cfws_draw_mask_keys": ([_sz, _vp, _vp], None),
@@ -289,6 +295,48 @@ def deserialize(wire_t, wire_size: int, index_t, payload_t, desc_t=None, status_
                                         _stream(stream)),
            "cfws_deserialize_batch")
     return desc_t, status_t, total_t
+
+
+# ---- HIP graphs of a batch (cfws_graph_*) -----------------------------------
+
+class Graph:
+    """One captured cfws_serialize_batch / cfws_deserialize_batch over fixed
+    arenas (the tensors must outlive the graph); launch() replays it."""
+
+    def __init__(self, h):
+        self.h = h
+
+    @classmethod
+    def serialize(cls, payload_t, desc_t, wire_t, ws_t, total_t):
+        h = _vp()
+        _check(lib().cfws_graph_serialize(_p(payload_t), _p(desc_t), desc_t.shape[0], _p(wire_t),
+                                          wire_t.numel(), _p(total_t), _p(ws_t), ws_t.numel(),
+                                          C.byref(h)), "cfws_graph_serialize")
+        return cls(h)
+
+    @classmethod
+    def deserialize(cls, wire_t, wire_size: int, index_t, desc_t, status_t, payload_t, ws_t, total_t,
+                    max_payload: int = DEFAULT_MAX_PAYLOAD, align: int = 16, flags: int = 0):
+        h = _vp()
+        _check(lib().cfws_graph_deserialize(_p(wire_t), wire_size, _p(index_t), index_t.numel(),
+                                            max_payload, align, flags, _p(desc_t), _p(status_t),
+                                            _p(payload_t), payload_t.numel(), _p(total_t), _p(ws_t),
+                                            ws_t.numel(), C.byref(h)), "cfws_graph_deserialize")
+        return cls(h)
+
+    def launch(self, stream=None) -> None:
+        _check(lib().cfws_graph_launch(self.h, _stream(stream)), "cfws_graph_launch")
+
+    def close(self):
+        if self.h:
+            lib().cfws_graph_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 # ---- host memory ---------------------------------------------------------------

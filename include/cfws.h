@@ -325,6 +325,27 @@ int cfws_pipeline_set_d2h(cfws_pipeline_t* pipeline, int mode);
 int cfws_copy_to_host(const void* d_src, void* h_dst, uint64_t n, void* stream);
 void* cfws_mapped_device_pointer(const void* h_ptr);
 
+/* ---- HIP graphs of a batch (cfws_graph.cpp) ------------------------------
+ * A batch shape replayed over the same arenas: cfws_serialize_batch /
+ * cfws_deserialize_batch with these exact arguments, captured once into a
+ * hipGraph and launched with one call on any stream. Pointers, frame count
+ * and capacities are fixed at capture; descriptor contents and payload /
+ * wire bytes may change between launches (the plans run on the device at
+ * every launch). For small batches, where launch latency rather than HBM
+ * bounds a call. cfws_h2_deserialize_batch
+ * synchronises and cannot be captured. */
+typedef struct cfws_graph cfws_graph_t;
+int cfws_graph_serialize(const void* d_payload, cfws_frame_desc_t* d_desc, size_t n, void* d_wire,
+                         uint64_t wire_capacity, uint64_t* d_wire_total, void* d_workspace,
+                         size_t workspace_size, cfws_graph_t** graph);
+int cfws_graph_deserialize(const void* d_wire, uint64_t wire_size, const uint64_t* d_index, size_t n,
+                           uint64_t max_payload, uint32_t align, uint32_t flags,
+                           cfws_frame_desc_t* d_desc, int32_t* d_status, void* d_payload,
+                           uint64_t payload_capacity, uint64_t* d_payload_total, void* d_workspace,
+                           size_t workspace_size, cfws_graph_t** graph);
+int cfws_graph_launch(cfws_graph_t* graph, void* stream);
+void cfws_graph_destroy(cfws_graph_t* graph);
+
 /* ---- single-buffer XOR (used by the per-frame drop-in path) --------------
  * d_dst[i] = d_src[i] ^ key byte (i + key_phase) % 4, i < n. */
 int cfws_xor_mask(const void* d_src, void* d_dst, uint64_t n, uint32_t mask_key,
