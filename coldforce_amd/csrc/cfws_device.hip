@@ -612,6 +612,29 @@ __device__ __forceinline__ void general_region(const Pass& P, uint32_t f0, uint3
     }
 }
 
+// The region holding the pass end when a capacity cut ends the pass inside a
+// body: the body chunks below the end only, each store clipped at the
+// capacity (the other region paths write whole bodies' chunks, which would
+// run past a cut).
+template <int kMode>
+__device__ __forceinline__ void tail_region(const Pass& P, uint32_t f0, uint32_t f1, uint64_t base,
+                                            uint32_t lane)
+{
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+        const uint64_t D = base + u * kSlice + lane * kChunk;
+        if (D >= P.total) continue;
+        uint32_t lo = f0, hi = f1;                  // largest f with offs[f] <= D
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi + 1) >> 1;
+            if (P.offs[mid] <= D) lo = mid; else hi = mid - 1;
+        }
+        const FrameView v = frame_view<kMode>(P, lo);
+        if (D >= v.body_start && D + kChunk <= v.body_start + v.body_len)
+            store_chunk(P, D, body_chunk(P.src, v, D));
+    }
+}
+
 // Two threads per frame (part 0: the chunks before the body -- headers;
 // part 1: the chunks reaching past the body end -- the boundary into the
 // next frame, padding, the pass end): the 16-byte chunks that START inside
@@ -752,6 +775,10 @@ xform_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
         // region_map[r + 1] holds the NEXT region's first byte; frames that
         // start at or after this region's end do not touch it.
         if (f1 > f0 && offs[f0 + 1] >= end) f1 = f0;
+        if (end > P.total) {                  // the pass end (a capacity cut may fall in a body)
+            tail_region<kMode>(P, f0, f1, base, lane);
+            continue;
+        }
         const FrameView va = frame_view<kMode>(P, f0);
         if (f0 == f1) {
             if (base >= va.body_start && end <= va.body_start + va.body_len)
@@ -1216,6 +1243,286 @@ deserialize_finalize_kernel(cfws_frame_desc_t* __restrict__ desc, int32_t* __res
         hdr[1] = t1;
         hdr[2] = t0;
         if (user_total) *user_total = t0 + t1;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// small batches: plan and stream in one launch per direction
+// ---------------------------------------------------------------------------
+// A batch of up to kSmallFrames frames into at most kSmallBytes of output is
+// bound by launch latency, not HBM: plan (two launches) + execute (one) per
+// direction. Here every workgroup computes the batch's layout itself into
+// LDS (a 1,024-entry scan: a few microseconds, all reads from L2 after the
+// first workgroup), workgroup 0 writes the descriptors, statuses and totals
+// the plan would, and all workgroups then write their 16-byte output chunks:
+// a chunk inside one body takes body_chunk (two aligned loads + funnel), any
+// other chunk (headers, frame boundaries, padding) is assembled byte by byte.
+// Outputs are the normal path's, byte for byte, including the zeros the last
+// chunk writes past the total within the capacity.
+constexpr uint32_t kSmallFrames = 1024;
+constexpr uint64_t kSmallBytes = 4ull << 20;
+constexpr int kSmallItems = kSmallFrames / kThreads;
+#ifndef CFWS_SMALL_CPT
+#define CFWS_SMALL_CPT 1
+#endif
+constexpr uint32_t kSmallChunksPerThread = CFWS_SMALL_CPT;   // output chunks per thread
+
+// Frame k * kThreads + tid of a small batch is thread tid's k-th: every
+// thread loads (and parses) at most kSmallItems frames, all independent, and
+// a batch of up to kThreads frames keeps every thread busy.
+__device__ __forceinline__ uint32_t small_frame(int k) { return k * kThreads + threadIdx.x; }
+
+// s_off[f] = exclusive prefix of w over the frames (w[k]: frame
+// small_frame(k)), one block scan per slice of kThreads frames; s_off[n] =
+// the grand total (returned). Ends with a barrier.
+__device__ __forceinline__ uint64_t small_scan(const uint64_t (&w)[kSmallItems], uint32_t n,
+                                               uint64_t* s_off, uint64_t* s_wave)
+{
+    uint64_t carry = 0;
+#pragma unroll
+    for (int k = 0; k < kSmallItems; ++k) {
+        if (uint32_t(k) * kThreads >= n) break;          // uniform: the slice is empty
+        uint64_t tot;
+        const uint64_t ex = block_exclusive_scan(w[k], s_wave, &tot);
+        const uint32_t f = small_frame(k);
+        if (f < n) s_off[f] = carry + ex;
+        carry += tot;
+    }
+    if (threadIdx.x == 0) s_off[n] = carry;
+    __syncthreads();
+    return carry;
+}
+
+// Largest f < n with s_off[f] <= D (s_off[0] = 0 <= D).
+__device__ __forceinline__ uint32_t small_frame_of(const uint64_t* s_off, uint32_t n, uint64_t D)
+{
+    uint32_t lo = 0, hi = n - 1;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi + 1) >> 1;
+        if (s_off[mid] <= D) lo = mid; else hi = mid - 1;
+    }
+    return lo;
+}
+
+__device__ __forceinline__ void small_store(uint8_t* dst, uint64_t cap, uint64_t D, uint4 o)
+{
+    if (D + 16 <= cap) {
+        st16(dst + D, o);
+    } else {
+        for (uint32_t j = 0; D + j < cap; ++j) dst[D + j] = (uint8_t)(u4_byte(o, (int)j));
+    }
+}
+
+// A serialize frame's view from the LDS copy of its descriptor.
+__device__ __forceinline__ FrameView small_ser_view(const uint64_t* s_off, const uint64_t* s_src,
+                                                    const uint64_t* s_len, const uint32_t* s_key,
+                                                    const uint32_t* s_hb, uint32_t f)
+{
+    FrameView v = {};
+    v.out_off = s_off[f];
+    v.pre = s_hb[f] >> 16;
+    v.body_start = v.out_off + v.pre;
+    v.body_len = s_len[f];
+    v.src_off = s_src[f];
+    v.key = s_key[f];
+    v.hb = s_hb[f] & 0xffffu;
+    return v;
+}
+
+// co_ws_frame_serialize for every frame (co_ws_frame.c:34-97), frames back
+// to back from wire offset 0; as cfws_serialize_plan + cfws_serialize_execute.
+__global__ void __launch_bounds__(kThreads)
+serialize_small_kernel(const uint8_t* __restrict__ src, cfws_frame_desc_t* __restrict__ desc,
+                       uint32_t n, uint8_t* __restrict__ dst, uint64_t cap,
+                       uint64_t* __restrict__ ws_hdr, uint64_t* __restrict__ user_total)
+{
+    __shared__ uint64_t s_off[kSmallFrames + 1];
+    __shared__ uint64_t s_src[kSmallFrames];        // payload offset
+    __shared__ uint64_t s_len[kSmallFrames];        // payload size
+    __shared__ uint32_t s_key[kSmallFrames];        // mask key (0: unmasked)
+    __shared__ uint32_t s_hb[kSmallFrames];         // header byte 0 | mask bit << 8 | header size << 16
+    __shared__ uint64_t s_wave[kWaves];
+    uint64_t w[kSmallItems];
+#pragma unroll
+    for (int k = 0; k < kSmallItems; ++k) {
+        const uint32_t f = small_frame(k);
+        w[k] = 0;
+        if (f < n) {
+            const DescWords d = load_desc(desc, f);
+            const uint32_t hs = header_size_of(d.payload_size, d.mask() != 0);
+            w[k] = hs + d.payload_size;
+            s_src[f] = d.payload_off;
+            s_len[f] = d.payload_size;
+            s_key[f] = d.mask() ? d.key() : 0u;
+            s_hb[f] = ((d.opcode() | (d.fin() ? 0x80u : 0u)) & 0xffu) | (d.mask() ? 0x100u : 0u) | hs << 16;
+        }
+    }
+    const uint64_t g = small_scan(w, n, s_off, s_wave);      // (its barrier publishes the views)
+    const uint64_t total = g < cap ? g : cap;
+    if (blockIdx.x == 0) {
+        // the plan's outputs
+        for (uint32_t f = threadIdx.x; f < n; f += kThreads) {
+            desc[f].header_size = (uint8_t)(s_hb[f] >> 16);
+            desc[f].wire_off = s_off[f];
+        }
+        if (threadIdx.x == 0) {
+            ws_hdr[0] = total;
+            ws_hdr[3] = g;
+            if (user_total) *user_total = g;
+        }
+    }
+    const uint64_t n_chunks = (total + 15) / 16;
+    for (uint64_t c = uint64_t(blockIdx.x) * kThreads + threadIdx.x; c < n_chunks;
+         c += uint64_t(gridDim.x) * kThreads) {
+        const uint64_t D = c * 16;
+        uint32_t f = small_frame_of(s_off, n, D);
+        FrameView v = small_ser_view(s_off, s_src, s_len, s_key, s_hb, f);
+        uint4 o;
+        const uint64_t lim = D + 16 < total ? D + 16 : total;
+        const uint64_t o1 = f + 1 < n ? s_off[f + 1] : ~uint64_t(0);
+        const uint64_t o2 = f + 2 < n ? s_off[f + 2] : ~uint64_t(0);
+        if (D >= v.body_start && D + 16 <= v.body_start + v.body_len) {
+            o = body_chunk(src, v, D);
+        } else if (o2 >= lim) {
+            // at most two frames in the chunk: their body bytes lined up in
+            // registers (edge_chunk), headers generated
+            const FrameView vb = f + 1 < n ? small_ser_view(s_off, s_src, s_len, s_key, s_hb, f + 1) : v;
+            Pass P = {};
+            P.src = src;
+            P.total = total;
+            o = edge_chunk<kModeSer>(P, f, D, v, vb, o1, o2);
+        } else {
+            uint32_t b[16];
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                const uint64_t pos = D + j;
+                b[j] = 0;
+                if (pos >= total) continue;
+                while (pos >= s_off[f + 1]) v = small_ser_view(s_off, s_src, s_len, s_key, s_hb, ++f);
+                const uint64_t r = pos - v.out_off;
+                if (r < v.pre) {
+                    b[j] = view_header_byte(v, (uint32_t)r);
+                } else {
+                    const uint64_t k = r - v.pre;
+                    b[j] = (src[v.src_off + k] ^ (v.key >> (8 * (k & 3u)))) & 0xffu;
+                }
+            }
+            o = make_uint4(b[0] | b[1] << 8 | b[2] << 16 | b[3] << 24,
+                           b[4] | b[5] << 8 | b[6] << 16 | b[7] << 24,
+                           b[8] | b[9] << 8 | b[10] << 16 | b[11] << 24,
+                           b[12] | b[13] << 8 | b[14] << 16 | b[15] << 24);
+        }
+        small_store(dst, cap, D, o);
+    }
+}
+
+// A deserialize frame's view from LDS: no header in the output, the body
+// copied + unmasked, then zeros to the next frame (alignment padding).
+__device__ __forceinline__ FrameView small_de_view(const uint64_t* s_off, const uint64_t* s_src,
+                                                   const uint64_t* s_len, const uint32_t* s_key,
+                                                   uint32_t f)
+{
+    FrameView v = {};
+    v.out_off = s_off[f];
+    v.body_start = v.out_off;
+    v.body_len = s_len[f];
+    v.src_off = s_src[f];
+    v.key = s_key[f];
+    return v;
+}
+
+// co_ws_frame_deserialize at every index (co_ws_frame.c:121-247), payloads
+// laid out as cfws_deserialize_plan lays them out without reassembly;
+// as cfws_deserialize_plan + cfws_deserialize_execute (flags 0).
+__global__ void __launch_bounds__(kThreads)
+deserialize_small_kernel(const uint8_t* __restrict__ wire, uint64_t wire_size,
+                         const uint64_t* __restrict__ index, uint32_t n, uint64_t max_payload,
+                         uint64_t align, cfws_frame_desc_t* __restrict__ desc,
+                         int32_t* __restrict__ status, uint8_t* __restrict__ dst, uint64_t cap,
+                         uint64_t* __restrict__ ws_hdr, uint64_t* __restrict__ user_total)
+{
+    __shared__ uint64_t s_off[kSmallFrames + 1];
+    __shared__ uint64_t s_src[kSmallFrames];        // body source: wire offset + header size
+    __shared__ uint64_t s_len[kSmallFrames];        // body bytes copied (COMPLETE, fits)
+    __shared__ uint32_t s_key[kSmallFrames];
+    __shared__ uint64_t s_wave[kWaves];
+    cfws_frame_desc_t d[kSmallItems];
+    int32_t st[kSmallItems];
+    uint64_t w[kSmallItems];
+#pragma unroll
+    for (int k = 0; k < kSmallItems; ++k) {
+        const uint32_t f = small_frame(k);
+        w[k] = 0;
+        st[k] = CFWS_PARSE_COMPLETE;
+        if (f < n) {
+            st[k] = parse_ws_header(wire, wire_size, index[f], max_payload, d[k]);
+            const uint64_t len = st[k] == CFWS_PARSE_COMPLETE ? d[k].payload_size : 0;
+            w[k] = (len + align - 1) & ~(align - 1);
+        }
+    }
+    const uint64_t g = small_scan(w, n, s_off, s_wave);
+    const uint64_t total = g < cap ? g : cap;
+#pragma unroll
+    for (int k = 0; k < kSmallItems; ++k) {
+        const uint32_t f = small_frame(k);
+        if (f >= n) continue;
+        d[k].payload_off = s_off[f];
+        // the capacity rule: a COMPLETE payload that does not fit is OOM
+        // (the reference's failed malloc, co_ws_frame.c:216-223)
+        if (st[k] == CFWS_PARSE_COMPLETE && d[k].payload_size > 0 && s_off[f] + d[k].payload_size > cap)
+            st[k] = CFWS_ERROR_OUT_OF_MEMORY;
+        s_src[f] = d[k].wire_off + d[k].header_size;
+        s_len[f] = st[k] == CFWS_PARSE_COMPLETE ? d[k].payload_size : 0;
+        s_key[f] = d[k].mask ? d[k].mask_key : 0u;
+        if (blockIdx.x == 0) {
+            desc[f] = d[k];
+            status[f] = st[k];
+        }
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        ws_hdr[0] = total;
+        ws_hdr[1] = 0;
+        ws_hdr[2] = total;
+        ws_hdr[3] = g;
+        if (user_total) *user_total = total;
+    }
+    __syncthreads();
+    const uint64_t n_chunks = (total + 15) / 16;
+    for (uint64_t c = uint64_t(blockIdx.x) * kThreads + threadIdx.x; c < n_chunks;
+         c += uint64_t(gridDim.x) * kThreads) {
+        const uint64_t D = c * 16;
+        uint32_t f = small_frame_of(s_off, n, D);
+        uint4 o;
+        const uint64_t lim = D + 16 < total ? D + 16 : total;
+        const uint64_t o1 = f + 1 < n ? s_off[f + 1] : ~uint64_t(0);
+        const uint64_t o2 = f + 2 < n ? s_off[f + 2] : ~uint64_t(0);
+        if (D + 16 <= s_off[f] + s_len[f]) {          // D >= s_off[f] by the search
+            o = body_chunk(wire, small_de_view(s_off, s_src, s_len, s_key, f), D);
+        } else if (o2 >= lim) {
+            // at most two frames: bodies lined up in registers, padding zero
+            const FrameView va = small_de_view(s_off, s_src, s_len, s_key, f);
+            const FrameView vb = f + 1 < n ? small_de_view(s_off, s_src, s_len, s_key, f + 1) : va;
+            Pass P = {};
+            P.src = wire;
+            P.total = total;
+            o = edge_chunk<kModeDeser>(P, f, D, va, vb, o1, o2);
+        } else {
+            uint32_t b[16];
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                const uint64_t pos = D + j;
+                b[j] = 0;
+                if (pos >= total) continue;
+                while (pos >= s_off[f + 1]) ++f;
+                const uint64_t r = pos - s_off[f];
+                if (r < s_len[f]) b[j] = (wire[s_src[f] + r] ^ (s_key[f] >> (8 * (r & 3u)))) & 0xffu;
+            }
+            o = make_uint4(b[0] | b[1] << 8 | b[2] << 16 | b[3] << 24,
+                           b[4] | b[5] << 8 | b[6] << 16 | b[7] << 24,
+                           b[8] | b[9] << 8 | b[10] << 16 | b[11] << 24,
+                           b[12] | b[13] << 8 | b[14] << 16 | b[15] << 24);
+        }
+        small_store(dst, cap, D, o);
     }
 }
 
@@ -2053,6 +2360,26 @@ uint32_t grid_for(uint64_t items, uint64_t per_block)
     return (uint32_t)(g == 0 ? 1 : g);
 }
 
+// The single-launch small-batch path (CFWS_SMALL=0 turns it off: plan +
+// execute for every batch, for A/B and for tests of both paths).
+bool small_path()
+{
+    static int v = -1;
+    if (v < 0) {
+        const char* s = getenv("CFWS_SMALL");
+        v = (s && *s == '0') ? 0 : 1;
+    }
+    return v == 1;
+}
+
+// Workgroups of a small-batch launch: kSmallChunksPerThread output chunks
+// per thread at the capacity's size.
+uint32_t small_grid(uint64_t cap)
+{
+    const uint64_t per = uint64_t(kThreads) * kSmallChunksPerThread * 16;
+    return grid_for(cap, per);
+}
+
 // One 4 KiB region per wave (measured fastest: no grid-stride loop, every
 // wave's loads in flight at once); CFWS_GRID caps the workgroup count.
 uint32_t stream_grid(uint64_t regions)
@@ -2234,6 +2561,15 @@ int cfws_serialize_execute(const void* d_payload, const cfws_frame_desc_t* d_des
 int cfws_serialize_batch(const void* d_payload, cfws_frame_desc_t* d_desc, size_t n, void* d_wire,
                          uint64_t cap, uint64_t* d_total, void* ws, size_t ws_size, void* stream)
 {
+    // small batch, every argument valid: one launch (serialize_small_kernel)
+    if (small_path() && n > 0 && n <= kSmallFrames && cap <= kSmallBytes && check_init() == CFWS_OK &&
+        d_desc && ws && ws_size >= ws_layout(n, cap).bytes &&
+        (cap == 0 || (d_payload && d_wire && !misaligned(d_payload, d_wire)))) {
+        serialize_small_kernel<<<small_grid(cap), kThreads, 0, static_cast<hipStream_t>(stream)>>>(
+            static_cast<const uint8_t*>(d_payload), d_desc, (uint32_t)n, static_cast<uint8_t*>(d_wire),
+            cap, ws_ptr<uint64_t>(ws, ws_layout(n, cap).hdr), d_total);
+        return launch_check("serialize_batch(small)");
+    }
     if (int rc = cfws_serialize_plan(d_desc, n, cap, d_total, ws, ws_size, stream)) return rc;
     return cfws_serialize_execute(d_payload, d_desc, n, d_wire, cap, ws, stream);
 }
@@ -2316,6 +2652,17 @@ int cfws_deserialize_batch(const void* d_wire, uint64_t wire_size, const uint64_
                            uint64_t cap, uint64_t* d_total, void* ws, size_t ws_size,
                            void* stream)
 {
+    // small batch without reassembly, every argument valid: one launch
+    if (small_path() && n > 0 && n <= kSmallFrames && cap <= kSmallBytes && flags == 0 && align != 0 &&
+        (align & (align - 1)) == 0 && align <= 4096 && check_init() == CFWS_OK && d_wire && d_index &&
+        d_desc && d_status && ws && ws_size >= ws_layout(n, cap).bytes &&
+        (cap == 0 || (d_payload && !misaligned(d_payload, d_wire)))) {
+        deserialize_small_kernel<<<small_grid(cap), kThreads, 0, static_cast<hipStream_t>(stream)>>>(
+            static_cast<const uint8_t*>(d_wire), wire_size, d_index, (uint32_t)n, max_payload, align,
+            d_desc, d_status, static_cast<uint8_t*>(d_payload), cap,
+            ws_ptr<uint64_t>(ws, ws_layout(n, cap).hdr), d_total);
+        return launch_check("deserialize_batch(small)");
+    }
     if (int rc = cfws_deserialize_plan(d_wire, wire_size, d_index, n, max_payload, align, flags,
                                        d_desc, d_status, cap, d_total, ws, ws_size, stream))
         return rc;
