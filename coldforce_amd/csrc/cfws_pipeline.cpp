@@ -261,21 +261,63 @@ int cfws_pipeline_serialize(cfws_pipeline_t* p, const void* h_payload, cfws_fram
 // puts control frames after ALL data, which a chunked pass cannot know).
 // Precondition (what a receive loop's index satisfies): h_index increasing
 // and every frame ending at or before the next frame's start.
-int cfws_pipeline_deserialize(cfws_pipeline_t* p, const void* h_wire, uint64_t wire_size,
-                              const uint64_t* h_index, size_t n, uint64_t max_payload,
-                              uint32_t align, uint32_t flags, cfws_frame_desc_t* h_desc,
-                              int32_t* h_status, void* h_payload, uint64_t payload_capacity,
-                              uint64_t* payload_total)
+}  // extern "C"
+
+namespace {
+
+// The frame starts a chunked deserialize consumes: a caller's index, or the
+// receive loop's walk (cfws_index_frames, co_ws_server.c:107-169) run in
+// steps just ahead of the chunks, so the host walks chunk c + 1's frames
+// while the device copies and decodes chunk c (the walk is a chain of
+// dependent reads through host memory, ~100 ns per frame).
+struct StartSource {
+    const uint64_t* fixed = nullptr;     // a caller's index of n_fixed starts
+    size_t n_fixed = 0;
+    const void* buf = nullptr;           // or the walk over buf[pos, end)
+    uint64_t end = 0, max_payload = 0, pos = 0;
+    size_t cap = 0;                      // at most this many starts
+    std::vector<uint64_t> walked;
+    int32_t stop = CFWS_PARSE_COMPLETE;
+    bool done = true;
+    static constexpr size_t kStep = 2048;
+
+    // Does start k exist? (walks on until it is known)
+    bool has(size_t k)
+    {
+        if (fixed) return k < n_fixed;
+        while (k >= walked.size() && !done) step();
+        return k < walked.size();
+    }
+    uint64_t at(size_t k) const { return fixed ? fixed[k] : walked[k]; }
+    // Where the last frame's bytes end (has() said there is no next start):
+    // the walk's stop, so trailing incomplete bytes are never staged.
+    uint64_t last_end(uint64_t wire_size) const { return fixed ? wire_size : std::min(pos, wire_size); }
+    // Stepwise walks end as one walk over the whole buffer would:
+    // CFWS_INDEX_FULL only when another COMPLETE frame follows.
+    void step()
+    {
+        const size_t at0 = walked.size();
+        const size_t room = std::min(kStep, cap - at0);
+        walked.resize(at0 + room);
+        uint64_t used = pos;
+        int32_t why = CFWS_PARSE_COMPLETE;
+        const size_t got = cfws_index_frames(buf, pos, end, max_payload, walked.data() + at0, room,
+                                             &used, &why);
+        walked.resize(at0 + got);
+        pos = used;
+        stop = why;
+        if (why != CFWS_INDEX_FULL || walked.size() == cap) done = true;
+    }
+};
+
+int pipeline_deserialize(cfws_pipeline_t* p, const void* h_wire, uint64_t wire_size, StartSource& idx,
+                         uint64_t max_payload, uint32_t align, cfws_frame_desc_t* h_desc,
+                         int32_t* h_status, void* h_payload, uint64_t payload_capacity,
+                         uint64_t* payload_total)
 {
-    if (!p || (n && (!h_wire || !h_index || !h_desc || !h_status || !h_payload)))
-        return fail("null argument");
-    if (flags != 0) return fail("the pipeline supports flags = 0 only");
-    if (align == 0 || (align & (align - 1)) || align > 4096) return fail("bad align");
-    for (size_t i = 1; i < n; ++i)
-        if (h_index[i] < h_index[i - 1]) return fail("frame index must be increasing");
     const uint8_t* src = static_cast<const uint8_t*>(h_wire);
     uint8_t* dst = static_cast<uint8_t*>(h_payload);
-    uint8_t* dst_dev = n ? kernel_d2h_target(p->d2h_mode, h_payload, false) : nullptr;
+    uint8_t* dst_dev = idx.has(0) ? kernel_d2h_target(p->d2h_mode, h_payload, false) : nullptr;
 
     struct Chunk { size_t i, j; int slot; uint64_t wire_lo, base; };
     std::vector<Chunk> pend;         // launched; layout total not read yet
@@ -333,14 +375,16 @@ int cfws_pipeline_deserialize(cfws_pipeline_t* p, const void* h_wire, uint64_t w
 
     size_t i = 0;
     int c = 0;
-    while (i < n) {
-        const uint64_t lo = std::min(h_index[i], wire_size);
+    while (idx.has(i)) {
+        const uint64_t lo = std::min(idx.at(i), wire_size);
         // a frame's bytes end at the next frame's start (the index precondition)
-        auto end_of = [&](size_t k) { return k + 1 < n ? std::min(h_index[k + 1], wire_size) : wire_size; };
+        auto end_of = [&](size_t k) {
+            return idx.has(k + 1) ? std::min(idx.at(k + 1), wire_size) : idx.last_end(wire_size);
+        };
         // frames [i, j): their wire bytes plus the worst-case alignment
         // padding of their payloads must fit the slot's staging
         size_t j = i + 1;
-        while (j < n && j - i < p->max_frames &&
+        while (idx.has(j) && j - i < p->max_frames &&
                end_of(j) - (lo & ~uint64_t(15)) + (j + 1 - i) * uint64_t(align - 1) <= p->chunk)
             ++j;
         const uint64_t hi = end_of(j - 1);
@@ -364,7 +408,7 @@ int cfws_pipeline_deserialize(cfws_pipeline_t* p, const void* h_wire, uint64_t w
             }
         // the staging's last reader, this slot's previous chunk, was finished above
         auto* sidx = static_cast<uint64_t*>(S.h_stage);
-        for (size_t k = i; k < j; ++k) sidx[k - i] = h_index[k] - wire_lo;
+        for (size_t k = i; k < j; ++k) sidx[k - i] = idx.at(k) - wire_lo;
         CFWS_HIP(hipStreamWaitEvent(p->st_in, S.ev_exec, 0));   // d_in, d_index free
         CFWS_HIP(hipMemcpyAsync(S.d_in, src + wire_lo, hi - wire_lo, hipMemcpyHostToDevice, p->st_in));
         CFWS_HIP(hipMemcpyAsync(S.d_index, sidx, (j - i) * sizeof(uint64_t), hipMemcpyHostToDevice,
@@ -398,26 +442,56 @@ int cfws_pipeline_deserialize(cfws_pipeline_t* p, const void* h_wire, uint64_t w
     return CFWS_OK;
 }
 
+}  // namespace
+
+extern "C" {
+
+int cfws_pipeline_deserialize(cfws_pipeline_t* p, const void* h_wire, uint64_t wire_size,
+                              const uint64_t* h_index, size_t n, uint64_t max_payload,
+                              uint32_t align, uint32_t flags, cfws_frame_desc_t* h_desc,
+                              int32_t* h_status, void* h_payload, uint64_t payload_capacity,
+                              uint64_t* payload_total)
+{
+    if (!p || (n && (!h_wire || !h_index || !h_desc || !h_status || !h_payload)))
+        return fail("null argument");
+    if (flags != 0) return fail("the pipeline supports flags = 0 only");
+    if (align == 0 || (align & (align - 1)) || align > 4096) return fail("bad align");
+    for (size_t i = 1; i < n; ++i)
+        if (h_index[i] < h_index[i - 1]) return fail("frame index must be increasing");
+    StartSource idx;
+    idx.fixed = h_index;
+    idx.n_fixed = n;
+    return pipeline_deserialize(p, h_wire, wire_size, idx, max_payload, align, h_desc, h_status,
+                                h_payload, payload_capacity, payload_total);
+}
+
 int cfws_pipeline_receive(cfws_pipeline_t* p, const void* h_wire, uint64_t begin, uint64_t end,
                           uint64_t max_payload, uint32_t align, cfws_frame_desc_t* h_desc,
                           int32_t* h_status, size_t* n_frames, uint64_t* consumed, int32_t* stop,
                           void* h_payload, uint64_t payload_capacity, uint64_t* payload_total)
 {
     if (!p || !n_frames || (end > begin && !h_wire)) return fail("null argument");
+    if (*n_frames && (!h_desc || !h_status || !h_payload)) return fail("null argument");
+    if (align == 0 || (align & (align - 1)) || align > 4096) return fail("bad align");
     // the receive loop's walk (co_ws_server.c:107-169) on the host, where the
-    // bytes are; its starts drive the chunked device deserialize
-    std::vector<uint64_t> starts(*n_frames ? *n_frames : 1);
-    uint64_t used = begin;
-    int32_t why = CFWS_PARSE_COMPLETE;
-    const size_t n = cfws_index_frames(h_wire, begin, end, max_payload, starts.data(), *n_frames,
-                                       &used, &why);
-    *n_frames = n;
-    if (consumed) *consumed = used;
-    if (stop) *stop = why;
-    // every indexed frame is COMPLETE inside [begin, used): bytes past `used`
-    // (an incomplete or invalid frame) are not staged
-    return cfws_pipeline_deserialize(p, h_wire, used, starts.data(), n, max_payload, align, 0,
-                                     h_desc, h_status, h_payload, payload_capacity, payload_total);
+    // bytes are, a step ahead of the chunked device deserialize it drives.
+    // Every walked frame is COMPLETE inside [begin, consumed): the walk stops
+    // before an incomplete or invalid frame, whose bytes are never staged.
+    StartSource idx;
+    idx.buf = h_wire;
+    idx.pos = begin;
+    idx.end = end;
+    idx.max_payload = max_payload;
+    idx.cap = *n_frames;
+    idx.done = false;
+    idx.walked.reserve(std::min(*n_frames, size_t(1) << 20));
+    const int rc = pipeline_deserialize(p, h_wire, end, idx, max_payload, align, h_desc, h_status,
+                                        h_payload, payload_capacity, payload_total);
+    while (!idx.done) idx.step();       // an error above may leave the walk short
+    *n_frames = idx.walked.size();
+    if (consumed) *consumed = idx.pos;
+    if (stop) *stop = idx.stop;
+    return rc;
 }
 
 }  // extern "C"

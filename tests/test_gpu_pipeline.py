@@ -174,3 +174,30 @@ def test_pipeline_receive_indexes_then_deserializes(cut):
     assert tot == e_tot and (st == 0).all()
     assert np.array_equal(desc["payload_off"], e_d["payload_off"])
     assert np.array_equal(out[:tot], e_out[:tot])
+
+
+@pytest.mark.parametrize("max_frames,cut", [(4100, 0), (5000, 0), (2048, 0), (4999, 3), (0, 0)])
+def test_pipeline_receive_walk_in_steps(max_frames, cut):
+    """cfws_pipeline_receive walks the buffer a step (2,048 frames) ahead of
+    the chunks; the walk's end equals one cfws_index_frames call over the whole
+    buffer: the frame limit (CFWS_INDEX_FULL only when a COMPLETE frame
+    follows), a cut last frame (MORE_DATA), consumed bytes, and the payloads."""
+    rng = random.Random(max_frames + cut)
+    frames = [O.serialize_keyed(True, 2, rng.random() < .6, rng.getrandbits(32),
+                                rng.randbytes(rng.choice([0, 1, 9, 125, 126, 700])))
+              for _ in range(5000)]
+    raw = b"".join(frames)
+    raw = raw[:len(raw) - cut]
+    wire_t, wire = pinned(len(raw))
+    wire[:len(raw)] = np.frombuffer(raw, np.uint8)
+    e_st, e_con, e_stop = cfws.index_frames(wire[:len(raw)], 0, len(raw), max_starts=max_frames)
+    e_out, e_d, e_status, e_tot = O.deserialize_batch(wire[:e_con], e_st, align=16)
+    out_t, out = pinned(len(raw) + 16 * 5000 + 64)
+    pl = make_pipeline(chunk_bytes=1 << 20, max_frames=700, depth=3)
+    desc, st, consumed, stop, tot = pl.receive(wire_t.data_ptr(), 0, len(raw), out_t.data_ptr(),
+                                               out.size, max_frames=max_frames)
+    pl.close()
+    assert (consumed, stop) == (e_con, e_stop)
+    assert len(desc) == len(e_st) and np.array_equal(desc["wire_off"], e_st)
+    assert tot == e_tot and np.array_equal(st, e_status)
+    assert np.array_equal(out[:tot], e_out[:tot])
