@@ -55,7 +55,7 @@ BATCH_SYMBOLS = (
     "cfws_ws_accept_keys_batch", "cfws_encode_headers", "cfws_parse_headers",
     "cfws_mask_batch", "cfws_unmask_batch", "cfws_copy_to_host", "cfws_mapped_device_pointer",
     "cfws_pipeline_set_d2h", "cfws_graph_serialize", "cfws_graph_deserialize", "cfws_graph_launch",
-    "cfws_graph_destroy",
+    "cfws_graph_destroy", "cfws_pipeline_h2_serialize", "cfws_pipeline_h2_deserialize",
 )
 DROPIN_SYMBOLS = (
     "co_ws_frame_serialize", "co_ws_frame_deserialize", "co_ws_frame_create",
@@ -121,6 +121,9 @@ def lib(path: str = LIB_PATH) -> C.CDLL:
         "cfws_graph_deserialize": ([_vp, _u64, _vp, _sz, _u64, _u32, _u32, _vp, _vp, _vp, _u64, _vp,
                                     _vp, _sz, _vp], C.c_int),
         "cfws_graph_launch": ([_vp, _vp], C.c_int),
+        "cfws_pipeline_h2_serialize": ([_vp, _vp, _vp, _sz, _u32, _u32, _vp, _u64, _vp], C.c_int),
+        "cfws_pipeline_h2_deserialize": ([_vp, _vp, _u64, _vp, _sz, _u32, _u64, _u32, _vp, _vp, _vp,
+                                          _vp, _vp, _u64, _vp], C.c_int),
         "cfws_graph_destroy": ([_vp], None),
         "cfws_mapped_device_pointer": ([_vp], _vp),
         "cfws_xor_mask": ([_vp, _vp, _u64, _u32, _u32, _vp], C.c_int),
@@ -659,6 +662,36 @@ class Pipeline:
                                                payload_capacity, C.byref(tot)),
                "cfws_pipeline_deserialize")
         return desc, status, tot.value
+
+    def h2_serialize(self, payload_ptr: int, desc: np.ndarray, h2_ptr: int, h2_capacity: int,
+                     sid: int = 1, S: int = H2_DEFAULT_MAX_FRAME_SIZE) -> int:
+        """WS frames -> HTTP/2 DATA stream, host to host (cfws_pipeline_h2_serialize).
+        desc: host DESC_DTYPE array (wire_off/header_size filled in place)."""
+        tot = C.c_uint64()
+        _check(lib().cfws_pipeline_h2_serialize(self.h, payload_ptr, desc.ctypes.data, len(desc), sid, S,
+                                                h2_ptr, h2_capacity, C.byref(tot)),
+               "cfws_pipeline_h2_serialize")
+        return tot.value
+
+    def h2_deserialize(self, h2_ptr: int, h2_size: int, index: np.ndarray, payload_ptr: int,
+                       payload_capacity: int, S: int = H2_DEFAULT_MAX_FRAME_SIZE, align: int = 16,
+                       max_payload: int = DEFAULT_MAX_PAYLOAD):
+        """DATA frames at index -> messages -> payloads, host to host
+        (cfws_pipeline_h2_deserialize). Returns (h2_status, msg_desc,
+        msg_status, total)."""
+        idx = np.ascontiguousarray(index, dtype=np.uint64)
+        n = len(idx)
+        h2_status = np.zeros(max(n, 1), dtype=np.int32)
+        mdesc = np.zeros(max(n, 1), dtype=DESC_DTYPE)
+        mstatus = np.zeros(max(n, 1), dtype=np.int32)
+        nm, tot = C.c_size_t(0), C.c_uint64()
+        _check(lib().cfws_pipeline_h2_deserialize(self.h, h2_ptr, h2_size, idx.ctypes.data, n, S,
+                                                  max_payload, align, h2_status.ctypes.data,
+                                                  mdesc.ctypes.data, mstatus.ctypes.data, C.byref(nm),
+                                                  payload_ptr, payload_capacity, C.byref(tot)),
+               "cfws_pipeline_h2_deserialize")
+        m = nm.value
+        return h2_status[:n], mdesc[:m], mstatus[:m], tot.value
 
     def receive(self, wire_ptr: int, begin: int, end: int, payload_ptr: int, payload_capacity: int,
                 max_frames: int, align: int = 16, max_payload: int = DEFAULT_MAX_PAYLOAD):

@@ -3096,3 +3096,9 @@ int cfws_fill_splitmix(void* d_dst, uint64_t n, uint64_t seed, uint64_t byte_bas
 }
 
 }  // extern "C"
+
+uint64_t cfws_internal_h2_grand_total_offset(uint64_t n_h2, uint64_t pool_cap, uint64_t payload_cap)
+{
+    return h2_de_layout(n_h2, pool_cap, payload_cap).wsd + ws_layout(n_h2, payload_cap).hdr +
+           3 * sizeof(uint64_t);
+}

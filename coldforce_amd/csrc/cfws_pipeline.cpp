@@ -48,6 +48,12 @@ struct Slot {
     hipEvent_t ev_total = nullptr;     // the chunk's layout total is on the host
     hipEvent_t ev_in = nullptr;        // the chunk's H2D copies landed (host staging free)
     hipEvent_t ev_exec = nullptr;      // the chunk's kernels finished (d_in / d_index free)
+    // HTTP/2 (cfws_pipeline_h2_*), allocated at first use: WS wire / pool
+    // scratch, message statuses and the HTTP/2 workspace
+    void* d_aux = nullptr;
+    int32_t* d_status2 = nullptr;
+    void* d_ws2 = nullptr;
+    size_t ws2_size = 0;
 };
 
 uint32_t hdr_size(uint64_t n, bool mask)
@@ -131,7 +137,7 @@ int cfws_pipeline_create(uint64_t chunk_bytes, size_t max_frames, int depth, cfw
             hipMalloc(&S.d_index, max_frames * sizeof(uint64_t)) != hipSuccess ||
             hipMalloc(&S.d_total, 64) != hipSuccess ||
             hipMalloc(&S.d_ws, S.ws_size) != hipSuccess ||
-            hipHostMalloc(&S.h_stage, max_frames * (sizeof(cfws_frame_desc_t) + sizeof(int32_t))) != hipSuccess ||
+            hipHostMalloc(&S.h_stage, max_frames * (sizeof(cfws_frame_desc_t) + 2 * sizeof(int32_t))) != hipSuccess ||
             hipHostMalloc(reinterpret_cast<void**>(&S.h_total), 64) != hipSuccess ||
             hipEventCreateWithFlags(&S.ev_done, hipEventDisableTiming) != hipSuccess ||
             hipEventCreateWithFlags(&S.ev_total, hipEventDisableTiming) != hipSuccess ||
@@ -166,6 +172,9 @@ void cfws_pipeline_destroy(cfws_pipeline_t* p)
         if (S.h_total) (void)hipHostFree(S.h_total);
         if (S.ev_done) (void)hipEventDestroy(S.ev_done);
         if (S.ev_total) (void)hipEventDestroy(S.ev_total);
+        if (S.d_aux) (void)hipFree(S.d_aux);
+        if (S.d_status2) (void)hipFree(S.d_status2);
+        if (S.d_ws2) (void)hipFree(S.d_ws2);
         if (S.ev_in) (void)hipEventDestroy(S.ev_in);
         if (S.ev_exec) (void)hipEventDestroy(S.ev_exec);
         if (S.st) (void)hipStreamDestroy(S.st);
@@ -492,6 +501,323 @@ int cfws_pipeline_receive(cfws_pipeline_t* p, const void* h_wire, uint64_t begin
     if (consumed) *consumed = idx.pos;
     if (stop) *stop = idx.stop;
     return rc;
+}
+
+}  // extern "C"
+
+// ---- WebSocket over HTTP/2 through host memory -----------------------------
+
+namespace {
+
+uint64_t data_frames(uint64_t W, uint64_t S) { return W <= S ? 1 : (W + S - 1) / S; }
+
+// A slot's HTTP/2 resources, allocated at first use: WS wire / pool scratch,
+// message statuses, and an HTTP/2 workspace of at least ws_bytes.
+int h2_slot(cfws_pipeline* p, Slot& S, size_t ws_bytes)
+{
+    if (!S.d_aux && hipMalloc(&S.d_aux, p->chunk + 64) != hipSuccess)
+        return fail("pipeline allocation failed");
+    if (!S.d_status2 && hipMalloc(&S.d_status2, p->max_frames * sizeof(int32_t)) != hipSuccess)
+        return fail("pipeline allocation failed");
+    if (S.ws2_size < ws_bytes) {
+        if (S.d_ws2) {
+            (void)hipStreamSynchronize(S.st);
+            (void)hipFree(S.d_ws2);
+            S.d_ws2 = nullptr;
+            S.ws2_size = 0;
+        }
+        if (hipMalloc(&S.d_ws2, ws_bytes) != hipSuccess) return fail("pipeline allocation failed");
+        S.ws2_size = ws_bytes;
+    }
+    return CFWS_OK;
+}
+
+// The HTTP/2 frame at s of h2[0, size) as the device parse decides it
+// (co_http2_frame.c:211-300: MORE_DATA under 9 bytes or a short payload,
+// PARSE_ERROR over max_frame_size or bad padding, NOT_DATA for other types):
+// restated here because the receive pipeline cuts its chunks where no
+// message is open. *pooled = the DATA payload bytes it adds to the pool.
+int32_t h2_frame_host(const uint8_t* h2, uint64_t size, uint64_t s, uint64_t max_frame,
+                      uint64_t* pooled, bool* end_stream)
+{
+    *pooled = 0;
+    *end_stream = false;
+    if (s > size || size - s < 9) return CFWS_H2_PARSE_MORE_DATA;
+    const uint64_t len = (uint64_t)h2[s] << 16 | (uint64_t)h2[s + 1] << 8 | h2[s + 2];
+    if (len > max_frame) return CFWS_H2_PARSE_ERROR;
+    if (size - s - 9 < len) return CFWS_H2_PARSE_MORE_DATA;
+    const uint32_t type = h2[s + 3], flags = h2[s + 4];
+    if (type != 0) return CFWS_H2_NOT_DATA;
+    uint64_t pad = 0, hs = 9;
+    if (flags & 0x8u) {                                   // PADDED
+        if (len < 1) return CFWS_H2_PARSE_ERROR;
+        pad = h2[s + 9];
+        hs = 10;
+        if (pad + 1 > len) return CFWS_H2_PARSE_ERROR;
+    }
+    *pooled = len - (hs - 9) - pad;
+    *end_stream = (flags & 0x1u) != 0;
+    return CFWS_H2_PARSE_COMPLETE;
+}
+
+}  // namespace
+
+extern "C" {
+
+// co_http2_stream_send_ws_frame over a host batch (cfws_h2_serialize_batch
+// per chunk of WS frames): host payload arena -> host DATA-frame stream.
+// h_desc gets header_size / wire_off as cfws_serialize_plan writes them.
+int cfws_pipeline_h2_serialize(cfws_pipeline_t* p, const void* h_payload, cfws_frame_desc_t* h_desc,
+                               size_t n, uint32_t stream_id, uint32_t max_frame_size, void* h_h2,
+                               uint64_t h2_capacity, uint64_t* h2_total)
+{
+    if (!p || (n && (!h_payload || !h_desc || !h_h2))) return fail("null argument");
+    const uint64_t mfs = max_frame_size ? max_frame_size : CFWS_H2_DEFAULT_MAX_FRAME_SIZE;
+    // the WS layout (as cfws_serialize_plan) and each frame's DATA-stream bytes
+    uint64_t woff = 0, total = 0;
+    for (size_t f = 0; f < n; ++f) {
+        const uint32_t hs = hdr_size(h_desc[f].payload_size, h_desc[f].mask != 0);
+        h_desc[f].header_size = (uint8_t)hs;
+        h_desc[f].wire_off = woff;
+        const uint64_t W = hs + h_desc[f].payload_size;
+        woff += W;
+        total += W + 9 * data_frames(W, mfs);
+    }
+    if (h2_total) *h2_total = total;
+    const size_t ws_bytes = cfws_h2_serialize_workspace_size(p->max_frames, p->chunk + 64, p->chunk + 64,
+                                                             (uint32_t)mfs);
+    const uint8_t* src = static_cast<const uint8_t*>(h_payload);
+    uint8_t* dst = static_cast<uint8_t*>(h_h2);
+    uint8_t* dst_dev = n ? kernel_d2h_target(p->d2h_mode, h_h2, true) : nullptr;
+    size_t i = 0;
+    int c = 0;
+    uint64_t h2_lo = 0;
+    while (i < n) {
+        // chunk = WS frames [i, j): source span, WS wire bytes (the two-pass
+        // form's scratch) and DATA-stream bytes within the staging
+        uint64_t lo = h_desc[i].payload_off, hi = lo + h_desc[i].payload_size, wb = 0, hb = 0;
+        size_t j = i;
+        while (j < n && j - i < p->max_frames) {
+            const uint64_t a = std::min(lo, (uint64_t)h_desc[j].payload_off);
+            const uint64_t b = std::max(hi, (uint64_t)(h_desc[j].payload_off + h_desc[j].payload_size));
+            const uint64_t W = h_desc[j].header_size + h_desc[j].payload_size;
+            const uint64_t H = W + 9 * data_frames(W, mfs);
+            if (j > i && ((b - (a & ~uint64_t(15))) > p->chunk || wb + W > p->chunk || hb + H > p->chunk)) break;
+            lo = a;
+            hi = b;
+            wb += W;
+            hb += H;
+            ++j;
+        }
+        const uint64_t src_lo = lo & ~uint64_t(15);
+        if (hi - src_lo > p->chunk || wb > p->chunk || hb > p->chunk)
+            return fail("a frame is larger than the pipeline chunk");
+        Slot& S = p->slot[c % p->depth];
+        if (int rc = h2_slot(p, S, ws_bytes)) return rc;
+        CFWS_HIP(hipEventSynchronize(S.ev_in));       // the slot's last H2D read the staging
+        auto* stage = static_cast<cfws_frame_desc_t*>(S.h_stage);
+        for (size_t k = i; k < j; ++k) {
+            stage[k - i] = h_desc[k];
+            stage[k - i].payload_off -= src_lo;
+        }
+        CFWS_HIP(hipStreamWaitEvent(p->st_in, S.ev_exec, 0));   // d_in, d_desc free
+        CFWS_HIP(hipMemcpyAsync(S.d_in, src + src_lo, hi - src_lo, hipMemcpyHostToDevice, p->st_in));
+        CFWS_HIP(hipMemcpyAsync(S.d_desc, stage, (j - i) * sizeof(cfws_frame_desc_t),
+                                hipMemcpyHostToDevice, p->st_in));
+        CFWS_HIP(hipEventRecord(S.ev_in, p->st_in));
+        CFWS_HIP(hipStreamWaitEvent(S.st, S.ev_in, 0));
+        if (int rc = cfws_h2_serialize_batch(S.d_in, S.d_desc, j - i, stream_id, (uint32_t)mfs, S.d_aux,
+                                             p->chunk + 64, S.d_out, p->chunk + 64, S.d_total, S.d_ws2,
+                                             S.ws2_size, S.st))
+            return rc;
+        CFWS_HIP(hipEventRecord(S.ev_exec, S.st));
+        if (h2_lo < h2_capacity) {
+            const uint64_t m = std::min(hb, h2_capacity - h2_lo);
+            if (dst_dev) {
+                if (int rc = cfws_internal_copy_out(S.d_out, dst_dev + h2_lo, m, S.st)) return rc;
+            } else {
+                CFWS_HIP(hipMemcpyAsync(dst + h2_lo, S.d_out, m, hipMemcpyDeviceToHost, S.st));
+            }
+        }
+        CFWS_HIP(hipEventRecord(S.ev_done, S.st));
+        h2_lo += hb;
+        i = j;
+        ++c;
+    }
+    CFWS_HIP(hipStreamSynchronize(p->st_in));
+    for (int s = 0; s < p->depth; ++s) CFWS_HIP(hipStreamSynchronize(p->slot[s].st));
+    return CFWS_OK;
+}
+
+// co_http2_stream_receive_ws_frame over a host DATA-frame stream
+// (cfws_h2_deserialize_batch per chunk): the DATA frames at h_index[i] ->
+// HTTP/2 statuses, pooled messages -> co_ws_frame_deserialize -> payloads in
+// the host arena, laid out as the batch call lays them out. Chunks end where
+// no message is open (after a COMPLETE END_STREAM frame, or where no pooled
+// bytes wait), so every message is decoded whole; the next chunk's H2D is
+// queued before each batch call, which synchronises for its message count.
+// Same index precondition as cfws_pipeline_deserialize.
+int cfws_pipeline_h2_deserialize(cfws_pipeline_t* p, const void* h_h2, uint64_t h2_size,
+                                 const uint64_t* h_index, size_t n, uint32_t max_frame_size,
+                                 uint64_t max_payload, uint32_t align, int32_t* h_h2_status,
+                                 cfws_frame_desc_t* h_msg_desc, int32_t* h_msg_status,
+                                 size_t* n_messages, void* h_payload, uint64_t payload_capacity,
+                                 uint64_t* payload_total)
+{
+    if (!p || !n_messages ||
+        (n && (!h_h2 || !h_index || !h_h2_status || !h_msg_desc || !h_msg_status || !h_payload)))
+        return fail("null argument");
+    if (align == 0 || (align & (align - 1)) || align > 4096) return fail("bad align");
+    for (size_t i = 1; i < n; ++i)
+        if (h_index[i] < h_index[i - 1]) return fail("frame index must be increasing");
+    *n_messages = 0;
+    if (payload_total) *payload_total = 0;
+    if (n == 0) return CFWS_OK;
+    const uint64_t mfs = max_frame_size ? max_frame_size : CFWS_H2_DEFAULT_MAX_FRAME_SIZE;
+    const uint8_t* h2 = static_cast<const uint8_t*>(h_h2);
+    uint8_t* dst = static_cast<uint8_t*>(h_payload);
+    uint8_t* dst_dev = kernel_d2h_target(p->d2h_mode, h_payload, false);
+    const uint64_t out_slot = p->chunk + 64, pool_cap = p->chunk + 64;
+    const size_t ws_bytes = cfws_h2_deserialize_workspace_size(p->max_frames, pool_cap, out_slot);
+    auto end_of = [&](size_t k) { return k + 1 < n ? std::min(h_index[k + 1], h2_size) : h2_size; };
+
+    struct Cut { size_t i, j; uint64_t wire_lo, hi, pooled; };
+    // frames [i, j) up to the last point where no message is open, with the
+    // staged bytes and the payload layout (<= pooled bytes + padding) in the
+    // staging; the stream's tail (an unterminated message) ends the last chunk
+    auto next_cut = [&](size_t i, Cut& C) -> int {
+        const uint64_t wire_lo = std::min(h_index[i], h2_size) & ~uint64_t(15);
+        uint64_t open = 0, pooled = 0, best_pooled = 0;
+        size_t j = i, best = i;
+        while (j < n && j - i < p->max_frames &&
+               end_of(j) - wire_lo + (j + 1 - i) * uint64_t(align - 1) <= p->chunk) {
+            uint64_t pb = 0;
+            bool es = false;
+            if (h2_frame_host(h2, h2_size, h_index[j], mfs, &pb, &es) == CFWS_H2_PARSE_COMPLETE) {
+                pooled += pb;
+                open = es ? 0 : open + pb;
+            }
+            ++j;
+            if (open == 0) {
+                best = j;
+                best_pooled = pooled;
+            }
+        }
+        if (j == n) {
+            best = n;
+            best_pooled = pooled;
+        }
+        if (best == i) return fail("a message spans more bytes or DATA frames than a pipeline chunk holds");
+        C = Cut{i, best, wire_lo, end_of(best - 1), best_pooled};
+        return CFWS_OK;
+    };
+
+    struct Land { size_t i, j, m0, nm; int slot; uint64_t base, pool_base; };
+    std::vector<Land> landing;       // D2H enqueued; outputs not rebased yet
+    auto finish = [&](const Land& k) -> int {
+        Slot& S = p->slot[k.slot];
+        CFWS_HIP(hipEventSynchronize(S.ev_done));
+        const auto* mdesc = static_cast<const cfws_frame_desc_t*>(S.h_stage);
+        const auto* hst = reinterpret_cast<const int32_t*>(mdesc + p->max_frames);
+        const int32_t* mst = hst + p->max_frames;
+        for (size_t f = k.i; f < k.j; ++f) h_h2_status[f] = hst[f - k.i];
+        for (size_t m = 0; m < k.nm; ++m) {
+            h_msg_desc[k.m0 + m] = mdesc[m];
+            h_msg_desc[k.m0 + m].payload_off += k.base;
+            h_msg_desc[k.m0 + m].wire_off += k.pool_base;
+            h_msg_status[k.m0 + m] = mst[m];
+        }
+        return CFWS_OK;
+    };
+    // the slot's staging is free once its last chunk's outputs are rebased
+    auto free_slot = [&](int s) -> int {
+        for (size_t q = 0; q < landing.size(); ++q)
+            if (landing[q].slot == s) {
+                for (size_t r = 0; r <= q; ++r)
+                    if (int rc = finish(landing[r])) return rc;
+                landing.erase(landing.begin(), landing.begin() + q + 1);
+                break;
+            }
+        return CFWS_OK;
+    };
+    auto stage_in = [&](const Cut& C, int s) -> int {
+        Slot& S = p->slot[s];
+        if (int rc = free_slot(s)) return rc;
+        if (int rc = h2_slot(p, S, ws_bytes)) return rc;
+        auto* sidx = static_cast<uint64_t*>(S.h_stage);
+        for (size_t k = C.i; k < C.j; ++k) sidx[k - C.i] = h_index[k] - C.wire_lo;
+        CFWS_HIP(hipStreamWaitEvent(p->st_in, S.ev_exec, 0));   // d_in, d_index free
+        CFWS_HIP(hipMemcpyAsync(S.d_in, h2 + C.wire_lo, C.hi - C.wire_lo, hipMemcpyHostToDevice, p->st_in));
+        CFWS_HIP(hipMemcpyAsync(S.d_index, sidx, (C.j - C.i) * sizeof(uint64_t), hipMemcpyHostToDevice,
+                                p->st_in));
+        CFWS_HIP(hipEventRecord(S.ev_in, p->st_in));
+        return CFWS_OK;
+    };
+
+    uint64_t base = 0, pool_base = 0;
+    size_t m0 = 0;
+    Cut cur, nxt;
+    if (int rc = next_cut(0, cur)) return rc;
+    if (int rc = stage_in(cur, 0)) return rc;
+    for (int c = 0;; ++c) {
+        const int s = c % p->depth;
+        const bool more = cur.j < n;
+        if (more) {
+            if (int rc = next_cut(cur.j, nxt)) return rc;
+            if (p->depth > 1)
+                if (int rc = stage_in(nxt, (c + 1) % p->depth)) return rc;
+        }
+        Slot& S = p->slot[s];
+        CFWS_HIP(hipStreamWaitEvent(S.st, S.ev_in, 0));
+        const uint64_t cap = base >= payload_capacity ? 0 : std::min(out_slot, payload_capacity - base);
+        size_t nm = 0;
+        if (int rc = cfws_h2_deserialize_batch(S.d_in, cur.hi - cur.wire_lo, S.d_index, cur.j - cur.i,
+                                               (uint32_t)mfs, S.d_status, S.d_aux, pool_cap, max_payload,
+                                               align, S.d_desc, S.d_status2, S.d_out, cap, S.d_total,
+                                               &nm, S.d_ws2, S.ws2_size, S.st))
+            return rc;
+        CFWS_HIP(hipEventRecord(S.ev_exec, S.st));
+        // the unclamped payload layout total: offsets keep counting past the capacity
+        CFWS_HIP(hipMemcpyAsync(S.h_total,
+                                static_cast<char*>(S.d_ws2) +
+                                    cfws_internal_h2_grand_total_offset(cur.j - cur.i, pool_cap, cap),
+                                8, hipMemcpyDeviceToHost, S.st));
+        CFWS_HIP(hipEventRecord(S.ev_total, S.st));
+        CFWS_HIP(hipEventSynchronize(S.ev_total));
+        const uint64_t tot = nm ? *S.h_total : 0;
+        if (base < payload_capacity && tot) {
+            const uint64_t m = std::min(tot, payload_capacity - base);
+            if (dst_dev) {
+                if (int rc = cfws_internal_copy_out(S.d_out, dst_dev + base, m, S.st)) return rc;
+            } else {
+                CFWS_HIP(hipMemcpyAsync(dst + base, S.d_out, m, hipMemcpyDeviceToHost, S.st));
+            }
+        }
+        auto* mdesc = static_cast<cfws_frame_desc_t*>(S.h_stage);
+        auto* hst = reinterpret_cast<int32_t*>(mdesc + p->max_frames);
+        if (nm)
+            CFWS_HIP(hipMemcpyAsync(mdesc, S.d_desc, nm * sizeof(cfws_frame_desc_t), hipMemcpyDeviceToHost,
+                                    S.st));
+        CFWS_HIP(hipMemcpyAsync(hst, S.d_status, (cur.j - cur.i) * sizeof(int32_t), hipMemcpyDeviceToHost,
+                                S.st));
+        if (nm)
+            CFWS_HIP(hipMemcpyAsync(hst + p->max_frames, S.d_status2, nm * sizeof(int32_t),
+                                    hipMemcpyDeviceToHost, S.st));
+        CFWS_HIP(hipEventRecord(S.ev_done, S.st));
+        landing.push_back(Land{cur.i, cur.j, m0, nm, s, base, pool_base});
+        base += tot;
+        m0 += nm;
+        pool_base += cur.pooled;
+        if (!more) break;
+        if (p->depth == 1)
+            if (int rc = stage_in(nxt, 0)) return rc;
+        cur = nxt;
+    }
+    for (const Land& k : landing)
+        if (int rc = finish(k)) return rc;
+    *n_messages = m0;
+    if (payload_total) *payload_total = std::min(base, payload_capacity);
+    return CFWS_OK;
 }
 
 }  // extern "C"

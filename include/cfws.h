@@ -304,6 +304,25 @@ int cfws_pipeline_receive(cfws_pipeline_t* pipeline, const void* h_wire, uint64_
                           uint64_t* consumed, int32_t* stop, void* h_payload,
                           uint64_t payload_capacity, uint64_t* payload_total);
 
+/* WebSocket over HTTP/2 through host memory: cfws_h2_serialize_batch /
+ * cfws_h2_deserialize_batch per chunk, with the copies overlapped as above.
+ * Send: h_desc gets header_size / wire_off; *h2_total = DATA-stream bytes
+ * (unclamped). Receive: h_h2_status[i] per DATA frame, one message entry per
+ * pooled message (room for n entries), *n_messages, payloads laid out as the
+ * batch call lays them out; chunks end where no message is open, so a
+ * message larger than the chunk is an error. The index precondition of
+ * cfws_pipeline_deserialize holds for DATA frames too. */
+int cfws_pipeline_h2_serialize(cfws_pipeline_t* pipeline, const void* h_payload,
+                               cfws_frame_desc_t* h_desc, size_t n, uint32_t stream_id,
+                               uint32_t max_frame_size, void* h_h2, uint64_t h2_capacity,
+                               uint64_t* h2_total);
+int cfws_pipeline_h2_deserialize(cfws_pipeline_t* pipeline, const void* h_h2, uint64_t h2_size,
+                                 const uint64_t* h_index, size_t n, uint32_t max_frame_size,
+                                 uint64_t max_payload, uint32_t align, int32_t* h_h2_status,
+                                 cfws_frame_desc_t* h_msg_desc, int32_t* h_msg_status,
+                                 size_t* n_messages, void* h_payload, uint64_t payload_capacity,
+                                 uint64_t* payload_total);
+
 /* How the pipeline's D2H leg moves bytes into a MAPPED host output arena
  * (hipHostMalloc(..., hipHostMallocMapped)); unmapped arenas always take
  * SDMA. AUTO (the default): a kernel storing into the arena for serialize,

@@ -201,3 +201,73 @@ def test_pipeline_receive_walk_in_steps(max_frames, cut):
     assert len(desc) == len(e_st) and np.array_equal(desc["wire_off"], e_st)
     assert tot == e_tot and np.array_equal(st, e_status)
     assert np.array_equal(out[:tot], e_out[:tot])
+
+
+def _h2_batch(rng, n, sizes, payload_len):
+    d = np.zeros(n, dtype=cfws.DESC_DTYPE)
+    for i in range(n):
+        sz = rng.choice(sizes)
+        d[i] = (rng.randrange(0, payload_len - sz), 0, sz, rng.getrandbits(32), 1,
+                rng.choice([1, 2, 9]), rng.random() < .7, 0)
+    return d
+
+
+@pytest.mark.parametrize("chunk,depth,S", [(1 << 17, 1, 16384), (1 << 17, 3, 100), (1 << 20, 2, 16),
+                                           (1 << 20, 3, 16384)])
+def test_pipeline_h2_serialize_matches_oracle(chunk, depth, S):
+    """WS frames -> HTTP/2 DATA frames through host memory: the stream equals
+    the oracle's co_http2_stream_send_ws_frame restatement byte for byte."""
+    rng = random.Random(chunk + depth + S)
+    payload_t, payload = pinned(1 << 20)
+    payload[:] = O.fill_splitmix(1 << 20, S, 0)
+    d = _h2_batch(rng, 1500, [0, 1, 125, 126, 999, 16376, 16384, 40000, 70000], 1 << 20)
+    exp, exp_d = O.h2_serialize_batch(payload, d.copy(), 5, S)
+    out_t, out = pinned(len(exp) + 64)
+    pl = make_pipeline(chunk_bytes=chunk, max_frames=400, depth=depth)
+    tot = pl.h2_serialize(payload_t.data_ptr(), d, out_t.data_ptr(), out.size, 5, S)
+    pl.close()
+    assert tot == len(exp)
+    assert np.array_equal(d["header_size"], exp_d["header_size"])
+    assert np.array_equal(out[:tot], exp)
+
+
+@pytest.mark.parametrize("chunk,depth,S,align", [(1 << 18, 1, 16384, 16), (1 << 18, 3, 100, 1),
+                                                 (1 << 20, 2, 13, 16), (1 << 20, 3, 16384, 64)])
+def test_pipeline_h2_deserialize_matches_oracle(chunk, depth, S, align):
+    """DATA frames -> pooled messages -> payloads through host memory, cut
+    into chunks only where no message is open: HTTP/2 statuses, message
+    descriptors and statuses, payloads and the total equal the oracle's, with
+    corrupt headers, a non-DATA frame, an unterminated tail and a payload
+    capacity cut. (A corrupt END_STREAM frame merges two messages: the
+    chunks hold two of the largest.)"""
+    rng = random.Random(chunk + depth + S + align)
+    payload = O.fill_splitmix(1 << 20, 3, 0)
+    d = _h2_batch(rng, 1200, [0, 5, 126, 999, 16376, 20000, 70000], 1 << 20)
+    h2, _ = O.h2_serialize_batch(payload, d, 1, S)
+    index = O.h2_index(h2)
+    # a SETTINGS-like non-DATA frame between two DATA frames, an
+    # unterminated message at the end (its last DATA frame's END_STREAM
+    # cleared), and a few corrupt lengths
+    k = int(index[len(index) // 3])
+    h2 = np.concatenate([h2[:k], np.array([0, 0, 0, 4, 0, 0, 0, 0, 0], np.uint8), h2[k:]])
+    index = O.h2_index(h2)
+    h2[int(index[-1]) + 4] &= 0xFE
+    for q in range(7, len(index) - 1, 211):
+        h2[int(index[q])] = 0xFF                 # length > max_frame_size: PARSE_ERROR
+    h2_t, h2_np = pinned(len(h2))
+    h2_np[:len(h2)] = h2
+    full = len(h2) + align * len(index) + 64
+    pl = make_pipeline(chunk_bytes=chunk, max_frames=12000, depth=depth)
+    for cap in (full, full // 3):
+        out_t, out = pinned(cap)
+        st, md, ms, tot = pl.h2_deserialize(h2_t.data_ptr(), len(h2), index, out_t.data_ptr(), cap,
+                                            S=S, align=align)
+        e = O.h2_deserialize_batch(h2, index, S, O.DEFAULT_MAX_PAYLOAD, align, None, cap)
+        assert np.array_equal(st, e["h2_status"])
+        assert len(md) == e["n_msg"] and tot == e["total"]
+        assert np.array_equal(ms, e["msg_status"])
+        for f in ("payload_off", "wire_off", "payload_size", "mask_key", "fin", "opcode", "mask",
+                  "header_size"):
+            assert np.array_equal(md[f], e["msg_desc"][f]), (cap, f)
+        assert np.array_equal(out[:tot], e["payload"][:tot]), cap
+    pl.close()
