@@ -7,6 +7,7 @@
 HIPCC    ?= /opt/rocm/bin/hipcc
 ARCH     ?= gfx950
 HIPFLAGS ?= -O3 -std=c++17 -fPIC -Wall -Wno-unused-result
+DEVSRC   := cfws_device cfws_h2 cfws_ops
 HOSTSRC  := cfws_frame cfws_pipeline cfws_index cfws_graph
 HDR      := include/cfws.h include/cfws_co_ws_frame.h coldforce_amd/csrc/cfws_internal.h
 LIB      := coldforce_amd/libcfws.so
@@ -23,7 +24,7 @@ build/examples/batch_roundtrip: examples/batch_roundtrip.c $(LIB) $(HDR)
 	    -Lcoldforce_amd -lcfws -L/opt/rocm/lib -lamdhip64 \
 	    -Wl,-rpath,'$$ORIGIN/../../coldforce_amd' -Wl,-rpath,/opt/rocm/lib
 
-$(OBJDIR)/cfws_device.o: coldforce_amd/csrc/cfws_device.hip $(HDR)
+$(OBJDIR)/%.o: coldforce_amd/csrc/%.hip $(HDR) coldforce_amd/csrc/cfws_kernels.h
 	@mkdir -p $(OBJDIR)
 	$(HIPCC) --offload-arch=$(ARCH) $(HIPFLAGS) -Iinclude -Icoldforce_amd/csrc -c $< -o $@
 
@@ -31,7 +32,7 @@ $(OBJDIR)/%.o: coldforce_amd/csrc/%.cpp $(HDR)
 	@mkdir -p $(OBJDIR)
 	$(HIPCC) --offload-arch=$(ARCH) $(HIPFLAGS) -Iinclude -Icoldforce_amd/csrc -c $< -o $@
 
-$(LIB): $(OBJDIR)/cfws_device.o $(addprefix $(OBJDIR)/,$(addsuffix .o,$(HOSTSRC)))
+$(LIB): $(addprefix $(OBJDIR)/,$(addsuffix .o,$(DEVSRC) $(HOSTSRC)))
 	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $^
 
 oracle:
@@ -40,10 +41,11 @@ oracle:
 ref: all
 	$(MAKE) -s -C oracle ref
 
-asm: coldforce_amd/csrc/cfws_device.hip $(HDR)
+asm: $(HDR) coldforce_amd/csrc/cfws_kernels.h
 	@mkdir -p $(OBJDIR)/asm
-	$(HIPCC) --offload-arch=$(ARCH) $(HIPFLAGS) -Iinclude -Icoldforce_amd/csrc -c $< -o $(OBJDIR)/asm/cfws_device.o \
-	    -save-temps=obj -Rpass-analysis=kernel-resource-usage 2> $(OBJDIR)/asm/resource-usage.txt
+	rm -f $(OBJDIR)/asm/resource-usage.txt
+	for d in $(DEVSRC); do $(HIPCC) --offload-arch=$(ARCH) $(HIPFLAGS) -Iinclude -Icoldforce_amd/csrc -c coldforce_amd/csrc/$$d.hip -o $(OBJDIR)/asm/$$d.o \
+	    -save-temps=obj -Rpass-analysis=kernel-resource-usage 2>> $(OBJDIR)/asm/resource-usage.txt || exit 1; done
 
 clean:
 	rm -rf $(OBJDIR) $(LIB)
@@ -54,7 +56,7 @@ clean:
 # A/B build variants (kept out of git under build/): make variant V=nt F="-DCFWS_NT_STORE"
 variant: $(HDR)
 	@mkdir -p $(OBJDIR)/variants/$(V)
-	$(HIPCC) --offload-arch=$(ARCH) $(HIPFLAGS) $(F) -Iinclude -Icoldforce_amd/csrc -c coldforce_amd/csrc/cfws_device.hip -o $(OBJDIR)/variants/$(V)/cfws_device.o
+	for d in $(DEVSRC); do $(HIPCC) --offload-arch=$(ARCH) $(HIPFLAGS) $(F) -Iinclude -Icoldforce_amd/csrc -c coldforce_amd/csrc/$$d.hip -o $(OBJDIR)/variants/$(V)/$$d.o || exit 1; done
 	for h in $(HOSTSRC); do $(HIPCC) --offload-arch=$(ARCH) $(HIPFLAGS) $(F) -Iinclude -Icoldforce_amd/csrc -c coldforce_amd/csrc/$$h.cpp -o $(OBJDIR)/variants/$(V)/$$h.o || exit 1; done
 	$(HIPCC) --offload-arch=$(ARCH) -shared -o $(OBJDIR)/variants/libcfws_$(V).so $(OBJDIR)/variants/$(V)/*.o
 

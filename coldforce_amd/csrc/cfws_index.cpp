@@ -7,7 +7,7 @@
 // to find where the next one starts. The payloads are then copied + unmasked
 // on the GPU by cfws_deserialize_* / cfws_pipeline_*. This is the host half
 // of a receive loop whose bytes are in host memory (socket buffers); the
-// device-resident form is cfws_index_frames_batch (cfws_device.hip).
+// device-resident form is cfws_index_frames_batch (cfws_ops.hip).
 #include <cstdint>
 #include <cstring>
 

@@ -1,0 +1,1202 @@
+// cfws_kernels.h -- device code and launch helpers shared by the codec's
+// translation units (cfws_device.hip: WS plan / execute / batch ABI and the
+// small-batch path; cfws_h2.hip: WebSocket over HTTP/2; cfws_ops.hip: split
+// ops, handshake keys, device indexing, copies and fills). Everything here is
+// internal to each unit (anonymous namespace); the error state and the
+// deserialize plan, which the units share, are defined once in
+// cfws_device.hip (namespace cfws_rt).
+#ifndef CFWS_KERNELS_H
+#define CFWS_KERNELS_H
+
+#include <hip/hip_runtime.h>
+
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "cfws.h"
+#include "cfws_internal.h"
+
+// Each unit uses part of what follows.
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Wunused-function"
+
+namespace cfws_rt {
+extern thread_local char g_err[512];
+int set_err(int code, const char* what, hipError_t e);
+int check_init();
+int launch_check(const char* what);
+// cfws_deserialize_plan's body; d_ends (optional) bounds each frame's data
+// (the HTTP/2 receive passes each pooled message's end)
+int deserialize_plan_impl(const void* d_wire, uint64_t wire_size, const uint64_t* d_index,
+                          const uint64_t* d_ends, size_t n, uint64_t max_payload, uint32_t align,
+                          uint32_t flags, cfws_frame_desc_t* d_desc, int32_t* d_status, uint64_t cap,
+                          uint64_t* d_total, void* ws, size_t ws_size, void* stream);
+}  // namespace cfws_rt
+
+namespace {
+
+using cfws_rt::check_init;
+using cfws_rt::deserialize_plan_impl;
+using cfws_rt::launch_check;
+using cfws_rt::set_err;
+
+constexpr int kThreads = 256;
+constexpr int kWaves = kThreads / 64;
+#ifndef CFWS_UNROLL
+#define CFWS_UNROLL 4
+#endif
+constexpr int kUnroll = CFWS_UNROLL;                         // chunks per lane per region
+constexpr uint64_t kChunk = 16;
+constexpr uint64_t kSlice = 64 * kChunk;                     // one wave-instruction: 1 KiB
+constexpr uint64_t kRegion = kSlice * kUnroll;               // one wave's region: 4 KiB
+constexpr int kScanItems = 8;
+constexpr uint64_t kScanBlock = uint64_t(kThreads) * kScanItems;
+// Plan kernels: one frame per thread. Their per-frame work is a chain of
+// dependent loads (descriptor or header bytes), so parallelism beats items
+// per thread: 2,048-frame blocks left 224 of 256 CUs idle at 65,536 frames.
+constexpr int kPlanItems = 1;
+constexpr uint64_t kPlanBlock = uint64_t(kThreads) * kPlanItems;
+
+// Frame classes a pass copies (deserialize): all, data only, control only.
+enum : uint32_t { kClassAll = 0, kClassData = 1, kClassControl = 2 };
+
+// What a streaming pass produces.
+//   kModeSer:    WS serialize    -- header (2-14 B) + masked payload per frame
+//   kModeDeser:  WS deserialize  -- unmasked payload per frame (or any
+//                                   "strip a prefix, copy the body" pass:
+//                                   HTTP/2 DATA unwrap uses it too)
+//   kModeH2Wrap: HTTP/2 DATA wrap -- 9-byte DATA header + a slice of WS wire
+//   kModeH2Ser:  WS serialize straight into HTTP/2 DATA frames -- per DATA
+//                frame: 9-byte DATA header, the WS header when the slice
+//                starts the WS frame, then the masked payload slice (one
+//                pass: the WS wire bytes are never materialised)
+enum : int { kModeSer = 0, kModeDeser = 1, kModeH2Wrap = 2, kModeH2Ser = 3 };
+__host__ __device__ constexpr bool is_ser(int mode) { return mode != kModeDeser; }
+
+// ---------------------------------------------------------------------------
+// workspace layout (deterministic from n_frames and the output capacity)
+// ---------------------------------------------------------------------------
+// hdr[0] pass-0 total (clamped)   hdr[1] pass-1 total (clamped)
+// hdr[2] pass-1 output base       hdr[3] pass-0 grand total   hdr[4] pass-1 grand
+struct WsLayout {
+    uint64_t hdr;
+    uint64_t offs[2];      // u64[n] per pass: sizes, then exclusive offsets
+    uint64_t partials[2];  // u64[scan blocks + 1] per pass
+    uint64_t map[2];       // u32[regions + 2] per pass
+    uint64_t bytes;
+    uint64_t regions;
+    uint64_t scan_blocks;
+};
+
+inline uint64_t align_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
+
+WsLayout ws_layout(uint64_t n, uint64_t capacity)
+{
+    WsLayout L;
+    L.regions = (capacity + kRegion - 1) / kRegion;
+    L.scan_blocks = (n + kPlanBlock - 1) / kPlanBlock;     // >= any run_scan's blocks
+    uint64_t at = 0;
+    L.hdr = at;
+    at += 256;
+    for (int p = 0; p < 2; ++p) { L.offs[p] = at; at = align_up(at + 8 * n, 256); }
+    for (int p = 0; p < 2; ++p) { L.partials[p] = at; at = align_up(at + 8 * (L.scan_blocks + 1), 256); }
+    for (int p = 0; p < 2; ++p) { L.map[p] = at; at = align_up(at + 4 * (L.regions + 2), 256); }
+    L.bytes = at;
+    return L;
+}
+
+// ---------------------------------------------------------------------------
+// device helpers
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t header_size_of(uint64_t n, bool mask)
+{
+    return 2u + (n > 65535u ? 8u : (n > 125u ? 2u : 0u)) + (mask ? 4u : 0u);
+}
+
+__device__ __forceinline__ bool is_control(uint32_t opcode)
+{
+    return opcode <= 0x0fu && (opcode & 0x08u) != 0;       // co_ws_frame.h:32-34
+}
+
+__device__ __forceinline__ uint32_t rotr8(uint32_t key, uint32_t bytes)
+{
+    return __builtin_amdgcn_alignbyte(key, key, bytes & 3u);
+}
+
+// The descriptor is read as four 64-bit words so that a wave-uniform f
+// becomes one s_load_dwordx8 (byte-field loads would be vector loads).
+struct DescWords {
+    uint64_t payload_off, wire_off, payload_size, w3;
+    __device__ uint32_t key() const { return (uint32_t)w3; }
+    __device__ uint32_t fin() const { return (uint32_t)(w3 >> 32) & 0xffu; }
+    __device__ uint32_t opcode() const { return (uint32_t)(w3 >> 40) & 0xffu; }
+    __device__ uint32_t mask() const { return (uint32_t)(w3 >> 48) & 0xffu; }
+    __device__ uint32_t header_size() const { return (uint32_t)(w3 >> 56); }
+};
+
+__device__ __forceinline__ DescWords load_desc(const cfws_frame_desc_t* __restrict__ desc, uint32_t f)
+{
+    const uint64_t* q = reinterpret_cast<const uint64_t*>(desc) + 4 * uint64_t(f);
+    return DescWords{q[0], q[1], q[2], q[3]};
+}
+
+// Arguments of one streaming pass.
+struct Pass {
+    const uint8_t* src;
+    uint8_t* dst;                 // already offset by the pass base
+    const cfws_frame_desc_t* desc;
+    const int32_t* status;        // deserialize only
+    const uint64_t* offs;         // per-frame output offsets of this pass
+    uint64_t total;               // output bytes of this pass
+    uint64_t capacity;            // writable bytes from dst
+    uint32_t n_frames;
+    uint32_t klass;
+    uint32_t sid;                 // HTTP/2 stream id (kModeH2Wrap, kModeH2Ser)
+    const cfws_frame_desc_t* parent;   // kModeH2Ser: the WS frames
+};
+
+// What one frame contributes to a pass's output.
+//   [out_off, out_off + pre)              header bytes (serialize only)
+//   [out_off + pre, + body_len)           src[src_off + k] ^ key[k % 4]
+//   [.., next frame's out_off)            zero (deserialize alignment pad)
+struct FrameView {
+    uint64_t out_off;
+    uint64_t body_start;
+    uint64_t body_len;
+    uint64_t src_off;
+    uint32_t key;   // 0 when the frame is not masked: XOR becomes a copy
+    uint32_t pre;
+    uint32_t hb;    // serialize: header byte 0 | mask bit << 8; DATA: flags
+    uint32_t aux;   // kModeH2Ser: the parent WS frame
+    uint32_t s0;    // kModeH2Ser: the slice's first byte within the WS frame
+    uint64_t ws_len;  // kModeH2Ser: the WS frame's payload size, key and
+    uint32_t ws_key;  //   header byte 0 | mask bit << 8 (its header bytes
+    uint32_t ws_hb;   //   are generated from these)
+};
+
+// Byte r < pre of a serialize frame's header, from its view (co_ws_frame.c:34-91).
+__device__ __forceinline__ uint32_t view_header_byte(const FrameView& v, uint32_t r)
+{
+    const uint64_t n = v.body_len;
+    const uint32_t ext = n > 65535u ? 8u : (n > 125u ? 2u : 0u);
+    const uint32_t l7 = ext == 8 ? 127u : (ext == 2 ? 126u : (uint32_t)n);
+    const uint32_t key_b = (v.key >> (8 * ((r - 2 - ext) & 3u))) & 0xffu;
+    const uint32_t len_b = (uint32_t)(n >> (8 * ((ext - 1 - (r - 2)) & 7u))) & 0xffu;
+    return r == 0 ? (v.hb & 0xffu)
+         : r == 1 ? ((l7 | ((v.hb >> 1) & 0x80u)) & 0xffu)
+         : (r - 2 < ext) ? len_b : key_b;
+}
+
+template <int kMode>
+__device__ __forceinline__ FrameView frame_view(const Pass& P, uint32_t f)
+{
+    const DescWords d = load_desc(P.desc, f);
+    FrameView v;
+    v.key = d.mask() ? d.key() : 0u;
+    v.out_off = P.offs[f];
+    v.hb = 0;
+    v.aux = 0;
+    v.ws_len = 0;
+    v.ws_key = 0;
+    v.ws_hb = 0;
+    v.s0 = 0;
+    if (kMode == kModeH2Ser) {
+        // d: one DATA frame = a slice [payload_off, + payload_size) of the
+        // virtual WS wire arena; key field = its WS frame w
+        const uint32_t wf = d.key();
+        const DescWords w = load_desc(P.parent, wf);
+        const uint64_t s0 = d.payload_off - w.wire_off;
+        const uint64_t hs = w.header_size();
+        const uint64_t h_in = s0 < hs ? (hs - s0 < d.payload_size ? hs - s0 : d.payload_size) : 0;
+        const uint64_t q = s0 + h_in - hs;             // payload index of the body start
+        v.pre = d.payload_size ? 9u + (uint32_t)h_in : 0u;   // unused slots: empty
+        v.body_len = d.payload_size - h_in;
+        v.src_off = w.payload_off + q;
+        v.key = w.mask() ? rotr8(w.key(), (uint32_t)(q & 3u)) : 0u;
+        v.hb = d.fin() ? 0x1u : 0u;                      // DATA flags: END_STREAM
+        v.aux = wf;
+        v.s0 = (uint32_t)s0;                           // only read when h_in > 0 (s0 < 14)
+        v.ws_len = w.payload_size;
+        v.ws_key = w.mask() ? w.key() : 0u;
+        v.ws_hb = ((w.opcode() | (w.fin() ? 0x80u : 0u)) & 0xffu) | (w.mask() ? 0x100u : 0u);
+    } else if (is_ser(kMode)) {
+        v.pre = d.header_size();
+        v.body_len = d.payload_size;
+        v.src_off = d.payload_off;
+        v.hb = kMode == kModeH2Wrap
+                   ? (d.fin() ? 0x1u : 0u)                         // DATA flags: END_STREAM
+                   : ((d.opcode() | (d.fin() ? 0x80u : 0u)) & 0xffu) | (d.mask() ? 0x100u : 0u);
+    } else {
+        const bool ctl = is_control(d.opcode());
+        const bool take = P.klass == kClassAll || (P.klass == kClassControl) == ctl;
+        v.pre = 0;
+        v.body_len = (take && P.status[f] == CFWS_PARSE_COMPLETE) ? d.payload_size : 0;
+        v.src_off = d.wire_off + d.header_size();
+    }
+    v.body_start = v.out_off + v.pre;
+    return v;
+}
+
+// 16-byte global accesses of the streaming paths. Output is written once and
+// never re-read by the kernel, so stores carry the `nt` bit (measured +2-3 %
+// on config 2; -DCFWS_PLAIN_STORE turns it off). `nt` loads measured -10 %
+// and stay off unless -DCFWS_NT_LOAD.
+#ifndef CFWS_PLAIN_STORE
+#define CFWS_NT_STORE 1
+#endif
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint4 ld16(const uint8_t* p)
+{
+#ifdef CFWS_NT_LOAD
+    const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+#else
+    const u32x4 v = *reinterpret_cast<const u32x4*>(p);
+#endif
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+// The streaming kernel's body loads. Every source byte is read by exactly one
+// lane, once, yet `nt` measured slower here (config 2: 6.37/6.49 TB/s plain
+// vs 5.97/6.29 nt, profiles/r01_ab_dpp.json), although the bare copy probe
+// (tools/copy_probe.hip) gains from it; -DCFWS_STREAM_NT turns it on.
+__device__ __forceinline__ uint4 ld16_stream(const uint8_t* p)
+{
+#ifdef CFWS_STREAM_NT
+    const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+    return make_uint4(v.x, v.y, v.z, v.w);
+#else
+    return ld16(p);
+#endif
+}
+
+// Lane i receives lane i + 1's `v` (DPP wave_shl:1); lane 63, which has no
+// right neighbour, keeps `last`.
+__device__ __forceinline__ uint32_t from_next_lane(uint32_t v, uint32_t last)
+{
+    return __builtin_amdgcn_update_dpp(last, v, 0x130, 0xf, 0xf, false);
+}
+
+__device__ __forceinline__ uint4 from_next_lane(const uint4& v, const uint4& last)
+{
+    return make_uint4(from_next_lane(v.x, last.x), from_next_lane(v.y, last.y),
+                      from_next_lane(v.z, last.z), from_next_lane(v.w, last.w));
+}
+
+__device__ __forceinline__ void st16(uint8_t* p, uint4 o)
+{
+    const u32x4 v = {o.x, o.y, o.z, o.w};
+#ifdef CFWS_NT_STORE
+    __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(p));
+#else
+    *reinterpret_cast<u32x4*>(p) = v;
+#endif
+}
+
+// 16 output bytes starting `ph` bytes into the 32-byte window {A, B}.
+__device__ __forceinline__ uint4 funnel16(uint4 A, uint4 B, uint32_t ph)
+{
+    const bool s8 = (ph & 8u) != 0;
+    const bool s4 = (ph & 4u) != 0;
+    const uint32_t r = ph & 3u;
+    const uint32_t a0 = s8 ? A.z : A.x, a1 = s8 ? A.w : A.y, a2 = s8 ? B.x : A.z;
+    const uint32_t a3 = s8 ? B.y : A.w, a4 = s8 ? B.z : B.x, a5 = s8 ? B.w : B.y;
+    const uint32_t b0 = s4 ? a1 : a0, b1 = s4 ? a2 : a1, b2 = s4 ? a3 : a2;
+    const uint32_t b3 = s4 ? a4 : a3, b4 = s4 ? a5 : a4;
+    uint4 o;
+    o.x = __builtin_amdgcn_alignbyte(b1, b0, r);
+    o.y = __builtin_amdgcn_alignbyte(b2, b1, r);
+    o.z = __builtin_amdgcn_alignbyte(b3, b2, r);
+    o.w = __builtin_amdgcn_alignbyte(b4, b3, r);
+    return o;
+}
+
+__device__ __forceinline__ void xor4(uint4& o, uint32_t k)
+{
+    o.x ^= k; o.y ^= k; o.z ^= k; o.w ^= k;
+}
+
+// Byte r of an HTTP/2 DATA frame header (co_http2_frame.c:33-72: 24-bit BE
+// length, type 0, flags, 31-bit BE stream id).
+__device__ __forceinline__ uint32_t h2_header_byte(uint32_t len, uint32_t flags, uint32_t sid,
+                                                   uint32_t r)
+{
+    const uint32_t sidm = sid & 0x7fffffffu;
+    return r == 0 ? (len >> 16) & 0xffu
+         : r == 1 ? (len >> 8) & 0xffu
+         : r == 2 ? len & 0xffu
+         : r == 3 ? 0u
+         : r == 4 ? (flags & 0xffu)
+         : (sidm >> (8 * (8 - r))) & 0xffu;
+}
+
+template <int kMode>
+__device__ __forceinline__ uint32_t header_byte_of(const Pass& P, const FrameView& v, uint32_t r)
+{
+    if (kMode == kModeH2Wrap) return h2_header_byte((uint32_t)v.body_len, v.hb, P.sid, r);
+    if (kMode == kModeH2Ser) {
+        if (r < 9) return h2_header_byte(v.pre - 9u + (uint32_t)v.body_len, v.hb, P.sid, r);
+        // the WS frame's header (co_ws_frame.c:34-91)
+        FrameView wv;
+        wv.body_len = v.ws_len;
+        wv.key = v.ws_key;
+        wv.hb = v.ws_hb;
+        return view_header_byte(wv, r - 9u + v.s0);
+    }
+    return view_header_byte(v, r);
+}
+
+// One chunk entirely inside v's body.
+__device__ __forceinline__ uint4 body_chunk(const uint8_t* __restrict__ src, const FrameView& v,
+                                            uint64_t D)
+{
+    const uint64_t k0 = D - v.body_start;
+    const uint64_t s = v.src_off + k0;
+    const uint8_t* sp = src + (s & ~uint64_t(15));
+    const uint32_t ph = (uint32_t)(s & 15u);
+    uint4 o = ld16(sp);
+    // The aligned block holding the chunk's last byte: it contains a valid
+    // source byte, so it never lies past the allocation's last page.
+    if (ph != 0) o = funnel16(o, ld16(sp + 16), ph);
+    xor4(o, rotr8(v.key, (uint32_t)(k0 & 3u)));
+    return o;
+}
+
+// Chunks that hold more than two frames (runs of frames shorter than ~14
+// bytes): byte by byte, walking frames forward from f. (Loading the views of
+// four bytes at a time measured 30 % slower on config 3: the register cost
+// dropped the edge kernels' occupancy more than the shorter chains saved.)
+template <int kMode>
+__device__ __forceinline__ uint4 edge_chunk_bytes(const Pass& P, uint32_t f, uint64_t D)
+{
+    FrameView v = frame_view<kMode>(P, f);
+    uint64_t next = (f + 1 < P.n_frames) ? P.offs[f + 1] : ~uint64_t(0);
+    uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        const uint64_t pos = D + j;
+        uint32_t b = 0;
+        if (pos < P.total) {
+            while (pos >= next) {
+                ++f;
+                v = frame_view<kMode>(P, f);
+                next = (f + 1 < P.n_frames) ? P.offs[f + 1] : ~uint64_t(0);
+            }
+            const uint64_t r = pos - v.out_off;
+            if (r < v.pre) {
+                b = header_byte_of<kMode>(P, v, (uint32_t)r);
+            } else {
+                const uint64_t k = r - v.pre;
+                if (k < v.body_len) b = (P.src[v.src_off + k] ^ (v.key >> (8 * (k & 3u)))) & 0xffu;
+            }
+        }
+        const uint32_t sh = 8 * (j & 3);
+        if (j < 4) w0 |= b << sh;
+        else if (j < 8) w1 |= b << sh;
+        else if (j < 12) w2 |= b << sh;
+        else w3 |= b << sh;
+    }
+    return make_uint4(w0, w1, w2, w3);
+}
+
+// Frame v's (masked) body bytes lined up with the output chunk at D: byte j
+// of the result is the body byte at output position D + j, for every j
+// whose position lies inside v's body (other bytes are don't-care). One or
+// two aligned source blocks are read -- only blocks that hold a body byte
+// of the chunk -- and shifted once with funnel16; the per-byte assembly in
+// edge_chunk then indexes registers statically (a dynamic byte index into
+// {A, B} is lowered through scratch memory).
+__device__ __forceinline__ uint4 edge_body(const uint8_t* __restrict__ src, const FrameView& v,
+                                           uint64_t D, uint64_t lim)
+{
+    const uint64_t be = v.body_start + v.body_len;
+    const uint64_t lo = D > v.body_start ? D : v.body_start;
+    const uint64_t hi = lim < be ? lim : be;
+    uint4 W = make_uint4(0, 0, 0, 0);
+    if (hi > lo) {
+        const uint64_t s_first = v.src_off + (lo - v.body_start);
+        const uint64_t s_last = v.src_off + (hi - 1 - v.body_start);
+        const uint64_t abase = s_first & ~uint64_t(15);
+        const uint4 A = ld16(src + abase);
+        const uint4 B = ((s_last & ~uint64_t(15)) != abase) ? ld16(src + abase + 16) : A;
+        // window byte ph holds the body byte at output position lo
+        const uint32_t ph = (uint32_t)(s_first - abase);
+        const uint32_t j0 = (uint32_t)(lo - D);                   // 0..15
+        if (ph >= j0) {
+            W = funnel16(A, B, ph - j0);
+        } else {                                                   // body starts mid-chunk
+            W = funnel16(make_uint4(0, 0, 0, 0), A, 16u - (j0 - ph));
+        }
+        xor4(W, rotr8(v.key, (uint32_t)(D - v.body_start) & 3u));
+    }
+    return W;
+}
+
+__device__ __forceinline__ uint32_t u4_byte(const uint4& w, int j)
+{
+    const uint32_t d = j < 4 ? w.x : (j < 8 ? w.y : (j < 12 ? w.z : w.w));
+    return (d >> (8 * (j & 3))) & 0xffu;
+}
+
+// Byte at output position pos of frame v (pos inside v's output range),
+// given v's body bytes lined up with the chunk (edge_body).
+template <int kMode>
+__device__ __forceinline__ uint32_t edge_byte(const Pass& P, const FrameView& v, uint64_t pos,
+                                              const uint4& W, int j)
+{
+    const uint64_t r = pos - v.out_off;
+    if (r < v.pre) return header_byte_of<kMode>(P, v, (uint32_t)r);
+    return (r - v.pre < v.body_len) ? u4_byte(W, j) : 0u;
+}
+
+// A chunk that crosses a header, a frame boundary, padding or the end of
+// the pass. With at most two frames in it (every boundary of frames larger
+// than the chunk) all source blocks are loaded up front and the bytes are
+// assembled in registers: one memory round trip instead of sixteen.
+template <int kMode>
+__device__ __forceinline__ uint4 edge_chunk(const Pass& P, uint32_t f, uint64_t D,
+                                            const FrameView& va, const FrameView& vb, uint64_t o1,
+                                            uint64_t o2)
+{
+    const uint64_t lim = D + 16 < P.total ? D + 16 : P.total;
+    if (o2 < lim) return edge_chunk_bytes<kMode>(P, f, D);
+    const bool two = o1 < lim;
+    const uint4 Wa = edge_body(P.src, va, D, lim);
+    const uint4 Wb = two ? edge_body(P.src, vb, D, lim) : Wa;
+    uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        const uint64_t pos = D + j;
+        uint32_t b = 0;
+        if (pos < lim)
+            b = (two && pos >= o1) ? edge_byte<kMode>(P, vb, pos, Wb, j)
+                                   : edge_byte<kMode>(P, va, pos, Wa, j);
+        const uint32_t sh = 8 * (j & 3);
+        if (j < 4) w0 |= b << sh;
+        else if (j < 8) w1 |= b << sh;
+        else if (j < 12) w2 |= b << sh;
+        else w3 |= b << sh;
+    }
+    return make_uint4(w0, w1, w2, w3);
+}
+
+__device__ __forceinline__ void store_chunk(const Pass& P, uint64_t D, uint4 o)
+{
+    if (D + 16 <= P.capacity) {
+        st16(P.dst + D, o);
+    } else {
+        for (uint32_t j = 0; D + j < P.capacity; ++j) {
+            const uint32_t w = j < 4 ? o.x : (j < 8 ? o.y : (j < 12 ? o.z : o.w));
+            P.dst[D + j] = (uint8_t)(w >> (8 * (j & 3)));
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// the streaming kernel
+// ---------------------------------------------------------------------------
+
+// A region inside one frame's body: frame, source phase and rotated key are
+// wave-uniform (SGPRs); all kUnroll loads are in flight before the first
+// store. Each lane loads the one aligned source block A that holds its
+// chunk's first byte; when the source is misaligned against the output
+// (phase != 0) the block B after it is the next lane's A, taken over DPP, so
+// every source byte is loaded once (lane 63 loads its B itself).
+__device__ __forceinline__ void fast_region(const Pass& P, const FrameView& v, uint64_t base,
+                                            uint32_t lane)
+{
+    const uint64_t delta = v.src_off - v.body_start;           // src = out + delta
+    const uint32_t ph = (uint32_t)(delta & 15u);
+    const uint32_t kr = rotr8(v.key, (uint32_t)((0 - v.body_start) & 3u));
+    const uint8_t* s0 = P.src + ((base + delta) & ~uint64_t(15)) + lane * kChunk;
+    uint8_t* d0 = P.dst + base + lane * kChunk;
+    uint4 a[kUnroll];
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) a[u] = ld16_stream(s0 + u * kSlice);
+    if (ph == 0) {
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) {
+            xor4(a[u], kr);
+            st16(d0 + u * kSlice, a[u]);
+        }
+    } else {
+        // lane 63's B is the block after its A: it holds the chunk's last
+        // byte, a body byte, so it lies inside the source allocation.
+        uint4 e[kUnroll];
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) e[u] = make_uint4(0, 0, 0, 0);
+        if (lane == 63) {
+#pragma unroll
+            for (int u = 0; u < kUnroll; ++u) e[u] = ld16(s0 + u * kSlice + 16);
+        }
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) {
+            uint4 o = funnel16(a[u], from_next_lane(a[u], e[u]), ph);
+            xor4(o, kr);
+            st16(d0 + u * kSlice, o);
+        }
+    }
+}
+
+// A region crossed by exactly one frame boundary (the boundary case of large
+// frames): both views are wave-uniform, each lane picks one by comparing its
+// chunk with the boundary. Chunks not entirely inside a body are left to
+// edge_kernel. As in fast_region, a lane's block B comes from the next lane
+// over DPP when that lane loads it (same frame, chunk inside the body);
+// otherwise (lane 63, the last chunk before a body end) the lane loads it.
+template <int kMode>
+__device__ __forceinline__ void two_frame_region(const Pass& P, const FrameView& va,
+                                                 const FrameView& vb, uint64_t base, uint32_t lane)
+{
+    uint4 a[kUnroll], e[kUnroll];
+    bool fast[kUnroll];
+    uint32_t own_b = 0;
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+        const uint64_t D = base + u * kSlice + lane * kChunk;
+        const bool hi = D >= vb.out_off;
+        const uint64_t bs = hi ? vb.body_start : va.body_start;
+        const uint64_t be = bs + (hi ? vb.body_len : va.body_len);
+        const uint64_t s = (hi ? vb.src_off : va.src_off) + (D - bs);
+        const uint8_t* sp = P.src + (s & ~uint64_t(15));
+        fast[u] = D >= bs && D + kChunk <= be;
+        a[u] = make_uint4(0, 0, 0, 0);
+        e[u] = make_uint4(0, 0, 0, 0);
+        if (fast[u]) {
+            a[u] = ld16_stream(sp);
+            // the next lane's chunk D + 16 loads block sp + 16 iff it is in
+            // the same frame and inside the body
+            const bool next_loads = lane != 63 && (D + kChunk >= vb.out_off) == hi &&
+                                    D + 2 * kChunk <= be;
+            if ((s & 15u) && !next_loads) {
+                e[u] = ld16(sp + 16);
+                own_b |= 1u << u;
+            }
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+        const uint4 nb = from_next_lane(a[u], e[u]);     // every lane: DPP needs the full wave
+        if (!fast[u]) continue;
+        const uint64_t D = base + u * kSlice + lane * kChunk;
+        const bool hi = D >= vb.out_off;
+        const uint64_t k0 = D - (hi ? vb.body_start : va.body_start);
+        const uint32_t ph = (uint32_t)(((hi ? vb.src_off : va.src_off) + k0) & 15u);
+        uint4 o = ph ? funnel16(a[u], (own_b >> u) & 1u ? e[u] : nb, ph) : a[u];
+        xor4(o, rotr8(hi ? vb.key : va.key, (uint32_t)(k0 & 3u)));
+        st16(P.dst + D, o);
+    }
+}
+
+// Any other region (small frames, padding, pass end): every lane finds the
+// frame of each of its chunks by binary search over the region's frames and
+// writes it when it lies inside that frame's body.
+template <int kMode>
+__device__ __forceinline__ void general_region(const Pass& P, uint32_t f0, uint32_t f1,
+                                               uint64_t base, uint32_t lane)
+{
+    uint32_t fr[kUnroll];
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+        const uint64_t D = base + u * kSlice + lane * kChunk;
+        uint32_t lo = f0, hi = f1;                  // largest f with offs[f] <= D
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi + 1) >> 1;
+            if (P.offs[mid] <= D) lo = mid; else hi = mid - 1;
+        }
+        fr[u] = lo;
+    }
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+        const uint64_t D = base + u * kSlice + lane * kChunk;
+        const FrameView v = frame_view<kMode>(P, fr[u]);
+        if (D >= v.body_start && D + kChunk <= v.body_start + v.body_len)
+            st16(P.dst + D, body_chunk(P.src, v, D));
+    }
+}
+
+// The region holding the pass end when a capacity cut ends the pass inside a
+// body: the body chunks below the end only, each store clipped at the
+// capacity (the other region paths write whole bodies' chunks, which would
+// run past a cut).
+template <int kMode>
+__device__ __forceinline__ void tail_region(const Pass& P, uint32_t f0, uint32_t f1, uint64_t base,
+                                            uint32_t lane)
+{
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+        const uint64_t D = base + u * kSlice + lane * kChunk;
+        if (D >= P.total) continue;
+        uint32_t lo = f0, hi = f1;                  // largest f with offs[f] <= D
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi + 1) >> 1;
+            if (P.offs[mid] <= D) lo = mid; else hi = mid - 1;
+        }
+        const FrameView v = frame_view<kMode>(P, lo);
+        if (D >= v.body_start && D + kChunk <= v.body_start + v.body_len)
+            store_chunk(P, D, body_chunk(P.src, v, D));
+    }
+}
+
+// Two threads per frame (part 0: the chunks before the body -- headers;
+// part 1: the chunks reaching past the body end -- the boundary into the
+// next frame, padding, the pass end): the 16-byte chunks that START inside
+// the frame's output range and do not lie entirely inside its body. The
+// kernel is latency-bound (descriptor -> offsets -> source blocks -> store),
+// so the work is spread thin: 64-thread blocks, edge_chunk inlined.
+#ifndef CFWS_EDGE_THREADS
+#define CFWS_EDGE_THREADS 64
+#endif
+constexpr uint32_t kEdgeThreads = CFWS_EDGE_THREADS;
+
+// The edge chunks of frame f in pass P (part 0: before the body; part 1:
+// reaching past the body end).
+template <int kMode>
+__device__ __forceinline__ void edge_frame(const Pass& P, uint64_t f, uint32_t part)
+{
+    // Everything the chunks need that depends on f alone is loaded up front
+    // (frame f and f + 1's descriptors, statuses, offsets): one memory round
+    // trip before the source blocks instead of a chain of six.
+    const uint32_t n = P.n_frames;
+    const uint32_t fa = (uint32_t)f, fb = fa + 1 < n ? fa + 1 : fa;
+    const FrameView va = frame_view<kMode>(P, fa);
+    const FrameView vb = frame_view<kMode>(P, fb);
+    const uint64_t o2 = fa + 2 < n ? P.offs[fa + 2] : ~uint64_t(0);
+    const uint64_t o1 = fa + 1 < n ? vb.out_off : ~uint64_t(0);
+    const uint64_t lo = va.out_off;
+    uint64_t hi = fa + 1 < n ? vb.out_off : P.total;
+    if (hi > P.total) hi = P.total;
+    if (lo >= hi) return;
+    const FrameView& v = va;
+    const uint64_t be = v.body_start + v.body_len;
+    const uint64_t first = (lo + 15) & ~uint64_t(15);
+    if (part == 0) {
+        // chunks before the body (headers): D < body_start
+        for (uint64_t D = first; D < hi && D < v.body_start; D += 16)
+            store_chunk(P, D, edge_chunk<kMode>(P, fa, D, va, vb, o1, o2));
+        return;
+    }
+    // chunks reaching past the body end (boundary, padding, pass end)
+    uint64_t d0 = be >= 15 ? ((be - 15 + 15) & ~uint64_t(15)) : 0;  // first D with D + 16 > be
+    if (d0 < first) d0 = first;
+    if (d0 < v.body_start) d0 = (v.body_start + 15) & ~uint64_t(15);  // header chunks: part 0
+    for (uint64_t D = d0; D < hi; D += 16) {
+        if (D >= be && D + 16 <= hi)          // pure alignment padding / OOM body
+            store_chunk(P, D, make_uint4(0, 0, 0, 0));
+        else
+            store_chunk(P, D, edge_chunk<kMode>(P, fa, D, va, vb, o1, o2));
+    }
+}
+
+template <int kMode>
+__global__ void __launch_bounds__(kEdgeThreads)
+edge_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+            const cfws_frame_desc_t* __restrict__ desc, const int32_t* __restrict__ status,
+            const uint64_t* __restrict__ offs, const uint64_t* __restrict__ total_p,
+            const uint64_t* __restrict__ base_p, uint64_t capacity, uint32_t n_frames,
+            uint32_t klass, uint32_t sid, const cfws_frame_desc_t* __restrict__ parent)
+{
+    const uint64_t t = uint64_t(blockIdx.x) * kEdgeThreads + threadIdx.x;
+    const uint64_t f = t >> 1;
+    if (f >= n_frames) return;
+    const uint64_t out_base = base_p ? *base_p : 0;
+    Pass P;
+    P.src = src;
+    P.dst = dst + out_base;
+    P.desc = desc;
+    P.status = status;
+    P.offs = offs;
+    P.total = *total_p;
+    P.capacity = capacity - out_base;
+    P.n_frames = n_frames;
+    P.klass = klass;
+    P.sid = sid;
+    P.parent = parent;
+    edge_frame<kMode>(P, f, (uint32_t)(t & 1u));
+}
+
+// WS serialize / deserialize carry their edge chunks in the streaming
+// launch; the HTTP/2 modes keep a separate edge launch (their edge code
+// needs more registers than the merged kernel's 5-waves-per-EU budget).
+__host__ __device__ constexpr bool has_edge_blocks(int mode)
+{
+    return mode == kModeSer || mode == kModeDeser;
+}
+
+// The streaming kernel: serialize (kSer) = header + (masked) payload into
+// the wire arena; deserialize = copy + unmask into the payload arena.
+// The first `edge_blocks` workgroups write the edge chunks (edge_frame: two
+// threads per frame); the rest stream the regions, writing every 16-byte
+// chunk that lies inside one frame's body. The two chunk sets are disjoint.
+// Edge workgroups are dispatched first, so their latency-bound chains run
+// under the stream instead of as a launch of their own after it (which cost
+// 17 us serialize / 4 us deserialize on config 2, plus a kernel boundary).
+// The wave-per-EU floor keeps the merged kernel at <= 102 VGPRs, so the
+// 5 workgroups per CU the LDS reservation allows stay resident.
+template <int kMode>
+__global__ void __launch_bounds__(kThreads, 5)
+xform_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+             const cfws_frame_desc_t* __restrict__ desc, const int32_t* __restrict__ status,
+             const uint64_t* __restrict__ offs, const uint32_t* __restrict__ region_map,
+             const uint64_t* __restrict__ total_p, const uint64_t* __restrict__ base_p,
+             uint64_t capacity, uint32_t n_frames, uint32_t klass, uint32_t sid,
+             const cfws_frame_desc_t* __restrict__ parent, uint32_t edge_blocks)
+{
+    const uint64_t out_base = base_p ? *base_p : 0;
+    Pass P;
+    P.src = src;
+    P.dst = dst + out_base;
+    P.desc = desc;
+    P.status = status;
+    P.offs = offs;
+    P.total = *total_p;                              // clamped by the plan
+    P.capacity = capacity - out_base;
+    P.n_frames = n_frames;
+    P.klass = klass;
+    P.sid = sid;
+    P.parent = parent;
+    if (has_edge_blocks(kMode) && blockIdx.x < edge_blocks) {
+        const uint64_t t = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
+        if ((t >> 1) < n_frames) edge_frame<kMode>(P, t >> 1, (uint32_t)(t & 1u));
+        return;
+    }
+    const uint64_t n_regions = (P.total + kRegion - 1) / kRegion;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t stride = uint64_t(gridDim.x - edge_blocks) * kWaves;
+
+    for (uint64_t r = uint64_t(blockIdx.x - edge_blocks) * kWaves + wave; r < n_regions;
+         r += stride) {
+        const uint64_t base = r * kRegion;
+        const uint64_t end = base + kRegion;
+        // The plan writes every entry in [0, n_regions]; the clamps only keep
+        // a corrupted workspace from turning into an out-of-bounds read.
+        uint32_t f0 = region_map[r];
+        uint32_t f1 = region_map[r + 1];
+        if (f1 >= n_frames) f1 = n_frames - 1;
+        if (f0 > f1) f0 = f1;
+        // region_map[r + 1] holds the NEXT region's first byte; frames that
+        // start at or after this region's end do not touch it.
+        if (f1 > f0 && offs[f0 + 1] >= end) f1 = f0;
+        if (end > P.total) {                  // the pass end (a capacity cut may fall in a body)
+            tail_region<kMode>(P, f0, f1, base, lane);
+            continue;
+        }
+        const FrameView va = frame_view<kMode>(P, f0);
+        if (f0 == f1) {
+            if (base >= va.body_start && end <= va.body_start + va.body_len)
+                fast_region(P, va, base, lane);
+            else
+                two_frame_region<kMode>(P, va, va, base, lane);   // partial body, one frame
+        } else if (f1 == f0 + 1 || offs[f0 + 2] >= end) {
+            two_frame_region<kMode>(P, va, frame_view<kMode>(P, f0 + 1), base, lane);
+        } else {
+            general_region<kMode>(P, f0, f1, base, lane);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// plan kernels
+// ---------------------------------------------------------------------------
+// WS header at s of data[0, size) (co_ws_frame.c:131-213), with the callers'
+// two-byte precheck (co_ws_client.c:202-206): the reference's decisions in
+// its order (MORE_DATA before DATA_TOO_BIG). d gets what the reference has
+// written into the frame by the time it returns.
+__device__ __forceinline__ int32_t parse_ws_header(const uint8_t* __restrict__ wire, uint64_t size,
+                                                   uint64_t s, uint64_t max_payload,
+                                                   cfws_frame_desc_t& d)
+{
+    d.payload_off = 0;
+    d.wire_off = s;
+    d.payload_size = 0;
+    d.mask_key = 0;
+    d.fin = 0;
+    d.opcode = 0;
+    d.mask = 0;
+    d.header_size = 0;
+    if (s > size || size - s < 2) return CFWS_PARSE_MORE_DATA;
+    const uint32_t b0 = wire[s], b1 = wire[s + 1];
+    d.fin = (uint8_t)(b0 >> 7);
+    d.opcode = (uint8_t)(b0 & 0x7fu);
+    if (d.opcode > 0x0f) return CFWS_ERROR_INVALID_FRAME;
+    d.mask = (uint8_t)(b1 >> 7);
+    const uint32_t l7 = b1 & 0x7fu;
+    uint64_t p = s + 2;
+    if (l7 <= 125) {
+        d.payload_size = l7;
+    } else {
+        const uint32_t ext = (l7 == 126) ? 2u : 8u;
+        if (size - p < ext) return CFWS_PARSE_MORE_DATA;
+        uint64_t len = 0;
+        for (uint32_t i = 0; i < ext; ++i) len = (len << 8) | wire[p + i];
+        d.payload_size = len;
+        p += ext;
+    }
+    if (d.mask) {
+        if (size - p < 4) return CFWS_PARSE_MORE_DATA;
+        d.mask_key = (uint32_t)wire[p] | (uint32_t)wire[p + 1] << 8 |
+                     (uint32_t)wire[p + 2] << 16 | (uint32_t)wire[p + 3] << 24;
+        p += 4;
+    }
+    d.header_size = (uint8_t)(p - s);
+    if (size - p < d.payload_size) return CFWS_PARSE_MORE_DATA;
+    if (d.payload_size > max_payload) return CFWS_ERROR_DATA_TOO_BIG;
+    return CFWS_PARSE_COMPLETE;
+}
+
+// Exclusive block scan of one value per thread; *block_total gets the sum.
+__device__ __forceinline__ uint64_t block_exclusive_scan(uint64_t x, uint64_t* s_wave,
+                                                         uint64_t* block_total)
+{
+    const uint32_t lane = threadIdx.x & 63u, wid = threadIdx.x >> 6;
+    uint64_t inc = x;
+#pragma unroll
+    for (uint32_t o = 1; o < 64; o <<= 1) {
+        const uint64_t y = __shfl_up(inc, o, 64);
+        if (lane >= o) inc += y;
+    }
+    __syncthreads();
+    if (lane == 63) s_wave[wid] = inc;
+    __syncthreads();
+    uint64_t before = 0, all = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < kWaves; ++w) {
+        if (w < wid) before += s_wave[w];
+        all += s_wave[w];
+    }
+    *block_total = all;
+    return before + inc - x;
+}
+
+__global__ void __launch_bounds__(kThreads)
+scan_reduce_kernel(const uint64_t* __restrict__ vals, uint64_t n, uint64_t* __restrict__ partials)
+{
+    __shared__ uint64_t s_wave[kWaves];
+    const uint64_t b0 = uint64_t(blockIdx.x) * kScanBlock;
+    uint64_t sum = 0;
+#pragma unroll
+    for (int k = 0; k < kScanItems; ++k) {
+        const uint64_t i = b0 + uint64_t(k) * kThreads + threadIdx.x;
+        if (i < n) sum += vals[i];
+    }
+    uint64_t total;
+    block_exclusive_scan(sum, s_wave, &total);
+    if (threadIdx.x == 0) partials[blockIdx.x] = total;
+}
+
+__global__ void __launch_bounds__(kThreads)
+scan_partials_kernel(uint64_t* __restrict__ partials, uint64_t nb, uint64_t* __restrict__ grand)
+{
+    __shared__ uint64_t s_wave[kWaves];
+    uint64_t carry = 0;
+    for (uint64_t b = 0; b < nb; b += kThreads) {
+        const uint64_t i = b + threadIdx.x;
+        const uint64_t x = i < nb ? partials[i] : 0;
+        uint64_t tot;
+        const uint64_t ex = block_exclusive_scan(x, s_wave, &tot);
+        if (i < nb) partials[i] = carry + ex;
+        carry += tot;
+    }
+    if (threadIdx.x == 0) *grand = carry;
+}
+
+// scan_partials_kernel for up to two passes in one launch (block p: pass p).
+__global__ void __launch_bounds__(kThreads)
+scan_partials2_kernel(uint64_t* __restrict__ partials0, uint64_t* __restrict__ partials1, uint64_t nb,
+                      uint64_t* __restrict__ grand0, uint64_t* __restrict__ grand1)
+{
+    __shared__ uint64_t s_wave[kWaves];
+    uint64_t* partials = blockIdx.x ? partials1 : partials0;
+    uint64_t carry = 0;
+    for (uint64_t b = 0; b < nb; b += kThreads) {
+        const uint64_t i = b + threadIdx.x;
+        const uint64_t x = i < nb ? partials[i] : 0;
+        uint64_t tot;
+        const uint64_t ex = block_exclusive_scan(x, s_wave, &tot);
+        if (i < nb) partials[i] = carry + ex;
+        carry += tot;
+    }
+    if (threadIdx.x == 0) *(blockIdx.x ? grand1 : grand0) = carry;
+}
+
+__global__ void __launch_bounds__(kThreads)
+scan_apply_kernel(uint64_t* __restrict__ vals, uint64_t n, const uint64_t* __restrict__ partials)
+{
+    __shared__ uint64_t s_wave[kWaves];
+    const uint64_t i0 = uint64_t(blockIdx.x) * kScanBlock + uint64_t(threadIdx.x) * kScanItems;
+    uint64_t v[kScanItems];
+    uint64_t sum = 0;
+#pragma unroll
+    for (int k = 0; k < kScanItems; ++k) {
+        v[k] = (i0 + k < n) ? vals[i0 + k] : 0;
+        sum += v[k];
+    }
+    uint64_t tot;
+    uint64_t run = block_exclusive_scan(sum, s_wave, &tot) + partials[blockIdx.x];
+#pragma unroll
+    for (int k = 0; k < kScanItems; ++k) {
+        if (i0 + k < n) vals[i0 + k] = run;
+        run += v[k];
+    }
+}
+
+// Fills the region -> first-frame map of one pass over [0, total).
+__device__ __forceinline__ void map_regions(const uint64_t* __restrict__ offs, uint64_t f, uint64_t n,
+                                            uint64_t grand, uint64_t total, uint32_t* __restrict__ map)
+{
+    const uint64_t lo = offs[f];
+    const uint64_t hi = (f + 1 < n) ? offs[f + 1] : grand;
+    const uint64_t a = lo < total ? lo : total;
+    const uint64_t b = hi < total ? hi : total;
+    if (b > a) {
+        const uint64_t r1 = (b + kRegion - 1) / kRegion;
+        for (uint64_t r = (a + kRegion - 1) / kRegion; r < r1; ++r) map[r] = (uint32_t)f;
+    }
+    if (f == n - 1) map[(total + kRegion - 1) / kRegion] = (uint32_t)(n - 1);
+}
+
+// Region-map entries of one frame's output bytes [lo, hi) of a pass over
+// [0, total): every region whose first byte lies inside gets the frame.
+__device__ __forceinline__ void map_range(uint64_t lo, uint64_t hi, uint64_t f, uint64_t total,
+                                          uint32_t* __restrict__ map)
+{
+    const uint64_t a = lo < total ? lo : total;
+    const uint64_t b = hi < total ? hi : total;
+    if (b > a) {
+        const uint64_t r1 = (b + kRegion - 1) / kRegion;
+        for (uint64_t r = (a + kRegion - 1) / kRegion; r < r1; ++r) map[r] = (uint32_t)f;
+    }
+}
+
+// This block's exclusive prefix and the grand total, straight from the
+// per-block sums the reduce kernel wrote (plans of up to kSelfScanBlocks
+// blocks: every apply block reads them all, <= 16 KiB from L2, instead of
+// a scan launch between the two).
+constexpr uint64_t kSelfScanBlocks = 2048;
+
+__device__ __forceinline__ void prefix_from_partials(const uint64_t* __restrict__ partials, uint64_t nb,
+                                                     uint64_t b, uint64_t* s_wave, uint64_t& before,
+                                                     uint64_t& all)
+{
+    uint64_t xb = 0, xa = 0;
+    for (uint64_t i = threadIdx.x; i < nb; i += kThreads) {
+        const uint64_t v = partials[i];
+        xa += v;
+        if (i < b) xb += v;
+    }
+    block_exclusive_scan(xb, s_wave, &before);
+    block_exclusive_scan(xa, s_wave, &all);
+}
+
+// ---- plans: two launches each (three above kSelfScanBlocks blocks) ---------
+// 1. per frame: sizes (serialize: header size, co_ws_frame.c:41-91;
+//    deserialize: the header decode) + the block's sum;
+// (2. scan_partials_kernel: the block sums, one block per pass -- only when
+//    there are more than kSelfScanBlocks blocks; otherwise step 3 sums them);
+// 3. per block: exclusive offsets of its frames, then everything the
+//    offsets decide (descriptor offsets, capacity rule, region maps, totals).
+
+// Offsets into the descriptors, the capacity rule (a COMPLETE frame with a
+// payload that does not fit gets CFWS_ERROR_OUT_OF_MEMORY, like the
+// reference's failed malloc, co_ws_frame.c:216-223), region maps, totals.
+__global__ void __launch_bounds__(kThreads)
+deserialize_plan_apply_kernel(cfws_frame_desc_t* __restrict__ desc, int32_t* __restrict__ status,
+                              uint64_t* __restrict__ vals0, uint64_t* __restrict__ vals1, uint64_t n,
+                              const uint64_t* __restrict__ partials0,
+                              const uint64_t* __restrict__ partials1, uint64_t nb,
+                              uint32_t self_scan, uint64_t* __restrict__ hdr,
+                              uint64_t capacity, uint32_t reassemble, uint32_t* __restrict__ map0,
+                              uint32_t* __restrict__ map1, uint64_t* __restrict__ user_total)
+{
+    __shared__ uint64_t s_wave[kWaves];
+    uint64_t pre0, pre1 = 0, g0, g1 = 0;
+    if (self_scan) {
+        prefix_from_partials(partials0, nb, blockIdx.x, s_wave, pre0, g0);
+        if (reassemble) prefix_from_partials(partials1, nb, blockIdx.x, s_wave, pre1, g1);
+    } else {
+        pre0 = partials0[blockIdx.x];
+        g0 = hdr[3];
+        if (reassemble) {
+            pre1 = partials1[blockIdx.x];
+            g1 = hdr[4];
+        }
+    }
+    const uint64_t t0 = g0 < capacity ? g0 : capacity;
+    const uint64_t room1 = capacity - t0;
+    const uint64_t t1 = g1 < room1 ? g1 : room1;
+    const uint64_t i0 = uint64_t(blockIdx.x) * kPlanBlock + uint64_t(threadIdx.x) * kPlanItems;
+    uint64_t v0[kPlanItems], v1[kPlanItems];
+    uint64_t s0 = 0, s1 = 0;
+#pragma unroll
+    for (int k = 0; k < kPlanItems; ++k) {
+        v0[k] = (i0 + k < n) ? vals0[i0 + k] : 0;
+        v1[k] = (reassemble && i0 + k < n) ? vals1[i0 + k] : 0;
+        s0 += v0[k];
+        s1 += v1[k];
+    }
+    uint64_t tot;
+    uint64_t run0 = block_exclusive_scan(s0, s_wave, &tot) + pre0;
+    uint64_t run1 = 0;
+    if (reassemble) run1 = block_exclusive_scan(s1, s_wave, &tot) + pre1;
+#pragma unroll
+    for (int k = 0; k < kPlanItems; ++k) {
+        const uint64_t f = i0 + k;
+        if (f < n) {
+            vals0[f] = run0;
+            const bool ctl = reassemble && is_control(desc[f].opcode);
+            const uint64_t off = ctl ? g0 + run1 : run0;
+            desc[f].payload_off = off;
+            const uint64_t len = desc[f].payload_size;
+            if (status[f] == CFWS_PARSE_COMPLETE && len > 0 && off + len > capacity)
+                status[f] = CFWS_ERROR_OUT_OF_MEMORY;
+            map_range(run0, run0 + v0[k], f, t0, map0);
+            if (reassemble) {
+                vals1[f] = run1;
+                map_range(run1, run1 + v1[k], f, t1, map1);
+            }
+            if (f == n - 1) {
+                map0[(t0 + kRegion - 1) / kRegion] = (uint32_t)f;
+                if (reassemble) map1[(t1 + kRegion - 1) / kRegion] = (uint32_t)f;
+                hdr[0] = t0;
+                hdr[1] = t1;
+                hdr[2] = t0;
+                if (self_scan) {
+                    hdr[3] = g0;
+                    if (reassemble) hdr[4] = g1;
+                }
+                if (user_total) *user_total = t0 + t1;
+            }
+        }
+        run0 += v0[k];
+        run1 += v1[k];
+    }
+}
+
+// ---------------------------------------------------------------------------
+// host-side launch helpers
+// ---------------------------------------------------------------------------
+inline uint32_t grid_for(uint64_t items, uint64_t per_block)
+{
+    const uint64_t g = (items + per_block - 1) / per_block;
+    return (uint32_t)(g == 0 ? 1 : g);
+}
+
+// One 4 KiB region per wave (measured fastest: no grid-stride loop, every
+// wave's loads in flight at once); CFWS_GRID caps the workgroup count.
+inline uint32_t stream_grid(uint64_t regions)
+{
+    static uint64_t cap = 0;
+    if (cap == 0) {
+        const char* s = getenv("CFWS_GRID");
+        cap = s ? strtoull(s, nullptr, 10) : 0;
+        if (cap == 0) cap = 0x7fffffffull;
+    }
+    uint64_t g = (regions + kWaves - 1) / kWaves;
+    if (g > cap) g = cap;
+    return (uint32_t)(g == 0 ? 1 : g);
+}
+
+template <typename T>
+T* ws_ptr(const void* ws, uint64_t off)
+{
+    return reinterpret_cast<T*>(static_cast<char*>(const_cast<void*>(ws)) + off);
+}
+
+inline int run_scan(uint64_t* vals, uint64_t n, uint64_t* partials, uint64_t* grand, hipStream_t st)
+{
+    const uint32_t nb = grid_for(n, kScanBlock);
+    scan_reduce_kernel<<<nb, kThreads, 0, st>>>(vals, n, partials);
+    scan_partials_kernel<<<1, kThreads, 0, st>>>(partials, nb, grand);
+    scan_apply_kernel<<<nb, kThreads, 0, st>>>(vals, n, partials);
+    return launch_check("scan");
+}
+
+inline bool misaligned(const void* a, const void* b)
+{
+    return ((reinterpret_cast<uintptr_t>(a) | reinterpret_cast<uintptr_t>(b)) & 15u) != 0;
+}
+
+inline int zero_totals(const WsLayout& L, void* ws, uint64_t* d_total, hipStream_t st)
+{
+    (void)hipMemsetAsync(ws_ptr<uint64_t>(ws, L.hdr), 0, 64, st);
+    if (d_total) (void)hipMemsetAsync(d_total, 0, 8, st);
+    return launch_check("zero totals");
+}
+
+// Dynamic LDS the streaming kernel reserves per workgroup. It is never
+// touched: it only caps residency at 5 workgroups (20 waves) per CU. More
+// resident streams contend for HBM pages: at the register-limited 8 per CU
+// the kernel ran 8-12 % slower, at 7 6 % slower; 5 measured best with the
+// DPP body path (config 2: 6.44/6.46 TB/s vs 6.44/6.40 at 6 and 6.41/6.42 at
+// 4; profiles/r01_ab_dpp.json, tools/ab.sh). CFWS_XFORM_LDS overrides (0 = none).
+constexpr uint32_t kXformLdsDefault = 32000;     // 5 x fits 160 KiB, 6 x does not
+
+inline uint32_t xform_lds_bytes()
+{
+    static int64_t v = -1;
+    if (v < 0) {
+        const char* s = getenv("CFWS_XFORM_LDS");
+        v = s ? (int64_t)strtoull(s, nullptr, 10) : kXformLdsDefault;
+        if (v > 65536) v = 65536;
+    }
+    return (uint32_t)v;
+}
+
+// One pass: the streaming kernel with its edge workgroups in front
+// (CFWS_EDGE_SPLIT=1: the edge chunks as a launch of their own after it, the
+// previous layout, kept for A/B).
+inline bool edge_split()
+{
+    static int v = -1;
+    if (v < 0) {
+        const char* s = getenv("CFWS_EDGE_SPLIT");
+        v = (s && *s == '1') ? 1 : 0;
+    }
+    return v == 1;
+}
+
+template <int kMode>
+void launch_streaming(const void* src, void* dst, const cfws_frame_desc_t* desc,
+                      const int32_t* status, const uint64_t* offs, const uint32_t* map,
+                      const uint64_t* total_p, const uint64_t* base_p, uint64_t regions,
+                      uint64_t cap, size_t n, uint32_t klass, uint32_t sid, hipStream_t st,
+                      const cfws_frame_desc_t* parent = nullptr, bool edges = true)
+{
+    const bool split = edges && (edge_split() || !has_edge_blocks(kMode));
+    const uint32_t eb = (edges && !split) ? grid_for(2 * (uint64_t)n, kThreads) : 0;
+    xform_kernel<kMode><<<eb + stream_grid(regions), kThreads, xform_lds_bytes(), st>>>(
+        static_cast<const uint8_t*>(src), static_cast<uint8_t*>(dst), desc, status, offs, map,
+        total_p, base_p, cap, (uint32_t)n, klass, sid, parent, eb);
+    // (a separate edge launch on a second stream, overlapping the streaming
+    // kernel, measured no faster on config 5: the stream slowed by what the
+    // overlap saved)
+    if (split) edge_kernel<kMode><<<grid_for(2 * (uint64_t)n, kEdgeThreads), kEdgeThreads, 0, st>>>(
+        static_cast<const uint8_t*>(src), static_cast<uint8_t*>(dst), desc, status, offs,
+        total_p, base_p, cap, (uint32_t)n, klass, sid, parent);
+}
+
+template <int kMode>
+void launch_pass(const WsLayout& L, int p, const void* src, void* dst, const cfws_frame_desc_t* desc,
+                 const int32_t* status, const void* ws, uint64_t cap, size_t n, uint32_t klass,
+                 hipStream_t st, uint32_t sid = 0, bool edges = true)
+{
+    const uint64_t* hdr = ws_ptr<const uint64_t>(ws, L.hdr);
+    // Pass 1 (reassembly: control frames, <= 125-byte payloads each) is
+    // usually tiny or empty, and its size is only known on the device: a
+    // capped grid (the kernel strides over the regions) instead of one
+    // workgroup per 16 KiB of capacity, which cost ~20 us of empty dispatch.
+    const uint64_t regions = p == 1 ? (L.regions < 4096 ? L.regions : 4096) : L.regions;
+    launch_streaming<kMode>(src, dst, desc, status, ws_ptr<const uint64_t>(ws, L.offs[p]),
+                            ws_ptr<const uint32_t>(ws, L.map[p]), hdr + p,
+                            p == 1 ? hdr + 2 : nullptr, regions, cap, n, klass, sid, st, nullptr,
+                            edges);
+}
+
+}  // namespace
+
+#pragma clang diagnostic pop
+
+#endif

@@ -1,0 +1,513 @@
+// cfws_ops.hip -- the codec's smaller device operations and their C ABI
+// (include/cfws.h): split header / payload passes over caller-laid-out frames
+// (cfws_encode_headers, cfws_parse_headers, cfws_mask_batch,
+// cfws_unmask_batch), handshake accept keys, the multi-connection receive
+// walk, the single-buffer XOR of the per-frame drop-in, the D2H copy into
+// mapped host memory, and the synthetic fill.
+#include "cfws_kernels.h"
+
+namespace {
+
+// ---- split ops: header and payload passes over caller-laid-out frames -----
+
+// co_ws_frame.c:34-91 for every frame: its 2-14 header bytes at wire_off,
+// one thread per frame; bytes at or past cap are not written.
+__global__ void __launch_bounds__(kThreads)
+encode_headers_kernel(cfws_frame_desc_t* __restrict__ desc, uint64_t n, uint8_t* __restrict__ wire,
+                      uint64_t cap)
+{
+    const uint64_t f = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
+    if (f >= n) return;
+    const DescWords d = load_desc(desc, (uint32_t)f);
+    const uint32_t hs = header_size_of(d.payload_size, d.mask() != 0);
+    FrameView v;
+    v.body_len = d.payload_size;
+    v.key = d.mask() ? d.key() : 0u;
+    v.hb = ((d.opcode() | (d.fin() ? 0x80u : 0u)) & 0xffu) | (d.mask() ? 0x100u : 0u);
+#pragma unroll
+    for (uint32_t r = 0; r < 14; ++r)
+        if (r < hs && d.wire_off + r < cap) wire[d.wire_off + r] = (uint8_t)view_header_byte(v, r);
+    desc[f].header_size = (uint8_t)hs;
+}
+
+// co_ws_frame.c:131-213 (+ the callers' 2-byte precheck) at every frame
+// start, one thread per frame: cfws_deserialize_plan's decode without the
+// payload layout.
+__global__ void __launch_bounds__(kThreads)
+parse_headers_kernel(const uint8_t* __restrict__ wire, uint64_t size, const uint64_t* __restrict__ index,
+                     uint64_t n, uint64_t max_payload, cfws_frame_desc_t* __restrict__ desc,
+                     int32_t* __restrict__ status)
+{
+    const uint64_t f = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
+    if (f >= n) return;
+    cfws_frame_desc_t d;
+    status[f] = parse_ws_header(wire, size, index[f], max_payload, d);
+    desc[f] = d;
+}
+
+// The payload loops (mask: co_ws_frame.c:93-97, unmask: :232-242) of every
+// frame, each frame from its own source to its own destination. Work unit
+// (frame, piece): a workgroup writes the 16-byte destination chunks of one
+// frame, 1,024 per pass (4 per lane, loads in flight before the stores),
+// striding by `pieces` passes. Chunks inside the frame are one 16-byte store
+// (source funnel-shifted into place); the frame's first and last chunk, which
+// it may share with its neighbours, are written byte by byte.
+constexpr uint32_t kPieceChunks = 4 * kThreads;
+
+template <bool kUnmask>
+__global__ void __launch_bounds__(kThreads)
+payload_xor_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                   const cfws_frame_desc_t* __restrict__ desc, const int32_t* __restrict__ status,
+                   uint64_t n, uint32_t pieces, uint64_t cap)
+{
+    const uint64_t f = blockIdx.x / pieces;
+    const uint32_t p = blockIdx.x % pieces;
+    if (f >= n) return;
+    if (kUnmask && status && status[f] != CFWS_PARSE_COMPLETE) return;
+    const DescWords d = load_desc(desc, (uint32_t)f);
+    const uint64_t len = d.payload_size;
+    const uint64_t so = kUnmask ? d.wire_off + d.header_size() : d.payload_off;
+    const uint64_t dof = kUnmask ? d.payload_off : d.wire_off + header_size_of(len, d.mask() != 0);
+    const uint32_t key = d.mask() ? d.key() : 0u;
+    if (len == 0 || dof >= cap) return;
+    const uint64_t dend = len < cap - dof ? dof + len : cap;
+    const uint64_t c0 = dof & ~uint64_t(15);
+    const uint64_t nchunks = (dend - c0 + 15) >> 4;
+    // source phase against the 16-byte destination chunks: one per frame
+    const uint32_t ph = (uint32_t)((so - dof) & 15u);
+    const uint32_t lane = threadIdx.x & 63u;
+    for (uint64_t base = uint64_t(p) * kPieceChunks; base < nchunks;
+         base += uint64_t(pieces) * kPieceChunks) {
+        // a lane's block B is the next lane's A (DPP) when that lane's chunk
+        // is full too; lane 63 and the last full chunk load their own
+        uint4 a[4], e[4];
+        bool full[4];
+        uint32_t own_b = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint64_t A = c0 + 16 * (base + uint64_t(k) * kThreads + threadIdx.x);
+            full[k] = A >= dof && A + 16 <= dend;
+            a[k] = make_uint4(0, 0, 0, 0);
+            e[k] = make_uint4(0, 0, 0, 0);
+            if (full[k]) {
+                const uint8_t* sp = src + ((so + (A - dof)) & ~uint64_t(15));
+                a[k] = ld16(sp);
+                // the block holding the chunk's last source byte: a payload byte
+                if (ph && (lane == 63 || A + 32 > dend)) {
+                    e[k] = ld16(sp + 16);
+                    own_b |= 1u << k;
+                }
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint4 nb = from_next_lane(a[k], e[k]);     // every lane: DPP needs the full wave
+            const uint64_t c = base + uint64_t(k) * kThreads + threadIdx.x;
+            const uint64_t A = c0 + 16 * c;
+            if (full[k]) {
+                uint4 o = ph ? funnel16(a[k], (own_b >> k) & 1u ? e[k] : nb, ph) : a[k];
+                xor4(o, rotr8(key, (uint32_t)((A - dof) & 3u)));
+                st16(dst + A, o);
+            } else if (c < nchunks) {
+                for (uint32_t j = 0; j < 16; ++j) {
+                    const uint64_t x = A + j;
+                    if (x < dof || x >= dend) continue;
+                    const uint64_t kk = x - dof;
+                    dst[x] = (uint8_t)(src[so + kk] ^ (key >> (8 * (kk & 3u))));
+                }
+            }
+        }
+    }
+}
+
+// Device -> host copy by a kernel (cfws_copy_to_host): 16-byte stores into
+// device-mapped pinned host memory, any alignment on either side. Running the
+// D2H leg this way beside an SDMA H2D measured 43 GB/s each way against 28
+// for two SDMA copies (tools/pcie_probe2.hip). Each lane writes whole
+// destination-aligned 16-byte chunks (source funnel-shifted into place); the
+// first and last chunk, which the destination may share with other data,
+// byte by byte. The chunk grid starts on a kCopyOutAlign boundary of the
+// destination, so each wave's 64 x 16 B of stores is one aligned 1 KiB span
+// of PCIe writes wherever the caller's destination starts.
+#ifndef CFWS_COPY_OUT_ALIGN
+#define CFWS_COPY_OUT_ALIGN 1024
+#endif
+constexpr uintptr_t kCopyOutAlign = CFWS_COPY_OUT_ALIGN;
+
+__global__ void __launch_bounds__(kThreads)
+copy_out_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, uint64_t n)
+{
+    const uintptr_t d0 = reinterpret_cast<uintptr_t>(dst);
+    const uintptr_t c0 = d0 & ~(kCopyOutAlign - 1);
+    const uint64_t nchunks = (d0 + n - c0 + 15) >> 4;
+    const uint32_t ph = (uint32_t)((reinterpret_cast<uintptr_t>(src) - d0) & 15u);
+    const uint64_t stride = uint64_t(gridDim.x) * kThreads;
+    for (uint64_t c = uint64_t(blockIdx.x) * kThreads + threadIdx.x; c < nchunks; c += stride) {
+        const uintptr_t A = c0 + 16 * c;
+        if (A >= d0 && A + 16 <= d0 + n) {
+            const uint8_t* sp = reinterpret_cast<const uint8_t*>(
+                (reinterpret_cast<uintptr_t>(src) + (A - d0)) & ~uintptr_t(15));
+            uint4 o = ld16(sp);
+            if (ph) o = funnel16(o, ld16(sp + 16), ph);    // holds the chunk's last source byte
+            *reinterpret_cast<u32x4*>(A) = u32x4{o.x, o.y, o.z, o.w};
+        } else {
+            for (uint32_t j = 0; j < 16; ++j) {
+                const uintptr_t x = A + j;
+                if (x >= d0 && x < d0 + n) *reinterpret_cast<uint8_t*>(x) = src[x - d0];
+            }
+        }
+    }
+}
+
+__global__ void __launch_bounds__(kThreads)
+xor_mask_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, uint64_t n,
+                uint32_t key, uint32_t phase)
+{
+    const uint64_t stride = uint64_t(gridDim.x) * kThreads;
+    const uint64_t nv = n / 16;
+    const uint32_t kr = rotr8(key, phase);
+    const bool aligned = ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15u) == 0;
+    const uint64_t tid = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
+    if (aligned) {
+        for (uint64_t i = tid; i < nv; i += stride) {
+            uint4 v = reinterpret_cast<const uint4*>(src)[i];
+            xor4(v, kr);
+            reinterpret_cast<uint4*>(dst)[i] = v;
+        }
+        for (uint64_t i = nv * 16 + tid; i < n; i += stride)
+            dst[i] = src[i] ^ (uint8_t)(kr >> (8 * (i & 3)));
+    } else {
+        for (uint64_t i = tid; i < n; i += stride)
+            dst[i] = src[i] ^ (uint8_t)(kr >> (8 * (i & 3)));
+    }
+}
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t seed, uint64_t i)
+{
+    uint64_t z = seed + (i + 1) * 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+__global__ void __launch_bounds__(kThreads)
+fill_splitmix_kernel(uint8_t* __restrict__ dst, uint64_t n, uint64_t seed, uint64_t word_base)
+{
+    const uint64_t stride = uint64_t(gridDim.x) * kThreads;
+    const uint64_t nv = n / 16;
+    for (uint64_t i = uint64_t(blockIdx.x) * kThreads + threadIdx.x; i < nv; i += stride) {
+        const uint64_t a = splitmix64(seed, word_base + 2 * i);
+        const uint64_t b = splitmix64(seed, word_base + 2 * i + 1);
+        reinterpret_cast<uint4*>(dst)[i] =
+            make_uint4((uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32));
+    }
+    const uint64_t t = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
+    if (t < (n & 15u)) {
+        const uint64_t o = nv * 16 + t;
+        dst[o] = (uint8_t)(splitmix64(seed, word_base + o / 8) >> (8 * (o & 7)));
+    }
+}
+
+// ---------------------------------------------------------------------------
+// handshake accept keys (co_ws_create_base64_accept_key,
+// co_ws_http_extension.c:26-57): base64(SHA-1(key || GUID))
+// ---------------------------------------------------------------------------
+__constant__ char kWsGuid[37] = "258EAFA5-E914-47DA-95CA-C5AB0DC85B11";
+__constant__ char kB64[65] = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789+/";
+
+// Byte i of the SHA-1 input key || GUID || 0x80 || 0... || bit length (BE64)
+// over `blocks` 64-byte blocks.
+__device__ __forceinline__ uint32_t accept_msg_byte(const uint8_t* __restrict__ key, uint64_t L,
+                                                    uint64_t blocks, uint64_t i)
+{
+    const uint64_t m = L + 36;
+    if (i < L) return key[i];
+    if (i < m) return (uint8_t)kWsGuid[i - L];
+    if (i == m) return 0x80u;
+    const uint64_t end = blocks * 64;
+    if (i >= end - 8) return (uint32_t)((m * 8) >> (8 * (end - 1 - i))) & 0xffu;
+    return 0;
+}
+
+__device__ __forceinline__ uint32_t rol32(uint32_t v, int b) { return (v << b) | (v >> (32 - b)); }
+
+// One thread per connection: a connection storm's accept keys at once.
+__global__ void __launch_bounds__(kThreads)
+ws_accept_kernel(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ key_off, uint64_t n,
+                 char* __restrict__ out)
+{
+    const uint64_t c = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
+    if (c >= n) return;
+    const uint8_t* key = keys + key_off[c];
+    const uint64_t L = key_off[c + 1] - key_off[c];
+    const uint64_t blocks = (L + 36 + 9 + 63) / 64;
+    uint32_t st[5] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u, 0xc3d2e1f0u};
+    for (uint64_t b = 0; b < blocks; ++b) {
+        uint32_t w[16];
+#pragma unroll
+        for (int t = 0; t < 16; ++t) {
+            const uint64_t i = b * 64 + 4 * t;
+            w[t] = accept_msg_byte(key, L, blocks, i) << 24 | accept_msg_byte(key, L, blocks, i + 1) << 16 |
+                   accept_msg_byte(key, L, blocks, i + 2) << 8 | accept_msg_byte(key, L, blocks, i + 3);
+        }
+        uint32_t a = st[0], bb = st[1], cc = st[2], d = st[3], e = st[4];
+#pragma unroll
+        for (int r = 0; r < 80; ++r) {
+            if (r >= 16)
+                w[r & 15] = rol32(w[(r + 13) & 15] ^ w[(r + 8) & 15] ^ w[(r + 2) & 15] ^ w[r & 15], 1);
+            const uint32_t f = r < 20 ? ((bb & cc) | (~bb & d))
+                             : r < 40 ? (bb ^ cc ^ d)
+                             : r < 60 ? ((bb & cc) | (bb & d) | (cc & d)) : (bb ^ cc ^ d);
+            const uint32_t k = r < 20 ? 0x5a827999u : r < 40 ? 0x6ed9eba1u : r < 60 ? 0x8f1bbcdcu : 0xca62c1d6u;
+            const uint32_t t = rol32(a, 5) + f + e + k + w[r & 15];
+            e = d; d = cc; cc = rol32(bb, 30); bb = a; a = t;
+        }
+        st[0] += a; st[1] += bb; st[2] += cc; st[3] += d; st[4] += e;
+    }
+    // base64 of the 20 hash bytes: 6 full groups + 2 bytes -> 3 chars + '='
+    char* o = out + CFWS_WS_ACCEPT_SLOT * c;
+#pragma unroll
+    for (int g = 0; g < 7; ++g) {
+        uint32_t v = 0;
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            const int idx = 3 * g + j;
+            const uint32_t byte = idx < 20 ? (st[idx >> 2] >> (8 * (3 - (idx & 3)))) & 0xffu : 0u;
+            v = v << 8 | byte;
+        }
+        o[4 * g] = kB64[(v >> 18) & 63];
+        o[4 * g + 1] = kB64[(v >> 12) & 63];
+        o[4 * g + 2] = kB64[(v >> 6) & 63];
+        o[4 * g + 3] = g < 6 ? kB64[v & 63] : '=';
+    }
+    o[28] = 0;
+}
+
+// ---------------------------------------------------------------------------
+// receive-buffer frame indexing (co_ws_server.c:107-169)
+// ---------------------------------------------------------------------------
+
+// One connection per thread: the receive loop's walk over buf[begin, end).
+// The walk is a chain of dependent header reads, so a connection is one
+// thread and the parallelism is across connections (a server's event loop
+// tick holds the receive buffers of many). Pass 1 (kWrite = false) counts
+// and records consumed / stop; pass 2 walks again and writes the starts at
+// the scanned offsets.
+template <bool kWrite>
+__global__ void __launch_bounds__(kThreads)
+index_walk_kernel(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ begin,
+                  const uint64_t* __restrict__ end, uint64_t n, uint64_t max_payload,
+                  uint64_t* __restrict__ first, uint64_t* __restrict__ consumed,
+                  int32_t* __restrict__ stop, uint64_t* __restrict__ starts, uint64_t cap)
+{
+    const uint64_t c = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
+    if (c >= n) return;
+    const uint64_t e = end[c];
+    uint64_t p = begin[c];
+    uint64_t k = kWrite ? first[c] : 0;
+    int32_t st = CFWS_PARSE_COMPLETE;
+    while (e > p) {
+        if (e - p < 2) { st = CFWS_PARSE_MORE_DATA; break; }
+        cfws_frame_desc_t d;
+        st = parse_ws_header(buf, e, p, max_payload, d);
+        if (st != CFWS_PARSE_COMPLETE) break;
+        if (kWrite && k < cap) starts[k] = p;
+        ++k;
+        p += d.header_size + d.payload_size;
+    }
+    if (!kWrite) {
+        first[c] = k;
+        consumed[c] = p;
+        stop[c] = st;
+    }
+}
+
+}  // namespace
+
+int cfws_internal_copy_out(const void* d_src, void* dev_dst, uint64_t n, void* stream)
+{
+    if (n == 0) return CFWS_OK;
+    const uint64_t chunks = (n + kCopyOutAlign) / 16 + 1;
+    const uint64_t blocks = (chunks + kThreads - 1) / kThreads;
+    copy_out_kernel<<<(uint32_t)(blocks < 1024 ? blocks : 1024), kThreads, 0,
+                      static_cast<hipStream_t>(stream)>>>(static_cast<const uint8_t*>(d_src),
+                                                          static_cast<uint8_t*>(dev_dst), n);
+    return launch_check("copy_to_host");
+}
+
+extern "C" {
+
+size_t cfws_index_workspace_size(size_t n_conns)
+{
+    return 64 + sizeof(uint64_t) * (size_t)grid_for(n_conns, kScanBlock);
+}
+
+int cfws_index_frames_batch(const void* d_buf, const uint64_t* d_begin, const uint64_t* d_end,
+                            size_t n, uint64_t max_payload, uint64_t* d_starts, uint64_t cap,
+                            uint64_t* d_first, uint64_t* d_consumed, int32_t* d_stop,
+                            uint64_t* d_total, void* ws, size_t ws_size, void* stream)
+{
+    if (int rc = check_init()) return rc;
+    if (ws_size < cfws_index_workspace_size(n))
+        return set_err(CFWS_ERROR_WORKSPACE, "index workspace too small", hipSuccess);
+    if ((n && (!d_buf || !d_begin || !d_end || !d_first || !d_consumed || !d_stop)) ||
+        (cap && !d_starts) || !d_total || !ws)
+        return set_err(CFWS_ERROR_INVALID_ARGUMENT, "index: null pointer", hipSuccess);
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    if (n == 0) {
+        (void)hipMemsetAsync(d_total, 0, 8, st);
+        return launch_check("index");
+    }
+    const uint8_t* buf = static_cast<const uint8_t*>(d_buf);
+    uint64_t* partials = ws_ptr<uint64_t>(ws, 64);
+    const uint32_t g = grid_for(n, kThreads);
+    index_walk_kernel<false><<<g, kThreads, 0, st>>>(buf, d_begin, d_end, n, max_payload, d_first,
+                                                     d_consumed, d_stop, nullptr, 0);
+    if (int rc = run_scan(d_first, n, partials, d_total, st)) return rc;
+    index_walk_kernel<true><<<g, kThreads, 0, st>>>(buf, d_begin, d_end, n, max_payload, d_first,
+                                                    nullptr, nullptr, d_starts, cap);
+    return launch_check("index");
+}
+
+int cfws_ws_accept_keys_batch(const void* d_keys, const uint64_t* d_key_off, size_t n,
+                              char* d_accept, void* stream)
+{
+    if (int rc = check_init()) return rc;
+    if (n == 0) return CFWS_OK;
+    if (!d_keys || !d_key_off || !d_accept)
+        return set_err(CFWS_ERROR_INVALID_ARGUMENT, "accept keys: null pointer", hipSuccess);
+    ws_accept_kernel<<<grid_for(n, kThreads), kThreads, 0, static_cast<hipStream_t>(stream)>>>(
+        static_cast<const uint8_t*>(d_keys), d_key_off, n, d_accept);
+    return launch_check("ws_accept_keys");
+}
+
+void* cfws_mapped_device_pointer(const void* h_ptr)
+{
+    if (check_init() != CFWS_OK || !h_ptr) return nullptr;
+    unsigned flags = 0;
+    void* d = nullptr;
+    if (hipHostGetFlags(&flags, const_cast<void*>(h_ptr)) != hipSuccess || !(flags & hipHostMallocMapped) ||
+        hipHostGetDevicePointer(&d, const_cast<void*>(h_ptr), 0) != hipSuccess) {
+        (void)hipGetLastError();     // not a mapped HIP host allocation: no sticky error
+        return nullptr;
+    }
+    return d;
+}
+
+int cfws_copy_to_host(const void* d_src, void* h_dst, uint64_t n, void* stream)
+{
+    if (int rc = check_init()) return rc;
+    if (n == 0) return CFWS_OK;
+    if (!d_src || !h_dst) return set_err(CFWS_ERROR_INVALID_ARGUMENT, "null pointer", hipSuccess);
+    void* d = cfws_mapped_device_pointer(h_dst);
+    if (!d) return set_err(CFWS_ERROR_INVALID_ARGUMENT, "destination is not mapped pinned host memory",
+                           hipSuccess);
+    return cfws_internal_copy_out(d_src, d, n, stream);
+}
+
+int cfws_encode_headers(cfws_frame_desc_t* d_desc, size_t n, void* d_wire, uint64_t wire_capacity,
+                        void* stream)
+{
+    if (int rc = check_init()) return rc;
+    if (n == 0) return CFWS_OK;
+    if (!d_desc || !d_wire) return set_err(CFWS_ERROR_INVALID_ARGUMENT, "null pointer", hipSuccess);
+    if (n > 0xffffffffull) return set_err(CFWS_ERROR_INVALID_ARGUMENT, "too many frames", hipSuccess);
+    encode_headers_kernel<<<grid_for(n, kThreads), kThreads, 0, static_cast<hipStream_t>(stream)>>>(
+        d_desc, n, static_cast<uint8_t*>(d_wire), wire_capacity);
+    return launch_check("encode_headers");
+}
+
+int cfws_parse_headers(const void* d_wire, uint64_t wire_size, const uint64_t* d_frame_index, size_t n,
+                       uint64_t max_payload, cfws_frame_desc_t* d_desc, int32_t* d_status,
+                       void* stream)
+{
+    if (int rc = check_init()) return rc;
+    if (n == 0) return CFWS_OK;
+    if (!d_wire || !d_frame_index || !d_desc || !d_status)
+        return set_err(CFWS_ERROR_INVALID_ARGUMENT, "null pointer", hipSuccess);
+    parse_headers_kernel<<<grid_for(n, kThreads), kThreads, 0, static_cast<hipStream_t>(stream)>>>(
+        static_cast<const uint8_t*>(d_wire), wire_size, d_frame_index, n, max_payload, d_desc,
+        d_status);
+    return launch_check("parse_headers");
+}
+
+}  // extern "C"
+
+namespace {
+
+// Pieces per frame for the split payload ops: enough workgroups to cover the
+// largest frame in one pass, capped so the grid stays under 2^31 blocks.
+uint32_t payload_pieces(size_t n, uint64_t max_payload_size)
+{
+    const uint64_t chunks = max_payload_size / 16 + 2;
+    uint64_t pieces = (chunks + kPieceChunks - 1) / kPieceChunks;
+    if (pieces > 65536) pieces = 65536;
+    while (pieces > 1 && pieces * n > 0x7fffffffull) pieces >>= 1;
+    return (uint32_t)pieces;
+}
+
+template <bool kUnmask>
+int launch_payload_xor(const void* src, void* dst, const cfws_frame_desc_t* d_desc,
+                       const int32_t* d_status, size_t n, uint64_t max_payload_size, uint64_t cap,
+                       void* stream, const char* what)
+{
+    if (int rc = check_init()) return rc;
+    if (n == 0 || cap == 0) return CFWS_OK;
+    if (!src || !dst || !d_desc) return set_err(CFWS_ERROR_INVALID_ARGUMENT, "null pointer", hipSuccess);
+    if (misaligned(src, dst))
+        return set_err(CFWS_ERROR_INVALID_ARGUMENT, "arenas must be 16-byte aligned", hipSuccess);
+    if (n > 0x7fffffffull) return set_err(CFWS_ERROR_INVALID_ARGUMENT, "too many frames", hipSuccess);
+    const uint32_t pieces = payload_pieces(n, max_payload_size);
+    payload_xor_kernel<kUnmask><<<(uint32_t)(n * pieces), kThreads, xform_lds_bytes(),
+                                  static_cast<hipStream_t>(stream)>>>(
+        static_cast<const uint8_t*>(src), static_cast<uint8_t*>(dst), d_desc, d_status, n, pieces, cap);
+    return launch_check(what);
+}
+
+}  // namespace
+
+extern "C" {
+
+int cfws_mask_batch(const void* d_payload, const cfws_frame_desc_t* d_desc, size_t n,
+                    uint64_t max_payload_size, void* d_wire, uint64_t wire_capacity, void* stream)
+{
+    return launch_payload_xor<false>(d_payload, d_wire, d_desc, nullptr, n, max_payload_size,
+                                     wire_capacity, stream, "mask_batch");
+}
+
+int cfws_unmask_batch(const void* d_wire, const cfws_frame_desc_t* d_desc, const int32_t* d_status,
+                      size_t n, uint64_t max_payload_size, void* d_payload,
+                      uint64_t payload_capacity, void* stream)
+{
+    return launch_payload_xor<true>(d_wire, d_payload, d_desc, d_status, n, max_payload_size,
+                                    payload_capacity, stream, "unmask_batch");
+}
+
+int cfws_xor_mask(const void* d_src, void* d_dst, uint64_t n, uint32_t key, uint32_t phase,
+                  void* stream)
+{
+    if (int rc = check_init()) return rc;
+    if (n == 0) return CFWS_OK;
+    const uint64_t blocks = (n / 16 + kThreads - 1) / kThreads;
+    const uint32_t g = (uint32_t)(blocks == 0 ? 1 : (blocks < 4096 ? blocks : 4096));
+    xor_mask_kernel<<<g, kThreads, 0, static_cast<hipStream_t>(stream)>>>(
+        static_cast<const uint8_t*>(d_src), static_cast<uint8_t*>(d_dst), n, key, phase & 3u);
+    return launch_check("xor_mask");
+}
+
+int cfws_fill_splitmix(void* d_dst, uint64_t n, uint64_t seed, uint64_t byte_base, void* stream)
+{
+    if (int rc = check_init()) return rc;
+    if (byte_base & 7u) return set_err(CFWS_ERROR_INVALID_ARGUMENT, "byte_base % 8 != 0", hipSuccess);
+    if (reinterpret_cast<uintptr_t>(d_dst) & 15u)
+        return set_err(CFWS_ERROR_INVALID_ARGUMENT, "destination must be 16-byte aligned", hipSuccess);
+    if (n == 0) return CFWS_OK;
+    const uint64_t blocks = (n / 16 + kThreads - 1) / kThreads;
+    const uint32_t g = (uint32_t)(blocks == 0 ? 1 : (blocks < 8192 ? blocks : 8192));
+    fill_splitmix_kernel<<<g, kThreads, 0, static_cast<hipStream_t>(stream)>>>(
+        static_cast<uint8_t*>(d_dst), n, seed, byte_base / 8);
+    return launch_check("fill_splitmix");
+}
+
+}  // extern "C"
+
