@@ -1,5 +1,8 @@
-// cfws_device.hip -- MI355X (gfx950) kernels and batch C ABI of the
-// WebSocket frame codec (include/cfws.h).
+// cfws_device.hip -- MI355X (gfx950) WebSocket frame codec: the batch C ABI
+// (include/cfws.h: serialize / deserialize plan, execute, batch), its plan
+// kernels and the single-launch small-batch kernels, and the library's
+// error state. The streaming kernel and the device code the units share are
+// in cfws_kernels.h; HTTP/2 in cfws_h2.hip; the smaller ops in cfws_ops.hip.
 //
 // Reference behaviour restated on the device:
 //   header encode        co_ws_frame.c:34-68, :70-91
