@@ -1131,18 +1131,24 @@ inline int zero_totals(const WsLayout& L, void* ws, uint64_t* d_total, hipStream
 // resident streams contend for HBM pages: at the register-limited 8 per CU
 // the kernel ran 8-12 % slower, at 7 6 % slower; 5 measured best with the
 // DPP body path (config 2: 6.44/6.46 TB/s vs 6.44/6.40 at 6 and 6.41/6.42 at
-// 4; profiles/r01_ab_dpp.json, tools/ab.sh). CFWS_XFORM_LDS overrides (0 = none).
+// 4; profiles/r01_ab_dpp.json, tools/ab.sh). The WS serialize kernel (96
+// VGPRs) is register-limited to 5 per CU already, and there the reservation
+// only cost: config 3 serialize 6.20 TB/s without it against 6.02-6.10 with
+// (config 2 6.27 vs 6.29; the 78-80-VGPR modes reach 6 per CU without it and
+// lose 8 % on config 2 deserialize). So kModeSer reserves none by default.
+// CFWS_XFORM_LDS overrides for every mode (0 = none).
 constexpr uint32_t kXformLdsDefault = 32000;     // 5 x fits 160 KiB, 6 x does not
 
-inline uint32_t xform_lds_bytes()
+inline uint32_t xform_lds_bytes(int mode = -1)
 {
-    static int64_t v = -1;
-    if (v < 0) {
+    static int64_t v = -2;                      // -1: no override
+    if (v == -2) {
         const char* s = getenv("CFWS_XFORM_LDS");
-        v = s ? (int64_t)strtoull(s, nullptr, 10) : kXformLdsDefault;
+        v = s ? (int64_t)strtoull(s, nullptr, 10) : -1;
         if (v > 65536) v = 65536;
     }
-    return (uint32_t)v;
+    if (v >= 0) return (uint32_t)v;
+    return mode == kModeSer ? 0u : kXformLdsDefault;
 }
 
 // One pass: the streaming kernel with its edge workgroups in front
@@ -1167,7 +1173,7 @@ void launch_streaming(const void* src, void* dst, const cfws_frame_desc_t* desc,
 {
     const bool split = edges && (edge_split() || !has_edge_blocks(kMode));
     const uint32_t eb = (edges && !split) ? grid_for(2 * (uint64_t)n, kThreads) : 0;
-    xform_kernel<kMode><<<eb + stream_grid(regions), kThreads, xform_lds_bytes(), st>>>(
+    xform_kernel<kMode><<<eb + stream_grid(regions), kThreads, xform_lds_bytes(kMode), st>>>(
         static_cast<const uint8_t*>(src), static_cast<uint8_t*>(dst), desc, status, offs, map,
         total_p, base_p, cap, (uint32_t)n, klass, sid, parent, eb);
     // (a separate edge launch on a second stream, overlapping the streaming
