@@ -717,12 +717,15 @@ edge_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
     edge_frame<kMode>(P, f, (uint32_t)(t & 1u));
 }
 
-// WS serialize / deserialize carry their edge chunks in the streaming
-// launch; the HTTP/2 modes keep a separate edge launch (their edge code
-// needs more registers than the merged kernel's 5-waves-per-EU budget).
+// WS serialize / deserialize and the fused WS-over-HTTP/2 send carry their
+// edge chunks in the streaming launch. The send's edge code spills 112 bytes
+// per lane there (96 VGPRs, 5 waves per SIMD, the residency the LDS
+// reservation sets anyway) and still measured 12 us per config-5 step faster
+// than its own launch (xform<3> 352 us against 338 + 26). The two-pass wrap
+// (max_frame_size < 64) keeps a separate edge launch.
 __host__ __device__ constexpr bool has_edge_blocks(int mode)
 {
-    return mode == kModeSer || mode == kModeDeser;
+    return mode == kModeSer || mode == kModeDeser || mode == kModeH2Ser;
 }
 
 // The streaming kernel: serialize (kSer) = header + (masked) payload into
