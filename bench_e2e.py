@@ -25,6 +25,20 @@ sys.path.insert(0, ROOT)
 GIB = float(1 << 30)
 
 
+def bind_numa_node(node: int) -> list[int]:
+    """Restricts this process (every thread it starts from here on) to the
+    CPUs of NUMA node `node`, read from sysfs. Called before torch / HIP load,
+    so the pipeline's threads and the first touch of the host arenas stay on
+    that node (no numactl on the image)."""
+    cpus = []
+    with open(f"/sys/devices/system/node/node{node}/cpulist") as f:
+        for part in f.read().strip().split(","):
+            lo, _, hi = part.partition("-")
+            cpus.extend(range(int(lo), int(hi or lo) + 1))
+    os.sched_setaffinity(0, cpus)
+    return cpus
+
+
 def host_buffer(args, n):
     import torch
 
@@ -97,7 +111,8 @@ def e2e_h2(args):
             "serialize_GiBps": round(nbytes / t_ser / GIB, 2),
             "deserialize_GiBps": round(nbytes / t_de / GIB, 2),
             "round_trip_GiBps": round(2 * nbytes / (t_ser + t_de) / GIB, 2), "host": args.host,
-            "d2h": args.d2h, "timing": f"median of {args.reps} reps after one warm-up", "verified": ok}
+            "d2h": args.d2h, "numa_node": args.numa_node,
+            "timing": f"median of {args.reps} reps after one warm-up", "verified": ok}
     print(json.dumps(line), flush=True)
     return 0 if ok else 1
 
@@ -117,7 +132,11 @@ def main():
                     help="host arenas: mapped pinned memory (hipHostMallocMapped; the D2H leg "
                          "may be a kernel writing it, cfws_copy_to_host) or torch pinned memory "
                          "(the D2H leg is an SDMA copy)")
+    ap.add_argument("--numa-node", type=int, default=-1,
+                    help="bind to this NUMA node's CPUs before HIP loads (-1: the OS's choice)")
     args = ap.parse_args()
+    if args.numa_node >= 0:
+        bind_numa_node(args.numa_node)
 
     import numpy as np
     import torch
@@ -197,7 +216,7 @@ def main():
         "round_trip_GiBps": round(2 * nbytes / (t_ser + t_de) / GIB, 2),
         "receive_s": round(t_rx, 4), "receive_GiBps": round(nbytes / t_rx / GIB, 2),
         "timing": f"median of {args.reps} reps after one warm-up",
-        "host": args.host, "d2h": args.d2h,
+        "host": args.host, "d2h": args.d2h, "numa_node": args.numa_node,
         "pinned_h2d_GBps": round(h2d, 1), "pinned_d2h_GBps": round(d2h, 1),
         "verified": ok,
     }
