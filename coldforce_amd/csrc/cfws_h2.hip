@@ -388,6 +388,23 @@ h2_starts_kernel(const uint64_t* __restrict__ ends, const uint64_t* __restrict__
 // unmasks each DATA frame's slice of its message's WS payload directly from
 // the HTTP/2 arena (one streaming pass instead of pool + deserialize).
 
+// Bytes [b, b + k) of global memory, k <= 16, into w (little-endian; bytes
+// past k are unspecified): the up to five aligned dwords that hold them,
+// issued as independent loads, funnel-shifted by b's alignment. Only dwords
+// holding at least one of the k bytes are read (no access past the span's
+// last mapped dword).
+__device__ __forceinline__ void load_span16(const uint8_t* b, uint32_t k, uint32_t (&w)[4])
+{
+    const uint32_t o = (uint32_t)(reinterpret_cast<uintptr_t>(b) & 3u);
+    const uint32_t* p = reinterpret_cast<const uint32_t*>(b - o);
+    const uint32_t nd = k ? (o + k + 3u) >> 2 : 0u;
+    uint32_t x[5];
+#pragma unroll
+    for (uint32_t j = 0; j < 5; ++j) x[j] = j < nd ? p[j] : 0u;
+#pragma unroll
+    for (uint32_t t = 0; t < 4; ++t) w[t] = __builtin_amdgcn_alignbyte(x[t + 1], x[t], o);
+}
+
 // co_ws_frame_deserialize on each pooled message [starts[m], ends[m])
 // (co_ws_http2_extension.c:134-164), header bytes gathered from the DATA
 // frames; same outputs as deserialize_parse_kernel on the pool.
@@ -408,25 +425,29 @@ h2_msg_parse_kernel(const uint8_t* __restrict__ h2, const cfws_frame_desc_t* __r
     uint64_t v = 0;
     if (m < n_msg) {
         const uint64_t s = starts[m], len = ends[m] - s;
-        uint8_t hb[16];
         const uint32_t k = len < 14 ? (uint32_t)len : 14u;
         uint64_t d = first[m];
         const uint64_t l0 = h2_status[d] == CFWS_H2_PARSE_COMPLETE ? pdesc[d].payload_size : 0;
+        uint32_t w[4] = {0u, 0u, 0u, 0u};
         if (s + k <= poff[d] + l0) {
             // the whole header in the first DATA frame (every frame of >= 14
-            // bytes): one base, independent byte loads
-            const uint8_t* b = h2 + pdesc[d].wire_off + pdesc[d].header_size + (s - poff[d]);
-            for (uint32_t i = 0; i < k; ++i) hb[i] = b[i];
+            // bytes): the aligned dwords holding [b, b + k), issued together
+            // (a byte loop here compiled to one memory round trip per byte)
+            load_span16(h2 + pdesc[d].wire_off + pdesc[d].header_size + (s - poff[d]), k, w);
         } else {
-            for (uint32_t i = 0; i < k; ++i) {
+            // the header straddles DATA frames: walk them byte by byte
+#pragma unroll
+            for (uint32_t i = 0; i < 14; ++i) {
+                if (i >= k) break;
                 const uint64_t p = s + i;
                 while (p >= poff[d] + (h2_status[d] == CFWS_H2_PARSE_COMPLETE ? pdesc[d].payload_size : 0))
                     ++d;
-                hb[i] = h2[pdesc[d].wire_off + pdesc[d].header_size + (p - poff[d])];
+                w[i >> 2] |= (uint32_t)h2[pdesc[d].wire_off + pdesc[d].header_size + (p - poff[d])]
+                             << (8u * (i & 3u));
             }
         }
         cfws_frame_desc_t dd;
-        const int32_t st = parse_ws_header(hb, len, 0, max_payload, dd);
+        const int32_t st = parse_ws_header_regs(w, len, max_payload, dd);
         dd.wire_off = s;
         mdesc[m] = dd;
         mstatus[m] = st;

@@ -720,9 +720,11 @@ edge_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
 // WS serialize / deserialize and the fused WS-over-HTTP/2 send carry their
 // edge chunks in the streaming launch. The send's edge code spills 112 bytes
 // per lane there (96 VGPRs, 5 waves per SIMD, the residency the LDS
-// reservation sets anyway) and still measured 12 us per config-5 step faster
-// than its own launch (xform<3> 352 us against 338 + 26). The two-pass wrap
-// (max_frame_size < 64) keeps a separate edge launch.
+// reservation sets anyway); the spills sit in the edge branch only, none in
+// the region loop. It still measured 12 us per config-5 step faster than its
+// own launch (xform<3> 352 us against 338 + 26), and 1.5 % faster than 4
+// workgroups per CU without spills (CFWS_H2SER_MIN_BLOCKS=4: 122 VGPRs). The
+// two-pass wrap (max_frame_size < 64) keeps a separate edge launch.
 __host__ __device__ constexpr bool has_edge_blocks(int mode)
 {
     return mode == kModeSer || mode == kModeDeser || mode == kModeH2Ser;
@@ -738,8 +740,12 @@ __host__ __device__ constexpr bool has_edge_blocks(int mode)
 // 17 us serialize / 4 us deserialize on config 2, plus a kernel boundary).
 // The wave-per-EU floor keeps the merged kernel at <= 102 VGPRs, so the
 // 5 workgroups per CU the LDS reservation allows stay resident.
+// workgroups per CU the send's streaming kernel is compiled for (A/B knob)
+#ifndef CFWS_H2SER_MIN_BLOCKS
+#define CFWS_H2SER_MIN_BLOCKS 5
+#endif
 template <int kMode>
-__global__ void __launch_bounds__(kThreads, 5)
+__global__ void __launch_bounds__(kThreads, kMode == kModeH2Ser ? CFWS_H2SER_MIN_BLOCKS : 5)
 xform_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
              const cfws_frame_desc_t* __restrict__ desc, const int32_t* __restrict__ status,
              const uint64_t* __restrict__ offs, const uint32_t* __restrict__ region_map,
@@ -808,9 +814,11 @@ xform_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
 // two-byte precheck (co_ws_client.c:202-206): the reference's decisions in
 // its order (MORE_DATA before DATA_TOO_BIG). d gets what the reference has
 // written into the frame by the time it returns.
-__device__ __forceinline__ int32_t parse_ws_header(const uint8_t* __restrict__ wire, uint64_t size,
-                                                   uint64_t s, uint64_t max_payload,
-                                                   cfws_frame_desc_t& d)
+// `at(i)` returns byte i of the data (an arena, or header bytes held in
+// registers: parse_ws_header_regs).
+template <typename At>
+__device__ __forceinline__ int32_t parse_ws_header_by(At at, uint64_t size, uint64_t s,
+                                                      uint64_t max_payload, cfws_frame_desc_t& d)
 {
     d.payload_off = 0;
     d.wire_off = s;
@@ -821,7 +829,7 @@ __device__ __forceinline__ int32_t parse_ws_header(const uint8_t* __restrict__ w
     d.mask = 0;
     d.header_size = 0;
     if (s > size || size - s < 2) return CFWS_PARSE_MORE_DATA;
-    const uint32_t b0 = wire[s], b1 = wire[s + 1];
+    const uint32_t b0 = at(s), b1 = at(s + 1);
     d.fin = (uint8_t)(b0 >> 7);
     d.opcode = (uint8_t)(b0 & 0x7fu);
     if (d.opcode > 0x0f) return CFWS_ERROR_INVALID_FRAME;
@@ -834,20 +842,49 @@ __device__ __forceinline__ int32_t parse_ws_header(const uint8_t* __restrict__ w
         const uint32_t ext = (l7 == 126) ? 2u : 8u;
         if (size - p < ext) return CFWS_PARSE_MORE_DATA;
         uint64_t len = 0;
-        for (uint32_t i = 0; i < ext; ++i) len = (len << 8) | wire[p + i];
+        if (ext == 2) {
+            len = (uint64_t)at(p) << 8 | at(p + 1);
+        } else {
+#pragma unroll
+            for (uint32_t i = 0; i < 8; ++i) len = (len << 8) | at(p + i);
+        }
         d.payload_size = len;
         p += ext;
     }
     if (d.mask) {
         if (size - p < 4) return CFWS_PARSE_MORE_DATA;
-        d.mask_key = (uint32_t)wire[p] | (uint32_t)wire[p + 1] << 8 |
-                     (uint32_t)wire[p + 2] << 16 | (uint32_t)wire[p + 3] << 24;
+        d.mask_key = at(p) | at(p + 1) << 8 | at(p + 2) << 16 | at(p + 3) << 24;
         p += 4;
     }
     d.header_size = (uint8_t)(p - s);
     if (size - p < d.payload_size) return CFWS_PARSE_MORE_DATA;
     if (d.payload_size > max_payload) return CFWS_ERROR_DATA_TOO_BIG;
     return CFWS_PARSE_COMPLETE;
+}
+
+__device__ __forceinline__ int32_t parse_ws_header(const uint8_t* __restrict__ wire, uint64_t size,
+                                                   uint64_t s, uint64_t max_payload,
+                                                   cfws_frame_desc_t& d)
+{
+    return parse_ws_header_by([wire](uint64_t i) -> uint32_t { return wire[i]; }, size, s,
+                              max_payload, d);
+}
+
+// The same parse over header bytes gathered into registers: w holds bytes
+// 0-15 of the frame little-endian (a frame starts at 0, `size` bytes long).
+// Byte selection is by compare + select, so w stays in VGPRs (an indexed
+// byte array here was placed in LDS).
+__device__ __forceinline__ int32_t parse_ws_header_regs(const uint32_t (&w)[4], uint64_t size,
+                                                        uint64_t max_payload, cfws_frame_desc_t& d)
+{
+    const uint32_t w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3];
+    return parse_ws_header_by(
+        [=](uint64_t i) -> uint32_t {
+            const uint32_t q = (uint32_t)(i >> 2);
+            const uint32_t x = q == 0 ? w0 : q == 1 ? w1 : q == 2 ? w2 : w3;
+            return (x >> (8u * (uint32_t)(i & 3u))) & 0xffu;
+        },
+        size, 0, max_payload, d);
 }
 
 // Exclusive block scan of one value per thread; *block_total gets the sum.
