@@ -80,9 +80,8 @@ namespace {
 
 using cfws_rt::g_err;
 
-// Both reassembly passes in one launch: a frame has bytes in exactly one of
-// them (data frames in pass 0, control frames in pass 1), so each thread
-// serves its frame's pass only.
+// Both reassembly passes' edge chunks in one launch of their own (the
+// CFWS_EDGE_SPLIT=1 form; by default pass 0's streaming launch carries them).
 __global__ void __launch_bounds__(kEdgeThreads)
 edge_reasm_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
                   const cfws_frame_desc_t* __restrict__ desc, const int32_t* __restrict__ status,
@@ -90,25 +89,9 @@ edge_reasm_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
                   const uint64_t* __restrict__ hdr, uint64_t capacity, uint32_t n_frames)
 {
     const uint64_t t = uint64_t(blockIdx.x) * kEdgeThreads + threadIdx.x;
-    const uint64_t f = t >> 1;
-    if (f >= n_frames) return;
-    const uint32_t p = is_control(desc[f].opcode) ? 1u : 0u;
-    const uint64_t out_base = p ? hdr[2] : 0;
-    Pass P;
-    P.src = src;
-    P.dst = dst + out_base;
-    P.desc = desc;
-    P.status = status;
-    P.offs = p ? offs1 : offs0;
-    P.total = hdr[p];
-    // pass 0's last chunk must not write past the data bytes: pass 1 starts
-    // there (at an unaligned address) and runs concurrently in this launch
-    P.capacity = p ? capacity - out_base : (hdr[0] < capacity ? hdr[0] : capacity);
-    P.n_frames = n_frames;
-    P.klass = p ? kClassControl : kClassData;
-    P.sid = 0;
-    P.parent = nullptr;
-    edge_frame<kModeDeser>(P, f, (uint32_t)(t & 1u));
+    if ((t >> 1) >= n_frames) return;
+    reasm_edge_frame(src, dst, desc, status, offs0, offs1, hdr, capacity, n_frames, t >> 1,
+                     (uint32_t)(t & 1u));
 }
 
 // ---------------------------------------------------------------------------
@@ -661,14 +644,18 @@ int cfws_deserialize_execute(const void* d_wire, const cfws_frame_desc_t* d_desc
     const WsLayout L = ws_layout(n, cap);
     hipStream_t st = static_cast<hipStream_t>(stream);
     if (flags & CFWS_DESERIALIZE_REASSEMBLE) {
+        // every edge chunk of both passes is disjoint from the body chunks
+        // either streaming pass writes, so pass 0's launch carries them all
+        const bool split = edge_split();
         launch_pass<kModeDeser>(L, 0, d_wire, d_payload, d_desc, d_status, ws, cap, n, kClassData, st,
-                                0, false);
+                                0, !split, !split);
         launch_pass<kModeDeser>(L, 1, d_wire, d_payload, d_desc, d_status, ws, cap, n, kClassControl,
                                 st, 0, false);
-        edge_reasm_kernel<<<grid_for(2 * (uint64_t)n, kEdgeThreads), kEdgeThreads, 0, st>>>(
-            static_cast<const uint8_t*>(d_wire), static_cast<uint8_t*>(d_payload), d_desc, d_status,
-            ws_ptr<const uint64_t>(ws, L.offs[0]), ws_ptr<const uint64_t>(ws, L.offs[1]),
-            ws_ptr<const uint64_t>(ws, L.hdr), cap, (uint32_t)n);
+        if (split)
+            edge_reasm_kernel<<<grid_for(2 * (uint64_t)n, kEdgeThreads), kEdgeThreads, 0, st>>>(
+                static_cast<const uint8_t*>(d_wire), static_cast<uint8_t*>(d_payload), d_desc,
+                d_status, ws_ptr<const uint64_t>(ws, L.offs[0]), ws_ptr<const uint64_t>(ws, L.offs[1]),
+                ws_ptr<const uint64_t>(ws, L.hdr), cap, (uint32_t)n);
     } else {
         launch_pass<kModeDeser>(L, 0, d_wire, d_payload, d_desc, d_status, ws, cap, n, kClassAll, st);
     }

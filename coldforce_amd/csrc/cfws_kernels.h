@@ -717,6 +717,37 @@ edge_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
     edge_frame<kMode>(P, f, (uint32_t)(t & 1u));
 }
 
+// Deserialize with reassembly (CFWS_DESERIALIZE_REASSEMBLE): the edge chunks
+// of frame f in the one pass that holds its bytes (data frames in pass 0,
+// control frames in pass 1 from hdr[2]). Pass 0's stores stop at its data
+// bytes: pass 1 starts there, at an unaligned address, and its edge chunks
+// are written concurrently.
+__device__ __forceinline__ void reasm_edge_frame(const uint8_t* __restrict__ src,
+                                                 uint8_t* __restrict__ dst,
+                                                 const cfws_frame_desc_t* __restrict__ desc,
+                                                 const int32_t* __restrict__ status,
+                                                 const uint64_t* __restrict__ offs0,
+                                                 const uint64_t* __restrict__ offs1,
+                                                 const uint64_t* __restrict__ hdr, uint64_t capacity,
+                                                 uint32_t n_frames, uint64_t f, uint32_t part)
+{
+    const uint32_t p = is_control(desc[f].opcode) ? 1u : 0u;
+    const uint64_t out_base = p ? hdr[2] : 0;
+    Pass P;
+    P.src = src;
+    P.dst = dst + out_base;
+    P.desc = desc;
+    P.status = status;
+    P.offs = p ? offs1 : offs0;
+    P.total = hdr[p];
+    P.capacity = p ? capacity - out_base : (hdr[0] < capacity ? hdr[0] : capacity);
+    P.n_frames = n_frames;
+    P.klass = p ? kClassControl : kClassData;
+    P.sid = 0;
+    P.parent = nullptr;
+    edge_frame<kModeDeser>(P, f, part);
+}
+
 // WS serialize / deserialize and the fused WS-over-HTTP/2 send carry their
 // edge chunks in the streaming launch. The send's edge code spills 112 bytes
 // per lane there (96 VGPRs, 5 waves per SIMD, the residency the LDS
@@ -751,8 +782,17 @@ xform_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
              const uint64_t* __restrict__ offs, const uint32_t* __restrict__ region_map,
              const uint64_t* __restrict__ total_p, const uint64_t* __restrict__ base_p,
              uint64_t capacity, uint32_t n_frames, uint32_t klass, uint32_t sid,
-             const cfws_frame_desc_t* __restrict__ parent, uint32_t edge_blocks)
+             const cfws_frame_desc_t* __restrict__ parent, uint32_t edge_blocks,
+             const uint64_t* __restrict__ reasm_offs1)
 {
+    if (kMode == kModeDeser && reasm_offs1 && blockIdx.x < edge_blocks) {
+        // reassembly pass 0: the edge chunks of both passes (total_p = hdr)
+        const uint64_t t = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
+        if ((t >> 1) < n_frames)
+            reasm_edge_frame(src, dst, desc, status, offs, reasm_offs1, total_p, capacity, n_frames,
+                             t >> 1, (uint32_t)(t & 1u));
+        return;
+    }
     const uint64_t out_base = base_p ? *base_p : 0;
     Pass P;
     P.src = src;
@@ -1209,13 +1249,14 @@ void launch_streaming(const void* src, void* dst, const cfws_frame_desc_t* desc,
                       const int32_t* status, const uint64_t* offs, const uint32_t* map,
                       const uint64_t* total_p, const uint64_t* base_p, uint64_t regions,
                       uint64_t cap, size_t n, uint32_t klass, uint32_t sid, hipStream_t st,
-                      const cfws_frame_desc_t* parent = nullptr, bool edges = true)
+                      const cfws_frame_desc_t* parent = nullptr, bool edges = true,
+                      const uint64_t* reasm_offs1 = nullptr)
 {
     const bool split = edges && (edge_split() || !has_edge_blocks(kMode));
     const uint32_t eb = (edges && !split) ? grid_for(2 * (uint64_t)n, kThreads) : 0;
     xform_kernel<kMode><<<eb + stream_grid(regions), kThreads, xform_lds_bytes(kMode), st>>>(
         static_cast<const uint8_t*>(src), static_cast<uint8_t*>(dst), desc, status, offs, map,
-        total_p, base_p, cap, (uint32_t)n, klass, sid, parent, eb);
+        total_p, base_p, cap, (uint32_t)n, klass, sid, parent, eb, eb ? reasm_offs1 : nullptr);
     // (a separate edge launch on a second stream, overlapping the streaming
     // kernel, measured no faster on config 5: the stream slowed by what the
     // overlap saved)
@@ -1227,7 +1268,7 @@ void launch_streaming(const void* src, void* dst, const cfws_frame_desc_t* desc,
 template <int kMode>
 void launch_pass(const WsLayout& L, int p, const void* src, void* dst, const cfws_frame_desc_t* desc,
                  const int32_t* status, const void* ws, uint64_t cap, size_t n, uint32_t klass,
-                 hipStream_t st, uint32_t sid = 0, bool edges = true)
+                 hipStream_t st, uint32_t sid = 0, bool edges = true, bool reasm_edges = false)
 {
     const uint64_t* hdr = ws_ptr<const uint64_t>(ws, L.hdr);
     // Pass 1 (reassembly: control frames, <= 125-byte payloads each) is
@@ -1238,7 +1279,7 @@ void launch_pass(const WsLayout& L, int p, const void* src, void* dst, const cfw
     launch_streaming<kMode>(src, dst, desc, status, ws_ptr<const uint64_t>(ws, L.offs[p]),
                             ws_ptr<const uint32_t>(ws, L.map[p]), hdr + p,
                             p == 1 ? hdr + 2 : nullptr, regions, cap, n, klass, sid, st, nullptr,
-                            edges);
+                            edges, reasm_edges ? ws_ptr<const uint64_t>(ws, L.offs[1]) : nullptr);
 }
 
 }  // namespace
