@@ -451,10 +451,91 @@ __device__ __forceinline__ uint32_t edge_byte(const Pass& P, const FrameView& v,
     return (r - v.pre < v.body_len) ? u4_byte(W, j) : 0u;
 }
 
+// Bytes [a, b) of a 16-byte chunk as a mask (0 <= a, b <= 16).
+__device__ __forceinline__ uint32_t low_bytes(int k)
+{
+    return k <= 0 ? 0u : (k >= 4 ? 0xffffffffu : (1u << (8 * k)) - 1u);
+}
+
+__device__ __forceinline__ uint4 byte_range(uint32_t a, uint32_t b)
+{
+    const int ia = (int)a, ib = (int)b;
+    return make_uint4(low_bytes(ib) & ~low_bytes(ia), low_bytes(ib - 4) & ~low_bytes(ia - 4),
+                      low_bytes(ib - 8) & ~low_bytes(ia - 8), low_bytes(ib - 12) & ~low_bytes(ia - 12));
+}
+
+__device__ __forceinline__ uint4 and4(uint4 a, uint4 b)
+{
+    return make_uint4(a.x & b.x, a.y & b.y, a.z & b.z, a.w & b.w);
+}
+
+__device__ __forceinline__ uint4 or4(uint4 a, uint4 b)
+{
+    return make_uint4(a.x | b.x, a.y | b.y, a.z | b.z, a.w | b.w);
+}
+
+// Output position x relative to chunk D, clamped to [0, 16].
+__device__ __forceinline__ uint32_t chunk_rel(uint64_t x, uint64_t D)
+{
+    return x <= D ? 0u : (x - D >= 16 ? 16u : (uint32_t)(x - D));
+}
+
+// A frame's first 16 header bytes as little-endian words (bytes past `pre`
+// are don't-care). Serialize (co_ws_frame.c:34-91): byte 0, byte 1 (mask bit
+// | 7-bit length), the 0/2/8-byte big-endian extended length, the key. The
+// two-pass HTTP/2 wrap: its 9-byte DATA header, built from constant byte
+// indices.
+template <int kMode>
+__device__ __forceinline__ uint4 header_words(const Pass& P, const FrameView& v)
+{
+    if (kMode == kModeSer) {
+        const uint64_t n = v.body_len;
+        const uint32_t ext = n > 65535u ? 8u : (n > 125u ? 2u : 0u);
+        const uint32_t l7 = ext == 8 ? 127u : (ext == 2 ? 126u : (uint32_t)n);
+        const uint32_t b01 = (v.hb & 0xffu) | ((l7 | ((v.hb >> 1) & 0x80u)) & 0xffu) << 8;
+        const uint32_t k = v.key;
+        if (ext == 0) return make_uint4(b01 | k << 16, k >> 16, 0u, 0u);
+        if (ext == 2) return make_uint4(b01 | (uint32_t)__builtin_bswap16((uint16_t)n) << 16, k, 0u, 0u);
+        const uint64_t be = __builtin_bswap64(n);
+        return make_uint4(b01 | (uint32_t)(be & 0xffffu) << 16, (uint32_t)(be >> 16),
+                          (uint32_t)(be >> 48) | k << 16, k >> 16);
+    }
+    uint32_t h[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (uint32_t r = 0; r < 16; ++r)
+        if (r < v.pre) h[r >> 2] |= header_byte_of<kMode>(P, v, r) << (8u * (r & 3u));
+    return make_uint4(h[0], h[1], h[2], h[3]);
+}
+
+// Frame v's bytes in chunk D: its header (when the mode writes one), then its
+// body (W: edge_body's lined-up body bytes), zero elsewhere.
+template <int kMode>
+__device__ __forceinline__ uint4 view_chunk(const Pass& P, const FrameView& v, uint64_t D, uint4 W)
+{
+    uint4 o = and4(W, byte_range(chunk_rel(v.body_start, D), chunk_rel(v.body_start + v.body_len, D)));
+    if (kMode != kModeDeser && v.pre) {
+        const uint4 H = header_words<kMode>(P, v);
+        const uint4 z = make_uint4(0, 0, 0, 0);
+        uint4 Hs;
+        if (v.out_off >= D) {
+            const uint64_t q = v.out_off - D;              // header byte 0 at chunk byte q
+            Hs = q == 0 ? H : (q >= 16 ? z : funnel16(z, H, 16u - (uint32_t)q));
+        } else {
+            const uint64_t sft = D - v.out_off;            // chunk byte 0 is header byte sft
+            Hs = sft >= 16 ? z : funnel16(H, z, (uint32_t)sft);
+        }
+        o = or4(o, and4(Hs, byte_range(chunk_rel(v.out_off, D), chunk_rel(v.out_off + v.pre, D))));
+    }
+    return o;
+}
+
 // A chunk that crosses a header, a frame boundary, padding or the end of
 // the pass. With at most two frames in it (every boundary of frames larger
 // than the chunk) all source blocks are loaded up front and the bytes are
-// assembled in registers: one memory round trip instead of sixteen.
+// assembled in registers: one memory round trip instead of sixteen. Each
+// frame's header and body words are shifted into place and masked to their
+// byte ranges (word operations, not sixteen per-byte selects per frame);
+// the fused HTTP/2 send, whose header runs to 23 bytes, assembles bytes.
 template <int kMode>
 __device__ __forceinline__ uint4 edge_chunk(const Pass& P, uint32_t f, uint64_t D,
                                             const FrameView& va, const FrameView& vb, uint64_t o1,
@@ -465,6 +546,11 @@ __device__ __forceinline__ uint4 edge_chunk(const Pass& P, uint32_t f, uint64_t 
     const bool two = o1 < lim;
     const uint4 Wa = edge_body(P.src, va, D, lim);
     const uint4 Wb = two ? edge_body(P.src, vb, D, lim) : Wa;
+    if (kMode != kModeH2Ser) {
+        uint4 o = view_chunk<kMode>(P, va, D, Wa);
+        if (two) o = or4(o, view_chunk<kMode>(P, vb, D, Wb));
+        return and4(o, byte_range(0, chunk_rel(lim, D)));
+    }
     uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
