@@ -440,17 +440,6 @@ __device__ __forceinline__ uint32_t u4_byte(const uint4& w, int j)
     return (d >> (8 * (j & 3))) & 0xffu;
 }
 
-// Byte at output position pos of frame v (pos inside v's output range),
-// given v's body bytes lined up with the chunk (edge_body).
-template <int kMode>
-__device__ __forceinline__ uint32_t edge_byte(const Pass& P, const FrameView& v, uint64_t pos,
-                                              const uint4& W, int j)
-{
-    const uint64_t r = pos - v.out_off;
-    if (r < v.pre) return header_byte_of<kMode>(P, v, (uint32_t)r);
-    return (r - v.pre < v.body_len) ? u4_byte(W, j) : 0u;
-}
-
 // Bytes [a, b) of a 16-byte chunk as a mask (0 <= a, b <= 16).
 __device__ __forceinline__ uint32_t low_bytes(int k)
 {
@@ -480,31 +469,57 @@ __device__ __forceinline__ uint32_t chunk_rel(uint64_t x, uint64_t D)
     return x <= D ? 0u : (x - D >= 16 ? 16u : (uint32_t)(x - D));
 }
 
-// A frame's first 16 header bytes as little-endian words (bytes past `pre`
-// are don't-care). Serialize (co_ws_frame.c:34-91): byte 0, byte 1 (mask bit
-// | 7-bit length), the 0/2/8-byte big-endian extended length, the key. The
-// two-pass HTTP/2 wrap: its 9-byte DATA header, built from constant byte
-// indices.
-template <int kMode>
-__device__ __forceinline__ uint4 header_words(const Pass& P, const FrameView& v)
+// A WS frame's header (co_ws_frame.c:34-91) as little-endian words: byte 0,
+// byte 1 (mask bit | 7-bit length), the 0/2/8-byte big-endian extended
+// length, the key (hb: byte 0 | mask bit << 8; key 0 when unmasked).
+__device__ __forceinline__ uint4 ws_header_words(uint64_t n, uint32_t hb, uint32_t k)
 {
-    if (kMode == kModeSer) {
-        const uint64_t n = v.body_len;
-        const uint32_t ext = n > 65535u ? 8u : (n > 125u ? 2u : 0u);
-        const uint32_t l7 = ext == 8 ? 127u : (ext == 2 ? 126u : (uint32_t)n);
-        const uint32_t b01 = (v.hb & 0xffu) | ((l7 | ((v.hb >> 1) & 0x80u)) & 0xffu) << 8;
-        const uint32_t k = v.key;
-        if (ext == 0) return make_uint4(b01 | k << 16, k >> 16, 0u, 0u);
-        if (ext == 2) return make_uint4(b01 | (uint32_t)__builtin_bswap16((uint16_t)n) << 16, k, 0u, 0u);
-        const uint64_t be = __builtin_bswap64(n);
-        return make_uint4(b01 | (uint32_t)(be & 0xffffu) << 16, (uint32_t)(be >> 16),
-                          (uint32_t)(be >> 48) | k << 16, k >> 16);
+    const uint32_t ext = n > 65535u ? 8u : (n > 125u ? 2u : 0u);
+    const uint32_t l7 = ext == 8 ? 127u : (ext == 2 ? 126u : (uint32_t)n);
+    const uint32_t b01 = (hb & 0xffu) | ((l7 | ((hb >> 1) & 0x80u)) & 0xffu) << 8;
+    if (ext == 0) return make_uint4(b01 | k << 16, k >> 16, 0u, 0u);
+    if (ext == 2) return make_uint4(b01 | (uint32_t)__builtin_bswap16((uint16_t)n) << 16, k, 0u, 0u);
+    const uint64_t be = __builtin_bswap64(n);
+    return make_uint4(b01 | (uint32_t)(be & 0xffffu) << 16, (uint32_t)(be >> 16),
+                      (uint32_t)(be >> 48) | k << 16, k >> 16);
+}
+
+// The bytes a frame writes before its body, as little-endian words (lo:
+// bytes 0-15, hi: 16-31; bytes past `pre` are don't-care):
+// * serialize: its WS header;
+// * the two-pass HTTP/2 wrap: the 9-byte DATA header (co_http2_frame.c:33-72),
+//   from constant byte indices;
+// * the fused HTTP/2 send: the DATA header, then the WS header bytes the slice
+//   carries from s0 on (h_in = pre - 9 of them; with max_frame_size >= 64 a
+//   WS header lies whole in its frame's first slice).
+struct HeaderWords {
+    uint4 lo, hi;
+};
+
+template <int kMode>
+__device__ __forceinline__ HeaderWords header_words(const Pass& P, const FrameView& v)
+{
+    const uint4 z = make_uint4(0, 0, 0, 0);
+    if (kMode == kModeSer) return {ws_header_words(v.body_len, v.hb, v.key), z};
+    if (kMode == kModeH2Ser) {
+        const uint32_t len = v.pre - 9u + (uint32_t)v.body_len;
+        const uint32_t sid = P.sid & 0x7fffffffu;
+        uint4 w = z;
+        if (v.pre > 9u) w = funnel16(ws_header_words(v.ws_len, v.ws_hb, v.ws_key), z, v.s0 & 15u);
+        HeaderWords h;
+        h.lo.x = (len >> 16 & 0xffu) | (len >> 8 & 0xffu) << 8 | (len & 0xffu) << 16;
+        h.lo.y = (v.hb & 0xffu) | (sid >> 24 & 0xffu) << 8 | (sid >> 16 & 0xffu) << 16 |
+                 (sid >> 8 & 0xffu) << 24;
+        h.lo.z = (sid & 0xffu) | w.x << 8;
+        h.lo.w = w.x >> 24 | w.y << 8;
+        h.hi = make_uint4(w.y >> 24 | w.z << 8, w.z >> 24 | w.w << 8, 0u, 0u);
+        return h;
     }
     uint32_t h[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
     for (uint32_t r = 0; r < 16; ++r)
         if (r < v.pre) h[r >> 2] |= header_byte_of<kMode>(P, v, r) << (8u * (r & 3u));
-    return make_uint4(h[0], h[1], h[2], h[3]);
+    return {make_uint4(h[0], h[1], h[2], h[3]), z};
 }
 
 // Frame v's bytes in chunk D: its header (when the mode writes one), then its
@@ -514,15 +529,16 @@ __device__ __forceinline__ uint4 view_chunk(const Pass& P, const FrameView& v, u
 {
     uint4 o = and4(W, byte_range(chunk_rel(v.body_start, D), chunk_rel(v.body_start + v.body_len, D)));
     if (kMode != kModeDeser && v.pre) {
-        const uint4 H = header_words<kMode>(P, v);
+        const HeaderWords H = header_words<kMode>(P, v);
         const uint4 z = make_uint4(0, 0, 0, 0);
         uint4 Hs;
         if (v.out_off >= D) {
             const uint64_t q = v.out_off - D;              // header byte 0 at chunk byte q
-            Hs = q == 0 ? H : (q >= 16 ? z : funnel16(z, H, 16u - (uint32_t)q));
+            Hs = q == 0 ? H.lo : (q >= 16 ? z : funnel16(z, H.lo, 16u - (uint32_t)q));
         } else {
             const uint64_t sft = D - v.out_off;            // chunk byte 0 is header byte sft
-            Hs = sft >= 16 ? z : funnel16(H, z, (uint32_t)sft);
+            Hs = sft < 16 ? funnel16(H.lo, H.hi, (uint32_t)sft)
+                          : (sft < 32 ? funnel16(H.hi, z, (uint32_t)(sft - 16)) : z);
         }
         o = or4(o, and4(Hs, byte_range(chunk_rel(v.out_off, D), chunk_rel(v.out_off + v.pre, D))));
     }
@@ -534,8 +550,7 @@ __device__ __forceinline__ uint4 view_chunk(const Pass& P, const FrameView& v, u
 // than the chunk) all source blocks are loaded up front and the bytes are
 // assembled in registers: one memory round trip instead of sixteen. Each
 // frame's header and body words are shifted into place and masked to their
-// byte ranges (word operations, not sixteen per-byte selects per frame);
-// the fused HTTP/2 send, whose header runs to 23 bytes, assembles bytes.
+// byte ranges (word operations, not sixteen per-byte selects per frame).
 template <int kMode>
 __device__ __forceinline__ uint4 edge_chunk(const Pass& P, uint32_t f, uint64_t D,
                                             const FrameView& va, const FrameView& vb, uint64_t o1,
@@ -546,26 +561,9 @@ __device__ __forceinline__ uint4 edge_chunk(const Pass& P, uint32_t f, uint64_t 
     const bool two = o1 < lim;
     const uint4 Wa = edge_body(P.src, va, D, lim);
     const uint4 Wb = two ? edge_body(P.src, vb, D, lim) : Wa;
-    if (kMode != kModeH2Ser) {
-        uint4 o = view_chunk<kMode>(P, va, D, Wa);
-        if (two) o = or4(o, view_chunk<kMode>(P, vb, D, Wb));
-        return and4(o, byte_range(0, chunk_rel(lim, D)));
-    }
-    uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-        const uint64_t pos = D + j;
-        uint32_t b = 0;
-        if (pos < lim)
-            b = (two && pos >= o1) ? edge_byte<kMode>(P, vb, pos, Wb, j)
-                                   : edge_byte<kMode>(P, va, pos, Wa, j);
-        const uint32_t sh = 8 * (j & 3);
-        if (j < 4) w0 |= b << sh;
-        else if (j < 8) w1 |= b << sh;
-        else if (j < 12) w2 |= b << sh;
-        else w3 |= b << sh;
-    }
-    return make_uint4(w0, w1, w2, w3);
+    uint4 o = view_chunk<kMode>(P, va, D, Wa);
+    if (two) o = or4(o, view_chunk<kMode>(P, vb, D, Wb));
+    return and4(o, byte_range(0, chunk_rel(lim, D)));
 }
 
 __device__ __forceinline__ void store_chunk(const Pass& P, uint64_t D, uint4 o)
