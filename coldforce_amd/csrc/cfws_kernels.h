@@ -833,7 +833,7 @@ __device__ __forceinline__ void reasm_edge_frame(const uint8_t* __restrict__ src
 }
 
 // WS serialize / deserialize and the fused WS-over-HTTP/2 send carry their
-// edge chunks in the streaming launch. The send's edge code spills 112 bytes
+// edge chunks in the streaming launch. The send's edge code spills 88 bytes
 // per lane there (96 VGPRs, 5 waves per SIMD, the residency the LDS
 // reservation sets anyway); the spills sit in the edge branch only, none in
 // the region loop. It still measured 12 us per config-5 step faster than its
