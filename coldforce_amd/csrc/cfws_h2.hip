@@ -162,7 +162,8 @@ h2_ser_plan_reduce_kernel(cfws_frame_desc_t* __restrict__ desc, uint64_t n, uint
 // hdr[0] = DATA-stream bytes clamped by the capacity, hdr[3] = DATA frames;
 // hdr[4] / hdr[5] = the grand sums when a scan launch made them (more than
 // kSelfScanBlocks blocks). DATA frame d of WS frame f: a slice of its wire
-// bytes at 9 d + wire offset (h2_expand_kernel's layout).
+// bytes at 9 d + wire offset (h2_expand_kernel's output layout); its
+// descriptor holds what the send pass reads per region (see the loop).
 __global__ void __launch_bounds__(kThreads)
 h2_ser_plan_apply_kernel(cfws_frame_desc_t* __restrict__ desc, uint64_t n, uint64_t S,
                          const uint64_t* __restrict__ partials_w, const uint64_t* __restrict__ partials_k,
@@ -186,8 +187,10 @@ h2_ser_plan_apply_kernel(cfws_frame_desc_t* __restrict__ desc, uint64_t n, uint6
     const uint64_t total = T < capacity ? T : capacity;
     const uint64_t f = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
     uint64_t w = 0, k = 0;
+    DescWords wd = {};
     if (f < n) {
-        w = desc[f].header_size + desc[f].payload_size;
+        wd = load_desc(desc, (uint32_t)f);
+        w = wd.header_size() + wd.payload_size;
         k = data_frames_of(w, S);
     }
     uint64_t tot;
@@ -195,22 +198,34 @@ h2_ser_plan_apply_kernel(cfws_frame_desc_t* __restrict__ desc, uint64_t n, uint6
     const uint64_t d0 = block_exclusive_scan(k, s_wave, &tot) + pre_k;
     if (f < n) {
         desc[f].wire_off = w0;
+        const uint64_t hs = wd.header_size();
         for (uint64_t j = 0; j < k; ++j) {
             const uint64_t d = d0 + j;
             if (d >= n_max) break;
+            // DATA frame d: slice [s0, s0 + len) of WS frame f's wire bytes,
+            // h_in of them header; stored as the send pass reads it
+            // (frame_view<kModeH2Ser>): body source offset and length, key
+            // rotated to the body's first payload index, bytes before the
+            // body (9 + h_in), END_STREAM; the WS frame in wire_off, s0 in
+            // opcode (the output offset is doffs[d])
+            const uint64_t s0 = j * S;
+            const uint64_t len = (j + 1 < k) ? S : w - s0;
+            const uint64_t h_in = s0 < hs ? (hs - s0 < len ? hs - s0 : len) : 0;
+            const uint64_t q = s0 + h_in - hs;           // payload index of the body start
             cfws_frame_desc_t e;
-            e.payload_off = w0 + j * S;
-            e.wire_off = 9 * d + e.payload_off;
-            e.payload_size = (j + 1 < k) ? S : w - j * S;
-            e.mask_key = (uint32_t)f;                    // the WS frame (kModeH2Ser)
+            e.payload_off = wd.payload_off + q;
+            e.wire_off = f;
+            e.payload_size = len - h_in;
+            e.mask_key = wd.mask() ? rotr8(wd.key(), (uint32_t)(q & 3u)) : 0u;
             e.fin = (j + 1 == k) ? 1 : 0;
-            e.opcode = 0;
+            e.opcode = h_in ? (uint8_t)s0 : 0;
             e.mask = 0;
-            e.header_size = 9;
+            e.header_size = (uint8_t)(9 + h_in);
             ddesc[d] = e;
-            doffs[d] = e.wire_off;
+            const uint64_t out = 9 * d + w0 + s0;
+            doffs[d] = out;
             // DATA frames lie back to back: this one ends where d + 1 starts
-            map_range(e.wire_off, e.wire_off + 9 + e.payload_size, d, total, map);
+            map_range(out, out + 9 + len, d, total, map);
         }
     }
     // descriptor slots past the DATA frames: empty frames at the end

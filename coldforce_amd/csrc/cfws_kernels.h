@@ -169,11 +169,8 @@ struct FrameView {
     uint32_t key;   // 0 when the frame is not masked: XOR becomes a copy
     uint32_t pre;
     uint32_t hb;    // serialize: header byte 0 | mask bit << 8; DATA: flags
-    uint32_t aux;   // kModeH2Ser: the parent WS frame
+    uint32_t aux;   // kModeH2Ser: the parent WS frame (its header bytes come from it)
     uint32_t s0;    // kModeH2Ser: the slice's first byte within the WS frame
-    uint64_t ws_len;  // kModeH2Ser: the WS frame's payload size, key and
-    uint32_t ws_key;  //   header byte 0 | mask bit << 8 (its header bytes
-    uint32_t ws_hb;   //   are generated from these)
 };
 
 // Byte r < pre of a serialize frame's header, from its view (co_ws_frame.c:34-91).
@@ -198,29 +195,18 @@ __device__ __forceinline__ FrameView frame_view(const Pass& P, uint32_t f)
     v.out_off = P.offs[f];
     v.hb = 0;
     v.aux = 0;
-    v.ws_len = 0;
-    v.ws_key = 0;
-    v.ws_hb = 0;
     v.s0 = 0;
     if (kMode == kModeH2Ser) {
-        // d: one DATA frame = a slice [payload_off, + payload_size) of the
-        // virtual WS wire arena; key field = its WS frame w
-        const uint32_t wf = d.key();
-        const DescWords w = load_desc(P.parent, wf);
-        const uint64_t s0 = d.payload_off - w.wire_off;
-        const uint64_t hs = w.header_size();
-        const uint64_t h_in = s0 < hs ? (hs - s0 < d.payload_size ? hs - s0 : d.payload_size) : 0;
-        const uint64_t q = s0 + h_in - hs;             // payload index of the body start
-        v.pre = d.payload_size ? 9u + (uint32_t)h_in : 0u;   // unused slots: empty
-        v.body_len = d.payload_size - h_in;
-        v.src_off = w.payload_off + q;
-        v.key = w.mask() ? rotr8(w.key(), (uint32_t)(q & 3u)) : 0u;
+        // one DATA frame as h2_ser_plan_apply_kernel laid it out: body
+        // source offset and length, rotated key, 9 + h_in bytes before the
+        // body (0: an unused slot), END_STREAM, the WS frame, s0
+        v.pre = d.header_size();
+        v.body_len = d.payload_size;
+        v.src_off = d.payload_off;
+        v.key = d.key();
         v.hb = d.fin() ? 0x1u : 0u;                      // DATA flags: END_STREAM
-        v.aux = wf;
-        v.s0 = (uint32_t)s0;                           // only read when h_in > 0 (s0 < 14)
-        v.ws_len = w.payload_size;
-        v.ws_key = w.mask() ? w.key() : 0u;
-        v.ws_hb = ((w.opcode() | (w.fin() ? 0x80u : 0u)) & 0xffu) | (w.mask() ? 0x100u : 0u);
+        v.aux = (uint32_t)d.wire_off;
+        v.s0 = d.opcode();                             // only read when pre > 9 (s0 < 14)
     } else if (is_ser(kMode)) {
         v.pre = d.header_size();
         v.body_len = d.payload_size;
@@ -339,10 +325,11 @@ __device__ __forceinline__ uint32_t header_byte_of(const Pass& P, const FrameVie
     if (kMode == kModeH2Ser) {
         if (r < 9) return h2_header_byte(v.pre - 9u + (uint32_t)v.body_len, v.hb, P.sid, r);
         // the WS frame's header (co_ws_frame.c:34-91)
+        const DescWords w = load_desc(P.parent, v.aux);
         FrameView wv;
-        wv.body_len = v.ws_len;
-        wv.key = v.ws_key;
-        wv.hb = v.ws_hb;
+        wv.body_len = w.payload_size;
+        wv.key = w.mask() ? w.key() : 0u;
+        wv.hb = ((w.opcode() | (w.fin() ? 0x80u : 0u)) & 0xffu) | (w.mask() ? 0x100u : 0u);
         return view_header_byte(wv, r - 9u + v.s0);
     }
     return view_header_byte(v, r);
@@ -505,7 +492,11 @@ __device__ __forceinline__ HeaderWords header_words(const Pass& P, const FrameVi
         const uint32_t len = v.pre - 9u + (uint32_t)v.body_len;
         const uint32_t sid = P.sid & 0x7fffffffu;
         uint4 w = z;
-        if (v.pre > 9u) w = funnel16(ws_header_words(v.ws_len, v.ws_hb, v.ws_key), z, v.s0 & 15u);
+        if (v.pre > 9u) {
+            const DescWords p = load_desc(P.parent, v.aux);
+            const uint32_t hb = ((p.opcode() | (p.fin() ? 0x80u : 0u)) & 0xffu) | (p.mask() ? 0x100u : 0u);
+            w = funnel16(ws_header_words(p.payload_size, hb, p.mask() ? p.key() : 0u), z, v.s0 & 15u);
+        }
         HeaderWords h;
         h.lo.x = (len >> 16 & 0xffu) | (len >> 8 & 0xffu) << 8 | (len & 0xffu) << 16;
         h.lo.y = (v.hb & 0xffu) | (sid >> 24 & 0xffu) << 8 | (sid >> 16 & 0xffu) << 16 |
@@ -833,7 +824,7 @@ __device__ __forceinline__ void reasm_edge_frame(const uint8_t* __restrict__ src
 }
 
 // WS serialize / deserialize and the fused WS-over-HTTP/2 send carry their
-// edge chunks in the streaming launch. The send's edge code spills 88 bytes
+// edge chunks in the streaming launch. The send's edge code spills 12 bytes
 // per lane there (96 VGPRs, 5 waves per SIMD, the residency the LDS
 // reservation sets anyway); the spills sit in the edge branch only, none in
 // the region loop. It still measured 12 us per config-5 step faster than its
