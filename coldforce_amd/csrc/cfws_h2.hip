@@ -321,7 +321,7 @@ h2_de_plan_apply_kernel(cfws_frame_desc_t* __restrict__ desc, const int32_t* __r
                         uint64_t* __restrict__ phdr, uint64_t* __restrict__ poffs,
                         uint64_t* __restrict__ msg_id, uint64_t* __restrict__ n_msg_p,
                         uint64_t* __restrict__ starts, uint64_t* __restrict__ ends,
-                        uint64_t* __restrict__ first)
+                        uint64_t* __restrict__ first, uint64_t* __restrict__ host_counts)
 {
     __shared__ uint64_t s_wave[kWaves];
     uint64_t pre_p, pre_e, gp, ge;
@@ -333,6 +333,12 @@ h2_de_plan_apply_kernel(cfws_frame_desc_t* __restrict__ desc, const int32_t* __r
         pre_e = partials_e[blockIdx.x];
         gp = phdr[3];
         ge = *n_msg_p;
+    }
+    // message count and pooled total straight to the caller thread's mapped
+    // host words (read after one stream synchronize)
+    if (host_counts && blockIdx.x == 0 && threadIdx.x == 0) {
+        host_counts[0] = ge;
+        host_counts[1] = gp;
     }
     const uint64_t i = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
     uint64_t v = 0, e = 0;
@@ -615,6 +621,32 @@ H2DeLayout h2_de_layout(uint64_t n, uint64_t pool_cap, uint64_t payload_cap)
     return L;
 }
 
+// The calling thread's two mapped host words for the receive plan's
+// message count and pooled total (h2_de_plan_apply_kernel writes them; the
+// host reads them after one synchronize). Allocated once per host thread and
+// kept for its lifetime; null (the copies are used) if the allocation fails.
+volatile uint64_t* count_words(uint64_t** dev)
+{
+    thread_local uint64_t* h = nullptr;
+    thread_local uint64_t* d = nullptr;
+    thread_local bool tried = false;
+    if (!tried) {
+        tried = true;
+        void* p = nullptr;
+        void* q = nullptr;
+        if (hipHostMalloc(&p, 64, hipHostMallocMapped) == hipSuccess) {
+            if (hipHostGetDevicePointer(&q, p, 0) == hipSuccess && q) {
+                h = static_cast<uint64_t*>(p);
+                d = static_cast<uint64_t*>(q);
+            } else {
+                (void)hipHostFree(p);
+            }
+        }
+    }
+    *dev = d;
+    return h;
+}
+
 }  // namespace
 
 size_t cfws_h2_serialize_workspace_size(size_t n, uint64_t wire_cap, uint64_t h2_cap, uint32_t S)
@@ -720,6 +752,9 @@ int cfws_h2_deserialize_batch(const void* d_h2, uint64_t h2_size, const uint64_t
     uint64_t* ends = ws_ptr<uint64_t>(ws, L.ends);
     uint64_t* first = ws_ptr<uint64_t>(ws, L.first);
     const uint8_t* h2 = static_cast<const uint8_t*>(d_h2);
+    uint64_t counts[2] = {0, 0};       // messages, pooled bytes
+    uint64_t* d_words = nullptr;
+    volatile uint64_t* h_words = count_words(&d_words);
     {
         const uint32_t nb = grid_for(n, kPlanBlock);
         const uint32_t self_scan = nb <= kSelfScanBlocks ? 1u : 0u;
@@ -729,9 +764,9 @@ int cfws_h2_deserialize_batch(const void* d_h2, uint64_t h2_size, const uint64_t
                                                           d_h2_status, pp, pe);
         if (!self_scan) scan_partials2_kernel<<<2, kThreads, 0, st>>>(pp, pe, nb, phdr + 3, n_msg_d);
         h2_de_plan_apply_kernel<<<nb, kThreads, 0, st>>>(pdesc, d_h2_status, n, pp, pe, nb, self_scan,
-                                                         phdr, poffs, es, n_msg_d, starts, ends, first);
+                                                         phdr, poffs, es, n_msg_d, starts, ends, first,
+                                                         d_words);
     }
-    uint64_t counts[2] = {0, 0};       // messages, pooled bytes
     auto read_counts = [&]() -> int {
         hipError_t e = hipMemcpyAsync(&counts[0], n_msg_d, 8, hipMemcpyDeviceToHost, st);
         if (e == hipSuccess) e = hipMemcpyAsync(&counts[1], phdr + 3, 8, hipMemcpyDeviceToHost, st);
@@ -739,7 +774,16 @@ int cfws_h2_deserialize_batch(const void* d_h2, uint64_t h2_size, const uint64_t
         if (e != hipSuccess) return set_err(CFWS_ERROR_HIP, "h2_deserialize message count", e);
         return CFWS_OK;
     };
-    if (int rc = read_counts()) return rc;
+    if (h_words) {
+        // one synchronize; two pageable copies cost two staged round trips
+        // (~30 us of device idle per call on config 5)
+        const hipError_t e = hipStreamSynchronize(st);
+        if (e != hipSuccess) return set_err(CFWS_ERROR_HIP, "h2_deserialize message count", e);
+        counts[0] = h_words[0];
+        counts[1] = h_words[1];
+    } else if (int rc = read_counts()) {
+        return rc;
+    }
     void* wsd = ws_ptr<void>(ws, L.wsd);
     const WsLayout WL = ws_layout(n, payload_cap);
     if (counts[1] > pool_cap) {
