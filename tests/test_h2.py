@@ -302,3 +302,51 @@ def test_gpu_h2_roundtrip_600k_frames():
     index = O.h2_index(exp)
     assert len(index) == n
     check_h2_deserialize(exp, index, align=1)
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not gpu_present(), reason="needs the MI355X")
+def test_gpu_h2_deserialize_two_threads():
+    """The receive plan hands its message count to the host through mapped
+    host words, one pair per host thread: two threads decoding different
+    batches on their own streams at once each get their own counts and
+    payloads (ctypes releases the GIL during the call)."""
+    import threading
+    torch, cfws = _gpu()
+    cases = []
+    for seed, n in ((11, 300), (12, 700)):
+        rng = random.Random(seed)
+        payload = O.fill_splitmix(1 << 20, seed, 0)
+        d = np.zeros(n, dtype=O.DESC_DTYPE)
+        for i in range(n):
+            sz = rng.choice([0, 7, 126, 1000, 16376, 40000])
+            d[i] = (rng.randrange(0, (1 << 20) - sz), 0, sz, rng.getrandbits(32), 1, 2,
+                    rng.random() < .5, 0)
+        h2, _ = O.h2_serialize_batch(payload, d, 1, 16384)
+        index = O.h2_index(h2)
+        exp = O.h2_deserialize_batch(h2, index, 16384, O.DEFAULT_MAX_PAYLOAD, 16, None, None)
+        h = torch.from_numpy(np.concatenate([h2, np.zeros(16, np.uint8)])).cuda()
+        idx = torch.from_numpy(index.astype(np.int64)).cuda()
+        pool = torch.empty(len(h2) + 16, dtype=torch.uint8, device="cuda")
+        pay = torch.empty(len(h2) + 16 * len(index) + 16, dtype=torch.uint8, device="cuda")
+        cases.append((h, len(h2), idx, pool, pay, exp, torch.cuda.Stream()))
+    torch.cuda.synchronize()
+    errors = []
+
+    def run(case):
+        h, size, idx, pool, pay, exp, s = case
+        try:
+            for _ in range(8):
+                st, md, ms, tot, m = cfws.h2_deserialize(h, size, idx, pool, pay, stream=s)
+                s.synchronize()
+                assert m == exp["n_msg"] and int(tot.item()) == exp["total"]
+                assert np.array_equal(pay[:exp["total"]].cpu().numpy(), exp["payload"][:exp["total"]])
+        except Exception as e:          # reported from the main thread
+            errors.append(e)
+
+    ts = [threading.Thread(target=run, args=(c,)) for c in cases]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errors, errors
