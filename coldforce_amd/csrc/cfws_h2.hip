@@ -436,14 +436,25 @@ __global__ void __launch_bounds__(kThreads)
 h2_msg_parse_kernel(const uint8_t* __restrict__ h2, const cfws_frame_desc_t* __restrict__ pdesc,
                     const int32_t* __restrict__ h2_status, const uint64_t* __restrict__ poff,
                     uint64_t n_h2, const uint64_t* __restrict__ starts,
-                    const uint64_t* __restrict__ ends, uint64_t n_msg, uint64_t max_payload,
+                    const uint64_t* __restrict__ ends, const uint64_t* __restrict__ n_msg_p,
+                    uint64_t max_payload,
                     uint64_t align, cfws_frame_desc_t* __restrict__ mdesc,
                     int32_t* __restrict__ mstatus, uint64_t* __restrict__ vals,
                     const uint64_t* __restrict__ first, uint64_t* __restrict__ partials)
 {
     __shared__ uint64_t s_wave[kWaves];
     const uint64_t m = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
+    const uint64_t n_msg = *n_msg_p;
     uint64_t v = 0;
+    if (m >= n_msg && m < n_h2) {
+        // rows past the message count (the grid is sized before the host
+        // knows it): empty entries, no payload, so the layout over n_h2 rows
+        // equals the layout over the messages
+        cfws_frame_desc_t e = {};
+        mdesc[m] = e;
+        mstatus[m] = CFWS_PARSE_MORE_DATA;
+        vals[m] = 0;
+    }
     if (m < n_msg) {
         const uint64_t s = starts[m], len = ends[m] - s;
         const uint32_t k = len < 14 ? (uint32_t)len : 14u;
@@ -531,13 +542,14 @@ __device__ __forceinline__ uint64_t h2_unit(const cfws_frame_desc_t* __restrict_
 __global__ void __launch_bounds__(kThreads)
 h2_units_kernel(const cfws_frame_desc_t* __restrict__ pdesc, const int32_t* __restrict__ h2_status,
                 const uint64_t* __restrict__ poff, const uint64_t* __restrict__ msg_id, uint64_t n,
-                uint64_t n_msg, const uint64_t* __restrict__ starts,
+                const uint64_t* __restrict__ n_msg_p, const uint64_t* __restrict__ starts,
                 const cfws_frame_desc_t* __restrict__ mdesc, const int32_t* __restrict__ mstatus,
                 const uint64_t* __restrict__ hdr, cfws_frame_desc_t* __restrict__ udesc,
                 int32_t* __restrict__ ustatus, uint64_t* __restrict__ uoffs, uint32_t* __restrict__ map)
 {
     const uint64_t d = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
     if (d >= n) return;
+    const uint64_t n_msg = *n_msg_p;
     cfws_frame_desc_t u, u1;
     const uint64_t lo = h2_unit(pdesc, h2_status, poff, msg_id, d, n_msg, starts, mdesc, mstatus, hdr, u);
     const uint64_t hi = d + 1 < n ? h2_unit(pdesc, h2_status, poff, msg_id, d + 1, n_msg, starts, mdesc,
@@ -551,6 +563,45 @@ h2_units_kernel(const cfws_frame_desc_t* __restrict__ pdesc, const int32_t* __re
     if (d == n - 1) map[(total + kRegion - 1) / kRegion] = (uint32_t)(n - 1);
 }
 
+
+}  // namespace
+
+namespace {
+
+// The calling thread's receive-plan handoff: two mapped host words for the
+// message count and pooled total (h2_de_plan_apply_kernel writes them) and
+// an event recorded after the plan. The host waits on that event alone while
+// the rest of the call runs on. Made once per host thread and kept for its
+// lifetime; words null (the copies are used) if an allocation fails.
+struct CountWords {
+    uint64_t* h = nullptr;
+    uint64_t* d = nullptr;
+    hipEvent_t ev = nullptr;
+};
+
+const CountWords& count_words()
+{
+    thread_local CountWords w;
+    thread_local bool tried = false;
+    if (!tried) {
+        tried = true;
+        void* p = nullptr;
+        void* q = nullptr;
+        hipEvent_t ev = nullptr;
+        if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return w;
+        if (hipHostMalloc(&p, 64, hipHostMallocMapped) == hipSuccess) {
+            if (hipHostGetDevicePointer(&q, p, 0) == hipSuccess && q) {
+                w.h = static_cast<uint64_t*>(p);
+                w.d = static_cast<uint64_t*>(q);
+                w.ev = ev;
+                return w;
+            }
+            (void)hipHostFree(p);
+        }
+        (void)hipEventDestroy(ev);
+    }
+    return w;
+}
 
 }  // namespace
 
@@ -619,32 +670,6 @@ H2DeLayout h2_de_layout(uint64_t n, uint64_t pool_cap, uint64_t payload_cap)
     L.ustatus = at; at = align_up(at + 4 * n, 256);
     L.bytes = at;
     return L;
-}
-
-// The calling thread's two mapped host words for the receive plan's
-// message count and pooled total (h2_de_plan_apply_kernel writes them; the
-// host reads them after one synchronize). Allocated once per host thread and
-// kept for its lifetime; null (the copies are used) if the allocation fails.
-volatile uint64_t* count_words(uint64_t** dev)
-{
-    thread_local uint64_t* h = nullptr;
-    thread_local uint64_t* d = nullptr;
-    thread_local bool tried = false;
-    if (!tried) {
-        tried = true;
-        void* p = nullptr;
-        void* q = nullptr;
-        if (hipHostMalloc(&p, 64, hipHostMallocMapped) == hipSuccess) {
-            if (hipHostGetDevicePointer(&q, p, 0) == hipSuccess && q) {
-                h = static_cast<uint64_t*>(p);
-                d = static_cast<uint64_t*>(q);
-            } else {
-                (void)hipHostFree(p);
-            }
-        }
-    }
-    *dev = d;
-    return h;
 }
 
 }  // namespace
@@ -752,9 +777,10 @@ int cfws_h2_deserialize_batch(const void* d_h2, uint64_t h2_size, const uint64_t
     uint64_t* ends = ws_ptr<uint64_t>(ws, L.ends);
     uint64_t* first = ws_ptr<uint64_t>(ws, L.first);
     const uint8_t* h2 = static_cast<const uint8_t*>(d_h2);
+    if (align == 0 || (align & (align - 1)) || align > 4096)
+        return set_err(CFWS_ERROR_INVALID_ARGUMENT, "align must be a power of two <= 4096", hipSuccess);
     uint64_t counts[2] = {0, 0};       // messages, pooled bytes
-    uint64_t* d_words = nullptr;
-    volatile uint64_t* h_words = count_words(&d_words);
+    const CountWords& cw = count_words();
     {
         const uint32_t nb = grid_for(n, kPlanBlock);
         const uint32_t self_scan = nb <= kSelfScanBlocks ? 1u : 0u;
@@ -765,73 +791,32 @@ int cfws_h2_deserialize_batch(const void* d_h2, uint64_t h2_size, const uint64_t
         if (!self_scan) scan_partials2_kernel<<<2, kThreads, 0, st>>>(pp, pe, nb, phdr + 3, n_msg_d);
         h2_de_plan_apply_kernel<<<nb, kThreads, 0, st>>>(pdesc, d_h2_status, n, pp, pe, nb, self_scan,
                                                          phdr, poffs, es, n_msg_d, starts, ends, first,
-                                                         d_words);
+                                                         cw.d);
     }
-    auto read_counts = [&]() -> int {
-        hipError_t e = hipMemcpyAsync(&counts[0], n_msg_d, 8, hipMemcpyDeviceToHost, st);
-        if (e == hipSuccess) e = hipMemcpyAsync(&counts[1], phdr + 3, 8, hipMemcpyDeviceToHost, st);
-        if (e == hipSuccess) e = hipStreamSynchronize(st);
-        if (e != hipSuccess) return set_err(CFWS_ERROR_HIP, "h2_deserialize message count", e);
-        return CFWS_OK;
-    };
-    if (h_words) {
-        // one synchronize; two pageable copies cost two staged round trips
-        // (~30 us of device idle per call on config 5)
-        const hipError_t e = hipStreamSynchronize(st);
-        if (e != hipSuccess) return set_err(CFWS_ERROR_HIP, "h2_deserialize message count", e);
-        counts[0] = h_words[0];
-        counts[1] = h_words[1];
-    } else if (int rc = read_counts()) {
-        return rc;
+    if (cw.h) {
+        const hipError_t e = hipEventRecord(cw.ev, st);
+        if (e != hipSuccess) return set_err(CFWS_ERROR_HIP, "h2_deserialize plan event", e);
     }
     void* wsd = ws_ptr<void>(ws, L.wsd);
     const WsLayout WL = ws_layout(n, payload_cap);
-    if (counts[1] > pool_cap) {
-        // 2'. general form: the pool capacity cuts DATA payloads, and a frame
-        //     past it is OUT_OF_MEMORY and closes no message. Pool offsets
-        //     and the grand total stand; the capacity rule, END_STREAM flags
-        //     and messages are redone (co_http2_stream.c:550-608).
-        deserialize_finalize_kernel<<<grid_for(n, kThreads), kThreads, 0, st>>>(
-            pdesc, d_h2_status, poffs, poffs, phdr, n, pool_cap, 0, ws_ptr<uint32_t>(pws, PL.map[0]),
-            ws_ptr<uint32_t>(pws, PL.map[1]), nullptr);
-        h2_end_flags_kernel<<<grid_for(n, kThreads), kThreads, 0, st>>>(pdesc, d_h2_status, n, es);
-        if (int rc = run_scan(es, n, ws_ptr<uint64_t>(ws, L.es_part), n_msg_d, st)) return rc;
-        h2_messages_kernel<<<grid_for(n, kThreads), kThreads, 0, st>>>(pdesc, d_h2_status, es, n, ends);
-        h2_starts_kernel<<<grid_for(n, kThreads), kThreads, 0, st>>>(ends, n_msg_d, n, starts);
-        if (int rc = read_counts()) return rc;
-        if (n_messages) *n_messages = (size_t)counts[0];
-        // 3'. each pooled message through co_ws_frame_deserialize against
-        //     its own size (co_ws_http2_extension.c:134-164), from the
-        //     materialised pool (layout-first OOM rule)
-        if (pool_cap)
-            launch_pass<kModeDeser>(PL, 0, d_h2, d_pool, pdesc, d_h2_status, pws, pool_cap, n,
-                                    kClassAll, st);
-        if (int rc = deserialize_plan_impl(d_pool, pool_cap, starts, ends, counts[0], max_payload, align,
-                                           0, d_msg_desc, d_msg_status, payload_cap,
-                                           d_payload_total, wsd, WL.bytes, stream))
-            return rc;
-        return cfws_deserialize_execute(d_pool, d_msg_desc, d_msg_status, counts[0], 0, d_payload,
-                                        payload_cap, wsd, stream);
-    }
-    const uint64_t n_msg = counts[0];
-    if (n_messages) *n_messages = (size_t)n_msg;
-    // 2. fused: the pool is never written. Each message's WS header is
-    //    gathered from its DATA frames and parsed against the message's own
-    //    size (co_ws_http2_extension.c:134-164); then its layout.
-    if (align == 0 || (align & (align - 1)) || align > 4096)
-        return set_err(CFWS_ERROR_INVALID_ARGUMENT, "align must be a power of two <= 4096", hipSuccess);
     uint64_t* hdr = ws_ptr<uint64_t>(wsd, WL.hdr);
-    if (n_msg == 0) return zero_totals(WL, wsd, d_payload_total, st);
+    // 2. fused, queued before the host knows the message count (rows past it
+    //    are empty): the pool is never written. Each message's WS header is
+    //    gathered from its DATA frames and parsed against the message's own
+    //    size (co_ws_http2_extension.c:134-164); then its layout. Valid when
+    //    every DATA payload fits the pool capacity; otherwise the general
+    //    form below rewrites every output after it, in stream order (the
+    //    fused kernels store only inside the payload capacity).
     uint64_t* offs0 = ws_ptr<uint64_t>(wsd, WL.offs[0]);
     uint64_t* part0 = ws_ptr<uint64_t>(wsd, WL.partials[0]);
-    const uint32_t mb = grid_for(n_msg, kPlanBlock);
+    const uint32_t mb = grid_for(n, kPlanBlock);
     const uint32_t m_self = mb <= kSelfScanBlocks ? 1u : 0u;
-    h2_msg_parse_kernel<<<mb, kThreads, 0, st>>>(h2, pdesc, d_h2_status, poffs, n, starts, ends, n_msg,
+    h2_msg_parse_kernel<<<mb, kThreads, 0, st>>>(h2, pdesc, d_h2_status, poffs, n, starts, ends, n_msg_d,
                                                 max_payload, align, d_msg_desc, d_msg_status, offs0,
                                                 first, part0);
     if (!m_self) scan_partials_kernel<<<1, kThreads, 0, st>>>(part0, mb, hdr + 3);
     deserialize_plan_apply_kernel<<<mb, kThreads, 0, st>>>(
-        d_msg_desc, d_msg_status, offs0, ws_ptr<uint64_t>(wsd, WL.offs[1]), n_msg, part0,
+        d_msg_desc, d_msg_status, offs0, ws_ptr<uint64_t>(wsd, WL.offs[1]), n, part0,
         ws_ptr<uint64_t>(wsd, WL.partials[1]), mb, m_self, hdr, payload_cap, 0,
         ws_ptr<uint32_t>(wsd, WL.map[0]), ws_ptr<uint32_t>(wsd, WL.map[1]), d_payload_total);
     // 3. one payload-pass unit per DATA frame, and the pass's region map
@@ -840,12 +825,59 @@ int cfws_h2_deserialize_batch(const void* d_h2, uint64_t h2_size, const uint64_t
     uint64_t* uoffs = ws_ptr<uint64_t>(wsd, WL.offs[1]);
     uint32_t* umap = ws_ptr<uint32_t>(wsd, WL.map[1]);
     h2_units_kernel<<<grid_for(n, kThreads), kThreads, 0, st>>>(
-        pdesc, d_h2_status, poffs, es, n, n_msg, starts, d_msg_desc, d_msg_status, hdr, udesc,
+        pdesc, d_h2_status, poffs, es, n, n_msg_d, starts, d_msg_desc, d_msg_status, hdr, udesc,
         ustatus, uoffs, umap);
     if (payload_cap)
         launch_streaming<kModeDeser>(d_h2, d_payload, udesc, ustatus, uoffs, umap, hdr, nullptr,
                                      WL.regions, payload_cap, n, kClassAll, 0, st);
-    return launch_check("h2_deserialize");
+    if (int rc = launch_check("h2_deserialize")) return rc;
+    auto read_counts = [&]() -> int {
+        hipError_t e = hipMemcpyAsync(&counts[0], n_msg_d, 8, hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess) e = hipMemcpyAsync(&counts[1], phdr + 3, 8, hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess) e = hipStreamSynchronize(st);
+        if (e != hipSuccess) return set_err(CFWS_ERROR_HIP, "h2_deserialize message count", e);
+        return CFWS_OK;
+    };
+    if (cw.h) {
+        // the plan's event only: the kernels above keep the device busy while
+        // the host reads the counts (a stream synchronize here left it idle
+        // 25-46 us per call on config 5)
+        const hipError_t e = hipEventSynchronize(cw.ev);
+        if (e != hipSuccess) return set_err(CFWS_ERROR_HIP, "h2_deserialize message count", e);
+        const volatile uint64_t* hw = cw.h;
+        counts[0] = hw[0];
+        counts[1] = hw[1];
+    } else if (int rc = read_counts()) {
+        return rc;
+    }
+    if (counts[1] <= pool_cap) {
+        if (n_messages) *n_messages = (size_t)counts[0];
+        return CFWS_OK;
+    }
+    // 2'. general form: the pool capacity cuts DATA payloads, and a frame
+    //     past it is OUT_OF_MEMORY and closes no message. Pool offsets and
+    //     the grand total stand; the capacity rule, END_STREAM flags and
+    //     messages are redone (co_http2_stream.c:550-608).
+    deserialize_finalize_kernel<<<grid_for(n, kThreads), kThreads, 0, st>>>(
+        pdesc, d_h2_status, poffs, poffs, phdr, n, pool_cap, 0, ws_ptr<uint32_t>(pws, PL.map[0]),
+        ws_ptr<uint32_t>(pws, PL.map[1]), nullptr);
+    h2_end_flags_kernel<<<grid_for(n, kThreads), kThreads, 0, st>>>(pdesc, d_h2_status, n, es);
+    if (int rc = run_scan(es, n, ws_ptr<uint64_t>(ws, L.es_part), n_msg_d, st)) return rc;
+    h2_messages_kernel<<<grid_for(n, kThreads), kThreads, 0, st>>>(pdesc, d_h2_status, es, n, ends);
+    h2_starts_kernel<<<grid_for(n, kThreads), kThreads, 0, st>>>(ends, n_msg_d, n, starts);
+    if (int rc = read_counts()) return rc;
+    if (n_messages) *n_messages = (size_t)counts[0];
+    // 3'. each pooled message through co_ws_frame_deserialize against its
+    //     own size (co_ws_http2_extension.c:134-164), from the materialised
+    //     pool (layout-first OOM rule)
+    if (pool_cap)
+        launch_pass<kModeDeser>(PL, 0, d_h2, d_pool, pdesc, d_h2_status, pws, pool_cap, n, kClassAll, st);
+    if (int rc = deserialize_plan_impl(d_pool, pool_cap, starts, ends, counts[0], max_payload, align, 0,
+                                       d_msg_desc, d_msg_status, payload_cap, d_payload_total, wsd,
+                                       WL.bytes, stream))
+        return rc;
+    return cfws_deserialize_execute(d_pool, d_msg_desc, d_msg_status, counts[0], 0, d_payload,
+                                    payload_cap, wsd, stream);
 }
 
 }  // extern "C"

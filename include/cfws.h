@@ -239,10 +239,11 @@ int cfws_ws_accept_keys_batch(const void* d_keys, const uint64_t* d_key_off, siz
  * and every pooled message goes through co_ws_frame_deserialize against its
  * own size (co_ws_http2_extension.c:134-164): d_msg_desc / d_msg_status get
  * one entry per message (room for n_h2 entries), payloads land in d_payload
- * as cfws_deserialize_batch lays them out (flags = 0). Synchronises the
- * stream once to return *n_messages; the count reaches the host through 64
- * bytes of mapped pinned memory the library allocates once per calling
- * thread and keeps for its lifetime. When every DATA payload fits pool_capacity
+ * as cfws_deserialize_batch lays them out (flags = 0). *n_messages is final
+ * on return: the host waits on an event after the device plan, through 64
+ * bytes of mapped pinned memory and an event the library creates once per
+ * calling thread and keeps for its lifetime. The payload pass may still be
+ * running on the stream, as with the other batch calls. When every DATA payload fits pool_capacity
  * the pool is virtual: WS headers are gathered and payload slices copied +
  * unmasked straight out of the DATA frames in one pass, and d_pool is not
  * written; otherwise the pool is materialised first (the capacity rule
