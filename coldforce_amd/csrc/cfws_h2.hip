@@ -571,36 +571,44 @@ namespace {
 // The calling thread's receive-plan handoff: two mapped host words for the
 // message count and pooled total (h2_de_plan_apply_kernel writes them) and
 // an event recorded after the plan. The host waits on that event alone while
-// the rest of the call runs on. Made once per host thread and kept for its
-// lifetime; words null (the copies are used) if an allocation fails.
+// the rest of the call runs on. Made once per host thread and device and
+// kept for the thread's lifetime; words null (the copies are used) if an
+// allocation fails.
 struct CountWords {
     uint64_t* h = nullptr;
     uint64_t* d = nullptr;
     hipEvent_t ev = nullptr;
 };
 
+// Per host thread and current device (an event and a device pointer belong
+// to one device); devices past kCountDevices use the copies.
+constexpr int kCountDevices = 16;
+
 const CountWords& count_words()
 {
-    thread_local CountWords w;
-    thread_local bool tried = false;
-    if (!tried) {
-        tried = true;
+    static const CountWords none;
+    thread_local CountWords w[kCountDevices];
+    thread_local bool tried[kCountDevices] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kCountDevices) return none;
+    if (!tried[dev]) {
+        tried[dev] = true;
         void* p = nullptr;
         void* q = nullptr;
         hipEvent_t ev = nullptr;
-        if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return w;
+        if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return w[dev];
         if (hipHostMalloc(&p, 64, hipHostMallocMapped) == hipSuccess) {
             if (hipHostGetDevicePointer(&q, p, 0) == hipSuccess && q) {
-                w.h = static_cast<uint64_t*>(p);
-                w.d = static_cast<uint64_t*>(q);
-                w.ev = ev;
-                return w;
+                w[dev].h = static_cast<uint64_t*>(p);
+                w[dev].d = static_cast<uint64_t*>(q);
+                w[dev].ev = ev;
+                return w[dev];
             }
             (void)hipHostFree(p);
         }
         (void)hipEventDestroy(ev);
     }
-    return w;
+    return w[dev];
 }
 
 }  // namespace

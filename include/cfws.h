@@ -242,8 +242,9 @@ int cfws_ws_accept_keys_batch(const void* d_keys, const uint64_t* d_key_off, siz
  * as cfws_deserialize_batch lays them out (flags = 0). *n_messages is final
  * on return: the host waits on an event after the device plan, through 64
  * bytes of mapped pinned memory and an event the library creates once per
- * calling thread and keeps for its lifetime. The payload pass may still be
- * running on the stream, as with the other batch calls. When every DATA payload fits pool_capacity
+ * calling thread and device and keeps for the thread's lifetime. The payload
+ * pass may still be running on the stream, as with the other batch calls.
+ * When every DATA payload fits pool_capacity
  * the pool is virtual: WS headers are gathered and payload slices copied +
  * unmasked straight out of the DATA frames in one pass, and d_pool is not
  * written; otherwise the pool is materialised first (the capacity rule
