@@ -521,11 +521,14 @@ def h2_serialize(payload_t, desc_t, wire_t, h2_t, sid: int = 1, S: int = H2_DEFA
 
 
 def h2_deserialize(h2_t, h2_size: int, index_t, pool_t, payload_t, S: int = H2_DEFAULT_MAX_FRAME_SIZE,
-                   max_payload: int = DEFAULT_MAX_PAYLOAD, align: int = 16, ws_t=None, stream=None):
+                   max_payload: int = DEFAULT_MAX_PAYLOAD, align: int = 16, ws_t=None, stream=None,
+                   all_rows: bool = False):
     """HTTP/2 DATA frames at index_t -> pooled WS messages -> payloads.
     Returns (h2_status_t, msg_desc_t, msg_status_t, total_t, n_messages).
     n_messages is final on return; the tensors are written by work still
-    queued on `stream` (synchronise it before reading them on another)."""
+    queued on `stream` (synchronise it before reading them on another).
+    all_rows: return every message row (one per DATA frame; rows past
+    n_messages are empty entries) instead of the first n_messages."""
     import torch
     n = index_t.numel()
     dev = h2_t.device
@@ -544,6 +547,8 @@ def h2_deserialize(h2_t, h2_size: int, index_t, pool_t, payload_t, S: int = H2_D
                                            ws_t.numel(), _stream(stream)),
            "cfws_h2_deserialize_batch")
     m = n_msg.value
+    if all_rows:
+        return h2_status, msg_desc, msg_status, total, m
     return h2_status, msg_desc[:m], msg_status[:m], total, m
 
 

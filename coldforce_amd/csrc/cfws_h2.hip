@@ -6,6 +6,9 @@
 // batch C ABI cfws_h2_* (include/cfws.h). DESIGN.md section 3.4.
 #include "cfws_kernels.h"
 
+#include <mutex>
+#include <vector>
+
 namespace {
 
 // Offsets into the descriptors, the capacity rule (a COMPLETE frame with a
@@ -538,16 +541,20 @@ __device__ __forceinline__ uint64_t h2_unit(const cfws_frame_desc_t* __restrict_
 
 // One thread per DATA frame: its unit, and the region map of the payload
 // pass (a unit ends where unit d + 1 starts, computed here too, so no
-// second launch reads uoffs).
+// second launch reads uoffs). *pass_total: the payload pass's total, or 0
+// (the pass then stores nothing) when the pooled bytes exceed the pool
+// capacity and the general form redoes the call.
 __global__ void __launch_bounds__(kThreads)
 h2_units_kernel(const cfws_frame_desc_t* __restrict__ pdesc, const int32_t* __restrict__ h2_status,
                 const uint64_t* __restrict__ poff, const uint64_t* __restrict__ msg_id, uint64_t n,
                 const uint64_t* __restrict__ n_msg_p, const uint64_t* __restrict__ starts,
                 const cfws_frame_desc_t* __restrict__ mdesc, const int32_t* __restrict__ mstatus,
                 const uint64_t* __restrict__ hdr, cfws_frame_desc_t* __restrict__ udesc,
-                int32_t* __restrict__ ustatus, uint64_t* __restrict__ uoffs, uint32_t* __restrict__ map)
+                int32_t* __restrict__ ustatus, uint64_t* __restrict__ uoffs, uint32_t* __restrict__ map,
+                const uint64_t* __restrict__ pooled_p, uint64_t pool_cap, uint64_t* __restrict__ pass_total)
 {
     const uint64_t d = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
+    if (d == 0) *pass_total = *pooled_p <= pool_cap ? hdr[0] : 0;
     if (d >= n) return;
     const uint64_t n_msg = *n_msg_p;
     cfws_frame_desc_t u, u1;
@@ -568,47 +575,106 @@ h2_units_kernel(const cfws_frame_desc_t* __restrict__ pdesc, const int32_t* __re
 
 namespace {
 
-// The calling thread's receive-plan handoff: two mapped host words for the
-// message count and pooled total (h2_de_plan_apply_kernel writes them) and
-// an event recorded after the plan. The host waits on that event alone while
-// the rest of the call runs on. Made once per host thread and device and
-// kept for the thread's lifetime; words null (the copies are used) if an
-// allocation fails.
+// The receive-plan handoff: two mapped host words for the message count and
+// pooled total (h2_de_plan_apply_kernel writes them) and an event recorded
+// after the plan. The host waits on that event alone while the rest of the
+// call runs on. One entry per device of the call's STREAM (an event and the
+// words' device pointer belong to the device the kernels run on, which need
+// not be the thread's current device).
 struct CountWords {
     uint64_t* h = nullptr;
     uint64_t* d = nullptr;
     hipEvent_t ev = nullptr;
 };
 
-// Per host thread and current device (an event and a device pointer belong
-// to one device); devices past kCountDevices use the copies.
+// Devices past kCountDevices, and any entry that cannot be made, use the
+// copies (read_counts).
 constexpr int kCountDevices = 16;
 
-const CountWords& count_words()
+// Entries are made once and never freed: a host thread borrows one per device
+// on its first call and its thread_local holder hands it back at thread exit
+// (no HIP call at exit, so the runtime's own teardown order does not matter).
+// A server whose worker threads come and go reuses the same few entries: the
+// process holds at most one per device per thread alive at once.
+struct CountPool {
+    std::mutex mu;
+    std::vector<CountWords*> free_list[kCountDevices];
+};
+
+CountPool& count_pool()
 {
-    static const CountWords none;
-    thread_local CountWords w[kCountDevices];
-    thread_local bool tried[kCountDevices] = {};
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kCountDevices) return none;
-    if (!tried[dev]) {
-        tried[dev] = true;
-        void* p = nullptr;
-        void* q = nullptr;
-        hipEvent_t ev = nullptr;
-        if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return w[dev];
-        if (hipHostMalloc(&p, 64, hipHostMallocMapped) == hipSuccess) {
-            if (hipHostGetDevicePointer(&q, p, 0) == hipSuccess && q) {
-                w[dev].h = static_cast<uint64_t*>(p);
-                w[dev].d = static_cast<uint64_t*>(q);
-                w[dev].ev = ev;
-                return w[dev];
-            }
-            (void)hipHostFree(p);
-        }
-        (void)hipEventDestroy(ev);
+    static CountPool* pool = new CountPool;   // outlives every thread's holder
+    return *pool;
+}
+
+struct CountHolder {
+    CountWords* w[kCountDevices] = {};
+    bool tried[kCountDevices] = {};
+    ~CountHolder()
+    {
+        CountPool& pool = count_pool();
+        std::lock_guard<std::mutex> lock(pool.mu);
+        for (int i = 0; i < kCountDevices; ++i)
+            if (w[i]) pool.free_list[i].push_back(w[i]);
     }
-    return w[dev];
+};
+
+CountWords* make_count_words(int dev)
+{
+    int cur = -1;
+    if (hipGetDevice(&cur) != hipSuccess) return nullptr;
+    if (cur != dev && hipSetDevice(dev) != hipSuccess) return nullptr;
+    CountWords* cw = nullptr;
+    void* p = nullptr;
+    void* q = nullptr;
+    hipEvent_t ev = nullptr;
+    if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess) {
+        if (hipHostMalloc(&p, 64, hipHostMallocMapped | hipHostMallocPortable) == hipSuccess) {
+            if (hipHostGetDevicePointer(&q, p, 0) == hipSuccess && q) {
+                cw = new CountWords;
+                cw->h = static_cast<uint64_t*>(p);
+                cw->d = static_cast<uint64_t*>(q);
+                cw->ev = ev;
+            } else {
+                (void)hipHostFree(p);
+            }
+        }
+        if (!cw) (void)hipEventDestroy(ev);
+    }
+    if (cur != dev) (void)hipSetDevice(cur);
+    (void)hipGetLastError();                 // a failure here only means: use the copies
+    return cw;
+}
+
+// The calling thread's entry for device `dev`, or null (use the copies).
+CountWords* count_words(int dev)
+{
+    thread_local CountHolder holder;
+    if (dev < 0 || dev >= kCountDevices) return nullptr;
+    if (holder.w[dev] || holder.tried[dev]) return holder.w[dev];
+    holder.tried[dev] = true;
+    {
+        CountPool& pool = count_pool();
+        std::lock_guard<std::mutex> lock(pool.mu);
+        if (!pool.free_list[dev].empty()) {
+            holder.w[dev] = pool.free_list[dev].back();
+            pool.free_list[dev].pop_back();
+            return holder.w[dev];
+        }
+    }
+    holder.w[dev] = make_count_words(dev);
+    return holder.w[dev];
+}
+
+// The device the stream's work runs on (the null stream: the current device).
+int stream_device(hipStream_t st)
+{
+    hipDevice_t dev = -1;
+    if (hipStreamGetDevice(st, &dev) != hipSuccess) {
+        (void)hipGetLastError();
+        return -1;
+    }
+    return dev;
 }
 
 }  // namespace
@@ -653,6 +719,7 @@ struct H2DeLayout {
     uint64_t es;         // u64[n_h2]: END_STREAM flags -> message ids
     uint64_t es_part;
     uint64_t es_total;   // u64: message count
+    uint64_t pass_total; // u64: the fused payload pass's total (0: the pool overflowed)
     uint64_t starts, ends;   // u64[n_h2]
     uint64_t first;      // u64[n_h2]: a message's first DATA frame
     uint64_t wsd;        // WS deserialize workspace
@@ -670,6 +737,7 @@ H2DeLayout h2_de_layout(uint64_t n, uint64_t pool_cap, uint64_t payload_cap)
     L.es = at; at = align_up(at + 8 * n, 256);
     L.es_part = at; at = align_up(at + 8 * ((n + kScanBlock - 1) / kScanBlock + 1), 256);
     L.es_total = at; at += 256;
+    L.pass_total = at; at += 256;
     L.starts = at; at = align_up(at + 8 * n, 256);
     L.ends = at; at = align_up(at + 8 * n, 256);
     L.first = at; at = align_up(at + 8 * n, 256);
@@ -788,7 +856,7 @@ int cfws_h2_deserialize_batch(const void* d_h2, uint64_t h2_size, const uint64_t
     if (align == 0 || (align & (align - 1)) || align > 4096)
         return set_err(CFWS_ERROR_INVALID_ARGUMENT, "align must be a power of two <= 4096", hipSuccess);
     uint64_t counts[2] = {0, 0};       // messages, pooled bytes
-    const CountWords& cw = count_words();
+    CountWords* cw = count_words(stream_device(st));
     {
         const uint32_t nb = grid_for(n, kPlanBlock);
         const uint32_t self_scan = nb <= kSelfScanBlocks ? 1u : 0u;
@@ -799,12 +867,21 @@ int cfws_h2_deserialize_batch(const void* d_h2, uint64_t h2_size, const uint64_t
         if (!self_scan) scan_partials2_kernel<<<2, kThreads, 0, st>>>(pp, pe, nb, phdr + 3, n_msg_d);
         h2_de_plan_apply_kernel<<<nb, kThreads, 0, st>>>(pdesc, d_h2_status, n, pp, pe, nb, self_scan,
                                                          phdr, poffs, es, n_msg_d, starts, ends, first,
-                                                         cw.d);
+                                                         cw ? cw->d : nullptr);
     }
-    if (cw.h) {
-        const hipError_t e = hipEventRecord(cw.ev, st);
-        if (e != hipSuccess) return set_err(CFWS_ERROR_HIP, "h2_deserialize plan event", e);
+    // the plan's event; if it cannot be recorded, the copies below read the
+    // counts instead (the words are still written, and nothing reads them)
+    bool plan_event = false;
+    if (cw) {
+        plan_event = hipEventRecord(cw->ev, st) == hipSuccess;
+        if (!plan_event) (void)hipGetLastError();
     }
+    // an early return below still lets the plan finish first: the words are
+    // the thread's, and a later call must not see this call's counts land
+    auto fail = [&](int rc) {
+        if (plan_event) (void)hipEventSynchronize(cw->ev);
+        return rc;
+    };
     void* wsd = ws_ptr<void>(ws, L.wsd);
     const WsLayout WL = ws_layout(n, payload_cap);
     uint64_t* hdr = ws_ptr<uint64_t>(wsd, WL.hdr);
@@ -832,13 +909,16 @@ int cfws_h2_deserialize_batch(const void* d_h2, uint64_t h2_size, const uint64_t
     int32_t* ustatus = ws_ptr<int32_t>(ws, L.ustatus);
     uint64_t* uoffs = ws_ptr<uint64_t>(wsd, WL.offs[1]);
     uint32_t* umap = ws_ptr<uint32_t>(wsd, WL.map[1]);
+    // the pass's total, or 0 when the pool overflows (it then stores nothing;
+    // the general form below does the call's work once)
+    uint64_t* pass_total = ws_ptr<uint64_t>(ws, L.pass_total);
     h2_units_kernel<<<grid_for(n, kThreads), kThreads, 0, st>>>(
         pdesc, d_h2_status, poffs, es, n, n_msg_d, starts, d_msg_desc, d_msg_status, hdr, udesc,
-        ustatus, uoffs, umap);
+        ustatus, uoffs, umap, phdr + 3, pool_cap, pass_total);
     if (payload_cap)
-        launch_streaming<kModeDeser>(d_h2, d_payload, udesc, ustatus, uoffs, umap, hdr, nullptr,
+        launch_streaming<kModeDeser>(d_h2, d_payload, udesc, ustatus, uoffs, umap, pass_total, nullptr,
                                      WL.regions, payload_cap, n, kClassAll, 0, st);
-    if (int rc = launch_check("h2_deserialize")) return rc;
+    if (int rc = launch_check("h2_deserialize")) return fail(rc);
     auto read_counts = [&]() -> int {
         hipError_t e = hipMemcpyAsync(&counts[0], n_msg_d, 8, hipMemcpyDeviceToHost, st);
         if (e == hipSuccess) e = hipMemcpyAsync(&counts[1], phdr + 3, 8, hipMemcpyDeviceToHost, st);
@@ -846,13 +926,13 @@ int cfws_h2_deserialize_batch(const void* d_h2, uint64_t h2_size, const uint64_t
         if (e != hipSuccess) return set_err(CFWS_ERROR_HIP, "h2_deserialize message count", e);
         return CFWS_OK;
     };
-    if (cw.h) {
+    if (plan_event) {
         // the plan's event only: the kernels above keep the device busy while
         // the host reads the counts (a stream synchronize here left it idle
         // 25-46 us per call on config 5)
-        const hipError_t e = hipEventSynchronize(cw.ev);
+        const hipError_t e = hipEventSynchronize(cw->ev);
         if (e != hipSuccess) return set_err(CFWS_ERROR_HIP, "h2_deserialize message count", e);
-        const volatile uint64_t* hw = cw.h;
+        const volatile uint64_t* hw = cw->h;
         counts[0] = hw[0];
         counts[1] = hw[1];
     } else if (int rc = read_counts()) {
@@ -875,6 +955,15 @@ int cfws_h2_deserialize_batch(const void* d_h2, uint64_t h2_size, const uint64_t
     h2_starts_kernel<<<grid_for(n, kThreads), kThreads, 0, st>>>(ends, n_msg_d, n, starts);
     if (int rc = read_counts()) return rc;
     if (n_messages) *n_messages = (size_t)counts[0];
+    // rows past the message count are empty entries, as in the fused form
+    // (which wrote its own, longer, parse into some of them)
+    if (counts[0] < n) {
+        hipError_t e = hipMemsetAsync(d_msg_desc + counts[0], 0, sizeof(cfws_frame_desc_t) * (n - counts[0]), st);
+        if (e == hipSuccess)
+            e = hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(d_msg_status + counts[0]),
+                                  CFWS_PARSE_MORE_DATA, n - counts[0], st);
+        if (e != hipSuccess) return set_err(CFWS_ERROR_HIP, "h2_deserialize empty rows", e);
+    }
     // 3'. each pooled message through co_ws_frame_deserialize against its
     //     own size (co_ws_http2_extension.c:134-164), from the materialised
     //     pool (layout-first OOM rule)

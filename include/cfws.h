@@ -238,17 +238,20 @@ int cfws_ws_accept_keys_batch(const void* d_keys, const uint64_t* d_key_off, siz
  * payloads pooled into d_pool until END_STREAM (co_http2_stream.c:550-608),
  * and every pooled message goes through co_ws_frame_deserialize against its
  * own size (co_ws_http2_extension.c:134-164): d_msg_desc / d_msg_status get
- * one entry per message (room for n_h2 entries), payloads land in d_payload
- * as cfws_deserialize_batch lays them out (flags = 0). *n_messages is final
- * on return: the host waits on an event after the device plan, through 64
- * bytes of mapped pinned memory and an event the library creates once per
- * calling thread and device and keeps for the thread's lifetime. The payload
- * pass may still be running on the stream, as with the other batch calls.
- * When every DATA payload fits pool_capacity
- * the pool is virtual: WS headers are gathered and payload slices copied +
- * unmasked straight out of the DATA frames in one pass, and d_pool is not
- * written; otherwise the pool is materialised first (the capacity rule
- * needs it). */
+ * one entry per message (room for n_h2 entries; entries n_messages..n_h2-1
+ * are empty: status CFWS_PARSE_MORE_DATA, no payload, no header, payload_off
+ * unspecified), payloads land in d_payload as cfws_deserialize_batch lays
+ * them out (flags = 0). *n_messages is final on return: the host waits on an
+ * event after the device plan, through 64 bytes of mapped pinned memory and
+ * an event made once per device of `stream` (where the kernels run; not
+ * necessarily the current device). A calling thread borrows them for its
+ * lifetime and hands them back at exit, so threads that come and go reuse
+ * them. The payload pass may still be running on the stream, as with the
+ * other batch calls. When every DATA payload fits pool_capacity the pool is
+ * virtual: WS headers are gathered and payload slices copied + unmasked
+ * straight out of the DATA frames in one pass, and d_pool is not written;
+ * otherwise the pool is materialised first (the capacity rule needs it) and
+ * the one-pass form, already queued, stores nothing. */
 #define CFWS_H2_DEFAULT_MAX_FRAME_SIZE 16384u
 #define CFWS_H2_PARSE_COMPLETE    0     /* co_http.h:40-42 */
 #define CFWS_H2_PARSE_MORE_DATA   1

@@ -350,3 +350,108 @@ def test_gpu_h2_deserialize_two_threads():
     for t in ts:
         t.join()
     assert not errors, errors
+
+
+def _h2_case(seed, n, sizes=(0, 7, 126, 1000, 16376, 40000)):
+    rng = random.Random(seed)
+    payload = O.fill_splitmix(1 << 20, seed, 0)
+    d = np.zeros(n, dtype=O.DESC_DTYPE)
+    for i in range(n):
+        sz = rng.choice(sizes)
+        d[i] = (rng.randrange(0, (1 << 20) - sz), 0, sz, rng.getrandbits(32), 1, 2,
+                rng.random() < .5, 0)
+    h2, _ = O.h2_serialize_batch(payload, d, 1, 16384)
+    return h2, O.h2_index(h2)
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not gpu_present(), reason="needs the MI355X")
+@pytest.mark.parametrize("pool_div", [None, 2, 5])
+def test_gpu_h2_rows_past_message_count_are_empty(pool_div):
+    """Every message row past n_messages is an empty entry (no payload, no
+    header, MORE_DATA), whether the fused form ran or the pool overflowed and the
+    general form redid the call with fewer messages; the payloads still
+    equal the oracle's (the fused payload pass stores nothing on overflow)."""
+    torch, cfws = _gpu()
+    h2, index = _h2_case(21, 400)
+    pool_cap = None if pool_div is None else len(h2) // pool_div
+    exp = O.h2_deserialize_batch(h2, index, 16384, O.DEFAULT_MAX_PAYLOAD, 16, pool_cap, None)
+    h = torch.from_numpy(np.concatenate([h2, np.zeros(16, np.uint8)])).cuda()
+    idx = torch.from_numpy(index.astype(np.int64)).cuda()
+    pool = torch.empty(len(h2) if pool_cap is None else pool_cap, dtype=torch.uint8, device="cuda")
+    pay = torch.full((len(h2) + 16 * len(index) + 16,), 0xEE, dtype=torch.uint8, device="cuda")
+    st, md, ms, tot, m = cfws.h2_deserialize(h, len(h2), idx, pool, pay, all_rows=True)
+    torch.cuda.synchronize()
+    assert m == exp["n_msg"] and int(tot.item()) == exp["total"]
+    assert m < len(index)
+    assert np.array_equal(pay[:exp["total"]].cpu().numpy(), exp["payload"][:exp["total"]])
+    assert np.array_equal(ms[:m].cpu().numpy(), exp["msg_status"])
+    # empty entries: no payload, no header; payload_off is the layout's
+    # position (the end of the messages' payloads in the fused form)
+    rest = cfws.desc_from_device(md[m:])
+    for f in ("wire_off", "payload_size", "mask_key", "fin", "opcode", "mask", "header_size"):
+        assert not rest[f].any(), f
+    assert bool((ms[m:] == O.PARSE_MORE_DATA).all())
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not gpu_present(), reason="needs the MI355X")
+def test_gpu_h2_deserialize_thread_churn():
+    """Short-lived host threads, one call each, three at a time: each thread
+    borrows the receive handoff (mapped count words + event) for the stream's
+    device and hands it back when it exits, so later threads reuse it. Every
+    call gets its own counts and payloads."""
+    import threading
+    torch, cfws = _gpu()
+    h2, index = _h2_case(31, 300)
+    exp = O.h2_deserialize_batch(h2, index, 16384, O.DEFAULT_MAX_PAYLOAD, 16, None, None)
+    h = torch.from_numpy(np.concatenate([h2, np.zeros(16, np.uint8)])).cuda()
+    idx = torch.from_numpy(index.astype(np.int64)).cuda()
+    bufs = [(torch.empty(len(h2) + 16, dtype=torch.uint8, device="cuda"),
+             torch.empty(len(h2) + 16 * len(index) + 16, dtype=torch.uint8, device="cuda"),
+             torch.cuda.Stream()) for _ in range(3)]
+    torch.cuda.synchronize()
+    errors = []
+
+    def run(k):
+        pool, pay, s = bufs[k]
+        try:
+            st, md, ms, tot, m = cfws.h2_deserialize(h, len(h2), idx, pool, pay, stream=s)
+            s.synchronize()
+            assert m == exp["n_msg"] and int(tot.item()) == exp["total"]
+            assert np.array_equal(pay[:exp["total"]].cpu().numpy(), exp["payload"][:exp["total"]])
+        except Exception as e:          # reported from the main thread
+            errors.append(e)
+
+    for _ in range(8):
+        ts = [threading.Thread(target=run, args=(k,)) for k in range(3)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+    assert not errors, errors
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not gpu_present(), reason="needs the MI355X")
+def test_gpu_h2_deserialize_stream_on_other_device():
+    """The receive handoff is keyed by the STREAM's device, not the thread's
+    current one: a call whose stream and buffers live on device 1 while
+    device 0 is current decodes correctly (needs two GPUs)."""
+    torch, cfws = _gpu()
+    if torch.cuda.device_count() < 2:
+        pytest.skip("needs two GPUs")
+    h2, index = _h2_case(41, 200)
+    exp = O.h2_deserialize_batch(h2, index, 16384, O.DEFAULT_MAX_PAYLOAD, 16, None, None)
+    dev = torch.device("cuda", 1)
+    h = torch.from_numpy(np.concatenate([h2, np.zeros(16, np.uint8)])).to(dev)
+    idx = torch.from_numpy(index.astype(np.int64)).to(dev)
+    pool = torch.empty(len(h2) + 16, dtype=torch.uint8, device=dev)
+    pay = torch.empty(len(h2) + 16 * len(index) + 16, dtype=torch.uint8, device=dev)
+    s = torch.cuda.Stream(device=dev)
+    torch.cuda.set_device(0)
+    for _ in range(2):
+        st, md, ms, tot, m = cfws.h2_deserialize(h, len(h2), idx, pool, pay, stream=s)
+        s.synchronize()
+        assert m == exp["n_msg"] and int(tot.item()) == exp["total"]
+        assert np.array_equal(pay[:exp["total"]].cpu().numpy(), exp["payload"][:exp["total"]])
