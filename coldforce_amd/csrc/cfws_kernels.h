@@ -248,14 +248,30 @@ __device__ __forceinline__ uint4 ld16(const uint8_t* p)
 // lane, once, yet `nt` measured slower here (config 2: 6.37/6.49 TB/s plain
 // vs 5.97/6.29 nt, profiles/r01_ab_dpp.json), although the bare copy probe
 // (tools/copy_probe.hip) gains from it; -DCFWS_STREAM_NT turns it on.
+#ifdef CFWS_STREAM_NT
+#define CFWS_STREAM_NT_SEND 1
+#define CFWS_STREAM_NT_RECV 1
+#endif
+template <int kMode>
 __device__ __forceinline__ uint4 ld16_stream(const uint8_t* p)
 {
-#ifdef CFWS_STREAM_NT
-    const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
-    return make_uint4(v.x, v.y, v.z, v.w);
+#if defined(CFWS_STREAM_NT_SEND) || defined(CFWS_STREAM_NT_RECV)
+#ifdef CFWS_STREAM_NT_SEND
+    constexpr bool send_nt = true;
 #else
-    return ld16(p);
+    constexpr bool send_nt = false;
 #endif
+#ifdef CFWS_STREAM_NT_RECV
+    constexpr bool recv_nt = true;
+#else
+    constexpr bool recv_nt = false;
+#endif
+    if (kMode == kModeDeser ? recv_nt : send_nt) {
+        const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+        return make_uint4(v.x, v.y, v.z, v.w);
+    }
+#endif
+    return ld16(p);
 }
 
 // Lane i receives lane i + 1's `v` (DPP wave_shl:1); lane 63, which has no
@@ -279,6 +295,32 @@ __device__ __forceinline__ void st16(uint8_t* p, uint4 o)
 #else
     *reinterpret_cast<u32x4*>(p) = v;
 #endif
+}
+
+// Body stores of the streaming regions, at byte `off` of the wave's output
+// region `rb` (wave-uniform), with a cache policy per direction. Policy
+// bits (gfx940+): sc0 1, nt 2, sc1 16; 0 = the global `nt` store (st16).
+// Writing the payload arena (deserialize) measured fastest write-through
+// (`sc0 sc1 nt`, a buffer store over the region): 6.49 -> 6.60 TB/s on
+// config 2, while writing the wire (serialize) lost 1-2 % that way and keeps
+// `nt` (profiles/r02_ab_store.txt). CFWS_STORE_AUX_SEND / _RECV override.
+#ifndef CFWS_STORE_AUX_SEND
+#define CFWS_STORE_AUX_SEND 0
+#endif
+#ifndef CFWS_STORE_AUX_RECV
+#define CFWS_STORE_AUX_RECV 19
+#endif
+template <int kMode>
+__device__ __forceinline__ void st16_region(uint8_t* rb, uint32_t off, uint4 o)
+{
+    constexpr int aux = kMode == kModeDeser ? CFWS_STORE_AUX_RECV : CFWS_STORE_AUX_SEND;
+    if (aux == 0) {
+        st16(rb + off, o);
+    } else {
+        const u32x4 v = {o.x, o.y, o.z, o.w};
+        const auto r = __builtin_amdgcn_make_buffer_rsrc(rb, 0, (int)kRegion, 0x00020000);
+        __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)off, 0, aux);
+    }
 }
 
 // 16 output bytes starting `ph` bytes into the 32-byte window {A, B}.
@@ -579,6 +621,7 @@ __device__ __forceinline__ void store_chunk(const Pass& P, uint64_t D, uint4 o)
 // chunk's first byte; when the source is misaligned against the output
 // (phase != 0) the block B after it is the next lane's A, taken over DPP, so
 // every source byte is loaded once (lane 63 loads its B itself).
+template <int kMode>
 __device__ __forceinline__ void fast_region(const Pass& P, const FrameView& v, uint64_t base,
                                             uint32_t lane)
 {
@@ -586,15 +629,16 @@ __device__ __forceinline__ void fast_region(const Pass& P, const FrameView& v, u
     const uint32_t ph = (uint32_t)(delta & 15u);
     const uint32_t kr = rotr8(v.key, (uint32_t)((0 - v.body_start) & 3u));
     const uint8_t* s0 = P.src + ((base + delta) & ~uint64_t(15)) + lane * kChunk;
-    uint8_t* d0 = P.dst + base + lane * kChunk;
+    uint8_t* const rb = P.dst + base;
+    const uint32_t l0 = lane * (uint32_t)kChunk;
     uint4 a[kUnroll];
 #pragma unroll
-    for (int u = 0; u < kUnroll; ++u) a[u] = ld16_stream(s0 + u * kSlice);
+    for (int u = 0; u < kUnroll; ++u) a[u] = ld16_stream<kMode>(s0 + u * kSlice);
     if (ph == 0) {
 #pragma unroll
         for (int u = 0; u < kUnroll; ++u) {
             xor4(a[u], kr);
-            st16(d0 + u * kSlice, a[u]);
+            st16_region<kMode>(rb, l0 + u * (uint32_t)kSlice, a[u]);
         }
     } else {
         // lane 63's B is the block after its A: it holds the chunk's last
@@ -610,7 +654,7 @@ __device__ __forceinline__ void fast_region(const Pass& P, const FrameView& v, u
         for (int u = 0; u < kUnroll; ++u) {
             uint4 o = funnel16(a[u], from_next_lane(a[u], e[u]), ph);
             xor4(o, kr);
-            st16(d0 + u * kSlice, o);
+            st16_region<kMode>(rb, l0 + u * (uint32_t)kSlice, o);
         }
     }
 }
@@ -640,7 +684,7 @@ __device__ __forceinline__ void two_frame_region(const Pass& P, const FrameView&
         a[u] = make_uint4(0, 0, 0, 0);
         e[u] = make_uint4(0, 0, 0, 0);
         if (fast[u]) {
-            a[u] = ld16_stream(sp);
+            a[u] = ld16_stream<kMode>(sp);
             // the next lane's chunk D + 16 loads block sp + 16 iff it is in
             // the same frame and inside the body
             const bool next_loads = lane != 63 && (D + kChunk >= vb.out_off) == hi &&
@@ -661,7 +705,7 @@ __device__ __forceinline__ void two_frame_region(const Pass& P, const FrameView&
         const uint32_t ph = (uint32_t)(((hi ? vb.src_off : va.src_off) + k0) & 15u);
         uint4 o = ph ? funnel16(a[u], (own_b >> u) & 1u ? e[u] : nb, ph) : a[u];
         xor4(o, rotr8(hi ? vb.key : va.key, (uint32_t)(k0 & 3u)));
-        st16(P.dst + D, o);
+        st16_region<kMode>(P.dst + base, (uint32_t)(D - base), o);
     }
 }
 
@@ -688,7 +732,7 @@ __device__ __forceinline__ void general_region(const Pass& P, uint32_t f0, uint3
         const uint64_t D = base + u * kSlice + lane * kChunk;
         const FrameView v = frame_view<kMode>(P, fr[u]);
         if (D >= v.body_start && D + kChunk <= v.body_start + v.body_len)
-            st16(P.dst + D, body_chunk(P.src, v, D));
+            st16_region<kMode>(P.dst + base, (uint32_t)(D - base), body_chunk(P.src, v, D));
     }
 }
 
@@ -911,7 +955,7 @@ xform_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
         const FrameView va = frame_view<kMode>(P, f0);
         if (f0 == f1) {
             if (base >= va.body_start && end <= va.body_start + va.body_len)
-                fast_region(P, va, base, lane);
+                fast_region<kMode>(P, va, base, lane);
             else
                 two_frame_region<kMode>(P, va, va, base, lane);   // partial body, one frame
         } else if (f1 == f0 + 1 || offs[f0 + 2] >= end) {
