@@ -17,6 +17,9 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <mutex>
+#include <vector>
+
 #include "cfws.h"
 #include "cfws_co_ws_frame.h"
 
@@ -30,6 +33,7 @@ size_t g_max_receive_payload_size = 32u * 1024u * 1024u;
 // device staging buffer for frames above the zero-copy limit; all reused
 // across frames (coldforce runs each connection on one co_thread).
 struct ThreadDevice {
+    int device = -1;               // the device the stream and buf belong to
     hipStream_t stream = nullptr;
     void* buf = nullptr;           // device memory (DMA path)
     size_t cap = 0;
@@ -37,7 +41,58 @@ struct ThreadDevice {
     void* host_dev = nullptr;      // its device-side address
     size_t host_cap = 0;
 };
-thread_local ThreadDevice t_dev;
+
+// A thread borrows its resources from a process-wide free list (per device)
+// on its first frame and hands them back when it exits, so a server whose
+// threads come and go reuses the same few streams and staging buffers. No
+// HIP call at thread exit (the runtime may be tearing down); the free list
+// is never destroyed.
+constexpr int kPoolDevices = 16;
+struct DevicePool {
+    std::mutex mu;
+    std::vector<ThreadDevice> free_list[kPoolDevices];
+};
+
+DevicePool& device_pool()
+{
+    static DevicePool* pool = new DevicePool;
+    return *pool;
+}
+
+struct ThreadDeviceHolder {
+    ThreadDevice d;
+    bool borrowed = false;
+    ~ThreadDeviceHolder()
+    {
+        if (d.device < 0 || d.device >= kPoolDevices || !(d.stream || d.buf || d.host)) return;
+        DevicePool& pool = device_pool();
+        std::lock_guard<std::mutex> lock(pool.mu);
+        pool.free_list[d.device].push_back(d);
+    }
+};
+thread_local ThreadDeviceHolder t_holder;
+
+// The calling thread's resources (borrowed on first use for the current
+// device; a thread keeps them for its lifetime, as before).
+ThreadDevice& tdev()
+{
+    ThreadDevice& d = t_holder.d;
+    if (!t_holder.borrowed) {
+        t_holder.borrowed = true;
+        int dev = 0;
+        if (hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < kPoolDevices) {
+            DevicePool& pool = device_pool();
+            std::lock_guard<std::mutex> lock(pool.mu);
+            if (!pool.free_list[dev].empty()) {
+                d = pool.free_list[dev].back();
+                pool.free_list[dev].pop_back();
+            } else {
+                d.device = dev;
+            }
+        }
+    }
+    return d;
+}
 
 // Frames up to this size take the zero-copy path: the payload is copied into
 // the pinned buffer and the XOR kernel reads and writes it over PCIe, so a
@@ -58,6 +113,7 @@ size_t zero_copy_max()
 bool stream_ready()
 {
     if (cfws_init() != CFWS_OK) return false;
+    ThreadDevice& t_dev = tdev();
     if (!t_dev.stream && hipStreamCreateWithFlags(&t_dev.stream, hipStreamNonBlocking) != hipSuccess) {
         fprintf(stderr, "cfws: hipStreamCreate failed\n");
         t_dev.stream = nullptr;
@@ -69,6 +125,7 @@ bool stream_ready()
 bool device_stage(size_t n)
 {
     if (!stream_ready()) return false;
+    ThreadDevice& t_dev = tdev();
     if (t_dev.cap < n) {
         size_t cap = 1u << 16;
         while (cap < n) cap <<= 1;
@@ -87,6 +144,7 @@ bool device_stage(size_t n)
 bool host_stage(size_t n)
 {
     if (!stream_ready()) return false;
+    ThreadDevice& t_dev = tdev();
     if (t_dev.host_cap < n) {
         size_t cap = 1u << 16;
         while (cap < n) cap <<= 1;
@@ -135,6 +193,7 @@ bool device_xor(const uint8_t* src, uint8_t* dst, size_t n, uint32_t key)
     RandomStateGuard keep_random_stream;
     const bool zero_copy = n <= zero_copy_max();
     if (zero_copy ? !host_stage(n) : !device_stage(n)) return false;
+    ThreadDevice& t_dev = tdev();
     hipStream_t st = t_dev.stream;
     if (zero_copy) {
         memcpy(t_dev.host, src, n);
@@ -308,14 +367,17 @@ void cfws_draw_mask_keys(size_t n, const uint8_t* mask_flags, uint32_t* keys)
     }
 }
 
-// Frees the calling thread's staging buffer and stream (optional; a thread
-// that exits without calling it leaks them until process exit).
+// Frees the calling thread's staging buffers and stream now (optional: a
+// thread that exits without calling it hands them back for reuse by later
+// threads instead).
 void cfws_release_thread_resources(void)
 {
+    ThreadDevice& t_dev = t_holder.d;
     if (t_dev.buf) (void)hipFree(t_dev.buf);
     if (t_dev.host) (void)hipHostFree(t_dev.host);
     if (t_dev.stream) (void)hipStreamDestroy(t_dev.stream);
     t_dev = ThreadDevice{};
+    t_holder.borrowed = false;
 }
 
 }  // extern "C"

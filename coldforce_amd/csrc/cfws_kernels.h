@@ -669,43 +669,50 @@ template <int kMode>
 __device__ __forceinline__ void two_frame_region(const Pass& P, const FrameView& va,
                                                  const FrameView& vb, uint64_t base, uint32_t lane)
 {
-    uint4 a[kUnroll], e[kUnroll];
-    bool fast[kUnroll];
-    uint32_t own_b = 0;
+    // Everything per frame is wave-uniform and taken relative to the region
+    // base (offsets clamped into [0, kRegion + 32], enough for every compare
+    // below), so a lane only selects between two sets of scalars: its chunk
+    // r (a multiple of 16) is in frame B iff r >= ob; the source block, the
+    // phase and the rotated key follow (phase and key rotation are the same
+    // for every chunk of a frame, because r is a multiple of 16).
+    auto rel = [base](uint64_t x) -> uint32_t {
+        return x <= base ? 0u : (x - base >= kRegion + 32 ? (uint32_t)(kRegion + 32) : (uint32_t)(x - base));
+    };
+    const uint32_t ob = rel(vb.out_off);
+    const uint32_t a_lo = rel(va.body_start), a_hi = rel(va.body_start + va.body_len);
+    const uint32_t b_lo = rel(vb.body_start), b_hi = rel(vb.body_start + vb.body_len);
+    const uint64_t sA = base + (va.src_off - va.body_start);
+    const uint64_t sB = base + (vb.src_off - vb.body_start);
+    const uint32_t phA = (uint32_t)(sA & 15u), phB = (uint32_t)(sB & 15u);
+    const uint32_t krA = rotr8(va.key, (uint32_t)(base - va.body_start) & 3u);
+    const uint32_t krB = rotr8(vb.key, (uint32_t)(base - vb.body_start) & 3u);
+    const uint8_t* sp[kUnroll];
+    bool fast[kUnroll], own[kUnroll], hi[kUnroll];
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u) {
-        const uint64_t D = base + u * kSlice + lane * kChunk;
-        const bool hi = D >= vb.out_off;
-        const uint64_t bs = hi ? vb.body_start : va.body_start;
-        const uint64_t be = bs + (hi ? vb.body_len : va.body_len);
-        const uint64_t s = (hi ? vb.src_off : va.src_off) + (D - bs);
-        const uint8_t* sp = P.src + (s & ~uint64_t(15));
-        fast[u] = D >= bs && D + kChunk <= be;
-        a[u] = make_uint4(0, 0, 0, 0);
-        e[u] = make_uint4(0, 0, 0, 0);
-        if (fast[u]) {
-            a[u] = ld16_stream<kMode>(sp);
-            // the next lane's chunk D + 16 loads block sp + 16 iff it is in
-            // the same frame and inside the body
-            const bool next_loads = lane != 63 && (D + kChunk >= vb.out_off) == hi &&
-                                    D + 2 * kChunk <= be;
-            if ((s & 15u) && !next_loads) {
-                e[u] = ld16(sp + 16);
-                own_b |= 1u << u;
-            }
-        }
+        const uint32_t r = u * (uint32_t)kSlice + lane * (uint32_t)kChunk;
+        hi[u] = r >= ob;
+        const uint32_t lo_ = hi[u] ? b_lo : a_lo, hi_ = hi[u] ? b_hi : a_hi;
+        fast[u] = r >= lo_ && r + 16 <= hi_;
+        // the next lane's chunk loads block sp + 16 iff it is in the same
+        // frame and inside the body
+        const bool next_loads = lane != 63 && (r + 16 >= ob) == hi[u] && r + 32 <= hi_;
+        own[u] = fast[u] && (hi[u] ? phB : phA) != 0 && !next_loads;
+        sp[u] = P.src + (((hi[u] ? sB : sA) + r) & ~uint64_t(15));
     }
+    uint4 a[kUnroll], e[kUnroll];
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) a[u] = fast[u] ? ld16_stream<kMode>(sp[u]) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) e[u] = own[u] ? ld16(sp[u] + 16) : make_uint4(0, 0, 0, 0);
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u) {
         const uint4 nb = from_next_lane(a[u], e[u]);     // every lane: DPP needs the full wave
         if (!fast[u]) continue;
-        const uint64_t D = base + u * kSlice + lane * kChunk;
-        const bool hi = D >= vb.out_off;
-        const uint64_t k0 = D - (hi ? vb.body_start : va.body_start);
-        const uint32_t ph = (uint32_t)(((hi ? vb.src_off : va.src_off) + k0) & 15u);
-        uint4 o = ph ? funnel16(a[u], (own_b >> u) & 1u ? e[u] : nb, ph) : a[u];
-        xor4(o, rotr8(hi ? vb.key : va.key, (uint32_t)(k0 & 3u)));
-        st16_region<kMode>(P.dst + base, (uint32_t)(D - base), o);
+        const uint32_t ph = hi[u] ? phB : phA;
+        uint4 o = ph ? funnel16(a[u], own[u] ? e[u] : nb, ph) : a[u];
+        xor4(o, hi[u] ? krB : krA);
+        st16_region<kMode>(P.dst + base, u * (uint32_t)kSlice + lane * (uint32_t)kChunk, o);
     }
 }
 

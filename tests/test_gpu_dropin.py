@@ -155,3 +155,37 @@ def test_link_level_dropin_harness(zc_max):
     for n in sizes[:4]:
         at += 2 * n + O.header_size(n, False) + O.header_size(n, True)
     assert lines[2] == f"codes 1 -7001 -7005 index {at}"
+
+
+def test_thread_churn_reuses_resources():
+    """Short-lived threads, three at a time, each decoding masked frames
+    through the drop-in: every thread borrows a stream and staging buffers
+    on its first frame and hands them back at exit (cfws_frame.cpp), so
+    later threads reuse them; a thread that releases its resources early
+    (cfws_release_thread_resources) gets fresh ones on its next frame."""
+    import threading
+    L = O.lib()
+    O.srandom(L, 77)
+    frames = []
+    for n in (1, 126, 4000, 70000, (1 << 20) + 5):
+        data = random.Random(n).randbytes(n)
+        frames.append((O.ref_serialize(L, True, 2, True, data), data))
+    errors = []
+
+    def run(k):
+        try:
+            for j, (w, data) in enumerate(frames):
+                r = cfws.frame_deserialize(w)
+                assert r["rc"] == 0 and r["payload"] == data + b"\0", (k, j)
+                if k == 1 and j == 2:
+                    cfws.lib().cfws_release_thread_resources()
+        except Exception as e:          # reported from the main thread
+            errors.append(e)
+
+    for _ in range(6):
+        ts = [threading.Thread(target=run, args=(k,)) for k in range(3)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+    assert not errors, errors

@@ -293,6 +293,28 @@ int main(int argc, char** argv)
             run_write<19, 4>(lds);
         }
     }
+    if (sweep == 3) {
+        // relative placement of the two streams: dst shifted by `off` bytes
+        // against src (both 16-B aligned), same copy kernel
+        static const uint64_t offs[] = {0, 256, 512, 1024, 2048, 3072, 4096, 6144, 8192, 12288, 16384,
+                                        24576, 32768, 49152, 65536, 131072, 262144, 524288, 1048576};
+        uint8_t* base_dst = g_dst;
+        for (int rep = 0; rep < 2; ++rep)
+            for (uint64_t off : offs) {
+                g_dst = base_dst + off;
+                const uint64_t per_block = 4 * 4096;
+                const uint32_t blocks = (uint32_t)((g_bytes - 2 * 1048576) / per_block);
+                auto k = gcopy_kernel<false, 0, 4>;
+                CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+                const double t = time_it([&] { k<<<blocks, 256, 32000>>>(g_src, g_dst, 0x9e3779b9u); },
+                                         2.0 * double(blocks) * per_block);
+                printf("{\"kind\": \"offset\", \"dst_minus_src_mod\": %llu, \"TBps\": %.3f}\n",
+                       (unsigned long long)off, t);
+                fflush(stdout);
+            }
+        g_dst = base_dst;
+        return 0;
+    }
     if (sweep == 2) {
         for (int rep = 0; rep < 2; ++rep)
             for (int lds : {0, 27000, 40000, 54000}) {

@@ -25,6 +25,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--frames", type=int, default=65536)
+    ap.add_argument("--orders", default="", help="e.g. SSSS,DDDD,SDSD: time each execute after another")
     args = ap.parse_args()
     import torch
     from coldforce_amd import cfws, shard
@@ -79,6 +80,34 @@ def main():
     payload = torch.empty(n, dtype=torch.uint8, device=dev)
     wire = torch.empty(wn, dtype=torch.uint8, device=dev)
     back = torch.empty(n + 64, dtype=torch.uint8, device=dev)
+    if args.orders:
+        # each execute's time by what ran before it (same arenas)
+        cfws.fill_splitmix(payload, 0x5EED0002, 0)
+        ws_ser = cfws.workspace(F, wire.numel(), dev)
+        ws_de = cfws.workspace(F, back.numel(), dev)
+        cfws.serialize_plan(desc_ser, wire.numel(), tot_ser, ws_ser)
+        cfws.serialize_execute(payload, desc_ser, wire, ws_ser)
+        cfws.deserialize_plan(wire, wire_total, index, desc_de, status, back.numel(), tot_de, ws_de, align=16)
+        ops = {"S": lambda: cfws.serialize_execute(payload, desc_ser, wire, ws_ser),
+               "D": lambda: cfws.deserialize_execute(wire, desc_de, status, back, ws_de),
+               "C": lambda: back[:n].copy_(payload)}
+        for seq in args.orders.split(","):
+            times = {k: [] for k in range(len(seq))}
+            for _ in range(args.reps):
+                ev = [torch.cuda.Event(enable_timing=True) for _ in range(len(seq) + 1)]
+                ev[0].record()
+                for k, c in enumerate(seq):
+                    ops[c]()
+                    ev[k + 1].record()
+                torch.cuda.synchronize()
+                for k in range(len(seq)):
+                    times[k].append(ev[k].elapsed_time(ev[k + 1]))
+            out = []
+            for k, c in enumerate(seq):
+                t = sorted(times[k])[len(times[k]) // 2]
+                out.append({"op": c, "ms": round(t, 4), "TBps": round(alg / t / 1e9, 3)})
+            print(json.dumps({"order": seq, "ops": out}), flush=True)
+        return
     run("separate", payload, wire, back)
     run("separate_swapped_roles", back[:n], wire, payload[:n])   # payload from the third allocation
     del payload, wire, back
