@@ -384,8 +384,9 @@ int cfws_xor_mask(const void* d_src, void* d_dst, uint64_t n, uint32_t mask_key,
  * means every frame is masked; unmasked frames get key 0. Host memory. */
 void cfws_draw_mask_keys(size_t n_frames, const uint8_t* mask_flags, uint32_t* keys);
 
-/* Frees the calling thread's drop-in staging buffer and stream
- * (cfws_frame.cpp); optional. */
+/* Frees the calling thread's drop-in staging buffers and stream
+ * (cfws_frame.cpp) now; optional: a thread that exits without calling it
+ * hands them back for reuse by later threads. */
 void cfws_release_thread_resources(void);
 
 /* ---- synthetic input (bench / tests) -------------------------------------
