@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--frames", type=int, default=65536)
     ap.add_argument("--orders", default="", help="e.g. SSSS,DDDD,SDSD: time each execute after another")
+    ap.add_argument("--align", type=int, default=16, help="deserialize payload alignment (orders mode)")
     args = ap.parse_args()
     import torch
     from coldforce_amd import cfws, shard
@@ -87,9 +88,17 @@ def main():
         ws_de = cfws.workspace(F, back.numel(), dev)
         cfws.serialize_plan(desc_ser, wire.numel(), tot_ser, ws_ser)
         cfws.serialize_execute(payload, desc_ser, wire, ws_ser)
-        cfws.deserialize_plan(wire, wire_total, index, desc_de, status, back.numel(), tot_de, ws_de, align=16)
+        cfws.deserialize_plan(wire, wire_total, index, desc_de, status, back.numel(), tot_de, ws_de,
+                              align=args.align)
+        # T: serialize reading the unmasked copy D wrote; E: deserialize from a
+        # second wire arena written once at setup and never again
+        wire2 = torch.empty_like(wire)
+        wire2.copy_(wire)
+        back2 = torch.empty_like(back)
         ops = {"S": lambda: cfws.serialize_execute(payload, desc_ser, wire, ws_ser),
                "D": lambda: cfws.deserialize_execute(wire, desc_de, status, back, ws_de),
+               "T": lambda: cfws.serialize_execute(back, desc_ser, wire, ws_ser),
+               "E": lambda: cfws.deserialize_execute(wire2, desc_de, status, back2, ws_de),
                "C": lambda: back[:n].copy_(payload)}
         for seq in args.orders.split(","):
             times = {k: [] for k in range(len(seq))}
@@ -106,7 +115,8 @@ def main():
             for k, c in enumerate(seq):
                 t = sorted(times[k])[len(times[k]) // 2]
                 out.append({"op": c, "ms": round(t, 4), "TBps": round(alg / t / 1e9, 3)})
-            print(json.dumps({"order": seq, "ops": out}), flush=True)
+            print(json.dumps({"order": seq, "align": args.align, "edge_split": os.environ.get("CFWS_EDGE_SPLIT", "0"),
+                              "ops": out}), flush=True)
         return
     run("separate", payload, wire, back)
     run("separate_swapped_roles", back[:n], wire, payload[:n])   # payload from the third allocation
