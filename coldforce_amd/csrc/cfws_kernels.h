@@ -298,14 +298,17 @@ __device__ __forceinline__ void st16(uint8_t* p, uint4 o)
 }
 
 // Body stores of the streaming regions, at byte `off` of the wave's output
-// region `rb` (wave-uniform), with a cache policy per direction. Policy
-// bits (gfx940+): sc0 1, nt 2, sc1 16; 0 = the global `nt` store (st16).
-// Writing the payload arena (deserialize) measured fastest write-through
-// (`sc0 sc1 nt`, a buffer store over the region): 6.49 -> 6.60 TB/s on
-// config 2, while writing the wire (serialize) lost 1-2 % that way and keeps
-// `nt` (profiles/r02_ab_store.txt). CFWS_STORE_AUX_SEND / _RECV override.
-#ifndef CFWS_STORE_AUX_SEND
-#define CFWS_STORE_AUX_SEND 0
+// region `rb` (wave-uniform), with a cache policy per mode. Policy bits
+// (gfx940+): sc0 1, nt 2, sc1 16; 0 = the global `nt` store (st16).
+// WS serialize and deserialize store write-through (`sc0 sc1 nt`, a buffer
+// store over the region): deserialize 6.49 -> 6.52-6.60 TB/s on config 2;
+// serialize gains only at 4 workgroups per CU (xform_lds_bytes), where it
+// went from 6.34-6.37 to 6.44-6.48 TB/s (at 5 per CU it lost 1-2 %;
+// profiles/r02_ab_store.txt, r02_ab_sendwt_lds.txt, r02_ab_fs.txt). The
+// HTTP/2 send keeps `nt` (write-through measured no faster there).
+// CFWS_STORE_AUX_SER / _RECV override at build time.
+#ifndef CFWS_STORE_AUX_SER
+#define CFWS_STORE_AUX_SER 19
 #endif
 #ifndef CFWS_STORE_AUX_RECV
 #define CFWS_STORE_AUX_RECV 19
@@ -313,7 +316,7 @@ __device__ __forceinline__ void st16(uint8_t* p, uint4 o)
 template <int kMode>
 __device__ __forceinline__ void st16_region(uint8_t* rb, uint32_t off, uint4 o)
 {
-    constexpr int aux = kMode == kModeDeser ? CFWS_STORE_AUX_RECV : CFWS_STORE_AUX_SEND;
+    constexpr int aux = kMode == kModeDeser ? CFWS_STORE_AUX_RECV : (kMode == kModeSer ? CFWS_STORE_AUX_SER : 0);
     if (aux == 0) {
         st16(rb + off, o);
     } else {
@@ -716,12 +719,13 @@ __device__ __forceinline__ void two_frame_region(const Pass& P, const FrameView&
     }
 }
 
-// Any other region (small frames, padding, pass end): every lane finds the
-// frame of each of its chunks by binary search over the region's frames and
-// writes it when it lies inside that frame's body.
+// Any other region (small frames, padding, pass end) with more than 64
+// frames: every lane finds the frame of each of its chunks by binary search
+// over the region's frames and writes it when it lies inside that frame's
+// body.
 template <int kMode>
-__device__ __forceinline__ void general_region(const Pass& P, uint32_t f0, uint32_t f1,
-                                               uint64_t base, uint32_t lane)
+__device__ __forceinline__ void general_region_search(const Pass& P, uint32_t f0, uint32_t f1,
+                                                      uint64_t base, uint32_t lane)
 {
     uint32_t fr[kUnroll];
 #pragma unroll
@@ -740,6 +744,77 @@ __device__ __forceinline__ void general_region(const Pass& P, uint32_t f0, uint3
         const FrameView v = frame_view<kMode>(P, fr[u]);
         if (D >= v.body_start && D + kChunk <= v.body_start + v.body_len)
             st16_region<kMode>(P.dst + base, (uint32_t)(D - base), body_chunk(P.src, v, D));
+    }
+}
+
+// A region touched by 3..64 frames (runs of small frames): lane l loads what
+// the chunks need of frame f0 + l, all lanes at once (one round of loads
+// instead of a search and a view per chunk, each a chain of dependent
+// loads), reduced to four words relative to the region base: the frame's
+// output start, its body range, its source delta and its key rotated for
+// 16-aligned chunks. Each chunk then finds its frame by a binary search over
+// the lanes (shuffles) and loads only its source blocks.
+template <int kMode>
+__device__ __forceinline__ void general_region(const Pass& P, uint32_t f0, uint32_t f1, uint64_t base,
+                                               uint32_t lane)
+{
+    const uint32_t nf = f1 - f0 + 1;
+#ifdef CFWS_GENERAL_SEARCH
+    const bool search = true;                   // A/B: the per-chunk search everywhere
+#else
+    const bool search = nf > 64;
+#endif
+    if (search) {
+        general_region_search<kMode>(P, f0, f1, base, lane);
+        return;
+    }
+    auto rel = [base](uint64_t x, uint64_t hi) -> uint32_t {
+        return x <= base ? 0u : (x - base >= hi ? (uint32_t)hi : (uint32_t)(x - base));
+    };
+    uint32_t ro = (uint32_t)kRegion, rng = 0, kr = 0, dlo = 0, dhi = 0;
+    if (lane < nf) {
+        const FrameView v = frame_view<kMode>(P, f0 + lane);
+        ro = rel(v.out_off, kRegion);
+        rng = rel(v.body_start + v.body_len, kRegion + kChunk) << 16 | rel(v.body_start, kRegion);
+        const uint64_t delta = v.src_off - v.body_start;           // src = out + delta
+        dlo = (uint32_t)delta;
+        dhi = (uint32_t)(delta >> 32);
+        kr = rotr8(v.key, (uint32_t)(base - v.body_start) & 3u);
+    }
+    const uint8_t* sp[kUnroll];
+    uint32_t ph[kUnroll], key[kUnroll];
+    bool fast[kUnroll];
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+        const uint32_t r = u * (uint32_t)kSlice + lane * (uint32_t)kChunk;
+        uint32_t j = 0;                             // largest frame with start <= r
+#pragma unroll
+        for (uint32_t step = 32; step >= 1; step >>= 1) {
+            const uint32_t c = j + step;
+            const uint32_t oc = (uint32_t)__shfl((int)ro, (int)(c & 63u), 64);
+            if (c < nf && oc <= r) j = c;
+        }
+        const uint32_t rg = (uint32_t)__shfl((int)rng, (int)j, 64);
+        const uint64_t d = (uint64_t)(uint32_t)__shfl((int)dlo, (int)j, 64) |
+                           (uint64_t)(uint32_t)__shfl((int)dhi, (int)j, 64) << 32;
+        key[u] = (uint32_t)__shfl((int)kr, (int)j, 64);
+        fast[u] = r >= (rg & 0xffffu) && r + kChunk <= (rg >> 16);
+        const uint64_t s = base + r + d;
+        ph[u] = (uint32_t)(s & 15u);
+        sp[u] = P.src + (s & ~uint64_t(15));
+    }
+    uint4 a[kUnroll], b[kUnroll];
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) a[u] = fast[u] ? ld16(sp[u]) : make_uint4(0, 0, 0, 0);
+    // the block holding the chunk's last byte: a body byte, inside the source
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) b[u] = fast[u] && ph[u] ? ld16(sp[u] + 16) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+        if (!fast[u]) continue;
+        uint4 o = ph[u] ? funnel16(a[u], b[u], ph[u]) : a[u];
+        xor4(o, key[u]);
+        st16_region<kMode>(P.dst + base, u * (uint32_t)kSlice + lane * (uint32_t)kChunk, o);
     }
 }
 
@@ -1341,10 +1416,20 @@ inline int zero_totals(const WsLayout& L, void* ws, uint64_t* d_total, hipStream
 // VGPRs) is register-limited to 5 per CU already, and there the reservation
 // only cost: config 3 serialize 6.20 TB/s without it against 6.02-6.10 with
 // (config 2 6.27 vs 6.29; the 78-80-VGPR modes reach 6 per CU without it and
-// lose 8 % on config 2 deserialize). So kModeSer reserves none by default.
+// lose 8 % on config 2 deserialize). With its write-through stores (round 2)
+// serialize runs best at 4 per CU (CFWS_SER_LDS = 40000): 6.44-6.48 TB/s on
+// config 2, and ahead at every uniform frame size from 16 KiB to 1 MiB
+// (6.35-6.46 against 6.00-6.37); config 3 holds its rate since the
+// small-frame regions load their frames in one round (general_region).
 // CFWS_XFORM_LDS overrides for every mode (0 = none).
 constexpr uint32_t kXformLdsDefault = 32000;     // 5 x fits 160 KiB, 6 x does not
 
+#ifndef CFWS_SER_LDS
+#define CFWS_SER_LDS 40000                       // 4 x fits 160 KiB, 5 x does not
+#endif
+#ifndef CFWS_H2SER_LDS
+#define CFWS_H2SER_LDS kXformLdsDefault
+#endif
 inline uint32_t xform_lds_bytes(int mode = -1)
 {
     static int64_t v = -2;                      // -1: no override
@@ -1354,7 +1439,9 @@ inline uint32_t xform_lds_bytes(int mode = -1)
         if (v > 65536) v = 65536;
     }
     if (v >= 0) return (uint32_t)v;
-    return mode == kModeSer ? 0u : kXformLdsDefault;
+    if (mode == kModeSer) return CFWS_SER_LDS;
+    if (mode == kModeH2Ser) return CFWS_H2SER_LDS;
+    return kXformLdsDefault;
 }
 
 // One pass: the streaming kernel with its edge workgroups in front
