@@ -313,3 +313,29 @@ def test_xor_mask(n):
             kb = np.array([0xD4, 0xC3, 0xB2, 0xA1], np.uint8)
             exp = s ^ kb[(np.arange(n) + phase) % 4]
             assert np.array_equal(dst.cpu().numpy()[so:so + n], exp)
+
+
+@pytest.mark.parametrize("seed", [21, 22])
+def test_small_frame_regions_both_forms(seed):
+    """Runs of 30-80-byte frames put 40-130 frames into a 4 KiB output region,
+    on both sides of the 64-frame line between general_region's lane-parallel
+    form and its per-chunk search; occasional 5,000-byte frames add one- and
+    two-frame regions. Serialize, then deserialize the same wire packed
+    (align 1), aligned (16) and reassembled, against the oracle."""
+    rng = random.Random(seed)
+    n = 6000
+    payload = O.fill_splitmix(1 << 20, seed, 0)
+    sizes = [rng.randrange(30, 80) for _ in range(n)]
+    for i in range(0, n, 97):
+        sizes[i] = 5000
+    desc = random_desc(rng, n, 1 << 20, sizes=None)
+    desc["payload_size"] = sizes
+    desc["payload_off"] = [rng.randrange(0, (1 << 20) - s) for s in sizes]
+    desc["opcode"] = [rng.choice([0, 1, 2, 8, 9, 10]) for _ in range(n)]    # no RSV bits
+    wire, total = check_serialize(payload, desc)
+    w = wire[:total].copy()
+    starts, consumed = O.index_frames(w, n + 1)
+    assert consumed == total and len(starts) == n
+    for align in (1, 16):
+        check_deserialize(w, starts, align=align)
+    check_deserialize(w, starts, flags=cfws.DESERIALIZE_REASSEMBLE)
