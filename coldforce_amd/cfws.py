@@ -46,7 +46,8 @@ BATCH_SYMBOLS = (
     "cfws_init", "cfws_last_error", "cfws_version", "cfws_workspace_size",
     "cfws_serialize_plan", "cfws_serialize_execute", "cfws_serialize_batch",
     "cfws_deserialize_plan", "cfws_deserialize_execute", "cfws_deserialize_batch",
-    "cfws_xor_mask", "cfws_draw_mask_keys", "cfws_release_thread_resources",
+    "cfws_xor_mask", "cfws_draw_mask_keys", "cfws_draw_mask_keys_seeded",
+    "cfws_release_thread_resources",
     "cfws_fill_splitmix", "cfws_pipeline_create", "cfws_pipeline_destroy",
     "cfws_pipeline_serialize", "cfws_pipeline_deserialize", "cfws_pipeline_receive",
     "cfws_h2_serialize_workspace_size", "cfws_h2_serialize_batch",
@@ -128,6 +129,7 @@ def lib(path: str = LIB_PATH) -> C.CDLL:
         "cfws_mapped_device_pointer": ([_vp], _vp),
         "cfws_xor_mask": ([_vp, _vp, _u64, _u32, _u32, _vp], C.c_int),
         "cfws_draw_mask_keys": ([_sz, _vp, _vp], None),
+        "cfws_draw_mask_keys_seeded": ([_u32, _sz, _vp, _vp], C.c_int),
         "cfws_release_thread_resources": ([], None),
         "cfws_fill_splitmix": ([_vp, _u64, _u64, _u64, _vp], C.c_int),
         "cfws_h2_serialize_workspace_size": ([_sz, _u64, _u64, _u32], _sz),
@@ -195,13 +197,19 @@ def _stream(stream) -> int | None:
 # ---- host helpers ----------------------------------------------------------
 
 def draw_mask_keys(n: int, mask_flags=None, seed: int | None = None) -> np.ndarray:
-    """Keys exactly as n sequential co_ws_frame_serialize calls draw them
-    (after srandom(seed) when a seed is given)."""
-    if seed is not None:
-        C.CDLL(None).srandom(C.c_uint(seed))
+    """Keys exactly as n sequential co_ws_frame_serialize calls draw them:
+    from the process's random() state, or, with a seed, as they would right
+    after srandom(seed) (cfws_draw_mask_keys_seeded: a private copy of the
+    generator, which no other thread's rand() can disturb; the HIP and torch
+    runtimes' libraries call rand()/random() on threads of their own)."""
     keys = np.zeros(n, dtype=np.uint32)
     mf = None if mask_flags is None else np.ascontiguousarray(mask_flags, dtype=np.uint8)
-    lib().cfws_draw_mask_keys(n, None if mf is None else mf.ctypes.data, keys.ctypes.data)
+    mp = None if mf is None else mf.ctypes.data
+    if seed is None:
+        lib().cfws_draw_mask_keys(n, mp, keys.ctypes.data)
+    else:
+        _check(lib().cfws_draw_mask_keys_seeded(seed, n, mp, keys.ctypes.data),
+               "cfws_draw_mask_keys_seeded")
     return keys
 
 

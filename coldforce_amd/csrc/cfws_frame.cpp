@@ -367,6 +367,32 @@ void cfws_draw_mask_keys(size_t n, const uint8_t* mask_flags, uint32_t* keys)
     }
 }
 
+// The same keys from srandom(seed)'s stream, drawn on a private state
+// (glibc's reentrant random_r over a 128-byte TYPE_3 table: the generator
+// and seeding srandom uses on the default state), so no other thread's
+// rand()/random() call can interleave with the draws, and the process's
+// random() state is left alone.
+int cfws_draw_mask_keys_seeded(uint32_t seed, size_t n, const uint8_t* mask_flags, uint32_t* keys)
+{
+    char table[128];
+    struct random_data rd;
+    memset(&rd, 0, sizeof rd);
+    memset(table, 0, sizeof table);
+    if (initstate_r(seed, table, sizeof table, &rd) != 0) return CFWS_ERROR_INVALID_ARGUMENT;
+    for (size_t i = 0; i < n; ++i) {
+        uint32_t k = 0;
+        if (!mask_flags || mask_flags[i]) {
+            for (int j = 0; j < 4; ++j) {
+                int32_t r = 0;
+                (void)random_r(&rd, &r);
+                k |= static_cast<uint32_t>(static_cast<uint8_t>(r % 256)) << (8 * j);
+            }
+        }
+        keys[i] = k;
+    }
+    return CFWS_OK;
+}
+
 // Frees the calling thread's staging buffers and stream now (optional: a
 // thread that exits without calling it hands them back for reuse by later
 // threads instead).

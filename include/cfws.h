@@ -383,6 +383,12 @@ int cfws_xor_mask(const void* d_src, void* d_dst, uint64_t n, uint32_t mask_key,
  * (co_ws_frame.c:84 -> src/core/co_random.c:32-35). mask_flags == NULL
  * means every frame is masked; unmasked frames get key 0. Host memory. */
 void cfws_draw_mask_keys(size_t n_frames, const uint8_t* mask_flags, uint32_t* keys);
+/* The keys the same calls draw right after srandom(seed), taken from a
+ * private copy of that generator (glibc random_r): other threads' rand() /
+ * random() calls cannot interleave with the draws, and the process's
+ * random() state is not touched. CFWS_OK, or CFWS_ERROR_INVALID_ARGUMENT. */
+int cfws_draw_mask_keys_seeded(uint32_t seed, size_t n_frames, const uint8_t* mask_flags,
+                               uint32_t* keys);
 
 /* Frees the calling thread's drop-in staging buffers and stream
  * (cfws_frame.cpp) now; optional: a thread that exits without calling it

@@ -203,11 +203,30 @@ int orc_deserialize(orc_frame_t* f, const uint8_t* data, size_t data_size,
 
 /* ---- batch mirrors of the device ABI ---------------------------------- */
 
+/* The keys n sequential co_ws_frame_serialize calls draw right after
+ * srandom(seed) (co_net.c:46 seeds, co_random.c:32-35 draws): the same
+ * generator (glibc's TYPE_3 additive generator on a 128-byte table, what
+ * srandom seeds by default) run on a private copy through random_r, so no
+ * other thread's rand()/random() -- the GPU runtime's libraries make such
+ * calls on threads of their own -- can interleave with the draws. */
 void orc_keys(uint32_t seed, size_t n, const uint8_t* mask_flags, uint32_t* keys)
 {
-    srandom(seed);
-    for (size_t i = 0; i < n; ++i)
-        keys[i] = (mask_flags == NULL || mask_flags[i]) ? orc_draw_key() : 0u;
+    char table[128];
+    struct random_data rd;
+    memset(&rd, 0, sizeof rd);
+    memset(table, 0, sizeof table);
+    initstate_r(seed, table, sizeof table, &rd);
+    for (size_t i = 0; i < n; ++i) {
+        uint32_t k = 0;
+        if (mask_flags == NULL || mask_flags[i]) {
+            for (int j = 0; j < 4; ++j) {
+                int32_t r = 0;
+                random_r(&rd, &r);
+                k |= (uint32_t)(uint8_t)(r % 256) << (8 * j);
+            }
+        }
+        keys[i] = k;
+    }
 }
 
 uint64_t orc_serialize_batch(const uint8_t* payload, orc_desc_t* d, size_t n,

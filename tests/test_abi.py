@@ -78,6 +78,27 @@ def test_draw_mask_keys_matches_reference_stream():
                                      int.from_bytes(bytes.fromhex(ref[1]), "little"), 0]
 
 
+def test_seeded_key_draw_equals_srandom_stream_and_keeps_global_state():
+    """cfws_draw_mask_keys_seeded (a private random_r copy of the generator)
+    draws what srandom(seed) + cfws_draw_mask_keys draws, and leaves the
+    process's random() stream where it was."""
+    from coldforce_amd import cfws
+    libc = ctypes.CDLL(None)
+    libc.random.restype = ctypes.c_long
+    rng = np.random.default_rng(3)
+    for seed in (0, 1, 2, 5, 1234, 0xFFFFFFFF):
+        flags = (rng.random(3000) < .6).astype(np.uint8)
+        libc.srandom(ctypes.c_uint(seed))
+        glob = np.zeros(3000, np.uint32)
+        cfws.lib().cfws_draw_mask_keys(3000, flags.ctypes.data, glob.ctypes.data)
+        libc.srandom(ctypes.c_uint(99))
+        before = libc.random()
+        libc.srandom(ctypes.c_uint(99))
+        seeded = cfws.draw_mask_keys(3000, flags, seed=seed)
+        assert libc.random() == before                # global stream untouched
+        assert np.array_equal(seeded, glob), seed
+
+
 def test_dropin_host_paths_without_device():
     """Unmasked frames and header-only decisions never touch the device."""
     from coldforce_amd import cfws

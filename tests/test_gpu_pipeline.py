@@ -136,7 +136,15 @@ def test_pipeline_config2_reduced_digest():
     pl = make_pipeline(chunk_bytes=8 << 20, max_frames=4096, depth=3)
     tot = pl.serialize(payload_t.data_ptr(), desc, wire_t.data_ptr(), wire.size)
     assert tot == g["wire_len"]
-    assert hashlib.sha256(wire[:tot].tobytes()).hexdigest() == g["wire_sha256"]
+    if hashlib.sha256(wire[:tot].tobytes()).hexdigest() != g["wire_sha256"]:
+        # say where: the keys drawn, then the bytes against the oracle's wire
+        exp, _ = O.serialize_batch(payload, desc.view(O.DESC_DTYPE))
+        keys_ok = hashlib.sha256(exp.tobytes()).hexdigest() == g["wire_sha256"]
+        bad = np.nonzero(wire[:tot] != exp)[0]
+        frames = np.unique(np.searchsorted(desc["wire_off"], bad, side="right") - 1)
+        pytest.fail(f"wire differs: keys as the reference's {keys_ok}, {bad.size} bytes, "
+                    f"first at {bad[:4].tolist()}, frames {frames[:16].tolist()} "
+                    f"({frames.size} in all)")
     back_t, back = pinned(n * fs)
     d2, st, ptot = pl.deserialize(wire_t.data_ptr(), tot, desc["wire_off"], back_t.data_ptr(),
                                   back.size)
