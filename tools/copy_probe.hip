@@ -251,6 +251,55 @@ __global__ void __launch_bounds__(256) gcopy_kernel(const uint8_t* __restrict__ 
     }
 }
 
+// The codec's round-2 form: global loads (one per block, DPP neighbour for
+// the misaligned mode), stores as buffer stores over the wave's region with
+// cache-policy bits kAux (19 = sc0 sc1 nt: write-through; 2 = nt).
+template <int kAux, bool kNtLoad, bool kMis>
+__global__ void __launch_bounds__(256) wcopy_kernel(const uint8_t* __restrict__ src,
+                                                    uint8_t* __restrict__ dst, uint32_t key)
+{
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t region = (uint64_t(blockIdx.x) * 4 + wave) * 4096;
+    const u32x4* s = reinterpret_cast<const u32x4*>(src + region) + lane;
+    auto rd = __builtin_amdgcn_make_buffer_rsrc((void*)(dst + region), 0, 4096, 0x00020000);
+    u32x4 a[4], b[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) a[u] = kNtLoad ? __builtin_nontemporal_load(s + u * 64) : s[u * 64];
+    if (kMis && lane == 63) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) b[u] = s[u * 64 + 1];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        u32x4 o = a[u];
+        if (kMis) {
+            const uint32_t sh = __builtin_amdgcn_update_dpp(0u, a[u].x, 0x130, 0xf, 0xf, false);
+            const uint32_t nx = lane == 63 ? b[u].x : sh;
+            o.x = __builtin_amdgcn_alignbyte(a[u].y, a[u].x, 2);
+            o.y = __builtin_amdgcn_alignbyte(a[u].z, a[u].y, 2);
+            o.z = __builtin_amdgcn_alignbyte(a[u].w, a[u].z, 2);
+            o.w = __builtin_amdgcn_alignbyte(nx, a[u].w, 2);
+        }
+        o ^= key;
+        __builtin_amdgcn_raw_buffer_store_b128(o, rd, u * 1024 + lane * 16, 0, kAux);
+    }
+}
+
+template <int A, bool NL, bool M>
+static void run_wcopy(int lds)
+{
+    const uint64_t per_block = 4 * 4096;
+    const uint32_t blocks = (uint32_t)(g_bytes / per_block);
+    auto k = wcopy_kernel<A, NL, M>;
+    CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    const double t = time_it([&] { k<<<blocks, 256, lds>>>(g_src, g_dst, 0x9e3779b9u); },
+                             2.0 * double(blocks) * per_block);
+    printf("{\"kind\": \"wcopy\", \"store_aux\": %d, \"nt_load\": %d, \"misaligned\": %d, \"lds\": %d, \"TBps\": %.3f}\n",
+           A, (int)NL, (int)M, lds, t);
+    fflush(stdout);
+}
+
 template <bool NL, int M, int U>
 static void run_gcopy(int lds)
 {
@@ -292,6 +341,18 @@ int main(int argc, char** argv)
             run_write<0, 4>(lds);
             run_write<19, 4>(lds);
         }
+    }
+    if (sweep == 4) {
+        // write-through vs nt stores by occupancy (LDS pad: 0 = register
+        // bound, 27000 = 6, 32000 = 5, 40000 = 4, 54000 = 3 WG/CU)
+        for (int rep = 0; rep < 2; ++rep)
+            for (int lds : {0, 27000, 32000, 40000, 54000}) {
+                run_wcopy<2, false, true>(lds);
+                run_wcopy<19, false, true>(lds);
+                run_wcopy<19, true, true>(lds);
+                run_wcopy<19, false, false>(lds);
+            }
+        return 0;
     }
     if (sweep == 3) {
         // relative placement of the two streams: dst shifted by `off` bytes
