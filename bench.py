@@ -49,7 +49,11 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="target CPU time of the cpu_baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--workload", choices=["config2", "config3", "config4", "config5", "split"],
+    ap.add_argument("--keys", type=int, default=1 << 20, help="accept workload: client keys per GPU")
+    ap.add_argument("--connections", type=int, default=16384, help="index workload: connections")
+    ap.add_argument("--index-mib", type=int, default=1024, help="index workload: receive-buffer MiB")
+    ap.add_argument("--workload", choices=["config2", "config3", "config4", "config5", "split", "accept",
+                                           "index"],
                     default="config2",
                     help="config2: uniform 64 KiB frames (the metric's config); config3: Zipf "
                          "64 B-1 MiB messages in 1-8 continuation fragments, reassembled; "
@@ -57,7 +61,9 @@ def parse():
                          "(1,048,576 frames = 64 GiB per GPU); "
                          "config5: WebSocket over HTTP/2 DATA frames (--frame-size, default "
                          "16376); split: config 2 through the split ops (encode_headers + "
-                         "mask_batch, parse_headers + unmask_batch)")
+                         "mask_batch, parse_headers + unmask_batch); accept: handshake accept "
+                         "keys for a connection storm (--keys); index: the receive loop's frame "
+                         "walk over many connections (--connections, --index-mib)")
     return ap.parse_args()
 
 
@@ -235,6 +241,209 @@ def bench_split(args, rank, world, dev):
     return 0 if ok else 1
 
 
+VALU_PEAK_OPS = 256 * 4 * 32 * 2.4e9     # lane-ops/s: 256 CUs x 4 SIMDs x 32 lanes/clk x 2.4 GHz
+
+
+def load_pmc(name: str, key: str):
+    """A per-launch counter value from a committed PMC summary (profiles/)."""
+    try:
+        with open(os.path.join(ROOT, "profiles", name)) as f:
+            return json.load(f).get(key)
+    except (OSError, ValueError):
+        return None
+
+
+def bench_accept(args, rank, world, dev):
+    """Sec-WebSocket-Accept for a connection storm
+    (co_ws_create_base64_accept_key, co_ws_http_extension.c:26-57) -- one
+    cfws_ws_accept_keys_batch over N client keys (24-character base64 of 16
+    random bytes, RFC 6455 4.1) per step, device resident. Checked against the
+    oracle on a sample; the CPU baseline runs the reference's co_sha1.c +
+    co_base64.c (oracle/_ref) on the host's threads."""
+    import base64
+    import random
+
+    import numpy as np
+    import torch
+
+    import oracle as O
+    from coldforce_amd import cfws, shard
+    N = args.keys
+    rng = random.Random(0x5EED0006 + rank)
+    keys = [base64.b64encode(rng.randbytes(16)) for _ in range(N)]
+    raw = np.frombuffer(b"".join(keys), np.uint8).copy()
+    off = np.zeros(N + 1, dtype=np.int64)
+    off[1:] = np.cumsum([len(k) for k in keys])
+    d_keys = torch.from_numpy(raw).to(dev)
+    d_off = torch.from_numpy(off).to(dev)
+    out = torch.zeros(N * cfws.WS_ACCEPT_SLOT, dtype=torch.uint8, device=dev)
+
+    def step():
+        cfws._check(cfws.lib().cfws_ws_accept_keys_batch(cfws._p(d_keys), cfws._p(d_off), N,
+                                                         cfws._p(out), cfws._stream(None)),
+                    "cfws_ws_accept_keys_batch")
+
+    for _ in range(args.warmup):
+        step()
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(args.steps)]
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        ev[k][0].record()
+        step()
+        ev[k][1].record()
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    local = time.perf_counter() - t0
+    elapsed = shard.max_over_ranks(local, dev)
+    kms = sum(e[0].elapsed_time(e[1]) for e in ev) / args.steps
+    h = out.view(N, cfws.WS_ACCEPT_SLOT)
+    sample = list(range(0, N, max(1, N // 4096)))
+    got = h[sample, :28].cpu().numpy()
+    ok = all(bytes(got[j]).decode() == O.ws_accept_key(keys[i]) for j, i in enumerate(sample))
+    ok = shard.sum_over_ranks(1.0 if ok else 0.0, dev) == world
+    valu = load_pmc("pmc_accept.json", "SQ_INSTS_VALU_per_launch")
+    achieved = valu * 64 / (kms * 1e-3) if valu else None
+    line = {"metric": "WS handshake Sec-WebSocket-Accept keys/s (SHA-1 + base64), device resident",
+            "value": round(N * world * args.steps / elapsed, 1), "unit": "keys/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
+            "scaling": "weak", "dtype": "u32", "data": "synthetic (24-char base64 client keys)",
+            "config": {"workload": f"accept: {N} client keys per GPU, one accept key per thread"},
+            "roofline": {"bound": "valu", "kernel": "ws_accept_kernel", "avg_launch_ms": round(kms, 4),
+                         "achieved": round(achieved / 1e12, 2) if achieved else None,
+                         "peak": round(VALU_PEAK_OPS / 1e12, 1), "unit": "T lane-ops/s",
+                         "frac": round(achieved / VALU_PEAK_OPS, 4) if achieved else None,
+                         "valu_instructions_per_launch": valu},
+            "verified": ok}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        kind = "reference" if O.ref_lib("O2") is not None else "port"
+        threads = max(1, min(16, len(os.sched_getaffinity(0))))
+        n = min(N, 262144)
+        t1 = O.cpu_accept_bench(raw, off[:n + 1].astype(np.uint64), threads, 1, kind)
+        iters = max(1, int(math.ceil(args.cpu_seconds / max(t1, 1e-3))))
+        t = O.cpu_accept_bench(raw, off[:n + 1].astype(np.uint64), threads, iters, kind)
+        line["cpu_baseline"] = {"value": round(n * iters / t, 1), "unit": "keys/s", "cores": threads,
+                                "kind": kind, "sample": f"{n} keys x {iters} iters, one "
+                                f"co_sha1 + co_base64_encode per key, {threads} threads",
+                                "seconds": round(t, 2)}
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    return 0 if ok else 1
+
+
+def bench_index(args, rank, world, dev):
+    """the receive loop's frame walk
+    (co_ws_server.c:107-169) for many connections at once
+    (cfws_index_frames_batch, one thread per connection), device resident.
+    A server tick: args.connections receive buffers in one arena, each
+    holding a run of client-masked 1 KiB TEXT frames (config 1's frame) and
+    a cut last frame (MORE_DATA), args.index_mib MiB in all. Checked against
+    the oracle's walk on a sample of connections; the CPU baseline is that
+    walk on the host's threads over every connection."""
+    import numpy as np
+    import torch
+
+    import oracle as O
+    from coldforce_amd import cfws, shard
+    from coldforce_amd import workloads as W
+    fs = 1024
+    F = (args.index_mib << 20) // (fs + 8)
+    desc = W.uniform_batch(F, fs, 1 + rank, opcode=cfws.OPCODE_TEXT)
+    payload = torch.empty(F * fs + 16, dtype=torch.uint8, device=dev)
+    cfws.fill_splitmix(payload, 0x5EED0001 + rank, 0)
+    offs, wtotal = W.wire_layout(desc)
+    wire = torch.empty(W.round16(wtotal) + 16, dtype=torch.uint8, device=dev)
+    cfws.serialize(payload, cfws.desc_to_device(desc, dev), wire)
+    torch.cuda.synchronize()
+    C_ = args.connections
+    rng = np.random.default_rng(17 + rank)
+    first_frame = (np.arange(C_ + 1, dtype=np.int64) * F) // C_
+    fstarts = np.concatenate([offs.astype(np.int64), [wtotal]])
+    begin_np = fstarts[first_frame[:-1]]
+    # each buffer ends inside its last frame (a partial read), or whole
+    cut = rng.integers(0, fs + 8, C_)
+    end_np = np.maximum(begin_np, fstarts[first_frame[1:]] - cut)
+    d_begin = torch.from_numpy(begin_np).to(dev)
+    d_end = torch.from_numpy(end_np).to(dev)
+    starts_t = torch.empty(F + C_, dtype=torch.int64, device=dev)     # every frame start fits
+    ws_t = torch.empty(cfws.lib().cfws_index_workspace_size(C_), dtype=torch.uint8, device=dev)
+    first = torch.empty(C_, dtype=torch.int64, device=dev)
+    consumed = torch.empty(C_, dtype=torch.int64, device=dev)
+    stop = torch.empty(C_, dtype=torch.int32, device=dev)
+    total = torch.zeros(1, dtype=torch.int64, device=dev)
+
+    def step():
+        cfws._check(cfws.lib().cfws_index_frames_batch(
+            cfws._p(wire), cfws._p(d_begin), cfws._p(d_end), C_, cfws.DEFAULT_MAX_PAYLOAD,
+            cfws._p(starts_t), starts_t.numel(), cfws._p(first), cfws._p(consumed), cfws._p(stop),
+            cfws._p(total), cfws._p(ws_t), ws_t.numel(), cfws._stream(None)), "cfws_index_frames_batch")
+
+    for _ in range(args.warmup):
+        step()
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(args.steps)]
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        ev[k][0].record()
+        step()
+        ev[k][1].record()
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    local = time.perf_counter() - t0
+    elapsed = shard.max_over_ranks(local, dev)
+    kms = sum(e[0].elapsed_time(e[1]) for e in ev) / args.steps
+    n_frames = int(total.item())
+    host_wire = wire[:wtotal].cpu().numpy()
+    st_h, first_h = starts_t.cpu().numpy(), first.cpu().numpy()
+    con_h, stop_h = consumed.cpu().numpy(), stop.cpu().numpy()
+    ok = True
+    for c in range(0, C_, max(1, C_ // 256)):
+        e_st, e_con, e_stop = O.index_stream(host_wire, int(begin_np[c]), int(end_np[c]))
+        ok &= bool(np.array_equal(st_h[first_h[c]:first_h[c] + len(e_st)].astype(np.uint64), e_st)
+                   and con_h[c] == e_con and stop_h[c] == e_stop)
+    ok = shard.sum_over_ranks(1.0 if ok else 0.0, dev) == world
+    hops = n_frames / C_
+    line = {"metric": "WS receive-buffer frame indexing frames/s, many connections, device resident",
+            "value": round(n_frames * world * args.steps / elapsed, 1), "unit": "frames/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
+            "scaling": "weak", "dtype": "u8",
+            "data": "synthetic (client-masked 1 KiB TEXT frames, buffers cut inside their last frame)",
+            "config": {"workload": f"index: {C_} connections x {hops:.1f} frames, "
+                                   f"{args.index_mib} MiB of receive buffers",
+                       "wire_bytes": int(wtotal), "frames": n_frames, "connections": C_},
+            "roofline": {"bound": "latency", "avg_launch_ms": round(kms, 4),
+                         "note": "each connection is a chain of dependent header reads (count, "
+                                 "scan, then the walk again to write starts), so the launch is "
+                                 "bounded by hop latency x chain length, not HBM bytes",
+                         "ns_per_hop": round(kms * 1e6 / max(hops, 1e-9), 1)},
+            "verified": ok}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        threads = max(1, min(16, len(os.sched_getaffinity(0))))
+        ub = (begin_np.astype(np.uint64), end_np.astype(np.uint64))
+        t1, _ = O.cpu_index_bench(host_wire, ub[0], ub[1], 4096, threads)
+        reps = max(1, int(math.ceil(args.cpu_seconds / max(t1, 1e-3))))
+        t, f = 0.0, 0
+        for _ in range(reps):
+            ti, fi = O.cpu_index_bench(host_wire, ub[0], ub[1], 4096, threads)
+            t += ti
+            f += fi
+        line["cpu_baseline"] = {"value": round(f / t, 1), "unit": "frames/s", "cores": threads,
+                                "kind": "port", "sample": f"every connection x {reps}, the receive "
+                                f"loop's walk (orc_index_stream) over host memory, {threads} threads",
+                                "seconds": round(t, 2)}
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    return 0 if ok else 1
+
+
 def per_gpu_rows(rows, steps: int):
     """Per-rank rates from shard.gather_floats rows [elapsed_s, payload bytes,
     serialize execute ms, deserialize execute ms, algorithmic bytes per
@@ -270,8 +479,10 @@ def main():
     cfws.init()
 
     F, fs = args.frames, args.frame_size
-    if args.workload in ("config5", "split"):
-        rc = (bench_h2 if args.workload == "config5" else bench_split)(args, rank, world, dev)
+    if args.workload in ("config5", "split", "accept", "index"):
+        fn = {"config5": bench_h2, "split": bench_split, "accept": bench_accept,
+              "index": bench_index}[args.workload]
+        rc = fn(args, rank, world, dev)
         if world > 1:
             dist.destroy_process_group()
         sys.exit(rc)

@@ -412,22 +412,6 @@ h2_starts_kernel(const uint64_t* __restrict__ ends, const uint64_t* __restrict__
 // unmasks each DATA frame's slice of its message's WS payload directly from
 // the HTTP/2 arena (one streaming pass instead of pool + deserialize).
 
-// Bytes [b, b + k) of global memory, k <= 16, into w (little-endian; bytes
-// past k are unspecified): the up to five aligned dwords that hold them,
-// issued as independent loads, funnel-shifted by b's alignment. Only dwords
-// holding at least one of the k bytes are read (no access past the span's
-// last mapped dword).
-__device__ __forceinline__ void load_span16(const uint8_t* b, uint32_t k, uint32_t (&w)[4])
-{
-    const uint32_t o = (uint32_t)(reinterpret_cast<uintptr_t>(b) & 3u);
-    const uint32_t* p = reinterpret_cast<const uint32_t*>(b - o);
-    const uint32_t nd = k ? (o + k + 3u) >> 2 : 0u;
-    uint32_t x[5];
-#pragma unroll
-    for (uint32_t j = 0; j < 5; ++j) x[j] = j < nd ? p[j] : 0u;
-#pragma unroll
-    for (uint32_t t = 0; t < 4; ++t) w[t] = __builtin_amdgcn_alignbyte(x[t + 1], x[t], o);
-}
 
 // co_ws_frame_deserialize on each pooled message [starts[m], ends[m])
 // (co_ws_http2_extension.c:134-164), header bytes gathered from the DATA

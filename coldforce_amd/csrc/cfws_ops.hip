@@ -288,7 +288,8 @@ ws_accept_kernel(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ 
 // ---------------------------------------------------------------------------
 
 // One connection per thread: the receive loop's walk over buf[begin, end).
-// The walk is a chain of dependent header reads, so a connection is one
+// The walk is a chain of dependent header reads (one memory round trip per
+// frame), so a connection is one
 // thread and the parallelism is across connections (a server's event loop
 // tick holds the receive buffers of many). Pass 1 (kWrite = false) counts
 // and records consumed / stop; pass 2 walks again and writes the starts at
@@ -308,8 +309,13 @@ index_walk_kernel(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ 
     int32_t st = CFWS_PARSE_COMPLETE;
     while (e > p) {
         if (e - p < 2) { st = CFWS_PARSE_MORE_DATA; break; }
+        // the header's bytes (up to 14) in one round of independent loads,
+        // parsed from registers: one memory round trip per hop, where a
+        // byte-by-byte parse takes two (the length code, then the rest)
+        uint32_t w[4];
+        load_span16(buf + p, e - p < 14 ? (uint32_t)(e - p) : 14u, w);
         cfws_frame_desc_t d;
-        st = parse_ws_header(buf, e, p, max_payload, d);
+        st = parse_ws_header_regs(w, e - p, max_payload, d);
         if (st != CFWS_PARSE_COMPLETE) break;
         if (kWrite && k < cap) starts[k] = p;
         ++k;

@@ -275,6 +275,39 @@ def _bind_flat(L, prefix):
 _ref = {}
 
 
+def cpu_accept_bench(raw: np.ndarray, off: np.ndarray, threads: int, iters: int,
+                     kind: str = "port") -> float:
+    """Seconds for `iters` passes of co_ws_create_base64_accept_key over every
+    key raw[off[i]:off[i+1]] on `threads` host threads (kind "reference":
+    the reference's co_sha1.c + co_base64.c compiled in place)."""
+    L, fn = (lib(), "orc_accept_bench") if kind == "port" else (ref_lib("O2"), "ref_accept_bench")
+    if L is None:
+        raise FileNotFoundError("oracle/_ref not built")
+    f = getattr(L, fn)
+    f.argtypes = [_vp, _vp, _u64, C.c_int, C.c_int, C.POINTER(C.c_double)]
+    f.restype = C.c_int
+    o = np.ascontiguousarray(off, dtype=np.uint64)
+    sec = C.c_double(0)
+    if f(_ptr(raw), _ptr(o), len(o) - 1, threads, iters, C.byref(sec)) != 0:
+        raise RuntimeError("accept bench failed")
+    return sec.value
+
+
+def cpu_index_bench(buf: np.ndarray, begin: np.ndarray, end: np.ndarray, max_per_conn: int,
+                    threads: int) -> tuple[float, int]:
+    """The receive-loop walk (orc_index_stream) over every connection
+    buf[begin[c], end[c]) on `threads` host threads: (seconds, frames)."""
+    f = lib().orc_index_bench
+    f.argtypes = [_vp, _vp, _vp, _u64, _u64, C.c_int, C.POINTER(C.c_double), C.POINTER(_u64)]
+    f.restype = C.c_int
+    b = np.ascontiguousarray(begin, dtype=np.uint64)
+    e = np.ascontiguousarray(end, dtype=np.uint64)
+    sec, frames = C.c_double(0), _u64(0)
+    if f(_ptr(buf), _ptr(b), _ptr(e), len(b), max_per_conn, threads, C.byref(sec), C.byref(frames)) != 0:
+        raise RuntimeError("index bench failed")
+    return sec.value, frames.value
+
+
 def ref_lib(opt: str = "O2"):
     if opt not in _ref:
         path = REF_SO[opt]

@@ -21,6 +21,9 @@
 #include <time.h>
 
 #ifdef CFWS_BENCH_REF
+int ref_ws_accept_key(const char* key, unsigned long long key_len, char* out, unsigned long long cap);
+#define ACCEPT_BENCH_FN ref_accept_bench
+#define ACCEPT(k, n, out) ref_ws_accept_key((k), (n), (out), 29)
 #include <coldforce/core/co_byte_array.h>
 #include <coldforce/ws/co_ws_config.h>
 #include <coldforce/ws/co_ws_frame.h>
@@ -37,6 +40,8 @@ typedef co_ws_frame_t bench_frame_t;
 #define DESERIALIZE(f, p, n, idx) co_ws_frame_deserialize((f), (p), (n), (idx))
 #else
 #include "cfws_oracle.h"
+#define ACCEPT_BENCH_FN orc_accept_bench
+#define ACCEPT(k, n, out) orc_ws_accept_key((k), (n), (out))
 typedef orc_bytes_t bench_buf_t;
 typedef orc_frame_t bench_frame_t;
 #define BENCH_FN orc_cpu_bench
@@ -147,3 +152,120 @@ int BENCH_FN(uint64_t n_frames, uint64_t frame_size, int threads, int iters,
     *unmask_seconds = us;
     return fail ? -2 : 0;
 }
+
+/* ---- handshake accept keys ---------------------------
+ * co_ws_create_base64_accept_key (co_ws_http_extension.c:26-57) once per
+ * key, keys[off[i], off[i+1]), split into contiguous ranges over `threads`
+ * pthreads, `iters` times: the connection storm a server's threads meet one
+ * upgrade request at a time. */
+typedef struct {
+    const char* keys;
+    const uint64_t* off;
+    uint64_t first, count;
+    int iters;
+    volatile uint64_t sink;
+} accept_job_t;
+
+static void* accept_run(void* arg)
+{
+    accept_job_t* j = (accept_job_t*)arg;
+    char out[32];
+    uint64_t s = 0;
+    for (int it = 0; it < j->iters; ++it)
+        for (uint64_t i = j->first; i < j->first + j->count; ++i) {
+            ACCEPT(j->keys + j->off[i], j->off[i + 1] - j->off[i], out);
+            s += (uint8_t)out[0];
+        }
+    j->sink = s;
+    return NULL;
+}
+
+int ACCEPT_BENCH_FN(const char* keys, const uint64_t* off, uint64_t n, int threads, int iters,
+                    double* seconds)
+{
+    if (threads < 1) threads = 1;
+    if (threads > 256) threads = 256;
+    accept_job_t* jobs = (accept_job_t*)calloc((size_t)threads, sizeof(*jobs));
+    if (!jobs) return -1;
+    uint64_t per = n / (uint64_t)threads, rem = n % (uint64_t)threads, at = 0;
+    for (int t = 0; t < threads; ++t) {
+        uint64_t c = per + ((uint64_t)t < rem ? 1 : 0);
+        jobs[t].keys = keys;
+        jobs[t].off = off;
+        jobs[t].first = at;
+        jobs[t].count = c;
+        jobs[t].iters = iters;
+        at += c;
+    }
+    pthread_t tid[256];
+    double t0 = bench_now();
+    for (int t = 0; t < threads; ++t) pthread_create(&tid[t], NULL, accept_run, &jobs[t]);
+    for (int t = 0; t < threads; ++t) pthread_join(tid[t], NULL);
+    *seconds = bench_now() - t0;
+    free(jobs);
+    return 0;
+}
+
+#ifndef CFWS_BENCH_REF
+/* ---- receive-buffer indexing, port only --------------
+ * The receive loop's walk over each connection's bytes [begin[c], end[c])
+ * (orc_index_stream: co_ws_server.c:107-169's header decisions), connections
+ * split over `threads` pthreads. Returns the frames found. */
+typedef struct {
+    const uint8_t* buf;
+    const uint64_t* begin;
+    const uint64_t* end;
+    uint64_t first, count;
+    uint64_t* scratch;
+    uint64_t scratch_n;
+    uint64_t frames;
+} index_job_t;
+
+static void* index_run(void* arg)
+{
+    index_job_t* j = (index_job_t*)arg;
+    uint64_t f = 0;
+    for (uint64_t c = j->first; c < j->first + j->count; ++c) {
+        uint64_t consumed = 0;
+        int32_t stop = 0;
+        f += orc_index_stream(j->buf, j->begin[c], j->end[c], (uint64_t)32 << 20, j->scratch,
+                              j->scratch_n, &consumed, &stop);
+    }
+    j->frames = f;
+    return NULL;
+}
+
+int orc_index_bench(const uint8_t* buf, const uint64_t* begin, const uint64_t* end, uint64_t n_conn,
+                    uint64_t max_frames_per_conn, int threads, double* seconds, uint64_t* frames)
+{
+    if (threads < 1) threads = 1;
+    if (threads > 256) threads = 256;
+    index_job_t* jobs = (index_job_t*)calloc((size_t)threads, sizeof(*jobs));
+    if (!jobs) return -1;
+    uint64_t per = n_conn / (uint64_t)threads, rem = n_conn % (uint64_t)threads, at = 0;
+    for (int t = 0; t < threads; ++t) {
+        uint64_t c = per + ((uint64_t)t < rem ? 1 : 0);
+        jobs[t].buf = buf;
+        jobs[t].begin = begin;
+        jobs[t].end = end;
+        jobs[t].first = at;
+        jobs[t].count = c;
+        jobs[t].scratch_n = max_frames_per_conn;
+        jobs[t].scratch = (uint64_t*)malloc(sizeof(uint64_t) * (max_frames_per_conn ? max_frames_per_conn : 1));
+        at += c;
+    }
+    pthread_t tid[256];
+    double t0 = bench_now();
+    for (int t = 0; t < threads; ++t) pthread_create(&tid[t], NULL, index_run, &jobs[t]);
+    for (int t = 0; t < threads; ++t) pthread_join(tid[t], NULL);
+    *seconds = bench_now() - t0;
+    uint64_t f = 0;
+    for (int t = 0; t < threads; ++t) {
+        f += jobs[t].frames;
+        free(jobs[t].scratch);
+    }
+    *frames = f;
+    free(jobs);
+    return 0;
+}
+#endif
