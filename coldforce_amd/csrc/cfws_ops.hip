@@ -231,8 +231,43 @@ __device__ __forceinline__ uint32_t accept_msg_byte(const uint8_t* __restrict__ 
 
 __device__ __forceinline__ uint32_t rol32(uint32_t v, int b) { return (v << b) | (v >> (32 - b)); }
 
+// One SHA-1 block (80 rounds over a 16-word schedule kept in registers).
+// When w is a compile-time constant (the second block of a 24-byte key's
+// message), the whole schedule folds into constants.
+__device__ __forceinline__ void sha1_block(uint32_t (&st)[5], uint32_t (&w)[16])
+{
+    uint32_t a = st[0], bb = st[1], cc = st[2], d = st[3], e = st[4];
+#pragma unroll
+    for (int r = 0; r < 80; ++r) {
+        if (r >= 16)
+            w[r & 15] = rol32(w[(r + 13) & 15] ^ w[(r + 8) & 15] ^ w[(r + 2) & 15] ^ w[r & 15], 1);
+        const uint32_t f = r < 20 ? ((bb & cc) | (~bb & d))
+                         : r < 40 ? (bb ^ cc ^ d)
+                         : r < 60 ? ((bb & cc) | (bb & d) | (cc & d)) : (bb ^ cc ^ d);
+        const uint32_t k = r < 20 ? 0x5a827999u : r < 40 ? 0x6ed9eba1u : r < 60 ? 0x8f1bbcdcu : 0xca62c1d6u;
+        const uint32_t t = rol32(a, 5) + f + e + k + w[r & 15];
+        e = d; d = cc; cc = rol32(bb, 30); bb = a; a = t;
+    }
+    st[0] += a; st[1] += bb; st[2] += cc; st[3] += d; st[4] += e;
+}
+
+// The GUID's bytes as big-endian words (it follows a 24-byte key at word 6).
+__device__ __forceinline__ uint32_t guid_word(int j)
+{
+    constexpr char g[] = "258EAFA5-E914-47DA-95CA-C5AB0DC85B11";
+    return (uint32_t)(uint8_t)g[4 * j] << 24 | (uint32_t)(uint8_t)g[4 * j + 1] << 16 |
+           (uint32_t)(uint8_t)g[4 * j + 2] << 8 | (uint32_t)(uint8_t)g[4 * j + 3];
+}
+
 // One thread per connection: a connection storm's accept keys at once.
-__global__ void __launch_bounds__(kThreads)
+// A key of 24 bytes (every RFC 6455 client key: base64 of 16 bytes) takes
+// the fast form: its SHA-1 input is 6 key words + 9 GUID words + the 0x80
+// pad in block 0, and a constant block 1 (zeros and the 480-bit length).
+// Any other length builds the message byte by byte.
+#ifndef CFWS_ACCEPT_MIN_BLOCKS
+#define CFWS_ACCEPT_MIN_BLOCKS 1
+#endif
+__global__ void __launch_bounds__(kThreads, CFWS_ACCEPT_MIN_BLOCKS)
 ws_accept_kernel(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ key_off, uint64_t n,
                  char* __restrict__ out)
 {
@@ -240,29 +275,34 @@ ws_accept_kernel(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ 
     if (c >= n) return;
     const uint8_t* key = keys + key_off[c];
     const uint64_t L = key_off[c + 1] - key_off[c];
-    const uint64_t blocks = (L + 36 + 9 + 63) / 64;
     uint32_t st[5] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u, 0xc3d2e1f0u};
-    for (uint64_t b = 0; b < blocks; ++b) {
+    if (L == 24) {
         uint32_t w[16];
 #pragma unroll
-        for (int t = 0; t < 16; ++t) {
-            const uint64_t i = b * 64 + 4 * t;
-            w[t] = accept_msg_byte(key, L, blocks, i) << 24 | accept_msg_byte(key, L, blocks, i + 1) << 16 |
-                   accept_msg_byte(key, L, blocks, i + 2) << 8 | accept_msg_byte(key, L, blocks, i + 3);
-        }
-        uint32_t a = st[0], bb = st[1], cc = st[2], d = st[3], e = st[4];
+        for (int t = 0; t < 6; ++t)
+            w[t] = (uint32_t)key[4 * t] << 24 | (uint32_t)key[4 * t + 1] << 16 |
+                   (uint32_t)key[4 * t + 2] << 8 | (uint32_t)key[4 * t + 3];
 #pragma unroll
-        for (int r = 0; r < 80; ++r) {
-            if (r >= 16)
-                w[r & 15] = rol32(w[(r + 13) & 15] ^ w[(r + 8) & 15] ^ w[(r + 2) & 15] ^ w[r & 15], 1);
-            const uint32_t f = r < 20 ? ((bb & cc) | (~bb & d))
-                             : r < 40 ? (bb ^ cc ^ d)
-                             : r < 60 ? ((bb & cc) | (bb & d) | (cc & d)) : (bb ^ cc ^ d);
-            const uint32_t k = r < 20 ? 0x5a827999u : r < 40 ? 0x6ed9eba1u : r < 60 ? 0x8f1bbcdcu : 0xca62c1d6u;
-            const uint32_t t = rol32(a, 5) + f + e + k + w[r & 15];
-            e = d; d = cc; cc = rol32(bb, 30); bb = a; a = t;
+        for (int t = 6; t < 15; ++t) w[t] = guid_word(t - 6);
+        w[15] = 0x80000000u;
+        sha1_block(st, w);
+        uint32_t w2[16];
+#pragma unroll
+        for (int t = 0; t < 15; ++t) w2[t] = 0;
+        w2[15] = 60u * 8u;
+        sha1_block(st, w2);
+    } else {
+        const uint64_t blocks = (L + 36 + 9 + 63) / 64;
+        for (uint64_t b = 0; b < blocks; ++b) {
+            uint32_t w[16];
+#pragma unroll
+            for (int t = 0; t < 16; ++t) {
+                const uint64_t i = b * 64 + 4 * t;
+                w[t] = accept_msg_byte(key, L, blocks, i) << 24 | accept_msg_byte(key, L, blocks, i + 1) << 16 |
+                       accept_msg_byte(key, L, blocks, i + 2) << 8 | accept_msg_byte(key, L, blocks, i + 3);
+            }
+            sha1_block(st, w);
         }
-        st[0] += a; st[1] += bb; st[2] += cc; st[3] += d; st[4] += e;
     }
     // base64 of the 20 hash bytes: 6 full groups + 2 bytes -> 3 chars + '='
     char* o = out + CFWS_WS_ACCEPT_SLOT * c;
