@@ -329,23 +329,28 @@ ws_accept_kernel(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ 
 
 // One connection per thread: the receive loop's walk over buf[begin, end).
 // The walk is a chain of dependent header reads (one memory round trip per
-// frame), so a connection is one
-// thread and the parallelism is across connections (a server's event loop
-// tick holds the receive buffers of many). Pass 1 (kWrite = false) counts
-// and records consumed / stop; pass 2 walks again and writes the starts at
-// the scanned offsets.
-template <bool kWrite>
+// frame), so a connection is one thread and the parallelism is across
+// connections (a server's event loop tick holds the receive buffers of
+// many). The walk runs once: it counts, records consumed / stop, and keeps
+// the first kIndexSlots starts in the connection's workspace slots (where
+// they wait for the scan that places them) and where frame kIndexSlots
+// starts. After the scan, index_place_kernel copies the kept starts to
+// their places, and only connections with more frames than slots walk on
+// from there (index_rest_kernel).
+constexpr uint32_t kIndexSlots = 64;
+
 __global__ void __launch_bounds__(kThreads)
 index_walk_kernel(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ begin,
                   const uint64_t* __restrict__ end, uint64_t n, uint64_t max_payload,
                   uint64_t* __restrict__ first, uint64_t* __restrict__ consumed,
-                  int32_t* __restrict__ stop, uint64_t* __restrict__ starts, uint64_t cap)
+                  int32_t* __restrict__ stop, uint64_t* __restrict__ slots, uint64_t* __restrict__ resume)
 {
     const uint64_t c = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
     if (c >= n) return;
     const uint64_t e = end[c];
     uint64_t p = begin[c];
-    uint64_t k = kWrite ? first[c] : 0;
+    uint64_t k = 0, r = e;
+    uint64_t* my = slots + c * kIndexSlots;
     int32_t st = CFWS_PARSE_COMPLETE;
     while (e > p) {
         if (e - p < 2) { st = CFWS_PARSE_MORE_DATA; break; }
@@ -357,14 +362,53 @@ index_walk_kernel(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ 
         cfws_frame_desc_t d;
         st = parse_ws_header_regs(w, e - p, max_payload, d);
         if (st != CFWS_PARSE_COMPLETE) break;
-        if (kWrite && k < cap) starts[k] = p;
+        if (k < kIndexSlots) my[k] = p;
+        else if (k == kIndexSlots) r = p;
         ++k;
         p += d.header_size + d.payload_size;
     }
-    if (!kWrite) {
-        first[c] = k;
-        consumed[c] = p;
-        stop[c] = st;
+    first[c] = k;
+    consumed[c] = p;
+    stop[c] = st;
+    resume[c] = r;
+}
+
+// The kept starts to their places: thread (c, j) copies connection c's j-th
+// start (j < kIndexSlots), after the scan turned the counts into firsts.
+__global__ void __launch_bounds__(kThreads)
+index_place_kernel(const uint64_t* __restrict__ first, const uint64_t* __restrict__ slots,
+                   const uint64_t* __restrict__ total, uint64_t n, uint64_t* __restrict__ starts,
+                   uint64_t cap)
+{
+    const uint64_t t = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
+    const uint64_t c = t / kIndexSlots, j = t % kIndexSlots;
+    if (c >= n) return;
+    const uint64_t next = c + 1 < n ? first[c + 1] : *total;
+    const uint64_t k = next - first[c];
+    if (j < k && first[c] + j < cap) starts[first[c] + j] = slots[t];
+}
+
+// Connections with more than kIndexSlots frames: the walk on from frame
+// kIndexSlots, writing the rest of their starts in place.
+__global__ void __launch_bounds__(kThreads)
+index_rest_kernel(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ end, uint64_t n,
+                  uint64_t max_payload, const uint64_t* __restrict__ first,
+                  const uint64_t* __restrict__ total, const uint64_t* __restrict__ resume,
+                  uint64_t* __restrict__ starts, uint64_t cap)
+{
+    const uint64_t c = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
+    if (c >= n) return;
+    const uint64_t next = c + 1 < n ? first[c + 1] : *total;
+    if (next - first[c] <= kIndexSlots) return;
+    const uint64_t e = end[c];
+    uint64_t p = resume[c];
+    for (uint64_t k = first[c] + kIndexSlots; k < next; ++k) {
+        uint32_t w[4];
+        load_span16(buf + p, e - p < 14 ? (uint32_t)(e - p) : 14u, w);
+        cfws_frame_desc_t d;
+        (void)parse_ws_header_regs(w, e - p, max_payload, d);   // COMPLETE: the first walk's frames
+        if (k < cap) starts[k] = p;
+        p += d.header_size + d.payload_size;
     }
 }
 
@@ -383,9 +427,26 @@ int cfws_internal_copy_out(const void* d_src, void* dev_dst, uint64_t n, void* s
 
 extern "C" {
 
+// [0, 64): header; then the scan partials, each connection's kIndexSlots
+// kept starts and its resume position.
+struct IndexLayout {
+    uint64_t partials, slots, resume, bytes;
+};
+
+IndexLayout index_layout(uint64_t n)
+{
+    IndexLayout L;
+    uint64_t at = 64;
+    L.partials = at; at = align_up(at + sizeof(uint64_t) * grid_for(n, kScanBlock), 256);
+    L.slots = at; at = align_up(at + sizeof(uint64_t) * kIndexSlots * n, 256);
+    L.resume = at; at = align_up(at + sizeof(uint64_t) * n, 256);
+    L.bytes = at;
+    return L;
+}
+
 size_t cfws_index_workspace_size(size_t n_conns)
 {
-    return 64 + sizeof(uint64_t) * (size_t)grid_for(n_conns, kScanBlock);
+    return (size_t)index_layout(n_conns).bytes;
 }
 
 int cfws_index_frames_batch(const void* d_buf, const uint64_t* d_begin, const uint64_t* d_end,
@@ -405,13 +466,19 @@ int cfws_index_frames_batch(const void* d_buf, const uint64_t* d_begin, const ui
         return launch_check("index");
     }
     const uint8_t* buf = static_cast<const uint8_t*>(d_buf);
-    uint64_t* partials = ws_ptr<uint64_t>(ws, 64);
+    const IndexLayout L = index_layout(n);
+    uint64_t* slots = ws_ptr<uint64_t>(ws, L.slots);
+    uint64_t* resume = ws_ptr<uint64_t>(ws, L.resume);
     const uint32_t g = grid_for(n, kThreads);
-    index_walk_kernel<false><<<g, kThreads, 0, st>>>(buf, d_begin, d_end, n, max_payload, d_first,
-                                                     d_consumed, d_stop, nullptr, 0);
-    if (int rc = run_scan(d_first, n, partials, d_total, st)) return rc;
-    index_walk_kernel<true><<<g, kThreads, 0, st>>>(buf, d_begin, d_end, n, max_payload, d_first,
-                                                    nullptr, nullptr, d_starts, cap);
+    index_walk_kernel<<<g, kThreads, 0, st>>>(buf, d_begin, d_end, n, max_payload, d_first, d_consumed,
+                                              d_stop, slots, resume);
+    if (int rc = run_scan(d_first, n, ws_ptr<uint64_t>(ws, L.partials), d_total, st)) return rc;
+    if (cap) {
+        index_place_kernel<<<grid_for(n * kIndexSlots, kThreads), kThreads, 0, st>>>(
+            d_first, slots, d_total, n, d_starts, cap);
+        index_rest_kernel<<<g, kThreads, 0, st>>>(buf, d_end, n, max_payload, d_first, d_total, resume,
+                                                  d_starts, cap);
+    }
     return launch_check("index");
 }
 

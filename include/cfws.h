@@ -204,7 +204,9 @@ size_t cfws_index_frames(const void* h_buf, uint64_t begin, uint64_t end, uint64
  * c = d_buf[d_begin[c], d_end[c]). d_first[c] = index of c's first start in
  * d_starts (exclusive prefix sum of the per-connection counts), *d_total =
  * all starts (unclamped); starts at positions >= starts_capacity are not
- * written. d_consumed / d_stop per connection as above. */
+ * written. d_consumed / d_stop per connection as above. The workspace
+ * (cfws_index_workspace_size) holds 64 starts per connection between the
+ * walk and the scan that places them: 520 bytes per connection. */
 size_t cfws_index_workspace_size(size_t n_conns);
 int cfws_index_frames_batch(const void* d_buf, const uint64_t* d_begin, const uint64_t* d_end,
                             size_t n_conns, uint64_t max_payload, uint64_t* d_starts,

@@ -149,3 +149,38 @@ def test_device_index_zipf_connections_then_deserialize(device):
     assert int(tot_t.item()) == exp_tot and (exp_st == 0).all()
     assert np.array_equal(st_t.cpu().numpy(), exp_st)
     assert np.array_equal(out[:exp_tot].cpu().numpy(), exp_out[:exp_tot])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cap_cut", [False, True])
+def test_device_index_long_connections(device, cap_cut):
+    """Connections of 1, 63, 64, 65, 130 and 700 small frames (the device walk
+    keeps 64 starts per connection and walks on past them only where there
+    are more), some ending inside a frame or on an invalid one; with
+    cap_cut the starts capacity ends inside a long connection's starts."""
+    import random
+    rng = random.Random(65)
+    streams, expect = [], []
+    for n in (1, 63, 64, 65, 130, 700, 64, 200):
+        frames = [O.serialize_keyed(True, rng.choice([1, 2, 9]), rng.random() < .7, rng.getrandbits(32),
+                                    rng.randbytes(rng.randrange(0, 40))) for _ in range(n)]
+        s = b"".join(frames)
+        tail = rng.choice([b"", b"\x82", b"\x82\xfe\x01", b"\xf2\x00"])   # cut frame / RSV junk
+        streams.append(s + tail)
+    buf, offs = _arena(streams, device)
+    host = np.frombuffer(b"".join(streams), np.uint8)
+    begin = torch.tensor(offs[:-1], dtype=torch.int64, device=device)
+    end = torch.tensor(offs[1:], dtype=torch.int64, device=device)
+    exp = [O.index_stream(host, int(offs[i]), int(offs[i + 1])) for i in range(len(streams))]
+    n_all = sum(len(e[0]) for e in exp)
+    cap = n_all - 100 if cap_cut else n_all + 8
+    starts_t = torch.full((max(cap, 1),), -1, dtype=torch.int64, device=device)
+    starts, first, consumed, stop, total = cfws.index_frames_batch(buf, begin, end, starts_t=starts_t)
+    starts, first = starts.cpu().numpy(), first.cpu().numpy()
+    consumed, stop = consumed.cpu().numpy(), stop.cpu().numpy()
+    assert total == n_all
+    allexp = np.concatenate([e[0] for e in exp]).astype(np.int64)
+    assert np.array_equal(starts[:min(cap, n_all)], allexp[:min(cap, n_all)])
+    for i, (e_st, e_con, e_stop) in enumerate(exp):
+        assert consumed[i] == e_con and stop[i] == e_stop, i
+        assert first[i] == sum(len(x[0]) for x in exp[:i])
