@@ -278,6 +278,13 @@ ws_accept_kernel(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ 
     const uint64_t c = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
     if (c >= n) return;
     const uint8_t* key = keys + key_off[c];
+    char* o = out + CFWS_WS_ACCEPT_SLOT * c;
+    if (key_off[c + 1] < key_off[c]) {
+        // offsets out of order: no key, an empty slot (a wrapped length would
+        // walk ~2^58 SHA-1 blocks)
+        for (int b = 0; b < CFWS_WS_ACCEPT_SLOT; ++b) o[b] = 0;
+        return;
+    }
     const uint64_t L = key_off[c + 1] - key_off[c];
     uint32_t st[5] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u, 0xc3d2e1f0u};
     if (L == 24) {
@@ -335,7 +342,6 @@ ws_accept_kernel(const uint8_t* __restrict__ keys, const uint64_t* __restrict__ 
         ow[g] = b64_char((v >> 18) & 63) | b64_char((v >> 12) & 63) << 8 | b64_char((v >> 6) & 63) << 16 |
                 c3 << 24;
     }
-    char* o = out + CFWS_WS_ACCEPT_SLOT * c;
     if ((reinterpret_cast<uintptr_t>(o) & 15u) == 0) {
         uint4* o16 = reinterpret_cast<uint4*>(o);
         o16[0] = make_uint4(ow[0], ow[1], ow[2], ow[3]);

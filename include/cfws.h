@@ -223,7 +223,8 @@ int cfws_index_frames_batch(const void* d_buf, const uint64_t* d_begin, const ui
  * d_keys[d_key_off[c], d_key_off[c + 1]) (n + 1 offsets, any length); its
  * 28-character accept value + NUL goes to d_accept + CFWS_WS_ACCEPT_SLOT * c
  * (the slot's last 3 bytes are written as zeros when d_accept is 16-byte
- * aligned, and left alone otherwise). */
+ * aligned, and left alone otherwise). Offsets must not decrease: a key with
+ * d_key_off[c + 1] < d_key_off[c] gets an all-zero slot (an empty string). */
 #define CFWS_WS_ACCEPT_SLOT 32
 int cfws_ws_accept_keys_batch(const void* d_keys, const uint64_t* d_key_off, size_t n,
                               char* d_accept, void* stream);
