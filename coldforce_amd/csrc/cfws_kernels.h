@@ -984,11 +984,21 @@ xform_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
              const uint64_t* __restrict__ total_p, const uint64_t* __restrict__ base_p,
              uint64_t capacity, uint32_t n_frames, uint32_t klass, uint32_t sid,
              const cfws_frame_desc_t* __restrict__ parent, uint32_t edge_blocks,
-             const uint64_t* __restrict__ reasm_offs1)
+             const uint64_t* __restrict__ reasm_offs1, uint32_t edge_stride)
 {
-    if (kMode == kModeDeser && reasm_offs1 && blockIdx.x < edge_blocks) {
+    // Which workgroups are edge workgroups: the first edge_blocks, or (edge
+    // stride s > 0) every s-th one, spread through the grid
+    uint32_t eidx = blockIdx.x, sidx = blockIdx.x - edge_blocks;
+    bool is_edge = blockIdx.x < edge_blocks;
+    if (edge_stride) {
+        const uint32_t k = blockIdx.x / edge_stride;
+        is_edge = blockIdx.x == k * edge_stride && k < edge_blocks;
+        eidx = k;
+        sidx = blockIdx.x - (k + 1 < edge_blocks ? k + 1 : edge_blocks);
+    }
+    if (kMode == kModeDeser && reasm_offs1 && is_edge) {
         // reassembly pass 0: the edge chunks of both passes (total_p = hdr)
-        const uint64_t t = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
+        const uint64_t t = uint64_t(eidx) * kThreads + threadIdx.x;
         if ((t >> 1) < n_frames)
             reasm_edge_frame(src, dst, desc, status, offs, reasm_offs1, total_p, capacity, n_frames,
                              t >> 1, (uint32_t)(t & 1u));
@@ -1007,8 +1017,8 @@ xform_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
     P.klass = klass;
     P.sid = sid;
     P.parent = parent;
-    if (has_edge_blocks(kMode) && blockIdx.x < edge_blocks) {
-        const uint64_t t = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
+    if (has_edge_blocks(kMode) && is_edge) {
+        const uint64_t t = uint64_t(eidx) * kThreads + threadIdx.x;
         if ((t >> 1) < n_frames) edge_frame<kMode>(P, t >> 1, (uint32_t)(t & 1u));
         return;
     }
@@ -1017,7 +1027,7 @@ xform_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t stride = uint64_t(gridDim.x - edge_blocks) * kWaves;
 
-    for (uint64_t r = uint64_t(blockIdx.x - edge_blocks) * kWaves + wave; r < n_regions;
+    for (uint64_t r = uint64_t(sidx) * kWaves + wave; r < n_regions;
          r += stride) {
         const uint64_t base = r * kRegion;
         const uint64_t end = base + kRegion;
@@ -1474,6 +1484,28 @@ inline bool edge_split()
     return v == 1;
 }
 
+// Where the edge workgroups go: first (their chains run beside the first
+// streaming waves), or spread through the grid, one every `stride`
+// workgroups, so that they never hold every slot at once. Spread pays when
+// frames are small -- one edge workgroup (128 frames) per <= 128 streaming
+// workgroups (2 MiB), i.e. frames averaging <= 16 KiB of output: config 3
+// +1.1 %, 4 KiB frames +2.3 % -- and costs 64 KiB frames 3 % of serialize
+// (configs 2 and 4), where it lands each edge workgroup beside the regions of
+// its own frames (profiles/r02_ab_edge_order.txt). CFWS_EDGE_ORDER=0 / 1
+// forces first / spread.
+#ifndef CFWS_EDGE_SPREAD_MAX_STRIDE
+#define CFWS_EDGE_SPREAD_MAX_STRIDE 128
+#endif
+inline bool edge_interleave(uint32_t stride)
+{
+    static int v = -2;
+    if (v == -2) {
+        const char* s = getenv("CFWS_EDGE_ORDER");
+        v = (s && *s == '1') ? 1 : ((s && *s == '0') ? 0 : -1);
+    }
+    return v < 0 ? stride <= CFWS_EDGE_SPREAD_MAX_STRIDE : v == 1;
+}
+
 template <int kMode>
 void launch_streaming(const void* src, void* dst, const cfws_frame_desc_t* desc,
                       const int32_t* status, const uint64_t* offs, const uint32_t* map,
@@ -1484,9 +1516,14 @@ void launch_streaming(const void* src, void* dst, const cfws_frame_desc_t* desc,
 {
     const bool split = edges && (edge_split() || !has_edge_blocks(kMode));
     const uint32_t eb = (edges && !split) ? grid_for(2 * (uint64_t)n, kThreads) : 0;
-    xform_kernel<kMode><<<eb + stream_grid(regions), kThreads, xform_lds_bytes(kMode), st>>>(
+    const uint32_t sg = stream_grid(regions);
+    // edge workgroups first, or spread evenly through the grid (edge_interleave)
+    const uint32_t spread = eb ? (eb + sg) / eb : 0;
+    const uint32_t stride = (eb && edge_interleave(spread)) ? spread : 0;
+    xform_kernel<kMode><<<eb + sg, kThreads, xform_lds_bytes(kMode), st>>>(
         static_cast<const uint8_t*>(src), static_cast<uint8_t*>(dst), desc, status, offs, map,
-        total_p, base_p, cap, (uint32_t)n, klass, sid, parent, eb, eb ? reasm_offs1 : nullptr);
+        total_p, base_p, cap, (uint32_t)n, klass, sid, parent, eb, eb ? reasm_offs1 : nullptr,
+        stride);
     // (a separate edge launch on a second stream, overlapping the streaming
     // kernel, measured no faster on config 5: the stream slowed by what the
     // overlap saved)
