@@ -56,7 +56,10 @@ constexpr uint64_t kScanBlock = uint64_t(kThreads) * kScanItems;
 // Plan kernels: one frame per thread. Their per-frame work is a chain of
 // dependent loads (descriptor or header bytes), so parallelism beats items
 // per thread: 2,048-frame blocks left 224 of 256 CUs idle at 65,536 frames.
-constexpr int kPlanItems = 1;
+#ifndef CFWS_PLAN_ITEMS
+#define CFWS_PLAN_ITEMS 1
+#endif
+constexpr int kPlanItems = CFWS_PLAN_ITEMS;
 constexpr uint64_t kPlanBlock = uint64_t(kThreads) * kPlanItems;
 
 // Frame classes a pass copies (deserialize): all, data only, control only.
@@ -1113,14 +1116,6 @@ __device__ __forceinline__ int32_t parse_ws_header_by(At at, uint64_t size, uint
     return CFWS_PARSE_COMPLETE;
 }
 
-__device__ __forceinline__ int32_t parse_ws_header(const uint8_t* __restrict__ wire, uint64_t size,
-                                                   uint64_t s, uint64_t max_payload,
-                                                   cfws_frame_desc_t& d)
-{
-    return parse_ws_header_by([wire](uint64_t i) -> uint32_t { return wire[i]; }, size, s,
-                              max_payload, d);
-}
-
 // The same parse over header bytes gathered into registers: w holds bytes
 // 0-15 of the frame little-endian (a frame starts at 0, `size` bytes long).
 // Byte selection is by compare + select, so w stays in VGPRs (an indexed
@@ -1153,6 +1148,30 @@ __device__ __forceinline__ void load_span16(const uint8_t* b, uint32_t k, uint32
     for (uint32_t j = 0; j < 5; ++j) x[j] = j < nd ? p[j] : 0u;
 #pragma unroll
     for (uint32_t t = 0; t < 4; ++t) w[t] = __builtin_amdgcn_alignbyte(x[t + 1], x[t], o);
+}
+
+// The header at s of wire[0, size): its up to 14 bytes in one round of
+// independent dword loads (load_span16), parsed from registers. A byte-wise
+// parse from memory takes up to 14 single-byte requests in three dependent
+// rounds (first two bytes, the length, the key): with frames ~1 KiB apart
+// every request is a line of its own. On 4 M x 1 KiB frames the plan's
+// header pass went from 311 to 182-198 us (two aligned 16-byte loads instead
+// of the dwords: no faster).
+__device__ __forceinline__ int32_t parse_ws_header(const uint8_t* __restrict__ wire, uint64_t size,
+                                                   uint64_t s, uint64_t max_payload,
+                                                   cfws_frame_desc_t& d)
+{
+#ifdef CFWS_PARSE_BYTEWISE
+    return parse_ws_header_by([wire](uint64_t i) -> uint32_t { return wire[i]; }, size, s,
+                              max_payload, d);
+#else
+    const uint64_t avail = s <= size ? size - s : 0;
+    uint32_t w[4];
+    load_span16(wire + s, avail < 14 ? (uint32_t)avail : 14u, w);
+    const int32_t st = parse_ws_header_regs(w, avail, max_payload, d);
+    d.wire_off = s;
+    return st;
+#endif
 }
 
 // Exclusive block scan of one value per thread; *block_total gets the sum.
@@ -1195,20 +1214,45 @@ scan_reduce_kernel(const uint64_t* __restrict__ vals, uint64_t n, uint64_t* __re
     if (threadIdx.x == 0) partials[blockIdx.x] = total;
 }
 
+// One workgroup's exclusive scan of nb block sums, in place; *grand gets the
+// total. A step takes kThreads x kPartialItems sums, kPartialItems
+// consecutive ones per thread with all their loads in flight: the 16,384
+// sums of a 4 M-frame plan in one step, 19 us (one sum per thread per step:
+// 64 dependent steps, 46 us; 16 per thread through LDS with coalesced loads
+// and stores: 4 steps, 29-35 us -- each step's round trip costs more than
+// the strided access).
+constexpr int kPartialItems = 64;
+
+__device__ __forceinline__ void scan_partials_block(uint64_t* __restrict__ partials, uint64_t nb,
+                                                    uint64_t* __restrict__ grand, uint64_t* s_wave)
+{
+    uint64_t carry = 0;
+    for (uint64_t b = 0; b < nb; b += uint64_t(kThreads) * kPartialItems) {
+        const uint64_t i0 = b + uint64_t(threadIdx.x) * kPartialItems;
+        uint64_t v[kPartialItems];
+        uint64_t sum = 0;
+#pragma unroll
+        for (int k = 0; k < kPartialItems; ++k) {
+            v[k] = i0 + k < nb ? partials[i0 + k] : 0;
+            sum += v[k];
+        }
+        uint64_t tot;
+        uint64_t run = block_exclusive_scan(sum, s_wave, &tot) + carry;
+#pragma unroll
+        for (int k = 0; k < kPartialItems; ++k) {
+            if (i0 + k < nb) partials[i0 + k] = run;
+            run += v[k];
+        }
+        carry += tot;
+    }
+    if (threadIdx.x == 0) *grand = carry;
+}
+
 __global__ void __launch_bounds__(kThreads)
 scan_partials_kernel(uint64_t* __restrict__ partials, uint64_t nb, uint64_t* __restrict__ grand)
 {
     __shared__ uint64_t s_wave[kWaves];
-    uint64_t carry = 0;
-    for (uint64_t b = 0; b < nb; b += kThreads) {
-        const uint64_t i = b + threadIdx.x;
-        const uint64_t x = i < nb ? partials[i] : 0;
-        uint64_t tot;
-        const uint64_t ex = block_exclusive_scan(x, s_wave, &tot);
-        if (i < nb) partials[i] = carry + ex;
-        carry += tot;
-    }
-    if (threadIdx.x == 0) *grand = carry;
+    scan_partials_block(partials, nb, grand, s_wave);
 }
 
 // scan_partials_kernel for up to two passes in one launch (block p: pass p).
@@ -1217,17 +1261,7 @@ scan_partials2_kernel(uint64_t* __restrict__ partials0, uint64_t* __restrict__ p
                       uint64_t* __restrict__ grand0, uint64_t* __restrict__ grand1)
 {
     __shared__ uint64_t s_wave[kWaves];
-    uint64_t* partials = blockIdx.x ? partials1 : partials0;
-    uint64_t carry = 0;
-    for (uint64_t b = 0; b < nb; b += kThreads) {
-        const uint64_t i = b + threadIdx.x;
-        const uint64_t x = i < nb ? partials[i] : 0;
-        uint64_t tot;
-        const uint64_t ex = block_exclusive_scan(x, s_wave, &tot);
-        if (i < nb) partials[i] = carry + ex;
-        carry += tot;
-    }
-    if (threadIdx.x == 0) *(blockIdx.x ? grand1 : grand0) = carry;
+    scan_partials_block(blockIdx.x ? partials1 : partials0, nb, blockIdx.x ? grand1 : grand0, s_wave);
 }
 
 __global__ void __launch_bounds__(kThreads)
@@ -1457,7 +1491,35 @@ constexpr uint32_t kXformLdsDefault = 32000;     // 5 x fits 160 KiB, 6 x does n
 #ifndef CFWS_H2SER_LDS
 #define CFWS_H2SER_LDS kXformLdsDefault
 #endif
-inline uint32_t xform_lds_bytes(int mode = -1)
+// Batches of small frames (on average at most the mode's threshold of output
+// bytes per frame: cap / n at launch) run at the residency the registers
+// allow: their regions are latency-bound (a frame view, then the source
+// blocks, per region; edge chunks every frame), and more resident waves hide
+// that. Serialize: 512 B frames 3.47 -> 3.90 TB/s, 1 KiB 4.25 -> 4.84,
+// 2 KiB 4.44 -> 5.01, 4 KiB unchanged, 8 KiB and up slower. Deserialize:
+// 512 B 4.88 -> 5.36, 1 KiB 5.35 -> 5.82, but 2 KiB 6.46 -> 5.96 and slower
+// from there (profiles/r02_ab_occupancy_by_frame.txt). CFWS_OCC_FRAME_MAX
+// overrides both thresholds (0: never).
+#ifndef CFWS_OCC_FRAME_MAX_SER
+#define CFWS_OCC_FRAME_MAX_SER 4096
+#endif
+#ifndef CFWS_OCC_FRAME_MAX_RECV
+#define CFWS_OCC_FRAME_MAX_RECV 1536
+#endif
+inline uint64_t occ_frame_max(int mode)
+{
+    static int64_t v = -2;
+    if (v == -2) {
+        const char* s = getenv("CFWS_OCC_FRAME_MAX");
+        v = s ? (int64_t)strtoull(s, nullptr, 10) : -1;
+    }
+    if (v >= 0) return (uint64_t)v;
+    if (mode == kModeSer) return CFWS_OCC_FRAME_MAX_SER;
+    if (mode == kModeDeser) return CFWS_OCC_FRAME_MAX_RECV;
+    return 0;
+}
+
+inline uint32_t xform_lds_bytes(int mode = -1, uint64_t frame_bytes = ~uint64_t(0))
 {
     static int64_t v = -2;                      // -1: no override
     if (v == -2) {
@@ -1466,6 +1528,7 @@ inline uint32_t xform_lds_bytes(int mode = -1)
         if (v > 65536) v = 65536;
     }
     if (v >= 0) return (uint32_t)v;
+    if (frame_bytes <= occ_frame_max(mode)) return 0;
     if (mode == kModeSer) return CFWS_SER_LDS;
     if (mode == kModeH2Ser) return CFWS_H2SER_LDS;
     return kXformLdsDefault;
@@ -1520,7 +1583,7 @@ void launch_streaming(const void* src, void* dst, const cfws_frame_desc_t* desc,
     // edge workgroups first, or spread evenly through the grid (edge_interleave)
     const uint32_t spread = eb ? (eb + sg) / eb : 0;
     const uint32_t stride = (eb && edge_interleave(spread)) ? spread : 0;
-    xform_kernel<kMode><<<eb + sg, kThreads, xform_lds_bytes(kMode), st>>>(
+    xform_kernel<kMode><<<eb + sg, kThreads, xform_lds_bytes(kMode, n ? cap / n : cap), st>>>(
         static_cast<const uint8_t*>(src), static_cast<uint8_t*>(dst), desc, status, offs, map,
         total_p, base_p, cap, (uint32_t)n, klass, sid, parent, eb, eb ? reasm_offs1 : nullptr,
         stride);
