@@ -339,3 +339,26 @@ def test_small_frame_regions_both_forms(seed):
     for align in (1, 16):
         check_deserialize(w, starts, align=align)
     check_deserialize(w, starts, flags=cfws.DESERIALIZE_REASSEMBLE)
+
+
+@pytest.mark.parametrize("fs", [1000, 1024, 2048])
+def test_many_small_frames_round_trip(fs):
+    """Config 1's frame size in a batch of 128 MiB: the paths small frames
+    take on a large grid (edge workgroups spread through the grid,
+    register-limited residency, plans over > 2,048 blocks with the block-sum
+    scan) against the oracle, then deserialize back at 16-byte slots."""
+    n = (128 << 20) // fs
+    payload = O.fill_splitmix(n * fs, 0x5EED0001 + fs, 0)
+    desc = W.uniform_batch(n, fs, 1, opcode=cfws.OPCODE_TEXT)
+    wire, total = check_serialize(payload, desc)
+    offs, _ = W.wire_layout(desc)
+    slot = W.round16(fs)
+    w_t = torch.from_numpy(wire[:W.round16(total)].copy()).cuda()
+    idx = torch.from_numpy(offs.astype(np.int64)).cuda()
+    back = torch.empty(n * slot, dtype=torch.uint8, device="cuda")
+    _, st, ptot = cfws.deserialize(w_t, total, idx, back, align=16)
+    torch.cuda.synchronize()
+    assert ptot.item() == n * slot and bool((st == 0).all())
+    got = back.cpu().numpy().reshape(n, slot)
+    assert np.array_equal(got[:, :fs], payload.reshape(n, fs))
+    assert not got[:, fs:].any()          # the alignment padding is written as zeros
