@@ -80,6 +80,18 @@ namespace {
 
 using cfws_rt::g_err;
 
+// A/B knob: dynamic LDS the WS plan kernels reserve (CFWS_PLAN_LDS; default 0)
+uint32_t plan_lds_bytes()
+{
+    static int64_t v = -1;
+    if (v < 0) {
+        const char* s = getenv("CFWS_PLAN_LDS");
+        v = s ? (int64_t)strtoull(s, nullptr, 10) : 0;
+        if (v > 65536) v = 65536;
+    }
+    return (uint32_t)v;
+}
+
 // Both reassembly passes' edge chunks in one launch of their own (the
 // CFWS_EDGE_SPLIT=1 form; by default pass 0's streaming launch carries them).
 __global__ void __launch_bounds__(kEdgeThreads)
@@ -537,13 +549,13 @@ int deserialize_plan_impl(const void* d_wire, uint64_t wire_size, const uint64_t
     uint64_t* part0 = ws_ptr<uint64_t>(ws, L.partials[0]);
     uint64_t* part1 = ws_ptr<uint64_t>(ws, L.partials[1]);
     const uint32_t nb = grid_for(n, kPlanBlock);
-    deserialize_plan_reduce_kernel<<<nb, kThreads, 0, st>>>(
+    deserialize_plan_reduce_kernel<<<nb, kThreads, plan_lds_bytes(), st>>>(
         static_cast<const uint8_t*>(d_wire), wire_size, d_index, d_ends, n, max_payload, align, reasm,
         d_desc, d_status, offs0, offs1, part0, part1);
     const uint32_t self_scan = nb <= kSelfScanBlocks ? 1u : 0u;
     if (!self_scan)
         scan_partials2_kernel<<<reasm ? 2 : 1, kThreads, 0, st>>>(part0, part1, nb, hdr + 3, hdr + 4);
-    deserialize_plan_apply_kernel<<<nb, kThreads, 0, st>>>(
+    deserialize_plan_apply_kernel<<<nb, kThreads, plan_lds_bytes(), st>>>(
         d_desc, d_status, offs0, offs1, n, part0, part1, nb, self_scan, hdr, cap, reasm,
         ws_ptr<uint32_t>(ws, L.map[0]), ws_ptr<uint32_t>(ws, L.map[1]), d_total);
     return launch_check("deserialize_plan");
@@ -582,9 +594,9 @@ int cfws_serialize_plan(cfws_frame_desc_t* d_desc, size_t n, uint64_t cap, uint6
     uint64_t* partials = ws_ptr<uint64_t>(ws, L.partials[0]);
     const uint32_t nb = grid_for(n, kPlanBlock);
     const uint32_t self_scan = nb <= kSelfScanBlocks ? 1u : 0u;
-    serialize_plan_reduce_kernel<<<nb, kThreads, 0, st>>>(d_desc, offs, n, partials);
+    serialize_plan_reduce_kernel<<<nb, kThreads, plan_lds_bytes(), st>>>(d_desc, offs, n, partials);
     if (!self_scan) scan_partials_kernel<<<1, kThreads, 0, st>>>(partials, nb, hdr + 3);
-    serialize_plan_apply_kernel<<<nb, kThreads, 0, st>>>(d_desc, offs, n, partials, nb, self_scan,
+    serialize_plan_apply_kernel<<<nb, kThreads, plan_lds_bytes(), st>>>(d_desc, offs, n, partials, nb, self_scan,
                                                         hdr, cap, ws_ptr<uint32_t>(ws, L.map[0]),
                                                         d_total);
     return launch_check("serialize_plan");
