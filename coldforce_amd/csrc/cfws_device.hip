@@ -101,9 +101,9 @@ edge_reasm_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
                   const uint64_t* __restrict__ hdr, uint64_t capacity, uint32_t n_frames)
 {
     const uint64_t t = uint64_t(blockIdx.x) * kEdgeThreads + threadIdx.x;
-    if ((t >> 1) >= n_frames) return;
-    reasm_edge_frame(src, dst, desc, status, offs0, offs1, hdr, capacity, n_frames, t >> 1,
-                     (uint32_t)(t & 1u));
+    if (edge_thread_frame(t) >= n_frames) return;
+    reasm_edge_frame(src, dst, desc, status, offs0, offs1, hdr, capacity, n_frames, edge_thread_frame(t),
+                     edge_thread_part(t));
 }
 
 // ---------------------------------------------------------------------------
@@ -664,7 +664,7 @@ int cfws_deserialize_execute(const void* d_wire, const cfws_frame_desc_t* d_desc
         launch_pass<kModeDeser>(L, 1, d_wire, d_payload, d_desc, d_status, ws, cap, n, kClassControl,
                                 st, 0, false);
         if (split)
-            edge_reasm_kernel<<<grid_for(2 * (uint64_t)n, kEdgeThreads), kEdgeThreads, 0, st>>>(
+            edge_reasm_kernel<<<grid_for(edge_threads(n), kEdgeThreads), kEdgeThreads, 0, st>>>(
                 static_cast<const uint8_t*>(d_wire), static_cast<uint8_t*>(d_payload), d_desc,
                 d_status, ws_ptr<const uint64_t>(ws, L.offs[0]), ws_ptr<const uint64_t>(ws, L.offs[1]),
                 ws_ptr<const uint64_t>(ws, L.hdr), cap, (uint32_t)n);

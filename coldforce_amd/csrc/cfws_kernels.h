@@ -855,6 +855,17 @@ __device__ __forceinline__ void tail_region(const Pass& P, uint32_t f0, uint32_t
 #endif
 constexpr uint32_t kEdgeThreads = CFWS_EDGE_THREADS;
 
+// Edge thread t -> (frame, part): each 128 threads take 64 consecutive
+// frames, lanes 0-63 part 0 and lanes 64-127 part 1, so a wave runs one part
+// only. (Parts alternating by lane ran both parts' code in every wave: on
+// 4 M x 1 KiB frames the serialize edge pass issued 892 VALU instructions
+// per wave.) edge_threads(n) threads cover every frame's two parts.
+__host__ __device__ constexpr uint64_t edge_threads(uint64_t n) { return (n + 63) / 64 * 128; }
+
+__device__ __forceinline__ uint64_t edge_thread_frame(uint64_t t) { return (t >> 7) * 64 + (t & 63); }
+
+__device__ __forceinline__ uint32_t edge_thread_part(uint64_t t) { return (uint32_t)(t >> 6) & 1u; }
+
 // The edge chunks of frame f in pass P (part 0: before the body; part 1:
 // reaching past the body end).
 template <int kMode>
@@ -903,7 +914,7 @@ edge_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
             uint32_t klass, uint32_t sid, const cfws_frame_desc_t* __restrict__ parent)
 {
     const uint64_t t = uint64_t(blockIdx.x) * kEdgeThreads + threadIdx.x;
-    const uint64_t f = t >> 1;
+    const uint64_t f = edge_thread_frame(t);
     if (f >= n_frames) return;
     const uint64_t out_base = base_p ? *base_p : 0;
     Pass P;
@@ -918,7 +929,7 @@ edge_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
     P.klass = klass;
     P.sid = sid;
     P.parent = parent;
-    edge_frame<kMode>(P, f, (uint32_t)(t & 1u));
+    edge_frame<kMode>(P, f, edge_thread_part(t));
 }
 
 // Deserialize with reassembly (CFWS_DESERIALIZE_REASSEMBLE): the edge chunks
@@ -1002,9 +1013,9 @@ xform_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
     if (kMode == kModeDeser && reasm_offs1 && is_edge) {
         // reassembly pass 0: the edge chunks of both passes (total_p = hdr)
         const uint64_t t = uint64_t(eidx) * kThreads + threadIdx.x;
-        if ((t >> 1) < n_frames)
+        if (edge_thread_frame(t) < n_frames)
             reasm_edge_frame(src, dst, desc, status, offs, reasm_offs1, total_p, capacity, n_frames,
-                             t >> 1, (uint32_t)(t & 1u));
+                             edge_thread_frame(t), edge_thread_part(t));
         return;
     }
     const uint64_t out_base = base_p ? *base_p : 0;
@@ -1022,7 +1033,7 @@ xform_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
     P.parent = parent;
     if (has_edge_blocks(kMode) && is_edge) {
         const uint64_t t = uint64_t(eidx) * kThreads + threadIdx.x;
-        if ((t >> 1) < n_frames) edge_frame<kMode>(P, t >> 1, (uint32_t)(t & 1u));
+        if (edge_thread_frame(t) < n_frames) edge_frame<kMode>(P, edge_thread_frame(t), edge_thread_part(t));
         return;
     }
     const uint64_t n_regions = (P.total + kRegion - 1) / kRegion;
@@ -1578,7 +1589,7 @@ void launch_streaming(const void* src, void* dst, const cfws_frame_desc_t* desc,
                       const uint64_t* reasm_offs1 = nullptr)
 {
     const bool split = edges && (edge_split() || !has_edge_blocks(kMode));
-    const uint32_t eb = (edges && !split) ? grid_for(2 * (uint64_t)n, kThreads) : 0;
+    const uint32_t eb = (edges && !split) ? grid_for(edge_threads(n), kThreads) : 0;
     const uint32_t sg = stream_grid(regions);
     // edge workgroups first, or spread evenly through the grid (edge_interleave)
     const uint32_t spread = eb ? (eb + sg) / eb : 0;
@@ -1590,7 +1601,7 @@ void launch_streaming(const void* src, void* dst, const cfws_frame_desc_t* desc,
     // (a separate edge launch on a second stream, overlapping the streaming
     // kernel, measured no faster on config 5: the stream slowed by what the
     // overlap saved)
-    if (split) edge_kernel<kMode><<<grid_for(2 * (uint64_t)n, kEdgeThreads), kEdgeThreads, 0, st>>>(
+    if (split) edge_kernel<kMode><<<grid_for(edge_threads(n), kEdgeThreads), kEdgeThreads, 0, st>>>(
         static_cast<const uint8_t*>(src), static_cast<uint8_t*>(dst), desc, status, offs,
         total_p, base_p, cap, (uint32_t)n, klass, sid, parent);
 }
