@@ -83,13 +83,8 @@ using cfws_rt::g_err;
 // A/B knob: dynamic LDS the WS plan kernels reserve (CFWS_PLAN_LDS; default 0)
 uint32_t plan_lds_bytes()
 {
-    static int64_t v = -1;
-    if (v < 0) {
-        const char* s = getenv("CFWS_PLAN_LDS");
-        v = s ? (int64_t)strtoull(s, nullptr, 10) : 0;
-        if (v > 65536) v = 65536;
-    }
-    return (uint32_t)v;
+    static const int64_t v = env_knob("CFWS_PLAN_LDS", 0);
+    return (uint32_t)(v > 65536 ? 65536 : v);
 }
 
 // Both reassembly passes' edge chunks in one launch of their own (the
@@ -505,12 +500,8 @@ deserialize_small_kernel(const uint8_t* __restrict__ wire, uint64_t wire_size,
 // execute for every batch, for A/B and for tests of both paths).
 bool small_path()
 {
-    static int v = -1;
-    if (v < 0) {
-        const char* s = getenv("CFWS_SMALL");
-        v = (s && *s == '0') ? 0 : 1;
-    }
-    return v == 1;
+    static const bool v = env_knob("CFWS_SMALL", 1) != 0;
+    return v;
 }
 
 // Workgroups of a small-batch launch: kSmallChunksPerThread output chunks

@@ -102,11 +102,12 @@ ThreadDevice& tdev()
 // CFWS_DROPIN_ZC_MAX overrides (bytes; 0 = DMA path always).
 size_t zero_copy_max()
 {
-    static size_t v = static_cast<size_t>(-1);
-    if (v == static_cast<size_t>(-1)) {
+    // read once: a function-local static's initialiser runs under the C++
+    // runtime's guard, whichever thread calls first
+    static const size_t v = [] {
         const char* s = getenv("CFWS_DROPIN_ZC_MAX");
-        v = s ? static_cast<size_t>(strtoull(s, nullptr, 10)) : (size_t(1) << 20);
-    }
+        return s ? static_cast<size_t>(strtoull(s, nullptr, 10)) : (size_t(1) << 20);
+    }();
     return v;
 }
 

@@ -1437,16 +1437,23 @@ inline uint32_t grid_for(uint64_t items, uint64_t per_block)
     return (uint32_t)(g == 0 ? 1 : g);
 }
 
+// A numeric environment knob, or `dflt` when unset. Callers keep the value
+// in a function-local static: its initialiser runs once, under the C++
+// runtime's guard, whichever thread calls first.
+inline int64_t env_knob(const char* name, int64_t dflt)
+{
+    const char* s = getenv(name);
+    return s && *s ? (int64_t)strtoull(s, nullptr, 10) : dflt;
+}
+
 // One 4 KiB region per wave (measured fastest: no grid-stride loop, every
 // wave's loads in flight at once); CFWS_GRID caps the workgroup count.
 inline uint32_t stream_grid(uint64_t regions)
 {
-    static uint64_t cap = 0;
-    if (cap == 0) {
-        const char* s = getenv("CFWS_GRID");
-        cap = s ? strtoull(s, nullptr, 10) : 0;
-        if (cap == 0) cap = 0x7fffffffull;
-    }
+    static const uint64_t cap = [] {
+        const int64_t v = env_knob("CFWS_GRID", 0);
+        return v > 0 ? (uint64_t)v : 0x7fffffffull;
+    }();
     uint64_t g = (regions + kWaves - 1) / kWaves;
     if (g > cap) g = cap;
     return (uint32_t)(g == 0 ? 1 : g);
@@ -1519,11 +1526,7 @@ constexpr uint32_t kXformLdsDefault = 32000;     // 5 x fits 160 KiB, 6 x does n
 #endif
 inline uint64_t occ_frame_max(int mode)
 {
-    static int64_t v = -2;
-    if (v == -2) {
-        const char* s = getenv("CFWS_OCC_FRAME_MAX");
-        v = s ? (int64_t)strtoull(s, nullptr, 10) : -1;
-    }
+    static const int64_t v = env_knob("CFWS_OCC_FRAME_MAX", -1);
     if (v >= 0) return (uint64_t)v;
     if (mode == kModeSer) return CFWS_OCC_FRAME_MAX_SER;
     if (mode == kModeDeser) return CFWS_OCC_FRAME_MAX_RECV;
@@ -1532,12 +1535,10 @@ inline uint64_t occ_frame_max(int mode)
 
 inline uint32_t xform_lds_bytes(int mode = -1, uint64_t frame_bytes = ~uint64_t(0))
 {
-    static int64_t v = -2;                      // -1: no override
-    if (v == -2) {
-        const char* s = getenv("CFWS_XFORM_LDS");
-        v = s ? (int64_t)strtoull(s, nullptr, 10) : -1;
-        if (v > 65536) v = 65536;
-    }
+    static const int64_t v = [] {                 // -1: no override
+        const int64_t x = env_knob("CFWS_XFORM_LDS", -1);
+        return x > 65536 ? 65536 : x;
+    }();
     if (v >= 0) return (uint32_t)v;
     if (frame_bytes <= occ_frame_max(mode)) return 0;
     if (mode == kModeSer) return CFWS_SER_LDS;
@@ -1550,12 +1551,8 @@ inline uint32_t xform_lds_bytes(int mode = -1, uint64_t frame_bytes = ~uint64_t(
 // previous layout, kept for A/B).
 inline bool edge_split()
 {
-    static int v = -1;
-    if (v < 0) {
-        const char* s = getenv("CFWS_EDGE_SPLIT");
-        v = (s && *s == '1') ? 1 : 0;
-    }
-    return v == 1;
+    static const bool v = env_knob("CFWS_EDGE_SPLIT", 0) == 1;
+    return v;
 }
 
 // Where the edge workgroups go: first (their chains run beside the first
@@ -1572,11 +1569,7 @@ inline bool edge_split()
 #endif
 inline bool edge_interleave(uint32_t stride)
 {
-    static int v = -2;
-    if (v == -2) {
-        const char* s = getenv("CFWS_EDGE_ORDER");
-        v = (s && *s == '1') ? 1 : ((s && *s == '0') ? 0 : -1);
-    }
+    static const int64_t v = env_knob("CFWS_EDGE_ORDER", -1);
     return v < 0 ? stride <= CFWS_EDGE_SPREAD_MAX_STRIDE : v == 1;
 }
 
