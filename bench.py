@@ -285,7 +285,7 @@ def bench_accept(args, rank, world, dev):
 
     for _ in range(args.warmup):
         step()
-    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(args.steps)]
+    ev = [[cfws.TimingEvent() for _ in range(2)] for _ in range(args.steps)]
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
@@ -384,7 +384,7 @@ def bench_index(args, rank, world, dev):
 
     for _ in range(args.warmup):
         step()
-    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(args.steps)]
+    ev = [[cfws.TimingEvent() for _ in range(2)] for _ in range(args.steps)]
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
@@ -540,7 +540,7 @@ def main():
 
     for _ in range(args.warmup):
         step()
-    events = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(args.steps)]
+    events = [[cfws.TimingEvent() for _ in range(4)] for _ in range(args.steps)]
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

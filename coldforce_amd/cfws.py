@@ -369,6 +369,48 @@ def _hip():
 
 
 HIP_HOST_MALLOC_MAPPED = 0x2
+HIP_EVENT_DISABLE_SYSTEM_FENCE = 0x20000000
+
+
+class TimingEvent:
+    """A HIP timing event recorded on torch's current stream (or `stream`),
+    created with hipEventDisableSystemFence: recording it adds no
+    system-scope fence (cache writeback + invalidate) to the stream. Four
+    torch.cuda.Event records per config-2 step left ~6 us of idle GPU at
+    each one, 0.5 % of the step; these leave none, and time the same
+    (tools/event_gap_probe.py). Same calls as torch.cuda.Event: record(),
+    elapsed_time(end) in ms (after a synchronize)."""
+
+    def __init__(self):
+        h = _hip()
+        if not hasattr(h, "_cfws_event_sigs"):
+            h.hipEventCreateWithFlags.argtypes = [C.POINTER(_vp), C.c_uint]
+            h.hipEventRecord.argtypes = [_vp, _vp]
+            h.hipEventElapsedTime.argtypes = [C.POINTER(C.c_float), _vp, _vp]
+            h.hipEventDestroy.argtypes = [_vp]
+            h._cfws_event_sigs = True
+        self._h = h
+        self.ev = _vp()
+        rc = h.hipEventCreateWithFlags(C.byref(self.ev), HIP_EVENT_DISABLE_SYSTEM_FENCE)
+        if rc != 0:
+            raise CodecError(f"hipEventCreateWithFlags rc={rc}")
+
+    def record(self, stream=None) -> None:
+        rc = self._h.hipEventRecord(self.ev, _vp(_stream(stream)))
+        if rc != 0:
+            raise CodecError(f"hipEventRecord rc={rc}")
+
+    def elapsed_time(self, end: "TimingEvent") -> float:
+        ms = C.c_float()
+        rc = self._h.hipEventElapsedTime(C.byref(ms), self.ev, end.ev)
+        if rc != 0:
+            raise CodecError(f"hipEventElapsedTime rc={rc}")
+        return ms.value
+
+    def __del__(self):
+        if getattr(self, "ev", None) and self.ev.value:
+            self._h.hipEventDestroy(self.ev)
+            self.ev = _vp()
 
 
 def mapped_host(nbytes: int):
