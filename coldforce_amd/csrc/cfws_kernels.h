@@ -978,12 +978,14 @@ __host__ __device__ constexpr bool has_edge_blocks(int mode)
 
 // The streaming kernel: serialize (kSer) = header + (masked) payload into
 // the wire arena; deserialize = copy + unmask into the payload arena.
-// The first `edge_blocks` workgroups write the edge chunks (edge_frame: two
-// threads per frame); the rest stream the regions, writing every 16-byte
-// chunk that lies inside one frame's body. The two chunk sets are disjoint.
-// Edge workgroups are dispatched first, so their latency-bound chains run
-// under the stream instead of as a launch of their own after it (which cost
-// 17 us serialize / 4 us deserialize on config 2, plus a kernel boundary).
+// `edge_blocks` workgroups write the edge chunks (edge_frame: two threads
+// per frame, one part per wave); the rest stream the regions, writing every
+// 16-byte chunk that lies inside one frame's body. The two chunk sets are
+// disjoint. The edge workgroups ride in the streaming launch -- the first
+// ones dispatched, or every `edge_stride`-th when frames are small
+// (edge_interleave) -- so their latency-bound chains run under the stream
+// instead of as a launch of their own after it (which cost 17 us serialize /
+// 4 us deserialize on config 2, plus a kernel boundary).
 // The wave-per-EU floor keeps the merged kernel at <= 102 VGPRs, so the
 // 5 workgroups per CU the LDS reservation allows stay resident.
 // workgroups per CU the send's streaming kernel is compiled for (A/B knob)
