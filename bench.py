@@ -300,6 +300,7 @@ def bench_accept(args, rank, world, dev):
     local = time.perf_counter() - t0
     elapsed = shard.max_over_ranks(local, dev)
     kms = sum(e[0].elapsed_time(e[1]) for e in ev) / args.steps
+    del ev                                   # HIP events freed while the runtime is up
     h = out.view(N, cfws.WS_ACCEPT_SLOT)
     sample = list(range(0, N, max(1, N // 4096)))
     got = h[sample, :28].cpu().numpy()
@@ -399,6 +400,7 @@ def bench_index(args, rank, world, dev):
     local = time.perf_counter() - t0
     elapsed = shard.max_over_ranks(local, dev)
     kms = sum(e[0].elapsed_time(e[1]) for e in ev) / args.steps
+    del ev                                   # HIP events freed while the runtime is up
     n_frames = int(total.item())
     host_wire = wire[:wtotal].cpu().numpy()
     st_h, first_h = starts_t.cpu().numpy(), first.cpu().numpy()
@@ -571,6 +573,7 @@ def main():
 
     ser_ms = sum(e[0].elapsed_time(e[1]) for e in events) / args.steps
     de_ms = sum(e[2].elapsed_time(e[3]) for e in events) / args.steps
+    del events                               # HIP events freed while the runtime is up
     hdr = int(wire_total - arena_bytes)
     alg_bytes = 2 * arena_bytes + hdr       # read n + write n (+ headers) per launch
     kern = {
