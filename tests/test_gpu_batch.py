@@ -362,3 +362,24 @@ def test_many_small_frames_round_trip(fs):
     got = back.cpu().numpy().reshape(n, slot)
     assert np.array_equal(got[:, :fs], payload.reshape(n, fs))
     assert not got[:, fs:].any()          # the alignment padding is written as zeros
+
+
+def test_plans_over_two_block_sum_steps():
+    """4.3 M frames of 0-20 bytes: both plans have more than 16,384 blocks,
+    so the block-sum scan takes two of its 16,384-sum steps, and the edge
+    workgroups (67 K) are spread through the grid. Serialize and deserialize
+    (align 1: every boundary mid-chunk) against the oracle."""
+    n = 4_300_000
+    rng = np.random.default_rng(43)
+    payload = O.fill_splitmix(1 << 16, 43, 0)
+    desc = np.zeros(n, dtype=cfws.DESC_DTYPE)
+    sz = rng.integers(0, 21, n).astype(np.uint64)
+    desc["payload_size"] = sz
+    desc["payload_off"] = rng.integers(0, (1 << 16) - 32, n).astype(np.uint64)
+    desc["fin"] = 1
+    desc["opcode"] = 2
+    desc["mask"] = (rng.random(n) < 0.7).astype(np.uint8)
+    desc["mask_key"] = rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32) * desc["mask"]
+    wire, total = check_serialize(payload, desc)
+    offs, _ = W.wire_layout(desc)
+    check_deserialize(wire[:total].copy(), offs, align=1)
