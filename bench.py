@@ -14,7 +14,10 @@ value = payload bytes processed by both ops on all ranks / wall time of the
 K timed steps (max over ranks), in GiB/s (2^30). With N GPUs each rank owns
 its own 65,536-frame shard of one global batch (weak scaling, no collective
 on the data path; the only collectives are the timing barrier and max, and
-a gather of each rank's timings for the line's per_gpu rows).
+a gather of each rank's timings for the line's per_gpu rows). The executes
+are timed with HIP events on the stream they run on (cfws.TimingEvent:
+created without the system-scope fence, which torch.cuda.Event records and
+which left ~6 us of idle GPU in the stream at each record).
 
 Usage: python bench.py [--gpus N --steps K --warmup W]
        torchrun --nproc-per-node N bench.py --gpus N ...   (N > 1)
