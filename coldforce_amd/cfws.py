@@ -43,7 +43,7 @@ assert DESC_DTYPE.itemsize == 32
 # Every function include/*.h declares (tests check the exports against the
 # headers themselves).
 BATCH_SYMBOLS = (
-    "cfws_init", "cfws_last_error", "cfws_version", "cfws_workspace_size",
+    "cfws_init", "cfws_init_device", "cfws_bind_thread_device", "cfws_thread_device", "cfws_last_error", "cfws_version", "cfws_workspace_size",
     "cfws_serialize_plan", "cfws_serialize_execute", "cfws_serialize_batch",
     "cfws_deserialize_plan", "cfws_deserialize_execute", "cfws_deserialize_batch",
     "cfws_xor_mask", "cfws_draw_mask_keys", "cfws_draw_mask_keys_seeded",
@@ -131,6 +131,9 @@ def lib(path: str = LIB_PATH) -> C.CDLL:
         "cfws_draw_mask_keys": ([_sz, _vp, _vp], None),
         "cfws_draw_mask_keys_seeded": ([_u32, _sz, _vp, _vp], C.c_int),
         "cfws_release_thread_resources": ([], None),
+        "cfws_init_device": ([C.c_int], C.c_int),
+        "cfws_bind_thread_device": ([C.c_int], C.c_int),
+        "cfws_thread_device": ([], C.c_int),
         "cfws_fill_splitmix": ([_vp, _u64, _u64, _u64, _vp], C.c_int),
         "cfws_h2_serialize_workspace_size": ([_sz, _u64, _u64, _u32], _sz),
         "cfws_h2_serialize_batch": ([_vp, _vp, _sz, _u32, _u32, _vp, _u64, _vp, _u64, _vp, _vp,

@@ -30,10 +30,11 @@
 //     frames after them.
 #include "cfws_kernels.h"
 
+#include <mutex>
+
 namespace cfws_rt {
 
 thread_local char g_err[512] = "";
-int g_init_state = 0;   // 0 unknown, 1 ok, <0 error code
 
 int set_err(int code, const char* what, hipError_t e)
 {
@@ -43,29 +44,62 @@ int set_err(int code, const char* what, hipError_t e)
     return code;
 }
 
-int check_init()
+// Every visible device is probed once, by whichever thread gets here first
+// (std::call_once); afterwards the checks only read what the probe wrote.
+// A call runs on the caller's current device, which must be a gfx950.
+namespace {
+std::once_flag g_probe_once;
+int g_probe_rc = CFWS_OK;
+int g_dev_count = 0;
+uint64_t g_gfx950_mask = 0;        // bit d: device d is a gfx950 (d < 64)
+char g_probe_msg[256] = "";
+
+void probe_devices()
 {
-    if (g_init_state == 1) return CFWS_OK;
-    if (g_init_state < 0) return g_init_state;
     int count = 0;
     hipError_t e = hipGetDeviceCount(&count);
-    if (e != hipSuccess || count == 0) {
-        g_init_state = CFWS_ERROR_NO_DEVICE;
-        return set_err(CFWS_ERROR_NO_DEVICE, "no HIP device", e);
+    if (e != hipSuccess || count <= 0) {
+        g_probe_rc = set_err(CFWS_ERROR_NO_DEVICE, "no HIP device", e);
+        snprintf(g_probe_msg, sizeof g_probe_msg, "%s", g_err);
+        return;
     }
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    hipDeviceProp_t prop;
-    e = hipGetDeviceProperties(&prop, dev);
-    if (e != hipSuccess) return set_err(CFWS_ERROR_NO_DEVICE, "hipGetDeviceProperties", e);
-    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
-        g_init_state = CFWS_ERROR_NO_DEVICE;
-        snprintf(g_err, sizeof g_err, "device arch %s is not gfx950", prop.gcnArchName);
-        fprintf(stderr, "cfws: %s\n", g_err);
+    g_dev_count = count;
+    char first_arch[64] = "";
+    for (int d = 0; d < count && d < 64; ++d) {
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, d) != hipSuccess) continue;
+        if (d == 0) snprintf(first_arch, sizeof first_arch, "%s", prop.gcnArchName);
+        if (strncmp(prop.gcnArchName, "gfx950", 6) == 0) g_gfx950_mask |= uint64_t(1) << d;
+    }
+    if (g_gfx950_mask == 0) {
+        snprintf(g_probe_msg, sizeof g_probe_msg, "no gfx950 device (device 0 is %s)", first_arch);
+        g_probe_rc = set_err(CFWS_ERROR_NO_DEVICE, g_probe_msg, hipSuccess);
+    }
+}
+}  // namespace
+
+int check_device(int dev)
+{
+    std::call_once(g_probe_once, probe_devices);
+    if (g_probe_rc != CFWS_OK) {
+        snprintf(g_err, sizeof g_err, "%s", g_probe_msg);
+        return g_probe_rc;
+    }
+    if (dev < 0 || dev >= g_dev_count || dev >= 64 || !((g_gfx950_mask >> dev) & 1)) {
+        snprintf(g_err, sizeof g_err, "device %d is not a usable gfx950 device (%d visible)", dev, g_dev_count);
         return CFWS_ERROR_NO_DEVICE;
     }
-    g_init_state = 1;
     return CFWS_OK;
+}
+
+int check_init()
+{
+    std::call_once(g_probe_once, probe_devices);
+    if (g_probe_rc != CFWS_OK) return check_device(0);
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return set_err(CFWS_ERROR_NO_DEVICE, "hipGetDevice", e);
+    return check_device(dev);
 }
 
 int launch_check(const char* what)
@@ -562,6 +596,7 @@ uint64_t cfws_internal_grand_total_offset() { return ws_layout(0, 0).hdr + 3 * s
 extern "C" {
 
 int cfws_init(void) { return check_init(); }
+int cfws_init_device(int device) { return cfws_rt::check_device(device); }
 const char* cfws_last_error(void) { return g_err; }
 const char* cfws_version(void) { return "cfws 0.2 gfx950"; }
 

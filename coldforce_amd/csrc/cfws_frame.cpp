@@ -17,6 +17,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <atomic>
 #include <mutex>
 #include <vector>
 
@@ -28,26 +29,29 @@ namespace {
 // co_ws_config.c:12-15 -- one process-wide, unsynchronised setting.
 size_t g_max_receive_payload_size = 32u * 1024u * 1024u;
 
-// Per calling thread: one stream, a pinned host staging buffer the device
-// reads and writes in place (mapped into the GPU's address space), and a
-// device staging buffer for frames above the zero-copy limit; all reused
-// across frames (coldforce runs each connection on one co_thread).
+// Per calling thread and device: one stream, a pinned host staging buffer
+// the device reads and writes in place (mapped into the GPU's address
+// space), and a device staging buffer for frames above the zero-copy limit;
+// all reused across frames (coldforce runs each connection on one co_thread).
 struct ThreadDevice {
-    int device = -1;               // the device the stream and buf belong to
+    int device = -1;               // the device the stream and buffers belong to
     hipStream_t stream = nullptr;
     void* buf = nullptr;           // device memory (DMA path)
     size_t cap = 0;
     uint8_t* host = nullptr;       // pinned host memory (zero-copy path)
     void* host_dev = nullptr;      // its device-side address
     size_t host_cap = 0;
+    bool zc_warm = false;          // first zero-copy frame done
+    bool dma_warm = false;         // first DMA-path frame done
+    bool holds() const { return stream || buf || host; }
 };
 
 // A thread borrows its resources from a process-wide free list (per device)
-// on its first frame and hands them back when it exits, so a server whose
-// threads come and go reuses the same few streams and staging buffers. No
-// HIP call at thread exit (the runtime may be tearing down); the free list
-// is never destroyed.
-constexpr int kPoolDevices = 16;
+// and hands them back when it moves to another device or exits, so a server
+// whose threads come and go, or move between GPUs, reuses the same few
+// streams and staging buffers. No HIP call at thread exit (the runtime may
+// be tearing down); the free list is never destroyed.
+constexpr int kPoolDevices = 64;
 struct DevicePool {
     std::mutex mu;
     std::vector<ThreadDevice> free_list[kPoolDevices];
@@ -59,40 +63,73 @@ DevicePool& device_pool()
     return *pool;
 }
 
-struct ThreadDeviceHolder {
-    ThreadDevice d;
-    bool borrowed = false;
-    ~ThreadDeviceHolder()
-    {
-        if (d.device < 0 || d.device >= kPoolDevices || !(d.stream || d.buf || d.host)) return;
+void give_back(ThreadDevice& d)
+{
+    if (d.device >= 0 && d.device < kPoolDevices && d.holds()) {
         DevicePool& pool = device_pool();
         std::lock_guard<std::mutex> lock(pool.mu);
         pool.free_list[d.device].push_back(d);
     }
+    d = ThreadDevice{};
+}
+
+struct ThreadDeviceHolder {
+    ThreadDevice d;
+    int bound = -1;                // cfws_bind_thread_device(); -1 = follow hipGetDevice()
+    ~ThreadDeviceHolder() { give_back(d); }
 };
 thread_local ThreadDeviceHolder t_holder;
 
-// The calling thread's resources (borrowed on first use for the current
-// device; a thread keeps them for its lifetime, as before).
-ThreadDevice& tdev()
+// Device policy (cfws_bind_thread_device, include/cfws.h): a thread's frames
+// go to the device it was bound to, or else to its current HIP device, read
+// on every frame. A thread whose target changes hands its resources back and
+// borrows the new device's, so a co_thread per GPU (co_net_worker.c:240
+// hands accepted sockets to other threads) spreads the work over the GPUs.
+int target_device()
+{
+    if (t_holder.bound >= 0) return t_holder.bound;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return -1;
+    return dev;
+}
+
+ThreadDevice& tdev(int dev)
 {
     ThreadDevice& d = t_holder.d;
-    if (!t_holder.borrowed) {
-        t_holder.borrowed = true;
-        int dev = 0;
-        if (hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < kPoolDevices) {
-            DevicePool& pool = device_pool();
-            std::lock_guard<std::mutex> lock(pool.mu);
-            if (!pool.free_list[dev].empty()) {
-                d = pool.free_list[dev].back();
-                pool.free_list[dev].pop_back();
-            } else {
-                d.device = dev;
-            }
+    if (d.device == dev) return d;
+    give_back(d);
+    if (dev >= 0 && dev < kPoolDevices) {
+        DevicePool& pool = device_pool();
+        std::lock_guard<std::mutex> lock(pool.mu);
+        if (!pool.free_list[dev].empty()) {
+            d = pool.free_list[dev].back();
+            pool.free_list[dev].pop_back();
+            return d;
         }
     }
+    d.device = dev;
     return d;
 }
+
+// Runs HIP calls that act on the current device (stream creation,
+// allocation) against `dev`, restoring the caller's device afterwards.
+class CurrentDevice {
+public:
+    explicit CurrentDevice(int dev)
+    {
+        if (hipGetDevice(&saved_) == hipSuccess && saved_ != dev && hipSetDevice(dev) == hipSuccess) switched_ = true;
+    }
+    ~CurrentDevice()
+    {
+        if (switched_) (void)hipSetDevice(saved_);
+    }
+    CurrentDevice(const CurrentDevice&) = delete;
+    CurrentDevice& operator=(const CurrentDevice&) = delete;
+
+private:
+    int saved_ = 0;
+    bool switched_ = false;
+};
 
 // Frames up to this size take the zero-copy path: the payload is copied into
 // the pinned buffer and the XOR kernel reads and writes it over PCIe, so a
@@ -111,22 +148,20 @@ size_t zero_copy_max()
     return v;
 }
 
-bool stream_ready()
+bool stream_ready(ThreadDevice& t_dev)
 {
-    if (cfws_init() != CFWS_OK) return false;
-    ThreadDevice& t_dev = tdev();
-    if (!t_dev.stream && hipStreamCreateWithFlags(&t_dev.stream, hipStreamNonBlocking) != hipSuccess) {
-        fprintf(stderr, "cfws: hipStreamCreate failed\n");
+    if (t_dev.stream) return true;
+    if (hipStreamCreateWithFlags(&t_dev.stream, hipStreamNonBlocking) != hipSuccess) {
+        fprintf(stderr, "cfws: hipStreamCreate on device %d failed\n", t_dev.device);
         t_dev.stream = nullptr;
         return false;
     }
     return true;
 }
 
-bool device_stage(size_t n)
+bool device_stage(ThreadDevice& t_dev, size_t n)
 {
-    if (!stream_ready()) return false;
-    ThreadDevice& t_dev = tdev();
+    if (!stream_ready(t_dev)) return false;
     if (t_dev.cap < n) {
         size_t cap = 1u << 16;
         while (cap < n) cap <<= 1;
@@ -142,10 +177,9 @@ bool device_stage(size_t n)
     return true;
 }
 
-bool host_stage(size_t n)
+bool host_stage(ThreadDevice& t_dev, size_t n)
 {
-    if (!stream_ready()) return false;
-    ThreadDevice& t_dev = tdev();
+    if (!stream_ready(t_dev)) return false;
     if (t_dev.host_cap < n) {
         size_t cap = 1u << 16;
         while (cap < n) cap <<= 1;
@@ -172,29 +206,68 @@ bool host_stage(size_t n)
 }
 
 // The mask keys are the process's random() stream (co_random.c:32-35), so
-// the device work of a frame must not consume it: the HIP/HSA runtime may
-// call rand()/random() (glibc: one shared state) while it initialises.
-// While the guard lives, random() runs on a private state; the caller's
-// state is left exactly where the reference leaves it.
+// the drop-in's device work must not consume it. The HIP/HSA runtime calls
+// rand()/random() (glibc: one shared state) while it sets things up: its
+// initialisation, a new stream's first work (profiles/
+// r02_random_state_probe.jsonl), allocations. While a guard lives, random()
+// runs on a private state and the caller's state is put back exactly where
+// the reference would leave it. glibc's state pointer is process-wide, so
+// guards never overlap (one process-wide mutex) and are taken only around
+// set-up work: a thread's first frame on a device, a staging buffer that
+// grows, each path's first frame. A steady-state frame swaps nothing, so
+// another thread's random() is never redirected by it (INTEGRATION.md §1
+// notes the set-up window).
+std::mutex& random_guard_mutex()
+{
+    static std::mutex* mu = new std::mutex;
+    return *mu;
+}
+
 class RandomStateGuard {
 public:
-    RandomStateGuard() : saved_(initstate(0x5eedu, scratch_, sizeof scratch_)) {}
-    ~RandomStateGuard() { setstate(saved_); }
+    RandomStateGuard() : lock_(random_guard_mutex(), std::defer_lock) {}
+    void engage()
+    {
+        if (lock_.owns_lock()) return;
+        lock_.lock();
+        saved_ = initstate(0x5eedu, reinterpret_cast<char*>(scratch_), sizeof scratch_);
+    }
+    ~RandomStateGuard()
+    {
+        if (lock_.owns_lock()) setstate(saved_);
+    }
     RandomStateGuard(const RandomStateGuard&) = delete;
     RandomStateGuard& operator=(const RandomStateGuard&) = delete;
 
 private:
-    char scratch_[128];
-    char* saved_;
+    std::unique_lock<std::mutex> lock_;
+    int32_t scratch_[32];          // glibc reads the state as int32_t words
+    char* saved_ = nullptr;
 };
 
 // dst[i] = src[i] ^ key[i % 4] for a host buffer, through the device.
+std::atomic<bool> g_runtime_up{false};   // the HIP runtime has been initialised by us
+
 bool device_xor(const uint8_t* src, uint8_t* dst, size_t n, uint32_t key)
 {
     RandomStateGuard keep_random_stream;
+    // the first HIP call of the process (hipGetDevice included) initialises
+    // the runtime
+    if (!g_runtime_up.load(std::memory_order_acquire)) keep_random_stream.engage();
+    const int dev = target_device();
+    if ((dev < 0 ? cfws_init() : cfws_init_device(dev)) != CFWS_OK || dev < 0) {
+        fprintf(stderr, "cfws: drop-in has no usable device (%s)\n", cfws_last_error());
+        return false;
+    }
+    g_runtime_up.store(true, std::memory_order_release);
+    ThreadDevice& t_dev = tdev(dev);
     const bool zero_copy = n <= zero_copy_max();
-    if (zero_copy ? !host_stage(n) : !device_stage(n)) return false;
-    ThreadDevice& t_dev = tdev();
+    if (!t_dev.stream || (zero_copy ? (!t_dev.zc_warm || t_dev.host_cap < n) : (!t_dev.dma_warm || t_dev.cap < n)))
+        keep_random_stream.engage();
+    {
+        CurrentDevice on(dev);
+        if (zero_copy ? !host_stage(t_dev, n) : !device_stage(t_dev, n)) return false;
+    }
     hipStream_t st = t_dev.stream;
     if (zero_copy) {
         memcpy(t_dev.host, src, n);
@@ -209,7 +282,12 @@ bool device_xor(const uint8_t* src, uint8_t* dst, size_t n, uint32_t key)
         fprintf(stderr, "cfws: device XOR failed: %s\n", hipGetErrorString(e));
         return false;
     }
-    if (zero_copy) memcpy(dst, t_dev.host, n);
+    if (zero_copy) {
+        memcpy(dst, t_dev.host, n);
+        t_dev.zc_warm = true;
+    } else {
+        t_dev.dma_warm = true;
+    }
     return true;
 }
 
@@ -375,11 +453,11 @@ void cfws_draw_mask_keys(size_t n, const uint8_t* mask_flags, uint32_t* keys)
 // random() state is left alone.
 int cfws_draw_mask_keys_seeded(uint32_t seed, size_t n, const uint8_t* mask_flags, uint32_t* keys)
 {
-    char table[128];
+    int32_t table[32];             // glibc reads the state as int32_t words
     struct random_data rd;
     memset(&rd, 0, sizeof rd);
     memset(table, 0, sizeof table);
-    if (initstate_r(seed, table, sizeof table, &rd) != 0) return CFWS_ERROR_INVALID_ARGUMENT;
+    if (initstate_r(seed, reinterpret_cast<char*>(table), sizeof table, &rd) != 0) return CFWS_ERROR_INVALID_ARGUMENT;
     for (size_t i = 0; i < n; ++i) {
         uint32_t k = 0;
         if (!mask_flags || mask_flags[i]) {
@@ -404,7 +482,18 @@ void cfws_release_thread_resources(void)
     if (t_dev.host) (void)hipHostFree(t_dev.host);
     if (t_dev.stream) (void)hipStreamDestroy(t_dev.stream);
     t_dev = ThreadDevice{};
-    t_holder.borrowed = false;
 }
+
+int cfws_bind_thread_device(int device)
+{
+    if (device < -1 || device >= kPoolDevices) return CFWS_ERROR_INVALID_ARGUMENT;
+    if (device >= 0) {
+        if (int rc = cfws_init_device(device)) return rc;
+    }
+    t_holder.bound = device;
+    return CFWS_OK;
+}
+
+int cfws_thread_device(void) { return target_device(); }
 
 }  // extern "C"

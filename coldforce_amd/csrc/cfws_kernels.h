@@ -26,6 +26,7 @@ namespace cfws_rt {
 extern thread_local char g_err[512];
 int set_err(int code, const char* what, hipError_t e);
 int check_init();
+int check_device(int dev);
 int launch_check(const char* what);
 // cfws_deserialize_plan's body; d_ends (optional) bounds each frame's data
 // (the HTTP/2 receive passes each pooled message's end)

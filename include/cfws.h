@@ -72,8 +72,11 @@ typedef struct cfws_frame_desc {
     uint8_t  header_size;
 } cfws_frame_desc_t;
 
-/* Library / device check: CFWS_OK when a gfx950 device is usable. */
+/* Library / device check: CFWS_OK when the calling thread's current HIP
+ * device is a gfx950. Every visible device is probed once per process
+ * (thread-safe); cfws_init_device checks one device by ordinal. */
 int cfws_init(void);
+int cfws_init_device(int device);
 const char* cfws_last_error(void);
 const char* cfws_version(void);
 
@@ -399,6 +402,20 @@ int cfws_draw_mask_keys_seeded(uint32_t seed, size_t n_frames, const uint8_t* ma
  * (cfws_frame.cpp) now; optional: a thread that exits without calling it
  * hands them back for reuse by later threads. */
 void cfws_release_thread_resources(void);
+
+/* Device policy of the drop-in co_ws_frame_* calls (cfws_frame.cpp). By
+ * default (device -1) a thread's masked frames run on its current HIP device,
+ * read on every frame. cfws_bind_thread_device(d) pins the calling thread to
+ * device d whatever its current device is, so a server with one co_thread
+ * per GPU (the reference hands accepted sockets to other threads,
+ * co_net_worker.c:240) can spread its connections over the GPUs. A thread
+ * whose device changes hands its stream and staging buffers back to a
+ * per-device pool and borrows the new device's. CFWS_OK, or
+ * CFWS_ERROR_INVALID_ARGUMENT / CFWS_ERROR_NO_DEVICE (d not a gfx950).
+ * cfws_thread_device returns the device the next frame would use (-1 on
+ * error). */
+int cfws_bind_thread_device(int device);
+int cfws_thread_device(void);
 
 /* ---- synthetic input (bench / tests) -------------------------------------
  * d_dst[i] = byte ((byte_base + i) % 8) of splitmix64 output number
