@@ -9,7 +9,7 @@ ARCH     ?= gfx950
 HIPFLAGS ?= -O3 -std=c++17 -fPIC -Wall -Wno-unused-result
 DEVSRC   := cfws_device cfws_h2 cfws_ops
 HOSTSRC  := cfws_frame cfws_pipeline cfws_index cfws_graph
-HDR      := include/cfws.h include/cfws_co_ws_frame.h coldforce_amd/csrc/cfws_internal.h
+HDR      := include/cfws.h include/cfws_co_ws_frame.h coldforce_amd/csrc/cfws_internal.h coldforce_amd/csrc/cfws_devpolicy.h
 LIB      := coldforce_amd/libcfws.so
 OBJDIR   := build
 
@@ -53,7 +53,7 @@ clean:
 
 .PHONY: all oracle ref asm clean examples
 
-# A/B build variants (kept out of git under build/): make variant V=nt F="-DCFWS_NT_STORE"
+# A/B build variants of the numeric tunables (kept out of git under build/): make variant V=ser4 F="-DCFWS_SER_LDS=40000"
 variant: $(HDR)
 	@mkdir -p $(OBJDIR)/variants/$(V)
 	for d in $(DEVSRC); do $(HIPCC) --offload-arch=$(ARCH) $(HIPFLAGS) $(F) -Iinclude -Icoldforce_amd/csrc -c coldforce_amd/csrc/$$d.hip -o $(OBJDIR)/variants/$(V)/$$d.o || exit 1; done

@@ -70,48 +70,78 @@ def parse():
     return ap.parse_args()
 
 
+def host_cpus() -> int:
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:
+        return os.cpu_count() or 1
+
+
+def cgroup_cpu_limit():
+    """The job's cgroup CPU quota ("max" or "<quota> <period>"), if any: on
+    a shared box nproc can exceed the CPU time the job is given."""
+    for path in ("/sys/fs/cgroup/cpu.max", "/sys/fs/cgroup/cpu/cpu.cfs_quota_us"):
+        try:
+            with open(path) as f:
+                return f.read().strip()
+        except OSError:
+            continue
+    return None
+
+
 def cpu_baseline(frame_size: int, seconds: float):
-    """Reference codec (oracle/_ref, compiled from coldforce's own sources)
-    when it was built, else the clean-room port; timed on this host."""
+    """Reference codec (oracle/_ref, compiled from coldforce's own sources at
+    -O2) when it was built, else the clean-room port; timed on this host on
+    nproc threads, with a 1 / 8 / 32 / nproc sweep at -O2
+    and the as-shipped -O0 at 1 and nproc threads."""
     import oracle
     kind = "reference" if oracle.ref_lib("O2") is not None else "port"
-    try:
-        cpus = len(os.sched_getaffinity(0))
-    except AttributeError:
-        cpus = os.cpu_count() or 1
-    threads = max(1, min(16, cpus))
-    n = 1024 * threads // 4 if threads >= 4 else 1024
-    ms, us = oracle.cpu_bench(n, frame_size, threads, 1, kind)
-    iters = max(1, int(math.ceil(seconds / max(ms + us, 1e-3))))
-    if iters > 1:
-        ms, us = oracle.cpu_bench(n, frame_size, threads, iters, kind)
-    payload = n * frame_size * iters
+    cpus = host_cpus()
 
-    def one_thread(k):
-        """1-thread rate of `k` over ~2 s (the survey's 1-thread / N-thread pair)."""
-        m1, u1 = oracle.cpu_bench(64, frame_size, 1, 1, k)
-        it = max(1, int(math.ceil(2.0 / max(m1 + u1, 1e-3))))
-        m1, u1 = oracle.cpu_bench(64, frame_size, 1, it, k)
-        return round(2 * 64 * frame_size * it / (m1 + u1) / GIB, 3)
+    def frames_for(threads):
+        return max(256, 64 * threads)
 
-    single = {}
+    def rate(k, threads, target_s):
+        """GiB/s of payload (mask + unmask) of `k` on `threads` over ~target_s."""
+        n = frames_for(threads)
+        oracle.cpu_bench(n, frame_size, threads, 1, k)          # first touch of the heaps
+        m1, u1 = oracle.cpu_bench(n, frame_size, threads, 2, k)
+        it = max(1, int(math.ceil(2 * target_s / max(m1 + u1, 1e-3))))
+        if it > 1:
+            m1, u1 = oracle.cpu_bench(n, frame_size, threads, it, k)
+        payload = n * frame_size * it
+        return payload, m1, u1, it
+
+    payload, ms, us, iters = rate(kind, cpus, seconds)
+    sweep = []
+    for t in sorted({1, 8, 32, cpus}):
+        if t > cpus:
+            continue
+        p, m1, u1, _ = (payload, ms, us, iters) if t == cpus else rate(kind, t, 1.5)
+        sweep.append({"threads": t, "gibs": round(2 * p / (m1 + u1) / GIB, 3)})
+    as_shipped = {}
     if kind == "reference":
-        single = {"reference_O2": one_thread("reference"),
-                  "reference_O0_as_shipped": one_thread("reference_O0")}
-    single["port_O2"] = one_thread("port")
+        for t in sorted({1, cpus}):
+            p, m1, u1, _ = rate("reference_O0", t, 1.5)
+            as_shipped[str(t)] = round(2 * p / (m1 + u1) / GIB, 3)
+    p, m1, u1, _ = rate("port", 1, 1.5)
+    n = frames_for(cpus)
     return {
         "value": round(2 * payload / (ms + us) / GIB, 3),
         "unit": "GiB/s",
-        "cores": threads,
+        "cores": cpus,
         "kind": kind,
         "sample": (f"{n} x {frame_size // 1024} KiB binary frames x {iters} iters, per-frame "
                    f"co_ws_frame_serialize(mask) + co_ws_frame_deserialize"
                    f"{' (reference -O2, oracle/_ref)' if kind == 'reference' else ' (port, -O2)'},"
-                   f" {threads} threads"),
+                   f" {cpus} threads (nproc), each on a contiguous frame range"),
         "mask_gibs": round(payload / ms / GIB, 3),
         "unmask_gibs": round(payload / us / GIB, 3),
         "seconds": round(ms + us, 2),
-        "single_thread_gibs": single,
+        "scaling_O2": sweep,
+        "as_shipped_O0": as_shipped,
+        "port_O2_1_thread": round(2 * p / (m1 + u1) / GIB, 3),
+        "cgroup_cpu_max": cgroup_cpu_limit(),
     }
 
 
@@ -309,8 +339,10 @@ def bench_accept(args, rank, world, dev):
     got = h[sample, :28].cpu().numpy()
     ok = all(bytes(got[j]).decode() == O.ws_accept_key(keys[i]) for j, i in enumerate(sample))
     ok = shard.sum_over_ranks(1.0 if ok else 0.0, dev) == world
-    valu = load_pmc("pmc_accept.json", "SQ_INSTS_VALU_per_launch")
-    achieved = valu * 64 / (kms * 1e-3) if valu else None
+    # VALU lane-ops per key from the committed PMC pass (SQ_INSTS_VALU x 64 /
+    # keys, measured at 1,048,576 keys; per key, so it scales with --keys)
+    per_key = load_pmc("pmc_accept.json", "valu_instructions_per_key")
+    achieved = per_key * N / (kms * 1e-3) if per_key else None
     line = {"metric": "WS handshake Sec-WebSocket-Accept keys/s (SHA-1 + base64), device resident",
             "value": round(N * world * args.steps / elapsed, 1), "unit": "keys/s",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -321,11 +353,11 @@ def bench_accept(args, rank, world, dev):
                          "achieved": round(achieved / 1e12, 2) if achieved else None,
                          "peak": round(VALU_PEAK_OPS / 1e12, 1), "unit": "T lane-ops/s",
                          "frac": round(achieved / VALU_PEAK_OPS, 4) if achieved else None,
-                         "valu_instructions_per_launch": valu},
+                         "valu_lane_ops_per_launch": per_key * N if per_key else None},
             "verified": ok}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         kind = "reference" if O.ref_lib("O2") is not None else "port"
-        threads = max(1, min(16, len(os.sched_getaffinity(0))))
+        threads = host_cpus()
         n = min(N, 262144)
         t1 = O.cpu_accept_bench(raw, off[:n + 1].astype(np.uint64), threads, 1, kind)
         iters = max(1, int(math.ceil(args.cpu_seconds / max(t1, 1e-3))))
@@ -425,13 +457,16 @@ def bench_index(args, rank, world, dev):
                                    f"{args.index_mib} MiB of receive buffers",
                        "wire_bytes": int(wtotal), "frames": n_frames, "connections": C_},
             "roofline": {"bound": "latency", "avg_launch_ms": round(kms, 4),
-                         "note": "each connection is a chain of dependent header reads (count, "
-                                 "scan, then the walk again to write starts), so the launch is "
-                                 "bounded by hop latency x chain length, not HBM bytes",
+                         "note": "each connection is one walk, a chain of dependent header "
+                                 "reads that keeps its first 64 starts in the workspace; after "
+                                 "the scan of the counts, index_place copies them to their "
+                                 "places and index_rest walks on for connections longer than "
+                                 "64 frames. The launch is bounded by hop latency x chain "
+                                 "length, not HBM bytes",
                          "ns_per_hop": round(kms * 1e6 / max(hops, 1e-9), 1)},
             "verified": ok}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        threads = max(1, min(16, len(os.sched_getaffinity(0))))
+        threads = host_cpus()
         ub = (begin_np.astype(np.uint64), end_np.astype(np.uint64))
         t1, _ = O.cpu_index_bench(host_wire, ub[0], ub[1], 4096, threads)
         reps = max(1, int(math.ceil(args.cpu_seconds / max(t1, 1e-3))))

@@ -23,6 +23,7 @@
 
 #include "cfws.h"
 #include "cfws_co_ws_frame.h"
+#include "cfws_devpolicy.h"
 
 namespace {
 
@@ -46,16 +47,11 @@ struct ThreadDevice {
     bool holds() const { return stream || buf || host; }
 };
 
-// A thread borrows its resources from a process-wide free list (per device)
-// and hands them back when it moves to another device or exits, so a server
-// whose threads come and go, or move between GPUs, reuses the same few
-// streams and staging buffers. No HIP call at thread exit (the runtime may
-// be tearing down); the free list is never destroyed.
+// Device policy and per-device resource pool: cfws_devpolicy.h. The pool is
+// never destroyed (no HIP call at exit; the runtime may be tearing down).
 constexpr int kPoolDevices = 64;
-struct DevicePool {
-    std::mutex mu;
-    std::vector<ThreadDevice> free_list[kPoolDevices];
-};
+using DevicePool = cfws_policy::DevicePool<ThreadDevice, kPoolDevices>;
+using ThreadSlot = cfws_policy::ThreadSlot<ThreadDevice, DevicePool>;
 
 DevicePool& device_pool()
 {
@@ -63,53 +59,17 @@ DevicePool& device_pool()
     return *pool;
 }
 
-void give_back(ThreadDevice& d)
-{
-    if (d.device >= 0 && d.device < kPoolDevices && d.holds()) {
-        DevicePool& pool = device_pool();
-        std::lock_guard<std::mutex> lock(pool.mu);
-        pool.free_list[d.device].push_back(d);
-    }
-    d = ThreadDevice{};
-}
+thread_local ThreadSlot t_slot(device_pool());
 
-struct ThreadDeviceHolder {
-    ThreadDevice d;
-    int bound = -1;                // cfws_bind_thread_device(); -1 = follow hipGetDevice()
-    ~ThreadDeviceHolder() { give_back(d); }
-};
-thread_local ThreadDeviceHolder t_holder;
-
-// Device policy (cfws_bind_thread_device, include/cfws.h): a thread's frames
-// go to the device it was bound to, or else to its current HIP device, read
-// on every frame. A thread whose target changes hands its resources back and
-// borrows the new device's, so a co_thread per GPU (co_net_worker.c:240
-// hands accepted sockets to other threads) spreads the work over the GPUs.
 int target_device()
 {
-    if (t_holder.bound >= 0) return t_holder.bound;
     int dev = 0;
+    if (t_slot.bound() >= 0) return t_slot.bound();
     if (hipGetDevice(&dev) != hipSuccess) return -1;
-    return dev;
+    return t_slot.target(dev);
 }
 
-ThreadDevice& tdev(int dev)
-{
-    ThreadDevice& d = t_holder.d;
-    if (d.device == dev) return d;
-    give_back(d);
-    if (dev >= 0 && dev < kPoolDevices) {
-        DevicePool& pool = device_pool();
-        std::lock_guard<std::mutex> lock(pool.mu);
-        if (!pool.free_list[dev].empty()) {
-            d = pool.free_list[dev].back();
-            pool.free_list[dev].pop_back();
-            return d;
-        }
-    }
-    d.device = dev;
-    return d;
-}
+ThreadDevice& tdev(int dev) { return t_slot.on(dev); }
 
 // Runs HIP calls that act on the current device (stream creation,
 // allocation) against `dev`, restoring the caller's device afterwards.
@@ -477,11 +437,11 @@ int cfws_draw_mask_keys_seeded(uint32_t seed, size_t n, const uint8_t* mask_flag
 // threads instead).
 void cfws_release_thread_resources(void)
 {
-    ThreadDevice& t_dev = t_holder.d;
+    ThreadDevice& t_dev = t_slot.current();
     if (t_dev.buf) (void)hipFree(t_dev.buf);
     if (t_dev.host) (void)hipHostFree(t_dev.host);
     if (t_dev.stream) (void)hipStreamDestroy(t_dev.stream);
-    t_dev = ThreadDevice{};
+    t_slot.forget();
 }
 
 int cfws_bind_thread_device(int device)
@@ -490,7 +450,7 @@ int cfws_bind_thread_device(int device)
     if (device >= 0) {
         if (int rc = cfws_init_device(device)) return rc;
     }
-    t_holder.bound = device;
+    t_slot.bind(device);
     return CFWS_OK;
 }
 

@@ -680,7 +680,7 @@ struct H2SerLayout {
     uint64_t bytes, n_max, regions;
 };
 
-H2SerLayout h2_ser_layout(uint64_t n, uint64_t wire_cap, uint64_t h2_cap, uint64_t S)
+static H2SerLayout h2_ser_layout(uint64_t n, uint64_t wire_cap, uint64_t h2_cap, uint64_t S)
 {
     H2SerLayout L;
     L.n_max = n + wire_cap / S + 1;
@@ -712,7 +712,7 @@ struct H2DeLayout {
     uint64_t bytes;
 };
 
-H2DeLayout h2_de_layout(uint64_t n, uint64_t pool_cap, uint64_t payload_cap)
+static H2DeLayout h2_de_layout(uint64_t n, uint64_t pool_cap, uint64_t payload_cap)
 {
     H2DeLayout L;
     uint64_t at = 0;

@@ -231,51 +231,17 @@ __device__ __forceinline__ FrameView frame_view(const Pass& P, uint32_t f)
 
 // 16-byte global accesses of the streaming paths. Output is written once and
 // never re-read by the kernel, so stores carry the `nt` bit (measured +2-3 %
-// on config 2; -DCFWS_PLAIN_STORE turns it off). `nt` loads measured -10 %
-// and stay off unless -DCFWS_NT_LOAD.
-#ifndef CFWS_PLAIN_STORE
-#define CFWS_NT_STORE 1
-#endif
+// on config 2). Loads keep the default policy: every source byte is read by
+// exactly one lane, once, yet `nt` loads measured -10 % with two loads per
+// block and -3 % with the DPP path (6.37/6.49 TB/s plain vs 5.97/6.29 nt,
+// profiles/r01_ab_dpp.json), although the bare copy probe
+// (tools/copy_probe.hip) gains from them.
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ uint4 ld16(const uint8_t* p)
 {
-#ifdef CFWS_NT_LOAD
-    const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
-#else
     const u32x4 v = *reinterpret_cast<const u32x4*>(p);
-#endif
     return make_uint4(v.x, v.y, v.z, v.w);
-}
-
-// The streaming kernel's body loads. Every source byte is read by exactly one
-// lane, once, yet `nt` measured slower here (config 2: 6.37/6.49 TB/s plain
-// vs 5.97/6.29 nt, profiles/r01_ab_dpp.json), although the bare copy probe
-// (tools/copy_probe.hip) gains from it; -DCFWS_STREAM_NT turns it on.
-#ifdef CFWS_STREAM_NT
-#define CFWS_STREAM_NT_SEND 1
-#define CFWS_STREAM_NT_RECV 1
-#endif
-template <int kMode>
-__device__ __forceinline__ uint4 ld16_stream(const uint8_t* p)
-{
-#if defined(CFWS_STREAM_NT_SEND) || defined(CFWS_STREAM_NT_RECV)
-#ifdef CFWS_STREAM_NT_SEND
-    constexpr bool send_nt = true;
-#else
-    constexpr bool send_nt = false;
-#endif
-#ifdef CFWS_STREAM_NT_RECV
-    constexpr bool recv_nt = true;
-#else
-    constexpr bool recv_nt = false;
-#endif
-    if (kMode == kModeDeser ? recv_nt : send_nt) {
-        const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
-        return make_uint4(v.x, v.y, v.z, v.w);
-    }
-#endif
-    return ld16(p);
 }
 
 // Lane i receives lane i + 1's `v` (DPP wave_shl:1); lane 63, which has no
@@ -294,11 +260,7 @@ __device__ __forceinline__ uint4 from_next_lane(const uint4& v, const uint4& las
 __device__ __forceinline__ void st16(uint8_t* p, uint4 o)
 {
     const u32x4 v = {o.x, o.y, o.z, o.w};
-#ifdef CFWS_NT_STORE
     __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(p));
-#else
-    *reinterpret_cast<u32x4*>(p) = v;
-#endif
 }
 
 // Body stores of the streaming regions, at byte `off` of the wave's output
@@ -640,7 +602,7 @@ __device__ __forceinline__ void fast_region(const Pass& P, const FrameView& v, u
     const uint32_t l0 = lane * (uint32_t)kChunk;
     uint4 a[kUnroll];
 #pragma unroll
-    for (int u = 0; u < kUnroll; ++u) a[u] = ld16_stream<kMode>(s0 + u * kSlice);
+    for (int u = 0; u < kUnroll; ++u) a[u] = ld16(s0 + u * kSlice);
     if (ph == 0) {
 #pragma unroll
         for (int u = 0; u < kUnroll; ++u) {
@@ -709,7 +671,7 @@ __device__ __forceinline__ void two_frame_region(const Pass& P, const FrameView&
     }
     uint4 a[kUnroll], e[kUnroll];
 #pragma unroll
-    for (int u = 0; u < kUnroll; ++u) a[u] = fast[u] ? ld16_stream<kMode>(sp[u]) : make_uint4(0, 0, 0, 0);
+    for (int u = 0; u < kUnroll; ++u) a[u] = fast[u] ? ld16(sp[u]) : make_uint4(0, 0, 0, 0);
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u) e[u] = own[u] ? ld16(sp[u] + 16) : make_uint4(0, 0, 0, 0);
 #pragma unroll
@@ -763,12 +725,7 @@ __device__ __forceinline__ void general_region(const Pass& P, uint32_t f0, uint3
                                                uint32_t lane)
 {
     const uint32_t nf = f1 - f0 + 1;
-#ifdef CFWS_GENERAL_SEARCH
-    const bool search = true;                   // A/B: the per-chunk search everywhere
-#else
-    const bool search = nf > 64;
-#endif
-    if (search) {
+    if (nf > 64) {
         general_region_search<kMode>(P, f0, f1, base, lane);
         return;
     }
@@ -1175,17 +1132,12 @@ __device__ __forceinline__ int32_t parse_ws_header(const uint8_t* __restrict__ w
                                                    uint64_t s, uint64_t max_payload,
                                                    cfws_frame_desc_t& d)
 {
-#ifdef CFWS_PARSE_BYTEWISE
-    return parse_ws_header_by([wire](uint64_t i) -> uint32_t { return wire[i]; }, size, s,
-                              max_payload, d);
-#else
     const uint64_t avail = s <= size ? size - s : 0;
     uint32_t w[4];
     load_span16(wire + s, avail < 14 ? (uint32_t)avail : 14u, w);
     const int32_t st = parse_ws_header_regs(w, avail, max_payload, d);
     d.wire_off = s;
     return st;
-#endif
 }
 
 // Exclusive block scan of one value per thread; *block_total gets the sum.
@@ -1590,6 +1542,11 @@ void launch_streaming(const void* src, void* dst, const cfws_frame_desc_t* desc,
     // edge workgroups first, or spread evenly through the grid (edge_interleave)
     const uint32_t spread = eb ? (eb + sg) / eb : 0;
     const uint32_t stride = (eb && edge_interleave(spread)) ? spread : 0;
+    // The residency choice takes cap / n as the average output per frame: the
+    // output size itself is only known on the device. Callers whose capacity
+    // is far above their output (an oversized arena; the HTTP/2 receive passes
+    // len(h2) + 16 n) may get the large-frame residency for small frames --
+    // a speed effect only, the bytes written are the same.
     xform_kernel<kMode><<<eb + sg, kThreads, xform_lds_bytes(kMode, n ? cap / n : cap), st>>>(
         static_cast<const uint8_t*>(src), static_cast<uint8_t*>(dst), desc, status, offs, map,
         total_p, base_p, cap, (uint32_t)n, klass, sid, parent, eb, eb ? reasm_offs1 : nullptr,

@@ -462,7 +462,7 @@ struct IndexLayout {
     uint64_t partials, slots, resume, bytes;
 };
 
-IndexLayout index_layout(uint64_t n)
+static IndexLayout index_layout(uint64_t n)
 {
     IndexLayout L;
     uint64_t at = 64;

@@ -1,0 +1,86 @@
+"""TEST INFRASTRUCTURE ONLY -- the codec's parity cases under the library's
+launch-time knobs (read once per process from the environment, so
+tests/test_knobs.py runs this script once per setting):
+
+  CFWS_EDGE_SPLIT=1     edge chunks as a launch of their own after the stream
+  CFWS_EDGE_ORDER=0/1   edge workgroups first / spread through the grid
+  CFWS_SMALL=0          small batches on the general plan + execute path
+  CFWS_GRID=N           streaming grid capped at N workgroups (grid-stride)
+  CFWS_OCC_FRAME_MAX=0  no register-limited residency for small frames
+  CFWS_XFORM_LDS=N      the LDS reservation for every mode
+  CFWS_PLAN_LDS=N       LDS reserved by the plan kernels
+
+Each case is checked byte for byte against the oracle. Prints "KNOB OK".
+"""
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import oracle as O  # noqa: E402
+import torch  # noqa: E402
+from coldforce_amd import cfws  # noqa: E402
+from coldforce_amd import workloads as W  # noqa: E402
+
+
+def roundtrip(sizes, rng, seed, align, flags=0, opcodes=None, fins=None):
+    n = len(sizes)
+    desc = np.zeros(n, dtype=cfws.DESC_DTYPE)
+    desc["payload_size"] = sizes
+    desc["payload_off"] = np.concatenate([[0], np.cumsum(sizes[:-1])]) + 5
+    desc["fin"] = fins if fins is not None else rng.integers(0, 2, n)
+    desc["opcode"] = opcodes if opcodes is not None else rng.choice([0, 1, 2, 9, 10], n)
+    desc["mask"] = rng.integers(0, 2, n)
+    desc["mask_key"] = cfws.draw_mask_keys(n, desc["mask"], seed=seed)
+    payload_np = O.fill_splitmix(int(sizes.sum()) + 32, 0x5EED + seed, 0)
+    exp_wire, _ = O.serialize_batch(payload_np, desc.view(O.DESC_DTYPE))
+    payload = torch.from_numpy(payload_np).cuda()
+    offs, total = W.wire_layout(desc)
+    wire = torch.empty(W.round16(total) + 64, dtype=torch.uint8, device="cuda")
+    tot = cfws.serialize(payload, cfws.desc_to_device(desc), wire)
+    torch.cuda.synchronize()
+    assert tot.item() == total == len(exp_wire)
+    assert np.array_equal(wire[:total].cpu().numpy(), exp_wire), "serialize != oracle"
+    cap = int(sizes.sum()) + align * n + 64
+    out = torch.empty(cap, dtype=torch.uint8, device="cuda")
+    idx = torch.from_numpy(offs.astype(np.int64)).cuda()
+    d2, st, ptot = cfws.deserialize(wire, total, idx, out, align=align, flags=flags)
+    torch.cuda.synchronize()
+    e_out, e_d, e_st, e_tot = O.deserialize_batch(exp_wire, offs, align=align, capacity=cap, flags=flags)
+    assert ptot.item() == e_tot and np.array_equal(st.cpu().numpy(), e_st)
+    assert np.array_equal(out[:e_tot].cpu().numpy(), e_out[:e_tot]), "deserialize != oracle"
+
+
+def main():
+    cfws.init()
+    rng = np.random.default_rng(11)
+    # mixed sizes: fast / two-frame / general regions, edges, 64-bit lengths
+    sizes = rng.choice([0, 1, 3, 125, 126, 1000, 4096, 65535, 65536, 70000], size=3000)
+    for align in (1, 16):
+        roundtrip(sizes, rng, 1, align)
+    # 1 KiB frames in a large batch (spread edges, register-limited residency)
+    roundtrip(np.full(20000, 1024), rng, 2, 16, opcodes=np.full(20000, 1), fins=np.ones(20000))
+    # a small batch (single-launch path unless CFWS_SMALL=0)
+    roundtrip(np.full(256, 1000), rng, 3, 16)
+    # fragments + pings, reassembled (two passes, pass-1 capped grid)
+    desc, msgs = W.zipf_batch(48 << 20, 0x5EED0003, 3, ping_every=5)
+    arena = O.splitmix_words(0x5EED0003, 0, (msgs["arena_bytes"] + 7) // 8).view(np.uint8)[:msgs["arena_bytes"]]
+    exp_wire, d2 = O.serialize_batch(arena, desc.view(O.DESC_DTYPE))
+    wire = torch.from_numpy(exp_wire).cuda()
+    cap = len(arena) + 64
+    out = torch.empty(cap, dtype=torch.uint8, device="cuda")
+    idx = torch.from_numpy(d2["wire_off"].astype(np.int64)).cuda()
+    _, st, ptot = cfws.deserialize(wire, len(exp_wire), idx, out, flags=cfws.DESERIALIZE_REASSEMBLE)
+    torch.cuda.synchronize()
+    e_out, _, e_st, e_tot = O.deserialize_batch(exp_wire, d2["wire_off"], capacity=cap,
+                                                flags=O.DESERIALIZE_REASSEMBLE)
+    assert ptot.item() == e_tot and np.array_equal(st.cpu().numpy(), e_st)
+    assert np.array_equal(out[:e_tot].cpu().numpy(), e_out[:e_tot]), "reassembly != oracle"
+    print("KNOB OK", {k: v for k, v in os.environ.items() if k.startswith("CFWS_")}, flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -189,3 +189,72 @@ def test_thread_churn_reuses_resources():
         for t in ts:
             t.join()
     assert not errors, errors
+
+
+def test_device_policy_bind_and_follow():
+    """cfws_bind_thread_device: a bound thread's frames go to that device
+    whatever its current device; unbound threads follow hipGetDevice; an
+    ordinal that is not a visible gfx950 is refused."""
+    import threading
+    L = cfws.lib()
+    n_dev = torch.cuda.device_count()
+    assert L.cfws_bind_thread_device(n_dev) == -4          # CFWS_ERROR_NO_DEVICE
+    assert L.cfws_bind_thread_device(-2) == -1
+    data = random.Random(3).randbytes(5000)
+    Lo = O.lib()
+    O.srandom(Lo, 11)
+    w = O.ref_serialize(Lo, True, 2, True, data)
+    errors = []
+
+    def run(dev):
+        try:
+            assert L.cfws_bind_thread_device(dev) == 0
+            assert L.cfws_thread_device() == dev
+            for _ in range(20):
+                r = cfws.frame_deserialize(w)
+                assert r["rc"] == 0 and r["payload"] == data + b"\0"
+            assert L.cfws_bind_thread_device(-1) == 0
+            torch.cuda.set_device(0)
+            assert L.cfws_thread_device() == 0
+            assert cfws.frame_deserialize(w)["payload"] == data + b"\0"
+        except Exception as e:
+            errors.append(e)
+
+    ts = [threading.Thread(target=run, args=(d % n_dev,)) for d in range(2 * n_dev)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errors, errors
+
+
+def test_device_policy_spreads_over_gpus():
+    """One thread per GPU, each bound to its own device, masking and
+    unmasking concurrently: every thread's frames are correct and run on its
+    device (a multi-thread coldforce server, co_net_worker.c:240)."""
+    import threading
+    n_dev = torch.cuda.device_count()
+    if n_dev < 2:
+        pytest.skip("needs 2+ GPUs")
+    L = cfws.lib()
+    errors = []
+    data = random.Random(5).randbytes(70000)
+
+    def run(dev):
+        try:
+            assert L.cfws_bind_thread_device(dev) == 0
+            for k in range(50):
+                ok, w = cfws.frame_serialize(True, 2, True, data)
+                assert ok and w[1] & 0x80
+                r = cfws.frame_deserialize(w)
+                assert r["rc"] == 0 and r["payload"] == data + b"\0", (dev, k)
+            assert L.cfws_thread_device() == dev
+        except Exception as e:
+            errors.append(e)
+
+    ts = [threading.Thread(target=run, args=(d,)) for d in range(n_dev)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errors, errors
