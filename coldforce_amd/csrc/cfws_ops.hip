@@ -47,12 +47,17 @@ parse_headers_kernel(const uint8_t* __restrict__ wire, uint64_t size, const uint
 
 // The payload loops (mask: co_ws_frame.c:93-97, unmask: :232-242) of every
 // frame, each frame from its own source to its own destination. Work unit
-// (frame, piece): a workgroup writes the 16-byte destination chunks of one
-// frame, 1,024 per pass (4 per lane, loads in flight before the stores),
-// striding by `pieces` passes. Chunks inside the frame are one 16-byte store
-// (source funnel-shifted into place); the frame's first and last chunk, which
-// it may share with its neighbours, are written byte by byte.
-constexpr uint32_t kPieceChunks = 4 * kThreads;
+// (frame, piece): a frame's 16-byte destination chunks are split evenly over
+// the fewest pieces of at most 1,280 chunks (5 per lane, every load in flight
+// before the first store), so a 64 KiB frame at any alignment (4,097
+// chunks) is 4 equal workgroups, not 4 full ones and a near-empty fifth.
+// Chunks inside the frame are one 16-byte store (source funnel-shifted into
+// place; a lane's second source block comes from the next lane over DPP).
+// The frame's first and last chunk, which it may share with its
+// neighbours, are assembled the same way from the (at most two) source
+// blocks holding their bytes and stored byte by byte from registers.
+constexpr uint32_t kPieceK = 5;
+constexpr uint32_t kPieceChunks = kPieceK * kThreads;
 
 template <bool kUnmask>
 __global__ void __launch_bounds__(kThreads)
@@ -73,48 +78,66 @@ payload_xor_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
     const uint64_t dend = len < cap - dof ? dof + len : cap;
     const uint64_t c0 = dof & ~uint64_t(15);
     const uint64_t nchunks = (dend - c0 + 15) >> 4;
+    const uint64_t used = (nchunks + kPieceChunks - 1) / kPieceChunks;
     // source phase against the 16-byte destination chunks: one per frame
     const uint32_t ph = (uint32_t)((so - dof) & 15u);
     const uint32_t lane = threadIdx.x & 63u;
-    for (uint64_t base = uint64_t(p) * kPieceChunks; base < nchunks;
-         base += uint64_t(pieces) * kPieceChunks) {
-        // a lane's block B is the next lane's A (DPP) when that lane's chunk
-        // is full too; lane 63 and the last full chunk load their own
-        uint4 a[4], e[4];
-        bool full[4];
-        uint32_t own_b = 0;
+    // virtual pieces p, p + pieces, ...: a frame larger than the caller's
+    // max_payload_size (or a grid capped below 2^31 blocks) still gets every
+    // chunk written
+    for (uint64_t vp = p; vp < used; vp += pieces) {
+        const uint64_t pb = nchunks * vp / used, pe = nchunks * (vp + 1) / used;
+        uint4 a[kPieceK], e[kPieceK];
+        uint32_t full = 0, part = 0, own_b = 0;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const uint64_t A = c0 + 16 * (base + uint64_t(k) * kThreads + threadIdx.x);
-            full[k] = A >= dof && A + 16 <= dend;
+        for (int k = 0; k < (int)kPieceK; ++k) {
+            const uint64_t c = pb + uint64_t(k) * kThreads + threadIdx.x;
+            const uint64_t A = c0 + 16 * c;
             a[k] = make_uint4(0, 0, 0, 0);
             e[k] = make_uint4(0, 0, 0, 0);
-            if (full[k]) {
-                const uint8_t* sp = src + ((so + (A - dof)) & ~uint64_t(15));
-                a[k] = ld16(sp);
-                // the block holding the chunk's last source byte: a payload byte
-                if (ph && (lane == 63 || A + 32 > dend)) {
-                    e[k] = ld16(sp + 16);
+            if (c >= pe) continue;
+            // the aligned source blocks of the window this chunk funnels from
+            const int64_t w = (int64_t)so + (int64_t)A - (int64_t)dof;
+            const int64_t wa = w - (w & 15);
+            if (A >= dof && A + 16 <= dend) {
+                full |= 1u << k;
+                a[k] = ld16(src + wa);
+                // the block holding the chunk's last source byte, when the
+                // next lane does not load it: lane 63, the piece's last
+                // chunk, a partial chunk next
+                if (ph && (lane == 63 || c + 1 >= pe || A + 32 > dend)) {
+                    e[k] = ld16(src + wa + 16);
                     own_b |= 1u << k;
                 }
+            } else {
+                // the frame's first or last chunk: only the blocks that hold
+                // its bytes (wa >= 0 whenever s_lo < wa + 16)
+                part |= 1u << k;
+                const uint64_t lo = A > dof ? A : dof, hi = A + 16 < dend ? A + 16 : dend;
+                const int64_t s_lo = (int64_t)so + (int64_t)(lo - dof);
+                const int64_t s_hi = (int64_t)so + (int64_t)(hi - 1 - dof);
+                if (s_lo < wa + 16) a[k] = ld16(src + wa);
+                if (s_hi >= wa + 16) e[k] = ld16(src + wa + 16);
             }
         }
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
+        for (int k = 0; k < (int)kPieceK; ++k) {
             const uint4 nb = from_next_lane(a[k], e[k]);     // every lane: DPP needs the full wave
-            const uint64_t c = base + uint64_t(k) * kThreads + threadIdx.x;
+            const uint64_t c = pb + uint64_t(k) * kThreads + threadIdx.x;
             const uint64_t A = c0 + 16 * c;
-            if (full[k]) {
+            if ((full >> k) & 1u) {
                 uint4 o = ph ? funnel16(a[k], (own_b >> k) & 1u ? e[k] : nb, ph) : a[k];
                 xor4(o, rotr8(key, (uint32_t)((A - dof) & 3u)));
                 st16(dst + A, o);
-            } else if (c < nchunks) {
-                for (uint32_t j = 0; j < 16; ++j) {
-                    const uint64_t x = A + j;
-                    if (x < dof || x >= dend) continue;
-                    const uint64_t kk = x - dof;
-                    dst[x] = (uint8_t)(src[so + kk] ^ (key >> (8 * (kk & 3u))));
-                }
+            } else if ((part >> k) & 1u) {
+                uint4 o = ph ? funnel16(a[k], e[k], ph) : a[k];
+                xor4(o, rotr8(key, (uint32_t)((A - dof) & 3u)));
+                const uint32_t jb = A < dof ? (uint32_t)(dof - A) : 0u;
+                const uint32_t je = A + 16 <= dend ? 16u : (uint32_t)(dend - A);
+                const uint32_t ow[4] = {o.x, o.y, o.z, o.w};
+#pragma unroll
+                for (uint32_t j = 0; j < 16; ++j)
+                    if (j >= jb && j < je) dst[A + j] = (uint8_t)(ow[j >> 2] >> (8 * (j & 3u)));
             }
         }
     }
@@ -180,6 +203,27 @@ xor_mask_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, uint
         for (uint64_t i = tid; i < n; i += stride)
             dst[i] = src[i] ^ (uint8_t)(kr >> (8 * (i & 3)));
     }
+}
+
+// A plain streaming device-to-device copy: the practical HBM ceiling the
+// bench reports the codec against (copy_ceiling). The best bare-copy shape of
+// tools/copy_probe.hip (profiles/r01_copy_probe.jsonl): `nt` loads and
+// stores, 2 KiB per wave (2 x 16 B per lane), 4 workgroups per CU (an LDS
+// reservation of 40,000 B), one chunk per lane per slot, no grid-stride.
+constexpr uint32_t kCopyU = 2;
+
+__global__ void __launch_bounds__(kThreads)
+stream_copy_kernel(const u32x4* __restrict__ src, u32x4* __restrict__ dst, uint64_t n16)
+{
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t base = (uint64_t(blockIdx.x) * kWaves + wave) * (kCopyU * 64) + (threadIdx.x & 63u);
+    u32x4 a[kCopyU];
+#pragma unroll
+    for (uint32_t u = 0; u < kCopyU; ++u)
+        if (base + u * 64 < n16) a[u] = __builtin_nontemporal_load(src + base + u * 64);
+#pragma unroll
+    for (uint32_t u = 0; u < kCopyU; ++u)
+        if (base + u * 64 < n16) __builtin_nontemporal_store(a[u], dst + base + u * 64);
 }
 
 __device__ __forceinline__ uint64_t splitmix64(uint64_t seed, uint64_t i)
@@ -578,7 +622,9 @@ int cfws_parse_headers(const void* d_wire, uint64_t wire_size, const uint64_t* d
 namespace {
 
 // Pieces per frame for the split payload ops: enough workgroups to cover the
-// largest frame in one pass, capped so the grid stays under 2^31 blocks.
+// largest frame (max_payload_size, at any alignment) in pieces of at most
+// kPieceChunks chunks, capped so the grid stays under 2^31 blocks (the
+// kernel then strides over a frame's pieces).
 uint32_t payload_pieces(size_t n, uint64_t max_payload_size)
 {
     const uint64_t chunks = max_payload_size / 16 + 2;
@@ -635,6 +681,22 @@ int cfws_xor_mask(const void* d_src, void* d_dst, uint64_t n, uint32_t key, uint
     xor_mask_kernel<<<g, kThreads, 0, static_cast<hipStream_t>(stream)>>>(
         static_cast<const uint8_t*>(d_src), static_cast<uint8_t*>(d_dst), n, key, phase & 3u);
     return launch_check("xor_mask");
+}
+
+int cfws_device_copy(const void* d_src, void* d_dst, uint64_t n, void* stream)
+{
+    if (int rc = check_init()) return rc;
+    if (n == 0) return CFWS_OK;
+    if (misaligned(d_src, d_dst) || (n & 15u))
+        return set_err(CFWS_ERROR_INVALID_ARGUMENT, "copy needs 16-byte aligned pointers and size",
+                       hipSuccess);
+    const uint64_t n16 = n / 16;
+    const uint64_t per_block = uint64_t(kWaves) * kCopyU * 64;
+    const uint64_t blocks = (n16 + per_block - 1) / per_block;
+    if (blocks > 0x7fffffffull) return set_err(CFWS_ERROR_INVALID_ARGUMENT, "copy too large", hipSuccess);
+    stream_copy_kernel<<<(uint32_t)blocks, kThreads, 40000, static_cast<hipStream_t>(stream)>>>(
+        static_cast<const u32x4*>(d_src), static_cast<u32x4*>(d_dst), n16);
+    return launch_check("device_copy");
 }
 
 int cfws_fill_splitmix(void* d_dst, uint64_t n, uint64_t seed, uint64_t byte_base, void* stream)

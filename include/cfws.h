@@ -417,6 +417,12 @@ void cfws_release_thread_resources(void);
 int cfws_bind_thread_device(int device);
 int cfws_thread_device(void);
 
+/* ---- streaming device copy ------------------------------------------------
+ * d_dst[i] = d_src[i], i < n: a bare HBM stream (the bench's copy ceiling,
+ * the read + write shape of the codec without its frames). Pointers and n
+ * multiples of 16. */
+int cfws_device_copy(const void* d_src, void* d_dst, uint64_t n, void* stream);
+
 /* ---- synthetic input (bench / tests) -------------------------------------
  * d_dst[i] = byte ((byte_base + i) % 8) of splitmix64 output number
  * (byte_base + i) / 8 for `seed`; byte_base must be a multiple of 8. */

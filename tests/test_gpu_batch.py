@@ -383,3 +383,17 @@ def test_plans_over_two_block_sum_steps():
     wire, total = check_serialize(payload, desc)
     offs, _ = W.wire_layout(desc)
     check_deserialize(wire[:total].copy(), offs, align=1)
+
+
+def test_device_copy():
+    """cfws_device_copy (the bench's copy ceiling) copies exactly, including
+    sizes that end inside a wave's or a workgroup's span, and refuses
+    misaligned arguments."""
+    for n in (16, 1024, 2048 + 16, 4096 * 7 + 48, (8 << 20) + 16):
+        src = torch.randint(0, 256, (n + 16,), dtype=torch.uint8, device="cuda")
+        dst = torch.zeros(n + 16, dtype=torch.uint8, device="cuda")
+        cfws.device_copy(src, dst, n)
+        torch.cuda.synchronize()
+        assert torch.equal(dst[:n], src[:n]) and int(dst[n:].sum()) == 0, n
+    with pytest.raises(cfws.CodecError):
+        cfws.device_copy(src, dst, 15)
