@@ -226,6 +226,71 @@ stream_copy_kernel(const u32x4* __restrict__ src, u32x4* __restrict__ dst, uint6
         if (base + u * 64 < n16) __builtin_nontemporal_store(a[u], dst + base + u * 64);
 }
 
+// The drop-in's frame service (cfws_internal.h): the XOR of a masked frame
+// (co_ws_frame.c:93-97 / :234-242) without a launch per frame. One
+// workgroup; thread 0 polls the request word with system-scope loads
+// (s_sleep between polls), the workgroup XORs the frame in place in the
+// mapped host buffer (16-byte chunks, 4 per thread in flight; the buffer is
+// 16-byte aligned), every thread releases its stores at system scope, then
+// thread 0 publishes the seq in the done word. Exit: the stop word, or
+// idle_ticks without a request.
+__global__ void __launch_bounds__(kThreads)
+dropin_service_kernel(uint64_t* mbox, uint8_t* buf, uint64_t idle_ticks, uint32_t last_seq)
+{
+    __shared__ uint64_t s_req;
+    __shared__ uint32_t s_exit;
+    uint32_t last = last_seq & 0xffffu;
+    for (;;) {
+        if (threadIdx.x == 0) {
+            const uint64_t t0 = (uint64_t)wall_clock64();
+            uint32_t ex = 1;
+            uint64_t w = 0;
+            for (;;) {
+                w = __hip_atomic_load(&mbox[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                if ((uint32_t)(w >> 48) != last) {
+                    ex = 0;
+                    break;
+                }
+                if (__hip_atomic_load(&mbox[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0) break;
+                if ((uint64_t)wall_clock64() - t0 > idle_ticks) break;
+                __builtin_amdgcn_s_sleep(2);
+            }
+            s_req = w;
+            s_exit = ex;
+        }
+        __syncthreads();
+        if (s_exit) break;
+        const uint64_t w = s_req;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");   // the frame's bytes, written by the host
+        const uint32_t key = (uint32_t)w;
+        const uint32_t n = (uint32_t)((w >> 32) & 0xffffu) + 1u;
+        const uint32_t nv = n / 16;
+        for (uint32_t c0 = 0; c0 < nv; c0 += 4 * kThreads) {
+            u32x4 v[4];
+#pragma unroll
+            for (uint32_t k = 0; k < 4; ++k) {
+                const uint32_t c = c0 + k * kThreads + threadIdx.x;
+                if (c < nv) v[k] = reinterpret_cast<const u32x4*>(buf)[c];
+            }
+#pragma unroll
+            for (uint32_t k = 0; k < 4; ++k) {
+                const uint32_t c = c0 + k * kThreads + threadIdx.x;
+                if (c < nv) reinterpret_cast<u32x4*>(buf)[c] = v[k] ^ key;    // chunk starts at 16c: phase 0
+            }
+        }
+        if (threadIdx.x < n - nv * 16) {
+            const uint32_t i = nv * 16 + threadIdx.x;
+            buf[i] = (uint8_t)(buf[i] ^ (key >> (8 * (i & 3u))));
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");   // this thread's stores, before the done word
+        __syncthreads();
+        last = (uint32_t)(w >> 48);
+        if (threadIdx.x == 0) __hip_atomic_store(&mbox[1], (uint64_t)last << 48, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_SYSTEM);
+        __syncthreads();                                   // s_req / s_exit are rewritten next round
+    }
+}
+
 __device__ __forceinline__ uint64_t splitmix64(uint64_t seed, uint64_t i)
 {
     uint64_t z = seed + (i + 1) * 0x9E3779B97F4A7C15ull;
@@ -681,6 +746,14 @@ int cfws_xor_mask(const void* d_src, void* d_dst, uint64_t n, uint32_t key, uint
     xor_mask_kernel<<<g, kThreads, 0, static_cast<hipStream_t>(stream)>>>(
         static_cast<const uint8_t*>(d_src), static_cast<uint8_t*>(d_dst), n, key, phase & 3u);
     return launch_check("xor_mask");
+}
+
+int cfws_internal_service_launch(uint64_t* dev_mbox, uint8_t* dev_buf, uint64_t idle_ticks, uint32_t last_seq,
+                                 void* stream)
+{
+    dropin_service_kernel<<<1, kThreads, 0, static_cast<hipStream_t>(stream)>>>(dev_mbox, dev_buf, idle_ticks,
+                                                                              last_seq);
+    return launch_check("dropin_service");
 }
 
 int cfws_device_copy(const void* d_src, void* d_dst, uint64_t n, void* stream)

@@ -27,12 +27,28 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr uint32_t kRegion = 4096;
 
-template <int kMode, int kAux>   // kMode 0 none, 1 split, 2 whole; kAux store policy (0 = global nt)
+// kMode 0 none, 1 split, 2 whole (one lane, four stores), 3 whole4 (four
+// adjacent lanes, one store instruction per segment), 4 skip (the region
+// wave leaves the chunk out and nobody writes it: the region side of the
+// partial segments alone); kAux store policy of
+// the region stores (0 = global nt)
+template <int kMode, int kAux>
 __global__ void __launch_bounds__(256) probe_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
                                                     uint64_t bytes, uint32_t P, uint32_t edge_blocks)
 {
     extern __shared__ uint8_t lds_pad[];
     (void)lds_pad;
+    if (kMode == 3 && blockIdx.x < edge_blocks) {
+        // four lanes per edge segment, one 16-byte chunk each
+        const uint64_t t = uint64_t(blockIdx.x) * 256 + threadIdx.x;
+        const uint64_t s = (t >> 2) * P;
+        if (s * 64 >= bytes) return;
+        const uint64_t off = s * 64 + (t & 3) * 16;
+        u32x4 v = *reinterpret_cast<const u32x4*>(src + off);
+        v ^= 0x9e3779b9u;
+        __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(dst + off));
+        return;
+    }
     if (blockIdx.x < edge_blocks) {
         // one thread per edge segment (segments s with s % P == 0)
         const uint64_t e = uint64_t(blockIdx.x) * 256 + threadIdx.x;
@@ -58,7 +74,7 @@ __global__ void __launch_bounds__(256) probe_kernel(const uint8_t* __restrict__ 
     for (int u = 0; u < 4; ++u) {
         const uint64_t off = base + u * 1024 + lane * 16;
         const uint64_t s = off >> 6;
-        const bool edge = kMode != 0 && (s % P) == 0 && (kMode == 2 || (off & 63) == 0);
+        const bool edge = kMode != 0 && (s % P) == 0 && ((kMode == 2 || kMode == 3) || (off & 63) == 0);
         if (edge) continue;
         a[u] ^= 0x9e3779b9u;
         if (kAux == 0) {
@@ -77,7 +93,7 @@ double run(const uint8_t* src, uint8_t* dst, uint64_t bytes, uint32_t P, int lds
     CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     const uint64_t regions = bytes / kRegion;
     const uint32_t body_blocks = (uint32_t)((regions + 3) / 4);
-    const uint64_t edges = kMode ? (bytes / 64 + P - 1) / P : 0;
+    const uint64_t edges = (kMode && kMode != 4) ? (bytes / 64 + P - 1) / P * (kMode == 3 ? 4 : 1) : 0;
     const uint32_t edge_blocks = (uint32_t)((edges + 255) / 256);
     hipEvent_t a, b;
     CHECK(hipEventCreate(&a));
@@ -116,6 +132,12 @@ int main(int argc, char** argv)
                    run<1, 0>(src, dst, bytes, P, lds));
             printf("{\"mode\": \"whole\", \"aux\": \"nt\", \"P\": %u, \"TBps\": %.3f}\n", P,
                    run<2, 0>(src, dst, bytes, P, lds));
+            printf("{\"mode\": \"whole4\", \"aux\": \"nt\", \"P\": %u, \"TBps\": %.3f}\n", P,
+                   run<3, 0>(src, dst, bytes, P, lds));
+            printf("{\"mode\": \"whole4\", \"aux\": \"wt\", \"P\": %u, \"TBps\": %.3f}\n", P,
+                   run<3, 19>(src, dst, bytes, P, lds));
+            printf("{\"mode\": \"skip\", \"aux\": \"nt\", \"P\": %u, \"TBps\": %.3f}\n", P,
+                   run<4, 0>(src, dst, bytes, P, lds));
             printf("{\"mode\": \"split\", \"aux\": \"wt\", \"P\": %u, \"TBps\": %.3f}\n", P,
                    run<1, 19>(src, dst, bytes, P, lds));
             printf("{\"mode\": \"whole\", \"aux\": \"wt\", \"P\": %u, \"TBps\": %.3f}\n", P,

@@ -26,6 +26,7 @@ pmc() {  # name workload-args... ; counters in $C
 for s in "$@"; do
   case $s in
     pytest) step pytest 900 python3 -u -m pytest $R/tests -m gpu -x -v --timeout 300 --timeout-method thread ;;
+    pytest_sub) step pytest_sub 900 python3 -u -m pytest $(for f in $TESTS; do echo $R/tests/$f; done) -m gpu -x -v --timeout 300 --timeout-method thread ;;
     bench) step bench 400 python3 $R/bench.py ;;
     split) step split 200 python3 $R/bench.py --workload split --no-cpu-baseline ;;
     c5) step c5 200 python3 $R/bench.py --workload config5 --no-cpu-baseline ;;
