@@ -580,41 +580,6 @@ __device__ __forceinline__ void store_chunk(const Pass& P, uint64_t D, uint4 o)
     }
 }
 
-// Write ownership granule per mode. The send modes (serialize, the fused
-// HTTP/2 send) own output in 64-byte segments: a region wave writes a chunk
-// only when its whole 64-byte segment lies inside one frame's body, and the
-// edge threads write every other segment whole, four adjacent lanes to a
-// segment in one store instruction. A segment written part by a region wave
-// and part, at another time, by an edge thread leaves HBM two partial
-// writes: tools/partial_probe.hip measured a copy with one such segment in
-// 16 at 4.84 TB/s against 5.43 with those segments written whole by four
-// lanes (6.0 with none; one in 100, config 5's send: 5.86 against 6.01),
-// and TCC_EA0_WRREQ - TCC_EA0_WRREQ_64B counted 163 k partial writes per
-// config-5 send launch, none on the receive. The other modes keep 16-byte
-// granules (their payload slots are 16-aligned: few edges).
-__host__ __device__ constexpr uint32_t seg_bytes(int mode)
-{
-    return (mode == kModeSer || mode == kModeH2Ser) ? 64u : 16u;
-}
-
-// Is the granule holding position r (relative to a 16-aligned base; r a
-// multiple of 16) inside [lo, hi)?
-template <int kMode>
-__device__ __forceinline__ bool granule_inside(uint32_t r, uint32_t lo, uint32_t hi)
-{
-    constexpr uint32_t g = seg_bytes(kMode);
-    const uint32_t s = r & ~(g - 1u);
-    return s >= lo && s + g <= hi;
-}
-
-template <int kMode>
-__device__ __forceinline__ bool granule_inside_abs(uint64_t D, uint64_t lo, uint64_t hi)
-{
-    constexpr uint64_t g = seg_bytes(kMode);
-    const uint64_t s = D & ~(g - 1u);
-    return s >= lo && s + g <= hi;
-}
-
 // ---------------------------------------------------------------------------
 // the streaming kernel
 // ---------------------------------------------------------------------------
@@ -697,10 +662,10 @@ __device__ __forceinline__ void two_frame_region(const Pass& P, const FrameView&
         const uint32_t r = u * (uint32_t)kSlice + lane * (uint32_t)kChunk;
         hi[u] = r >= ob;
         const uint32_t lo_ = hi[u] ? b_lo : a_lo, hi_ = hi[u] ? b_hi : a_hi;
-        fast[u] = granule_inside<kMode>(r, lo_, hi_);
+        fast[u] = r >= lo_ && r + 16 <= hi_;
         // the next lane's chunk loads block sp + 16 iff it is in the same
-        // frame and written here (its granule inside the body)
-        const bool next_loads = lane != 63 && (r + 16 >= ob) == hi[u] && granule_inside<kMode>(r + 16, lo_, hi_);
+        // frame and inside the body
+        const bool next_loads = lane != 63 && (r + 16 >= ob) == hi[u] && r + 32 <= hi_;
         own[u] = fast[u] && (hi[u] ? phB : phA) != 0 && !next_loads;
         sp[u] = P.src + (((hi[u] ? sB : sA) + r) & ~uint64_t(15));
     }
@@ -743,7 +708,7 @@ __device__ __forceinline__ void general_region_search(const Pass& P, uint32_t f0
     for (int u = 0; u < kUnroll; ++u) {
         const uint64_t D = base + u * kSlice + lane * kChunk;
         const FrameView v = frame_view<kMode>(P, fr[u]);
-        if (granule_inside_abs<kMode>(D, v.body_start, v.body_start + v.body_len))
+        if (D >= v.body_start && D + kChunk <= v.body_start + v.body_len)
             st16_region<kMode>(P.dst + base, (uint32_t)(D - base), body_chunk(P.src, v, D));
     }
 }
@@ -794,7 +759,7 @@ __device__ __forceinline__ void general_region(const Pass& P, uint32_t f0, uint3
         const uint64_t d = (uint64_t)(uint32_t)__shfl((int)dlo, (int)j, 64) |
                            (uint64_t)(uint32_t)__shfl((int)dhi, (int)j, 64) << 32;
         key[u] = (uint32_t)__shfl((int)kr, (int)j, 64);
-        fast[u] = granule_inside<kMode>(r, rg & 0xffffu, rg >> 16);
+        fast[u] = r >= (rg & 0xffffu) && r + kChunk <= (rg >> 16);
         const uint64_t s = base + r + d;
         ph[u] = (uint32_t)(s & 15u);
         sp[u] = P.src + (s & ~uint64_t(15));
@@ -832,7 +797,7 @@ __device__ __forceinline__ void tail_region(const Pass& P, uint32_t f0, uint32_t
             if (P.offs[mid] <= D) lo = mid; else hi = mid - 1;
         }
         const FrameView v = frame_view<kMode>(P, lo);
-        if (granule_inside_abs<kMode>(D, v.body_start, v.body_start + v.body_len))
+        if (D >= v.body_start && D + kChunk <= v.body_start + v.body_len)
             store_chunk(P, D, body_chunk(P.src, v, D));
     }
 }
@@ -858,13 +823,6 @@ __host__ __device__ constexpr uint64_t edge_threads(uint64_t n) { return (n + 63
 __device__ __forceinline__ uint64_t edge_thread_frame(uint64_t t) { return (t >> 7) * 64 + (t & 63); }
 
 __device__ __forceinline__ uint32_t edge_thread_part(uint64_t t) { return (uint32_t)(t >> 6) & 1u; }
-
-// 64-byte granule modes: four adjacent threads per frame, one per chunk of
-// each edge segment (edge_frame_seg).
-__host__ __device__ constexpr uint64_t edge_threads_of(int mode, uint64_t n)
-{
-    return seg_bytes(mode) == 64 ? (n + 15) / 16 * 64 : edge_threads(n);
-}
 
 // The edge chunks of frame f in pass P (part 0: before the body; part 1:
 // reaching past the body end).
@@ -905,44 +863,6 @@ __device__ __forceinline__ void edge_frame(const Pass& P, uint64_t f, uint32_t p
     }
 }
 
-// The edge segments of frame f in a 64-byte-granule pass, chunk c (0-3) of
-// each: the segments whose first byte lies in f's output range
-// [out_off, next frame's out_off) and that are not wholly inside f's body --
-// the one holding its header start when it starts there, and from the
-// segment holding its body end on (the boundary into the next frame, whose
-// header it may hold, and the pass end). Every other 64-byte segment lies
-// inside one body and is a region wave's. Chunks are assembled by
-// edge_chunk from at most two frames (byte by byte across runs of frames
-// shorter than 16 bytes).
-template <int kMode>
-__device__ __forceinline__ void edge_frame_seg(const Pass& P, uint64_t f, uint32_t c)
-{
-    const uint32_t n = P.n_frames;
-    const uint32_t fa = (uint32_t)f, fb = fa + 1 < n ? fa + 1 : fa;
-    const FrameView va = frame_view<kMode>(P, fa);
-    const FrameView vb = frame_view<kMode>(P, fb);
-    const uint64_t o2 = fa + 2 < n ? P.offs[fa + 2] : ~uint64_t(0);
-    const uint64_t o1 = fa + 1 < n ? vb.out_off : ~uint64_t(0);
-    uint64_t own = fa + 1 < n ? vb.out_off : P.total;
-    if (own > P.total) own = P.total;
-    if (va.out_off >= own) return;
-    const uint64_t a = (va.out_off + 63) & ~uint64_t(63);
-    const uint64_t b = (own + 63) & ~uint64_t(63);
-    const uint64_t bs = va.body_start, be = bs + va.body_len;
-    const uint64_t head_end = b < bs ? b : bs;
-    uint64_t t0 = (bs + 63) & ~uint64_t(63);
-    if (t0 < a) t0 = a;
-    if (t0 < (be & ~uint64_t(63))) t0 = be & ~uint64_t(63);
-    // head segments [a, head_end), then tail segments [t0, b); t0 >= head_end
-    uint64_t S = a < head_end ? a : t0;
-    while (S < b) {
-        const uint64_t D = S + 16u * c;
-        if (D < P.total) store_chunk(P, D, edge_chunk<kMode>(P, fa, D, va, vb, o1, o2));
-        S += 64;
-        if (S >= head_end && S < t0) S = t0;
-    }
-}
-
 template <int kMode>
 __global__ void __launch_bounds__(kEdgeThreads)
 edge_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
@@ -952,7 +872,7 @@ edge_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
             uint32_t klass, uint32_t sid, const cfws_frame_desc_t* __restrict__ parent)
 {
     const uint64_t t = uint64_t(blockIdx.x) * kEdgeThreads + threadIdx.x;
-    const uint64_t f = seg_bytes(kMode) == 64 ? t >> 2 : edge_thread_frame(t);
+    const uint64_t f = edge_thread_frame(t);
     if (f >= n_frames) return;
     const uint64_t out_base = base_p ? *base_p : 0;
     Pass P;
@@ -967,10 +887,7 @@ edge_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
     P.klass = klass;
     P.sid = sid;
     P.parent = parent;
-    if (seg_bytes(kMode) == 64)
-        edge_frame_seg<kMode>(P, f, (uint32_t)(t & 3u));
-    else
-        edge_frame<kMode>(P, f, edge_thread_part(t));
+    edge_frame<kMode>(P, f, edge_thread_part(t));
 }
 
 // Deserialize with reassembly (CFWS_DESERIALIZE_REASSEMBLE): the edge chunks
@@ -1076,11 +993,7 @@ xform_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
     P.parent = parent;
     if (has_edge_blocks(kMode) && is_edge) {
         const uint64_t t = uint64_t(eidx) * kThreads + threadIdx.x;
-        if (seg_bytes(kMode) == 64) {
-            if ((t >> 2) < n_frames) edge_frame_seg<kMode>(P, t >> 2, (uint32_t)(t & 3u));
-        } else if (edge_thread_frame(t) < n_frames) {
-            edge_frame<kMode>(P, edge_thread_frame(t), edge_thread_part(t));
-        }
+        if (edge_thread_frame(t) < n_frames) edge_frame<kMode>(P, edge_thread_frame(t), edge_thread_part(t));
         return;
     }
     const uint64_t n_regions = (P.total + kRegion - 1) / kRegion;
@@ -1624,7 +1537,7 @@ void launch_streaming(const void* src, void* dst, const cfws_frame_desc_t* desc,
                       const uint64_t* reasm_offs1 = nullptr)
 {
     const bool split = edges && (edge_split() || !has_edge_blocks(kMode));
-    const uint32_t eb = (edges && !split) ? grid_for(edge_threads_of(kMode, n), kThreads) : 0;
+    const uint32_t eb = (edges && !split) ? grid_for(edge_threads(n), kThreads) : 0;
     const uint32_t sg = stream_grid(regions);
     // edge workgroups first, or spread evenly through the grid (edge_interleave)
     const uint32_t spread = eb ? (eb + sg) / eb : 0;
@@ -1641,7 +1554,7 @@ void launch_streaming(const void* src, void* dst, const cfws_frame_desc_t* desc,
     // (a separate edge launch on a second stream, overlapping the streaming
     // kernel, measured no faster on config 5: the stream slowed by what the
     // overlap saved)
-    if (split) edge_kernel<kMode><<<grid_for(edge_threads_of(kMode, n), kEdgeThreads), kEdgeThreads, 0, st>>>(
+    if (split) edge_kernel<kMode><<<grid_for(edge_threads(n), kEdgeThreads), kEdgeThreads, 0, st>>>(
         static_cast<const uint8_t*>(src), static_cast<uint8_t*>(dst), desc, status, offs,
         total_p, base_p, cap, (uint32_t)n, klass, sid, parent);
 }
