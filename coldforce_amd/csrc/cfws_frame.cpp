@@ -18,12 +18,14 @@
 #include <string.h>
 
 #include <atomic>
+#include <chrono>
 #include <mutex>
 #include <vector>
 
 #include "cfws.h"
 #include "cfws_co_ws_frame.h"
 #include "cfws_devpolicy.h"
+#include "cfws_internal.h"
 
 namespace {
 
@@ -44,7 +46,18 @@ struct ThreadDevice {
     size_t host_cap = 0;
     bool zc_warm = false;          // first zero-copy frame done
     bool dma_warm = false;         // first DMA-path frame done
-    bool holds() const { return stream || buf || host; }
+    // the frame service (frames up to kCfwsServiceMax): a resident kernel on
+    // svc_stream polling the mailbox; both in mapped pinned host memory
+    uint64_t* mbox = nullptr;      // host address (cfws_internal.h: request, done, stop)
+    uint64_t* mbox_dev = nullptr;
+    uint8_t* svc_buf = nullptr;    // kCfwsServiceMax bytes, the frame is XORed here in place
+    uint8_t* svc_buf_dev = nullptr;
+    hipStream_t svc_stream = nullptr;
+    uint32_t seq = 0;              // last request the service finished
+    bool svc_running = false;      // a service kernel was launched and may still run
+    bool svc_warm = false;         // first service frame done
+    double svc_last = 0;           // when the last request finished (steady clock, s)
+    bool holds() const { return stream || buf || host || mbox; }
 };
 
 // Device policy and per-device resource pool: cfws_devpolicy.h. The pool is
@@ -206,6 +219,161 @@ private:
 };
 
 // dst[i] = src[i] ^ key[i % 4] for a host buffer, through the device.
+// ---- the frame service ---------------------------------------------------
+// A masked frame of at most kCfwsServiceMax bytes (64 KiB) is XORed by a
+// resident kernel (dropin_service_kernel, cfws_ops.hip): the host copies
+// the frame into a mapped pinned buffer, posts one 64-bit request word
+// (key, length, seq) and spins on the done word, which the kernel writes
+// after its stores are released to system scope. No launch, no completion
+// signal per frame: config 1's 1 KiB frames go from a launch + synchronise
+// round trip to a PCIe round trip. The kernel exits
+// by itself after an idle spell (CFWS_DROPIN_SERVICE_IDLE_US, default 2000)
+// and is relaunched on the next frame; it is only ever relaunched after
+// hipStreamQuery has seen the previous one finish, so at most one kernel
+// serves a mailbox. CFWS_DROPIN_SERVICE=0 sends every frame through the
+// launch path instead.
+bool service_enabled()
+{
+    static const bool v = [] {
+        const char* s = getenv("CFWS_DROPIN_SERVICE");
+        return !(s && *s == '0');
+    }();
+    return v;
+}
+
+double service_idle_s()
+{
+    static const double v = [] {
+        const char* s = getenv("CFWS_DROPIN_SERVICE_IDLE_US");
+        const double us = s && *s ? strtod(s, nullptr) : 2000.0;
+        return (us < 50.0 ? 50.0 : us) * 1e-6;
+    }();
+    return v;
+}
+
+double now_s()
+{
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// Every mailbox ever created, so that process exit can tell the kernels to
+// stop (a plain host store each; no HIP call at exit).
+struct MailboxRegistry {
+    std::mutex mu;
+    std::vector<uint64_t*> boxes;
+};
+
+MailboxRegistry& mailboxes()
+{
+    static MailboxRegistry* r = new MailboxRegistry;
+    return *r;
+}
+
+void stop_all_services()
+{
+    MailboxRegistry& r = mailboxes();
+    std::lock_guard<std::mutex> lock(r.mu);
+    for (uint64_t* m : r.boxes) __atomic_store_n(&m[2], uint64_t(1), __ATOMIC_RELEASE);
+}
+
+bool service_setup(ThreadDevice& t_dev, int dev)
+{
+    if (t_dev.mbox) return true;
+    CurrentDevice on(dev);
+    void* m = nullptr;
+    void* b = nullptr;
+    if (hipHostMalloc(&m, 4096, hipHostMallocMapped) != hipSuccess ||
+        hipHostMalloc(&b, kCfwsServiceMax, hipHostMallocMapped) != hipSuccess) {
+        fprintf(stderr, "cfws: frame service: hipHostMalloc failed\n");
+        if (m) (void)hipHostFree(m);
+        if (b) (void)hipHostFree(b);
+        return false;
+    }
+    void* md = nullptr;
+    void* bd = nullptr;
+    if (hipHostGetDevicePointer(&md, m, 0) != hipSuccess || hipHostGetDevicePointer(&bd, b, 0) != hipSuccess ||
+        hipStreamCreateWithFlags(&t_dev.svc_stream, hipStreamNonBlocking) != hipSuccess) {
+        fprintf(stderr, "cfws: frame service: mapping or stream failed\n");
+        (void)hipHostFree(m);
+        (void)hipHostFree(b);
+        t_dev.svc_stream = nullptr;
+        return false;
+    }
+    memset(m, 0, 4096);
+    t_dev.mbox = static_cast<uint64_t*>(m);
+    t_dev.mbox_dev = static_cast<uint64_t*>(md);
+    t_dev.svc_buf = static_cast<uint8_t*>(b);
+    t_dev.svc_buf_dev = static_cast<uint8_t*>(bd);
+    t_dev.seq = 0;
+    t_dev.svc_running = false;
+    static std::once_flag exit_hook;
+    std::call_once(exit_hook, [] { atexit(stop_all_services); });
+    MailboxRegistry& r = mailboxes();
+    std::lock_guard<std::mutex> lock(r.mu);
+    r.boxes.push_back(t_dev.mbox);
+    return true;
+}
+
+bool service_launch(ThreadDevice& t_dev, int dev)
+{
+    int rate_khz = 0;
+    if (hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess || rate_khz <= 0)
+        rate_khz = 100000;
+    const uint64_t idle_ticks = (uint64_t)(service_idle_s() * 1e3 * (double)rate_khz);
+    __atomic_store_n(&t_dev.mbox[2], uint64_t(0), __ATOMIC_RELEASE);
+    CurrentDevice on(dev);
+    if (cfws_internal_service_launch(t_dev.mbox_dev, t_dev.svc_buf_dev, idle_ticks, t_dev.seq, t_dev.svc_stream) !=
+        CFWS_OK)
+        return false;
+    t_dev.svc_running = true;
+    return true;
+}
+
+// Has the service kernel finished (idled out)? hipStreamQuery on its stream.
+bool service_finished(ThreadDevice& t_dev)
+{
+    const hipError_t e = hipStreamQuery(t_dev.svc_stream);
+    if (e == hipErrorNotReady) return false;
+    if (e != hipSuccess) fprintf(stderr, "cfws: frame service: %s\n", hipGetErrorString(e));
+    return true;
+}
+
+bool service_xor(ThreadDevice& t_dev, int dev, const uint8_t* src, uint8_t* dst, size_t n, uint32_t key)
+{
+    if (!service_setup(t_dev, dev)) return false;
+    // the kernel idles out service_idle_s() after its last request: well
+    // inside that, it is still polling; past half of it, ask the stream
+    if (t_dev.svc_running && now_s() - t_dev.svc_last > 0.5 * service_idle_s() && service_finished(t_dev))
+        t_dev.svc_running = false;
+    memcpy(t_dev.svc_buf, src, n);
+    uint32_t seq = (t_dev.seq + 1) & 0xffffu;
+    const uint64_t word = (uint64_t)key | ((uint64_t)(n - 1) << 32) | ((uint64_t)seq << 48);
+    __atomic_store_n(&t_dev.mbox[0], word, __ATOMIC_RELEASE);
+    if (!t_dev.svc_running && !service_launch(t_dev, dev)) return false;
+    const double t0 = now_s();
+    for (uint64_t spin = 1;; ++spin) {
+        if ((uint32_t)(__atomic_load_n(&t_dev.mbox[1], __ATOMIC_ACQUIRE) >> 48) == seq) break;
+        if ((spin & 1023u) == 0) {
+            const double dt = now_s() - t0;
+            if (dt > 5.0) {
+                fprintf(stderr, "cfws: frame service: no answer in 5 s\n");
+                return false;
+            }
+            // an exit that raced the request: relaunch once the old kernel
+            // has finished (never two kernels on one mailbox)
+            if (dt > 20e-6 && service_finished(t_dev) &&
+                (uint32_t)(__atomic_load_n(&t_dev.mbox[1], __ATOMIC_ACQUIRE) >> 48) != seq &&
+                !service_launch(t_dev, dev))
+                return false;
+        }
+        __builtin_ia32_pause();
+    }
+    t_dev.seq = seq;
+    t_dev.svc_last = now_s();
+    memcpy(dst, t_dev.svc_buf, n);
+    return true;
+}
+
 std::atomic<bool> g_runtime_up{false};   // the HIP runtime has been initialised by us
 
 bool device_xor(const uint8_t* src, uint8_t* dst, size_t n, uint32_t key)
@@ -221,6 +389,12 @@ bool device_xor(const uint8_t* src, uint8_t* dst, size_t n, uint32_t key)
     }
     g_runtime_up.store(true, std::memory_order_release);
     ThreadDevice& t_dev = tdev(dev);
+    if (service_enabled() && n <= kCfwsServiceMax) {
+        if (!t_dev.svc_warm) keep_random_stream.engage();
+        if (!service_xor(t_dev, dev, src, dst, n, key)) return false;
+        t_dev.svc_warm = true;
+        return true;
+    }
     const bool zero_copy = n <= zero_copy_max();
     if (!t_dev.stream || (zero_copy ? (!t_dev.zc_warm || t_dev.host_cap < n) : (!t_dev.dma_warm || t_dev.cap < n)))
         keep_random_stream.engage();
@@ -438,6 +612,23 @@ int cfws_draw_mask_keys_seeded(uint32_t seed, size_t n, const uint8_t* mask_flag
 void cfws_release_thread_resources(void)
 {
     ThreadDevice& t_dev = t_slot.current();
+    if (t_dev.mbox) {
+        __atomic_store_n(&t_dev.mbox[2], uint64_t(1), __ATOMIC_RELEASE);
+        if (t_dev.svc_stream) (void)hipStreamSynchronize(t_dev.svc_stream);
+        {
+            MailboxRegistry& r = mailboxes();
+            std::lock_guard<std::mutex> lock(r.mu);
+            for (auto& m : r.boxes)
+                if (m == t_dev.mbox) {
+                    m = r.boxes.back();
+                    r.boxes.pop_back();
+                    break;
+                }
+        }
+        (void)hipHostFree(t_dev.mbox);
+        if (t_dev.svc_buf) (void)hipHostFree(t_dev.svc_buf);
+        if (t_dev.svc_stream) (void)hipStreamDestroy(t_dev.svc_stream);
+    }
     if (t_dev.buf) (void)hipFree(t_dev.buf);
     if (t_dev.host) (void)hipHostFree(t_dev.host);
     if (t_dev.stream) (void)hipStreamDestroy(t_dev.stream);

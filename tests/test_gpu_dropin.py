@@ -120,7 +120,7 @@ def _fnv1a(b: bytes) -> int:
     return h
 
 
-@pytest.mark.parametrize("zc_max", [None, "0", "1000"])
+@pytest.mark.parametrize("zc_max", [None, "0", "1000", "service_off"])
 def test_link_level_dropin_harness(zc_max):
     """oracle/_ref/dropin_link: a C program built against coldforce's own
     headers (co_ws_frame.h, co_ws_config.h, co_byte_array.h) and the
@@ -136,7 +136,10 @@ def test_link_level_dropin_harness(zc_max):
         pytest.skip("oracle/_ref/dropin_link not built (built where /root/reference exists)")
     env = dict(os.environ)
     env.pop("CFWS_DROPIN_ZC_MAX", None)
-    if zc_max is not None:
+    env.pop("CFWS_DROPIN_SERVICE", None)
+    if zc_max == "service_off":
+        env["CFWS_DROPIN_SERVICE"] = "0"          # every frame through the launch path
+    elif zc_max is not None:
         env["CFWS_DROPIN_ZC_MAX"] = zc_max
     r = subprocess.run([exe, "77"], capture_output=True, text=True, timeout=120, env=env)
     assert r.returncode == 0, r.stdout + r.stderr
@@ -258,3 +261,34 @@ def test_device_policy_spreads_over_gpus():
     for t in ts:
         t.join()
     assert not errors, errors
+
+
+def test_frame_service_idle_relaunch_and_seq_wrap():
+    """The frame service (frames <= 64 KiB, cfws_frame.cpp): frames spaced
+    wider than the service's idle timeout each find the kernel gone and
+    relaunch it; 70,000 back-to-back frames wrap the 16-bit request
+    sequence; sizes around the 16-byte chunk and the 64 KiB limit."""
+    import time
+    L = O.lib()
+    rng = random.Random(9)
+    cases = []
+    for n in (1, 15, 16, 17, 1023, 1024, 1025, 65535, 65536, 65537):
+        data = rng.randbytes(n)
+        O.srandom(L, n)
+        cases.append((O.ref_serialize(L, True, 1, True, data), data))
+    for w, data in cases:
+        assert cfws.frame_deserialize(w)["payload"] == data + b"\0"
+        time.sleep(0.006)                      # > CFWS_DROPIN_SERVICE_IDLE_US (2 ms)
+    w, data = cases[1]
+    for k in range(70_000):
+        r = cfws.frame_deserialize(w)
+        if k % 5000 == 0 or k > 65_530:
+            assert r["payload"] == data + b"\0", k
+    # and the serialize side, against the reference's wire for the same keys
+    import ctypes
+    libc = ctypes.CDLL(None)
+    for w, data in cases[:6]:
+        libc.srandom(77)
+        ok, got = cfws.frame_serialize(True, 2, True, data)
+        O.srandom(L, 77)
+        assert ok and got == O.ref_serialize(L, True, 2, True, data)
