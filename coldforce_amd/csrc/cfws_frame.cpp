@@ -241,6 +241,18 @@ bool service_enabled()
     return v;
 }
 
+// Largest frame the service takes (CFWS_DROPIN_SERVICE_MAX, at most
+// kCfwsServiceMax); larger frames take the launch path.
+size_t service_max()
+{
+    static const size_t v = [] {
+        const char* s = getenv("CFWS_DROPIN_SERVICE_MAX");
+        const size_t x = s && *s ? (size_t)strtoull(s, nullptr, 10) : (size_t)kCfwsServiceMax;
+        return x < (size_t)kCfwsServiceMax ? x : (size_t)kCfwsServiceMax;
+    }();
+    return v;
+}
+
 double service_idle_s()
 {
     static const double v = [] {
@@ -389,7 +401,7 @@ bool device_xor(const uint8_t* src, uint8_t* dst, size_t n, uint32_t key)
     }
     g_runtime_up.store(true, std::memory_order_release);
     ThreadDevice& t_dev = tdev(dev);
-    if (service_enabled() && n <= kCfwsServiceMax) {
+    if (service_enabled() && n <= service_max()) {
         if (!t_dev.svc_warm) keep_random_stream.engage();
         if (!service_xor(t_dev, dev, src, dst, n, key)) return false;
         t_dev.svc_warm = true;

@@ -228,13 +228,17 @@ stream_copy_kernel(const u32x4* __restrict__ src, u32x4* __restrict__ dst, uint6
 
 // The drop-in's frame service (cfws_internal.h): the XOR of a masked frame
 // (co_ws_frame.c:93-97 / :234-242) without a launch per frame. One
-// workgroup; thread 0 polls the request word with system-scope loads
-// (s_sleep between polls), the workgroup XORs the frame in place in the
-// mapped host buffer (16-byte chunks, 4 per thread in flight; the buffer is
-// 16-byte aligned), every thread releases its stores at system scope, then
+// workgroup of 1,024 threads; thread 0 polls the request word with
+// system-scope loads (s_sleep between polls), the workgroup XORs the frame
+// in place in the mapped host buffer (16-byte chunks, all of a 64 KiB frame
+// in flight at once; the buffer is 16-byte aligned: 4 KiB frames took one
+// round with 256 threads, 64 KiB four, 27 us), every thread releases its
+// stores at system scope, then
 // thread 0 publishes the seq in the done word. Exit: the stop word, or
 // idle_ticks without a request.
-__global__ void __launch_bounds__(kThreads)
+constexpr uint32_t kServiceThreads = 1024;         // 16 KiB per round of loads
+
+__global__ void __launch_bounds__(kServiceThreads)
 dropin_service_kernel(uint64_t* mbox, uint8_t* buf, uint64_t idle_ticks, uint32_t last_seq)
 {
     __shared__ uint64_t s_req;
@@ -265,18 +269,18 @@ dropin_service_kernel(uint64_t* mbox, uint8_t* buf, uint64_t idle_ticks, uint32_
         const uint32_t key = (uint32_t)w;
         const uint32_t n = (uint32_t)((w >> 32) & 0xffffu) + 1u;
         const uint32_t nv = n / 16;
-        for (uint32_t c0 = 0; c0 < nv; c0 += 4 * kThreads) {
-            u32x4 v[4];
+        // every load of the frame in flight at once (64 KiB = 4 per thread):
+        // each is a PCIe round trip
+        u32x4 v[4];
 #pragma unroll
-            for (uint32_t k = 0; k < 4; ++k) {
-                const uint32_t c = c0 + k * kThreads + threadIdx.x;
-                if (c < nv) v[k] = reinterpret_cast<const u32x4*>(buf)[c];
-            }
+        for (uint32_t k = 0; k < 4; ++k) {
+            const uint32_t c = k * kServiceThreads + threadIdx.x;
+            if (c < nv) v[k] = reinterpret_cast<const u32x4*>(buf)[c];
+        }
 #pragma unroll
-            for (uint32_t k = 0; k < 4; ++k) {
-                const uint32_t c = c0 + k * kThreads + threadIdx.x;
-                if (c < nv) reinterpret_cast<u32x4*>(buf)[c] = v[k] ^ key;    // chunk starts at 16c: phase 0
-            }
+        for (uint32_t k = 0; k < 4; ++k) {
+            const uint32_t c = k * kServiceThreads + threadIdx.x;
+            if (c < nv) reinterpret_cast<u32x4*>(buf)[c] = v[k] ^ key;    // chunk starts at 16c: phase 0
         }
         if (threadIdx.x < n - nv * 16) {
             const uint32_t i = nv * 16 + threadIdx.x;
@@ -751,8 +755,9 @@ int cfws_xor_mask(const void* d_src, void* d_dst, uint64_t n, uint32_t key, uint
 int cfws_internal_service_launch(uint64_t* dev_mbox, uint8_t* dev_buf, uint64_t idle_ticks, uint32_t last_seq,
                                  void* stream)
 {
-    dropin_service_kernel<<<1, kThreads, 0, static_cast<hipStream_t>(stream)>>>(dev_mbox, dev_buf, idle_ticks,
-                                                                              last_seq);
+    static_assert(4 * kServiceThreads * 16 >= kCfwsServiceMax, "one round of loads covers a frame");
+    dropin_service_kernel<<<1, kServiceThreads, 0, static_cast<hipStream_t>(stream)>>>(dev_mbox, dev_buf,
+                                                                                     idle_ticks, last_seq);
     return launch_check("dropin_service");
 }
 
