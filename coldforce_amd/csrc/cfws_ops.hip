@@ -265,28 +265,35 @@ dropin_service_kernel(uint64_t* mbox, uint8_t* buf, uint64_t idle_ticks, uint32_
         __syncthreads();
         if (s_exit) break;
         const uint64_t w = s_req;
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");   // the frame's bytes, written by the host
         const uint32_t key = (uint32_t)w;
         const uint32_t n = (uint32_t)((w >> 32) & 0xffffu) + 1u;
         const uint32_t nv = n / 16;
-        // every load of the frame in flight at once (64 KiB = 4 per thread):
-        // each is a PCIe round trip
-        u32x4 v[4];
+        // wave w takes chunks [256 w, 256 w + 256) (4 KiB, 4 per lane), all
+        // of them in flight at once (each load is a PCIe round trip); waves
+        // past the frame skip the work and the fence, so a 1 KiB frame costs
+        // one wave's release, not sixteen
+        const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+        const uint32_t c0 = wv * 256u;
+        if (c0 < nv || (c0 == nv && n > nv * 16)) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");   // the frame's bytes, written by the host
+            u32x4 v[4];
 #pragma unroll
-        for (uint32_t k = 0; k < 4; ++k) {
-            const uint32_t c = k * kServiceThreads + threadIdx.x;
-            if (c < nv) v[k] = reinterpret_cast<const u32x4*>(buf)[c];
-        }
+            for (uint32_t k = 0; k < 4; ++k) {
+                const uint32_t c = c0 + k * 64 + lane;
+                if (c < nv) v[k] = reinterpret_cast<const u32x4*>(buf)[c];
+            }
 #pragma unroll
-        for (uint32_t k = 0; k < 4; ++k) {
-            const uint32_t c = k * kServiceThreads + threadIdx.x;
-            if (c < nv) reinterpret_cast<u32x4*>(buf)[c] = v[k] ^ key;    // chunk starts at 16c: phase 0
+            for (uint32_t k = 0; k < 4; ++k) {
+                const uint32_t c = c0 + k * 64 + lane;
+                if (c < nv) reinterpret_cast<u32x4*>(buf)[c] = v[k] ^ key;    // chunk at 16c: phase 0
+            }
+            // the tail bytes, by the wave whose span holds them
+            if (nv / 256 == wv && lane < n - nv * 16) {
+                const uint32_t i = nv * 16 + lane;
+                buf[i] = (uint8_t)(buf[i] ^ (key >> (8 * (i & 3u))));
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");   // this wave's stores, before the done word
         }
-        if (threadIdx.x < n - nv * 16) {
-            const uint32_t i = nv * 16 + threadIdx.x;
-            buf[i] = (uint8_t)(buf[i] ^ (key >> (8 * (i & 3u))));
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");   // this thread's stores, before the done word
         __syncthreads();
         last = (uint32_t)(w >> 48);
         if (threadIdx.x == 0) __hip_atomic_store(&mbox[1], (uint64_t)last << 48, __ATOMIC_RELAXED,
