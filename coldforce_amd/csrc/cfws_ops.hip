@@ -46,18 +46,24 @@ parse_headers_kernel(const uint8_t* __restrict__ wire, uint64_t size, const uint
 }
 
 // The payload loops (mask: co_ws_frame.c:93-97, unmask: :232-242) of every
-// frame, each frame from its own source to its own destination. Work unit
-// (frame, piece): a frame's 16-byte destination chunks are split evenly over
-// the fewest pieces of at most 1,280 chunks (5 per lane, every load in flight
-// before the first store), so a 64 KiB frame at any alignment (4,097
-// chunks) is 4 equal workgroups, not 4 full ones and a near-empty fifth.
-// Chunks inside the frame are one 16-byte store (source funnel-shifted into
-// place; a lane's second source block comes from the next lane over DPP).
-// The frame's first and last chunk, which it may share with its
-// neighbours, are assembled the same way from the (at most two) source
-// blocks holding their bytes and stored byte by byte from registers.
+// frame, each frame from its own source to its own destination. A wave
+// writes one 1 KiB-aligned span of the destination per store instruction
+// (64 lanes x 16 B), as the streaming kernel's regions do, so interior
+// 64-byte segments are always written whole by one instruction (a span
+// grid starting at the frame's first chunk left every instruction's first
+// and last segment half-written: 5.6 / 5.9 TB/s against the streaming
+// kernel's 6.5). Work unit (frame, piece): the frame's spans are split
+// evenly over the fewest pieces of at most 20 spans (4 waves x 5 slots,
+// every load in flight before the first store), so a 64 KiB frame is 4
+// equal workgroups at any alignment. Chunks inside the frame are one
+// 16-byte store (source funnel-shifted into place; a lane's second source
+// block comes from the next lane over DPP). The frame's first and last
+// chunk, which it may share with its neighbours, are assembled the same way
+// from the (at most two) source blocks holding their bytes and stored byte
+// by byte from registers.
 constexpr uint32_t kPieceK = 5;
-constexpr uint32_t kPieceChunks = kPieceK * kThreads;
+constexpr uint32_t kSpanChunks = 64;
+constexpr uint32_t kPieceSpans = kPieceK * kWaves;
 
 template <bool kUnmask>
 __global__ void __launch_bounds__(kThreads)
@@ -76,26 +82,29 @@ payload_xor_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
     const uint32_t key = d.mask() ? d.key() : 0u;
     if (len == 0 || dof >= cap) return;
     const uint64_t dend = len < cap - dof ? dof + len : cap;
-    const uint64_t c0 = dof & ~uint64_t(15);
-    const uint64_t nchunks = (dend - c0 + 15) >> 4;
-    const uint64_t used = (nchunks + kPieceChunks - 1) / kPieceChunks;
+    // 1 KiB spans of the destination arena (dst is 16-byte aligned; spans
+    // count from it) holding the frame
+    const uint64_t s0 = dof / (16 * kSpanChunks), s1 = (dend - 1) / (16 * kSpanChunks) + 1;
+    const uint64_t ns = s1 - s0;
+    const uint64_t used = (ns + kPieceSpans - 1) / kPieceSpans;
     // source phase against the 16-byte destination chunks: one per frame
     const uint32_t ph = (uint32_t)((so - dof) & 15u);
     const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = threadIdx.x >> 6;
     // virtual pieces p, p + pieces, ...: a frame larger than the caller's
     // max_payload_size (or a grid capped below 2^31 blocks) still gets every
     // chunk written
     for (uint64_t vp = p; vp < used; vp += pieces) {
-        const uint64_t pb = nchunks * vp / used, pe = nchunks * (vp + 1) / used;
+        const uint64_t sb = s0 + ns * vp / used, se = s0 + ns * (vp + 1) / used;
         uint4 a[kPieceK], e[kPieceK];
         uint32_t full = 0, part = 0, own_b = 0;
 #pragma unroll
         for (int k = 0; k < (int)kPieceK; ++k) {
-            const uint64_t c = pb + uint64_t(k) * kThreads + threadIdx.x;
-            const uint64_t A = c0 + 16 * c;
+            const uint64_t span = sb + uint64_t(k) * kWaves + wave;
+            const uint64_t A = (span * kSpanChunks + lane) * 16;
             a[k] = make_uint4(0, 0, 0, 0);
             e[k] = make_uint4(0, 0, 0, 0);
-            if (c >= pe) continue;
+            if (span >= se || A + 16 <= dof || A >= dend) continue;
             // the aligned source blocks of the window this chunk funnels from
             const int64_t w = (int64_t)so + (int64_t)A - (int64_t)dof;
             const int64_t wa = w - (w & 15);
@@ -103,9 +112,9 @@ payload_xor_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
                 full |= 1u << k;
                 a[k] = ld16(src + wa);
                 // the block holding the chunk's last source byte, when the
-                // next lane does not load it: lane 63, the piece's last
-                // chunk, a partial chunk next
-                if (ph && (lane == 63 || c + 1 >= pe || A + 32 > dend)) {
+                // next lane does not load it: lane 63 (the span's last chunk)
+                // or a partial chunk next
+                if (ph && (lane == 63 || A + 32 > dend)) {
                     e[k] = ld16(src + wa + 16);
                     own_b |= 1u << k;
                 }
@@ -123,8 +132,8 @@ payload_xor_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
 #pragma unroll
         for (int k = 0; k < (int)kPieceK; ++k) {
             const uint4 nb = from_next_lane(a[k], e[k]);     // every lane: DPP needs the full wave
-            const uint64_t c = pb + uint64_t(k) * kThreads + threadIdx.x;
-            const uint64_t A = c0 + 16 * c;
+            const uint64_t span = sb + uint64_t(k) * kWaves + wave;
+            const uint64_t A = (span * kSpanChunks + lane) * 16;
             if ((full >> k) & 1u) {
                 uint4 o = ph ? funnel16(a[k], (own_b >> k) & 1u ? e[k] : nb, ph) : a[k];
                 xor4(o, rotr8(key, (uint32_t)((A - dof) & 3u)));
@@ -699,12 +708,12 @@ namespace {
 
 // Pieces per frame for the split payload ops: enough workgroups to cover the
 // largest frame (max_payload_size, at any alignment) in pieces of at most
-// kPieceChunks chunks, capped so the grid stays under 2^31 blocks (the
+// kPieceSpans 1 KiB spans, capped so the grid stays under 2^31 blocks (the
 // kernel then strides over a frame's pieces).
 uint32_t payload_pieces(size_t n, uint64_t max_payload_size)
 {
-    const uint64_t chunks = max_payload_size / 16 + 2;
-    uint64_t pieces = (chunks + kPieceChunks - 1) / kPieceChunks;
+    const uint64_t spans = max_payload_size / (16 * kSpanChunks) + 2;
+    uint64_t pieces = (spans + kPieceSpans - 1) / kPieceSpans;
     if (pieces > 65536) pieces = 65536;
     while (pieces > 1 && pieces * n > 0x7fffffffull) pieces >>= 1;
     return (uint32_t)pieces;
