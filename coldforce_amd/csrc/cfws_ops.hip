@@ -53,9 +53,12 @@ parse_headers_kernel(const uint8_t* __restrict__ wire, uint64_t size, const uint
 // grid starting at the frame's first chunk left every instruction's first
 // and last segment half-written: 5.6 / 5.9 TB/s against the streaming
 // kernel's 6.5). Work unit (frame, piece): the frame's spans are split
-// evenly over the fewest pieces of at most 20 spans (4 waves x 5 slots,
-// every load in flight before the first store), so a 64 KiB frame is 4
-// equal workgroups at any alignment. Chunks inside the frame are one
+// evenly over the fewest pieces of at most 20 spans, each wave taking a
+// contiguous run of up to 5 (every load in flight before the first store),
+// so a 64 KiB frame is 4 equal workgroups at any alignment. Stores are
+// write-through and the mask runs at 4 workgroups per CU, the unmask at 5,
+// as the streaming kernel (+0.6 % over `nt` stores and interleaved spans,
+// tools/split_ab.sh). Chunks inside the frame are one
 // 16-byte store (source funnel-shifted into place; a lane's second source
 // block comes from the next lane over DPP). The frame's first and last
 // chunk, which it may share with its neighbours, are assembled the same way
@@ -95,12 +98,15 @@ payload_xor_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
     // max_payload_size (or a grid capped below 2^31 blocks) still gets every
     // chunk written
     for (uint64_t vp = p; vp < used; vp += pieces) {
-        const uint64_t sb = s0 + ns * vp / used, se = s0 + ns * (vp + 1) / used;
+        const uint64_t sb = s0 + ns * vp / used, se_piece = s0 + ns * (vp + 1) / used;
+        // wave w streams a contiguous run of the piece's spans
+        const uint64_t m = se_piece - sb;
+        const uint64_t wb = sb + m * wave / kWaves, se = sb + m * (wave + 1) / kWaves;
         uint4 a[kPieceK], e[kPieceK];
         uint32_t full = 0, part = 0, own_b = 0;
 #pragma unroll
         for (int k = 0; k < (int)kPieceK; ++k) {
-            const uint64_t span = sb + uint64_t(k) * kWaves + wave;
+            const uint64_t span = wb + uint64_t(k);
             const uint64_t A = (span * kSpanChunks + lane) * 16;
             a[k] = make_uint4(0, 0, 0, 0);
             e[k] = make_uint4(0, 0, 0, 0);
@@ -132,12 +138,17 @@ payload_xor_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
 #pragma unroll
         for (int k = 0; k < (int)kPieceK; ++k) {
             const uint4 nb = from_next_lane(a[k], e[k]);     // every lane: DPP needs the full wave
-            const uint64_t span = sb + uint64_t(k) * kWaves + wave;
+            const uint64_t span = wb + uint64_t(k);
             const uint64_t A = (span * kSpanChunks + lane) * 16;
             if ((full >> k) & 1u) {
                 uint4 o = ph ? funnel16(a[k], (own_b >> k) & 1u ? e[k] : nb, ph) : a[k];
                 xor4(o, rotr8(key, (uint32_t)((A - dof) & 3u)));
-                st16(dst + A, o);
+                // write-through over the span, as the streaming kernel's
+                // regions (sc0 sc1 nt)
+                const u32x4 v = {o.x, o.y, o.z, o.w};
+                const auto r = __builtin_amdgcn_make_buffer_rsrc(dst + span * kSpanChunks * 16, 0,
+                                                                 (int)(kSpanChunks * 16), 0x00020000);
+                __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)(lane * 16), 0, 19);
             } else if ((part >> k) & 1u) {
                 uint4 o = ph ? funnel16(a[k], e[k], ph) : a[k];
                 xor4(o, rotr8(key, (uint32_t)((A - dof) & 3u)));
@@ -731,7 +742,7 @@ int launch_payload_xor(const void* src, void* dst, const cfws_frame_desc_t* d_de
         return set_err(CFWS_ERROR_INVALID_ARGUMENT, "arenas must be 16-byte aligned", hipSuccess);
     if (n > 0x7fffffffull) return set_err(CFWS_ERROR_INVALID_ARGUMENT, "too many frames", hipSuccess);
     const uint32_t pieces = payload_pieces(n, max_payload_size);
-    payload_xor_kernel<kUnmask><<<(uint32_t)(n * pieces), kThreads, xform_lds_bytes(),
+    payload_xor_kernel<kUnmask><<<(uint32_t)(n * pieces), kThreads, kUnmask ? 32000 : 40000,
                                   static_cast<hipStream_t>(stream)>>>(
         static_cast<const uint8_t*>(src), static_cast<uint8_t*>(dst), d_desc, d_status, n, pieces, cap);
     return launch_check(what);
