@@ -583,6 +583,9 @@ __device__ __forceinline__ void store_chunk(const Pass& P, uint64_t D, uint4 o)
 // ---------------------------------------------------------------------------
 // the streaming kernel
 // ---------------------------------------------------------------------------
+#ifndef CFWS_INLINE2
+#define CFWS_INLINE2 1
+#endif
 
 // A region inside one frame's body: frame, source phase and rotated key are
 // wave-uniform (SGPRs); all kUnroll loads are in flight before the first
@@ -682,9 +685,11 @@ __device__ __forceinline__ void two_frame_region(const Pass& P, uint32_t f0, con
     // instruction writes each 64-byte segment whole. Edge threads skip
     // these regions (edge_frame, inline_edges).
     const uint64_t o1 = two ? vb.out_off : ~uint64_t(0);
+#if CFWS_INLINE2
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u)
         if (!fast[u]) a[u] = edge_chunk<kMode>(P, f0, base + u * kSlice + lane * kChunk, va, vb, o1, ~uint64_t(0));
+#endif
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u) {
         const uint4 nb = from_next_lane(a[u], e[u]);     // every lane: DPP needs the full wave
@@ -693,6 +698,8 @@ __device__ __forceinline__ void two_frame_region(const Pass& P, uint32_t f0, con
             const uint32_t ph = hi[u] ? phB : phA;
             o = ph ? funnel16(a[u], own[u] ? e[u] : nb, ph) : a[u];
             xor4(o, hi[u] ? krB : krA);
+        } else if (!CFWS_INLINE2) {
+            continue;
         }
         st16_region<kMode>(P.dst + base, u * (uint32_t)kSlice + lane * (uint32_t)kChunk, o);
     }
@@ -849,6 +856,7 @@ __device__ __forceinline__ uint32_t edge_thread_part(uint64_t t) { return (uint3
 __device__ __forceinline__ bool inline_edges(const Pass& P, uint64_t D, uint64_t lo, uint64_t oprev,
                                              uint64_t o1, uint64_t o2)
 {
+    if (!CFWS_INLINE2) return false;
     const uint64_t base = D & ~uint64_t(kRegion - 1), end = base + kRegion;
     if (end > P.total) return false;                 // tail_region: edge threads
     return lo <= base ? o2 >= end : (oprev <= base && o1 >= end);
@@ -978,11 +986,11 @@ __host__ __device__ constexpr bool has_edge_blocks(int mode)
 // The wave-per-EU floor keeps the merged kernel at <= 102 VGPRs, so the
 // 5 workgroups per CU the LDS reservation allows stay resident.
 // workgroups per CU the send's streaming kernel is compiled for (A/B knob)
-#ifndef CFWS_H2SER_MIN_BLOCKS
-#define CFWS_H2SER_MIN_BLOCKS 5
+#ifndef CFWS_SEND_MIN_BLOCKS
+#define CFWS_SEND_MIN_BLOCKS 4
 #endif
 template <int kMode>
-__global__ void __launch_bounds__(kThreads, kMode == kModeH2Ser ? CFWS_H2SER_MIN_BLOCKS : 5)
+__global__ void __launch_bounds__(kThreads, (kMode == kModeH2Ser || kMode == kModeSer) ? CFWS_SEND_MIN_BLOCKS : 5)
 xform_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
              const cfws_frame_desc_t* __restrict__ desc, const int32_t* __restrict__ status,
              const uint64_t* __restrict__ offs, const uint32_t* __restrict__ region_map,
