@@ -583,9 +583,6 @@ __device__ __forceinline__ void store_chunk(const Pass& P, uint64_t D, uint4 o)
 // ---------------------------------------------------------------------------
 // the streaming kernel
 // ---------------------------------------------------------------------------
-#ifndef CFWS_INLINE2
-#define CFWS_INLINE2 1
-#endif
 
 // A region inside one frame's body: frame, source phase and rotated key are
 // wave-uniform (SGPRs); all kUnroll loads are in flight before the first
@@ -638,8 +635,8 @@ __device__ __forceinline__ void fast_region(const Pass& P, const FrameView& v, u
 // over DPP when that lane loads it (same frame, chunk inside the body);
 // otherwise (lane 63, the last chunk before a body end) the lane loads it.
 template <int kMode>
-__device__ __forceinline__ void two_frame_region(const Pass& P, uint32_t f0, const FrameView& va,
-                                                 const FrameView& vb, bool two, uint64_t base, uint32_t lane)
+__device__ __forceinline__ void two_frame_region(const Pass& P, const FrameView& va,
+                                                 const FrameView& vb, uint64_t base, uint32_t lane)
 {
     // Everything per frame is wave-uniform and taken relative to the region
     // base (offsets clamped into [0, kRegion + 32], enough for every compare
@@ -677,30 +674,13 @@ __device__ __forceinline__ void two_frame_region(const Pass& P, uint32_t f0, con
     for (int u = 0; u < kUnroll; ++u) a[u] = fast[u] ? ld16(sp[u]) : make_uint4(0, 0, 0, 0);
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u) e[u] = own[u] ? ld16(sp[u] + 16) : make_uint4(0, 0, 0, 0);
-    // The region's edge chunks (headers, the boundary, padding: every chunk
-    // not inside a body), assembled here from the two wave-uniform views
-    // after the body loads are in flight, into a[] (a fast lane whose next
-    // lane holds an edge chunk loads its own B, so the DPP exchange never
-    // reads one), and stored with the body chunks of their slot: one store
-    // instruction writes each 64-byte segment whole. Edge threads skip
-    // these regions (edge_frame, inline_edges).
-    const uint64_t o1 = two ? vb.out_off : ~uint64_t(0);
-#if CFWS_INLINE2
-#pragma unroll
-    for (int u = 0; u < kUnroll; ++u)
-        if (!fast[u]) a[u] = edge_chunk<kMode>(P, f0, base + u * kSlice + lane * kChunk, va, vb, o1, ~uint64_t(0));
-#endif
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u) {
         const uint4 nb = from_next_lane(a[u], e[u]);     // every lane: DPP needs the full wave
-        uint4 o = a[u];
-        if (fast[u]) {
-            const uint32_t ph = hi[u] ? phB : phA;
-            o = ph ? funnel16(a[u], own[u] ? e[u] : nb, ph) : a[u];
-            xor4(o, hi[u] ? krB : krA);
-        } else if (!CFWS_INLINE2) {
-            continue;
-        }
+        if (!fast[u]) continue;
+        const uint32_t ph = hi[u] ? phB : phA;
+        uint4 o = ph ? funnel16(a[u], own[u] ? e[u] : nb, ph) : a[u];
+        xor4(o, hi[u] ? krB : krA);
         st16_region<kMode>(P.dst + base, u * (uint32_t)kSlice + lane * (uint32_t)kChunk, o);
     }
 }
@@ -846,22 +826,6 @@ __device__ __forceinline__ uint32_t edge_thread_part(uint64_t t) { return (uint3
 
 // The edge chunks of frame f in pass P (part 0: before the body; part 1:
 // reaching past the body end).
-// Does chunk D (of frame fa: out_off lo, next frames at o1, o2; oprev = the
-// start of fa - 1) lie in a region the streaming wave writes whole -- edges
-// included (two_frame_region)? Exactly the regions xform_kernel hands to
-// two_frame_region: inside the pass (end <= total) and touched by at most
-// two frames. Computed from offsets the edge thread has already loaded; the
-// region map picks the non-empty frame holding the region's first byte, and
-// an empty frame between two others makes a region general there too.
-__device__ __forceinline__ bool inline_edges(const Pass& P, uint64_t D, uint64_t lo, uint64_t oprev,
-                                             uint64_t o1, uint64_t o2)
-{
-    if (!CFWS_INLINE2) return false;
-    const uint64_t base = D & ~uint64_t(kRegion - 1), end = base + kRegion;
-    if (end > P.total) return false;                 // tail_region: edge threads
-    return lo <= base ? o2 >= end : (oprev <= base && o1 >= end);
-}
-
 template <int kMode>
 __device__ __forceinline__ void edge_frame(const Pass& P, uint64_t f, uint32_t part)
 {
@@ -874,7 +838,6 @@ __device__ __forceinline__ void edge_frame(const Pass& P, uint64_t f, uint32_t p
     const FrameView vb = frame_view<kMode>(P, fb);
     const uint64_t o2 = fa + 2 < n ? P.offs[fa + 2] : ~uint64_t(0);
     const uint64_t o1 = fa + 1 < n ? vb.out_off : ~uint64_t(0);
-    const uint64_t oprev = fa > 0 ? P.offs[fa - 1] : 0;
     const uint64_t lo = va.out_off;
     uint64_t hi = fa + 1 < n ? vb.out_off : P.total;
     if (hi > P.total) hi = P.total;
@@ -885,8 +848,7 @@ __device__ __forceinline__ void edge_frame(const Pass& P, uint64_t f, uint32_t p
     if (part == 0) {
         // chunks before the body (headers): D < body_start
         for (uint64_t D = first; D < hi && D < v.body_start; D += 16)
-            if (!inline_edges(P, D, lo, oprev, o1, o2))
-                store_chunk(P, D, edge_chunk<kMode>(P, fa, D, va, vb, o1, o2));
+            store_chunk(P, D, edge_chunk<kMode>(P, fa, D, va, vb, o1, o2));
         return;
     }
     // chunks reaching past the body end (boundary, padding, pass end)
@@ -894,7 +856,6 @@ __device__ __forceinline__ void edge_frame(const Pass& P, uint64_t f, uint32_t p
     if (d0 < first) d0 = first;
     if (d0 < v.body_start) d0 = (v.body_start + 15) & ~uint64_t(15);  // header chunks: part 0
     for (uint64_t D = d0; D < hi; D += 16) {
-        if (inline_edges(P, D, lo, oprev, o1, o2)) continue;
         if (D >= be && D + 16 <= hi)          // pure alignment padding / OOM body
             store_chunk(P, D, make_uint4(0, 0, 0, 0));
         else
@@ -986,11 +947,11 @@ __host__ __device__ constexpr bool has_edge_blocks(int mode)
 // The wave-per-EU floor keeps the merged kernel at <= 102 VGPRs, so the
 // 5 workgroups per CU the LDS reservation allows stay resident.
 // workgroups per CU the send's streaming kernel is compiled for (A/B knob)
-#ifndef CFWS_SEND_MIN_BLOCKS
-#define CFWS_SEND_MIN_BLOCKS 4
+#ifndef CFWS_H2SER_MIN_BLOCKS
+#define CFWS_H2SER_MIN_BLOCKS 5
 #endif
 template <int kMode>
-__global__ void __launch_bounds__(kThreads, (kMode == kModeH2Ser || kMode == kModeSer) ? CFWS_SEND_MIN_BLOCKS : 5)
+__global__ void __launch_bounds__(kThreads, kMode == kModeH2Ser ? CFWS_H2SER_MIN_BLOCKS : 5)
 xform_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
              const cfws_frame_desc_t* __restrict__ desc, const int32_t* __restrict__ status,
              const uint64_t* __restrict__ offs, const uint32_t* __restrict__ region_map,
@@ -1062,9 +1023,9 @@ xform_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
             if (base >= va.body_start && end <= va.body_start + va.body_len)
                 fast_region<kMode>(P, va, base, lane);
             else
-                two_frame_region<kMode>(P, f0, va, va, false, base, lane);   // partial body, one frame
+                two_frame_region<kMode>(P, va, va, base, lane);   // partial body, one frame
         } else if (f1 == f0 + 1 || offs[f0 + 2] >= end) {
-            two_frame_region<kMode>(P, f0, va, frame_view<kMode>(P, f0 + 1), true, base, lane);
+            two_frame_region<kMode>(P, va, frame_view<kMode>(P, f0 + 1), base, lane);
         } else {
             general_region<kMode>(P, f0, f1, base, lane);
         }
