@@ -32,10 +32,6 @@
 
 #include <mutex>
 
-#ifndef CFWS_DESER_EDGE_FLAG
-#define CFWS_DESER_EDGE_FLAG 1
-#endif
-
 namespace cfws_rt {
 
 thread_local char g_err[512] = "";
@@ -223,9 +219,6 @@ deserialize_plan_reduce_kernel(const uint8_t* __restrict__ wire, uint64_t wire_s
     __shared__ uint64_t s_wave[kWaves];
     const uint64_t b0 = uint64_t(blockIdx.x) * kPlanBlock;
     uint64_t sum0 = 0, sum1 = 0;
-    // does any frame of this block leave a partial 16-byte chunk (edge work
-    // for the execute's edge threads)?
-    int edges = reassemble || (align & 15u) != 0;
 #pragma unroll
     for (int k = 0; k < kPlanItems; ++k) {
         const uint64_t f = b0 + uint64_t(k) * kThreads + threadIdx.x;
@@ -236,7 +229,6 @@ deserialize_plan_reduce_kernel(const uint8_t* __restrict__ wire, uint64_t wire_s
         desc[f] = d;
         status[f] = st;
         const uint64_t len = (st == CFWS_PARSE_COMPLETE) ? d.payload_size : 0;
-        edges |= (len & 15u) != 0;
         if (reassemble) {
             const bool ctl = is_control(d.opcode);
             vals0[f] = ctl ? 0 : len;
@@ -249,11 +241,6 @@ deserialize_plan_reduce_kernel(const uint8_t* __restrict__ wire, uint64_t wire_s
             sum0 += v;
         }
     }
-    // without reassembly pass 1's partials are free: they carry each
-    // block's edge bit to the apply kernel, which folds them into the
-    // workspace's edge flag (kEdgeFlagWord)
-    const int block_edges = __syncthreads_or(edges);
-    if (!reassemble && threadIdx.x == 0) partials1[blockIdx.x] = block_edges ? 1u : 0u;
     uint64_t total;
     block_exclusive_scan(sum0, s_wave, &total);
     if (threadIdx.x == 0) partials0[blockIdx.x] = total;
@@ -708,8 +695,7 @@ int cfws_deserialize_execute(const void* d_wire, const cfws_frame_desc_t* d_desc
                 d_status, ws_ptr<const uint64_t>(ws, L.offs[0]), ws_ptr<const uint64_t>(ws, L.offs[1]),
                 ws_ptr<const uint64_t>(ws, L.hdr), cap, (uint32_t)n);
     } else {
-        launch_pass<kModeDeser>(L, 0, d_wire, d_payload, d_desc, d_status, ws, cap, n, kClassAll, st, 0, true,
-                                false, CFWS_DESER_EDGE_FLAG != 0);
+        launch_pass<kModeDeser>(L, 0, d_wire, d_payload, d_desc, d_status, ws, cap, n, kClassAll, st);
     }
     return launch_check("deserialize_execute");
 }

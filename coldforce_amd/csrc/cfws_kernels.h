@@ -84,11 +84,6 @@ __host__ __device__ constexpr bool is_ser(int mode) { return mode != kModeDeser;
 // ---------------------------------------------------------------------------
 // hdr[0] pass-0 total (clamped)   hdr[1] pass-1 total (clamped)
 // hdr[2] pass-1 output base       hdr[3] pass-0 grand total   hdr[4] pass-1 grand
-// Workspace header word the WS deserialize plan sets when any frame has an
-// edge chunk (a payload slot that is not a whole number of 16-byte chunks,
-// a capacity cut, alignment below 16); zeroed with the totals.
-constexpr uint32_t kEdgeFlagWord = 6;
-
 struct WsLayout {
     uint64_t hdr;
     uint64_t offs[2];      // u64[n] per pass: sizes, then exclusive offsets
@@ -829,35 +824,6 @@ __device__ __forceinline__ uint64_t edge_thread_frame(uint64_t t) { return (t >>
 
 __device__ __forceinline__ uint32_t edge_thread_part(uint64_t t) { return (uint32_t)(t >> 6) & 1u; }
 
-// WS serialize runs one edge thread per frame, both parts (part 2): its
-// part 0 (chunks that start inside the header) is empty for most frames --
-// a header of 2-14 bytes rarely holds a chunk start, the chunk holding it is
-// the previous frame's part 1 -- so the second thread only loaded two views
-// to find nothing (round 2: 1 KiB serialize 4.55-4.81 -> 4.67-4.94 TB/s with
-// one thread per frame; deserialize, whose parts both have work when
-// payloads are packed, lost with it and keeps two).
-#ifndef CFWS_SER_EDGE1
-#define CFWS_SER_EDGE1 1
-#endif
-__host__ __device__ constexpr bool edge_one_thread(int mode) { return CFWS_SER_EDGE1 && mode == kModeSer; }
-
-__host__ __device__ constexpr uint64_t edge_threads_of(int mode, uint64_t n)
-{
-    return edge_one_thread(mode) ? (n + 63) / 64 * 64 : edge_threads(n);
-}
-
-template <int kMode>
-__device__ __forceinline__ uint64_t edge_frame_of(uint64_t t)
-{
-    return edge_one_thread(kMode) ? t : edge_thread_frame(t);
-}
-
-template <int kMode>
-__device__ __forceinline__ uint32_t edge_part_of(uint64_t t)
-{
-    return edge_one_thread(kMode) ? 2u : edge_thread_part(t);
-}
-
 // The edge chunks of frame f in pass P (part 0: before the body; part 1:
 // reaching past the body end).
 template <int kMode>
@@ -879,11 +845,11 @@ __device__ __forceinline__ void edge_frame(const Pass& P, uint64_t f, uint32_t p
     const FrameView& v = va;
     const uint64_t be = v.body_start + v.body_len;
     const uint64_t first = (lo + 15) & ~uint64_t(15);
-    if (part != 1) {
+    if (part == 0) {
         // chunks before the body (headers): D < body_start
         for (uint64_t D = first; D < hi && D < v.body_start; D += 16)
             store_chunk(P, D, edge_chunk<kMode>(P, fa, D, va, vb, o1, o2));
-        if (part == 0) return;
+        return;
     }
     // chunks reaching past the body end (boundary, padding, pass end)
     uint64_t d0 = be >= 15 ? ((be - 15 + 15) & ~uint64_t(15)) : 0;  // first D with D + 16 > be
@@ -906,7 +872,7 @@ edge_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
             uint32_t klass, uint32_t sid, const cfws_frame_desc_t* __restrict__ parent)
 {
     const uint64_t t = uint64_t(blockIdx.x) * kEdgeThreads + threadIdx.x;
-    const uint64_t f = edge_frame_of<kMode>(t);
+    const uint64_t f = edge_thread_frame(t);
     if (f >= n_frames) return;
     const uint64_t out_base = base_p ? *base_p : 0;
     Pass P;
@@ -921,7 +887,7 @@ edge_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
     P.klass = klass;
     P.sid = sid;
     P.parent = parent;
-    edge_frame<kMode>(P, f, edge_part_of<kMode>(t));
+    edge_frame<kMode>(P, f, edge_thread_part(t));
 }
 
 // Deserialize with reassembly (CFWS_DESERIALIZE_REASSEMBLE): the edge chunks
@@ -992,8 +958,7 @@ xform_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
              const uint64_t* __restrict__ total_p, const uint64_t* __restrict__ base_p,
              uint64_t capacity, uint32_t n_frames, uint32_t klass, uint32_t sid,
              const cfws_frame_desc_t* __restrict__ parent, uint32_t edge_blocks,
-             const uint64_t* __restrict__ reasm_offs1, uint32_t edge_stride,
-             const uint64_t* __restrict__ edge_flag)
+             const uint64_t* __restrict__ reasm_offs1, uint32_t edge_stride)
 {
     // Which workgroups are edge workgroups: the first edge_blocks, or (edge
     // stride s > 0) every s-th one, spread through the grid
@@ -1027,12 +992,8 @@ xform_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
     P.sid = sid;
     P.parent = parent;
     if (has_edge_blocks(kMode) && is_edge) {
-        // a WS deserialize whose plan found no edge chunk (every payload
-        // slot a whole number of 16-byte chunks, no frame cut by the
-        // capacity): nothing to do
-        if (edge_flag && *edge_flag == 0) return;
         const uint64_t t = uint64_t(eidx) * kThreads + threadIdx.x;
-        if (edge_frame_of<kMode>(t) < n_frames) edge_frame<kMode>(P, edge_frame_of<kMode>(t), edge_part_of<kMode>(t));
+        if (edge_thread_frame(t) < n_frames) edge_frame<kMode>(P, edge_thread_frame(t), edge_thread_part(t));
         return;
     }
     const uint64_t n_regions = (P.total + kRegion - 1) / kRegion;
@@ -1372,15 +1333,6 @@ deserialize_plan_apply_kernel(cfws_frame_desc_t* __restrict__ desc, int32_t* __r
         }
     }
     const uint64_t t0 = g0 < capacity ? g0 : capacity;
-    if (!reassemble && blockIdx.x == 0) {
-        // the edge flag: a block with a partial chunk (its bit in
-        // partials1), or a capacity cut (frames past it become OOM and their
-        // slots are zero-filled by the edge threads)
-        int any = g0 > capacity;
-        for (uint64_t b = threadIdx.x; b < nb && !any; b += kThreads) any |= partials1[b] != 0;
-        any = __syncthreads_or(any);
-        if (threadIdx.x == 0) hdr[kEdgeFlagWord] = any ? 1u : 0u;
-    }
     const uint64_t room1 = capacity - t0;
     const uint64_t t1 = g1 < room1 ? g1 : room1;
     const uint64_t i0 = uint64_t(blockIdx.x) * kPlanBlock + uint64_t(threadIdx.x) * kPlanItems;
@@ -1582,10 +1534,10 @@ void launch_streaming(const void* src, void* dst, const cfws_frame_desc_t* desc,
                       const uint64_t* total_p, const uint64_t* base_p, uint64_t regions,
                       uint64_t cap, size_t n, uint32_t klass, uint32_t sid, hipStream_t st,
                       const cfws_frame_desc_t* parent = nullptr, bool edges = true,
-                      const uint64_t* reasm_offs1 = nullptr, const uint64_t* edge_flag = nullptr)
+                      const uint64_t* reasm_offs1 = nullptr)
 {
     const bool split = edges && (edge_split() || !has_edge_blocks(kMode));
-    const uint32_t eb = (edges && !split) ? grid_for(edge_threads_of(kMode, n), kThreads) : 0;
+    const uint32_t eb = (edges && !split) ? grid_for(edge_threads(n), kThreads) : 0;
     const uint32_t sg = stream_grid(regions);
     // edge workgroups first, or spread evenly through the grid (edge_interleave)
     const uint32_t spread = eb ? (eb + sg) / eb : 0;
@@ -1598,11 +1550,11 @@ void launch_streaming(const void* src, void* dst, const cfws_frame_desc_t* desc,
     xform_kernel<kMode><<<eb + sg, kThreads, xform_lds_bytes(kMode, n ? cap / n : cap), st>>>(
         static_cast<const uint8_t*>(src), static_cast<uint8_t*>(dst), desc, status, offs, map,
         total_p, base_p, cap, (uint32_t)n, klass, sid, parent, eb, eb ? reasm_offs1 : nullptr,
-        stride, edge_flag);
+        stride);
     // (a separate edge launch on a second stream, overlapping the streaming
     // kernel, measured no faster on config 5: the stream slowed by what the
     // overlap saved)
-    if (split) edge_kernel<kMode><<<grid_for(edge_threads_of(kMode, n), kEdgeThreads), kEdgeThreads, 0, st>>>(
+    if (split) edge_kernel<kMode><<<grid_for(edge_threads(n), kEdgeThreads), kEdgeThreads, 0, st>>>(
         static_cast<const uint8_t*>(src), static_cast<uint8_t*>(dst), desc, status, offs,
         total_p, base_p, cap, (uint32_t)n, klass, sid, parent);
 }
@@ -1610,8 +1562,7 @@ void launch_streaming(const void* src, void* dst, const cfws_frame_desc_t* desc,
 template <int kMode>
 void launch_pass(const WsLayout& L, int p, const void* src, void* dst, const cfws_frame_desc_t* desc,
                  const int32_t* status, const void* ws, uint64_t cap, size_t n, uint32_t klass,
-                 hipStream_t st, uint32_t sid = 0, bool edges = true, bool reasm_edges = false,
-                 bool use_edge_flag = false)
+                 hipStream_t st, uint32_t sid = 0, bool edges = true, bool reasm_edges = false)
 {
     const uint64_t* hdr = ws_ptr<const uint64_t>(ws, L.hdr);
     // Pass 1 (reassembly: control frames, <= 125-byte payloads each) is
@@ -1622,8 +1573,7 @@ void launch_pass(const WsLayout& L, int p, const void* src, void* dst, const cfw
     launch_streaming<kMode>(src, dst, desc, status, ws_ptr<const uint64_t>(ws, L.offs[p]),
                             ws_ptr<const uint32_t>(ws, L.map[p]), hdr + p,
                             p == 1 ? hdr + 2 : nullptr, regions, cap, n, klass, sid, st, nullptr,
-                            edges, reasm_edges ? ws_ptr<const uint64_t>(ws, L.offs[1]) : nullptr,
-                            use_edge_flag ? hdr + kEdgeFlagWord : nullptr);
+                            edges, reasm_edges ? ws_ptr<const uint64_t>(ws, L.offs[1]) : nullptr);
 }
 
 }  // namespace
