@@ -188,3 +188,41 @@ def test_dropin_echo_small_frames_and_binary_sizes(tmp_path):
             _ok(r, frames)
             wires.append((_read(r["capture"]["client"]), _read(r["capture"]["server"])))
         assert wires[0] == wires[1], payload
+
+
+def _accept_pairs(tmp_path, seeds):
+    """(Sec-WebSocket-Key the stock client sent, Sec-WebSocket-Accept the
+    stock server answered) for each seed: the reference's own static
+    co_ws_create_base64_accept_key (co_ws_http_extension.c:26-57), reached
+    through co_http_response_create_ws_upgrade (:322-362)."""
+    import re
+    pairs = []
+    for seed in seeds:
+        r = run_echo("stock", "ws", 1, 16, window=1, seed=seed, capture_dir=str(tmp_path / str(seed)))
+        _ok(r, 1)
+        chead, _ = split_http(_read(r["capture"]["client"]))
+        shead, _ = split_http(_read(r["capture"]["server"]))
+        key = re.search(rb"Sec-WebSocket-Key: (\S+)\r\n", chead).group(1)
+        acc = re.search(rb"Sec-WebSocket-Accept: (\S+)\r\n", shead).group(1)
+        pairs.append((key, acc.decode()))
+    return pairs
+
+
+def test_stock_accept_key_matches_oracle(tmp_path):
+    """The oracle's accept key equals the reference's static function's, as
+    the stock server put it on the wire."""
+    _need("stock")
+    for key, acc in _accept_pairs(tmp_path, (1, 2, 3, 99, 12345)):
+        assert O.ws_accept_key(key) == acc, key
+
+
+@pytest.mark.gpu
+def test_device_accept_key_matches_reference_server(tmp_path):
+    """ws_accept_kernel (cfws_ws_accept_keys_batch) against the accept keys
+    the reference's own server code computed for the same client keys."""
+    _need("stock")
+    from coldforce_amd import cfws
+    cfws.init()
+    pairs = _accept_pairs(tmp_path, (1, 2, 3, 99, 12345))
+    got = cfws.ws_accept_keys([k for k, _ in pairs])
+    assert got == [a for _, a in pairs]
