@@ -89,6 +89,21 @@ def cgroup_cpu_limit():
     return None
 
 
+def effective_cpus() -> int:
+    """The CPUs this job may use at once: nproc, or fewer when the cgroup's
+    quota (cpu.max) grants fewer (the GPU box: 256 CPUs visible, a 16-CPU
+    quota). Threads beyond it only queue."""
+    n = host_cpus()
+    q = cgroup_cpu_limit()
+    try:
+        quota, period = q.split()[:2]
+        if quota != "max" and int(period) > 0:
+            n = max(1, min(n, int(quota) // int(period)))
+    except (AttributeError, ValueError):
+        pass
+    return n
+
+
 def cpu_baseline(frame_size: int, seconds: float):
     """Reference codec (oracle/_ref, compiled from coldforce's own sources at
     -O2) when it was built, else the clean-room port; timed on this host on
@@ -367,12 +382,13 @@ def bench_accept(args, rank, world, dev):
             "verified": ok}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         kind = "reference" if O.ref_lib("O2") is not None else "port"
-        threads = host_cpus()
+        threads = effective_cpus()
         n = min(N, 262144)
         t1 = O.cpu_accept_bench(raw, off[:n + 1].astype(np.uint64), threads, 1, kind)
         iters = max(1, int(math.ceil(args.cpu_seconds / max(t1, 1e-3))))
         t = O.cpu_accept_bench(raw, off[:n + 1].astype(np.uint64), threads, iters, kind)
         line["cpu_baseline"] = {"value": round(n * iters / t, 1), "unit": "keys/s", "cores": threads,
+                                "nproc": host_cpus(), "cgroup_cpu_max": cgroup_cpu_limit(),
                                 "kind": kind, "sample": f"{n} keys x {iters} iters, one "
                                 f"co_sha1 + co_base64_encode per key, {threads} threads",
                                 "seconds": round(t, 2)}
@@ -476,7 +492,7 @@ def bench_index(args, rank, world, dev):
                          "ns_per_hop": round(kms * 1e6 / max(hops, 1e-9), 1)},
             "verified": ok}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        threads = host_cpus()
+        threads = effective_cpus()
         ub = (begin_np.astype(np.uint64), end_np.astype(np.uint64))
         t1, _ = O.cpu_index_bench(host_wire, ub[0], ub[1], 4096, threads)
         reps = max(1, int(math.ceil(args.cpu_seconds / max(t1, 1e-3))))
@@ -486,6 +502,7 @@ def bench_index(args, rank, world, dev):
             t += ti
             f += fi
         line["cpu_baseline"] = {"value": round(f / t, 1), "unit": "frames/s", "cores": threads,
+                                "nproc": host_cpus(), "cgroup_cpu_max": cgroup_cpu_limit(),
                                 "kind": "port", "sample": f"every connection x {reps}, the receive "
                                 f"loop's walk (orc_index_stream) over host memory, {threads} threads",
                                 "seconds": round(t, 2)}
