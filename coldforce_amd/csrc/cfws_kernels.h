@@ -89,7 +89,6 @@ struct WsLayout {
     uint64_t offs[2];      // u64[n] per pass: sizes, then exclusive offsets
     uint64_t partials[2];  // u64[scan blocks + 1] per pass
     uint64_t map[2];       // u32[regions + 2] per pass
-    uint64_t edges;        // uint4[kEdgeSlots * n]: WS serialize's prepared edge chunks
     uint64_t bytes;
     uint64_t regions;
     uint64_t scan_blocks;
@@ -108,8 +107,6 @@ WsLayout ws_layout(uint64_t n, uint64_t capacity)
     for (int p = 0; p < 2; ++p) { L.offs[p] = at; at = align_up(at + 8 * n, 256); }
     for (int p = 0; p < 2; ++p) { L.partials[p] = at; at = align_up(at + 8 * (L.scan_blocks + 1), 256); }
     for (int p = 0; p < 2; ++p) { L.map[p] = at; at = align_up(at + 4 * (L.regions + 2), 256); }
-    L.edges = at;
-    at = align_up(at + 16 * 2 * n, 256);
     L.bytes = at;
     return L;
 }
@@ -162,18 +159,7 @@ struct Pass {
     uint32_t klass;
     uint32_t sid;                 // HTTP/2 stream id (kModeH2Wrap, kModeH2Ser)
     const cfws_frame_desc_t* parent;   // kModeH2Ser: the WS frames
-    const uint4* edges;           // prepared edge chunks (kEdgeSlots per frame), or null
 };
-
-// WS serialize prepares its edge chunks before the stream (edge_prep_kernel):
-// slot 0 = the chunk that starts inside the frame's header (a 2-14 byte
-// header holds at most one chunk start), slot 1 = the chunk reaching past
-// its body end into the next frame (frames are packed: at most one). The
-// region waves then load a ready chunk for every position that is not inside
-// a body, in the same round as their body blocks, and store it in the same
-// instruction as the body chunks beside it: each 64-byte segment leaves L2
-// whole, and no edge workgroup shares the stream (§3.4, §3.7).
-constexpr uint32_t kEdgeSlots = 2;
 
 // What one frame contributes to a pass's output.
 //   [out_off, out_off + pre)              header bytes (serialize only)
@@ -594,12 +580,6 @@ __device__ __forceinline__ void store_chunk(const Pass& P, uint64_t D, uint4 o)
     }
 }
 
-// The prepared chunk for position D of frame f (its view v).
-__device__ __forceinline__ uint4 prepared_edge(const Pass& P, uint32_t f, const FrameView& v, uint64_t D)
-{
-    return ld16(reinterpret_cast<const uint8_t*>(P.edges + uint64_t(f) * kEdgeSlots + (D < v.body_start ? 0 : 1)));
-}
-
 // ---------------------------------------------------------------------------
 // the streaming kernel
 // ---------------------------------------------------------------------------
@@ -655,8 +635,8 @@ __device__ __forceinline__ void fast_region(const Pass& P, const FrameView& v, u
 // over DPP when that lane loads it (same frame, chunk inside the body);
 // otherwise (lane 63, the last chunk before a body end) the lane loads it.
 template <int kMode>
-__device__ __forceinline__ void two_frame_region(const Pass& P, uint32_t f0, const FrameView& va,
-                                                 const FrameView& vb, bool two, uint64_t base, uint32_t lane)
+__device__ __forceinline__ void two_frame_region(const Pass& P, const FrameView& va,
+                                                 const FrameView& vb, uint64_t base, uint32_t lane)
 {
     // Everything per frame is wave-uniform and taken relative to the region
     // base (offsets clamped into [0, kRegion + 32], enough for every compare
@@ -690,30 +670,17 @@ __device__ __forceinline__ void two_frame_region(const Pass& P, uint32_t f0, con
         sp[u] = P.src + (((hi[u] ? sB : sA) + r) & ~uint64_t(15));
     }
     uint4 a[kUnroll], e[kUnroll];
-    // prepared edge chunks (WS serialize): every other chunk of the region,
-    // loaded into a[] in the same round (a fast lane whose next lane holds
-    // one loads its own B, so the DPP exchange never reads it)
-    const bool prep = kMode == kModeSer && P.edges != nullptr;
 #pragma unroll
-    for (int u = 0; u < kUnroll; ++u) {
-        const uint64_t D = base + u * kSlice + lane * kChunk;
-        a[u] = fast[u] ? ld16(sp[u])
-                       : (prep ? prepared_edge(P, (two && hi[u]) ? f0 + 1 : f0, hi[u] ? vb : va, D)
-                               : make_uint4(0, 0, 0, 0));
-    }
+    for (int u = 0; u < kUnroll; ++u) a[u] = fast[u] ? ld16(sp[u]) : make_uint4(0, 0, 0, 0);
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u) e[u] = own[u] ? ld16(sp[u] + 16) : make_uint4(0, 0, 0, 0);
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u) {
         const uint4 nb = from_next_lane(a[u], e[u]);     // every lane: DPP needs the full wave
-        uint4 o = a[u];
-        if (fast[u]) {
-            const uint32_t ph = hi[u] ? phB : phA;
-            o = ph ? funnel16(a[u], own[u] ? e[u] : nb, ph) : a[u];
-            xor4(o, hi[u] ? krB : krA);
-        } else if (!prep) {
-            continue;
-        }
+        if (!fast[u]) continue;
+        const uint32_t ph = hi[u] ? phB : phA;
+        uint4 o = ph ? funnel16(a[u], own[u] ? e[u] : nb, ph) : a[u];
+        xor4(o, hi[u] ? krB : krA);
         st16_region<kMode>(P.dst + base, u * (uint32_t)kSlice + lane * (uint32_t)kChunk, o);
     }
 }
@@ -743,8 +710,6 @@ __device__ __forceinline__ void general_region_search(const Pass& P, uint32_t f0
         const FrameView v = frame_view<kMode>(P, fr[u]);
         if (D >= v.body_start && D + kChunk <= v.body_start + v.body_len)
             st16_region<kMode>(P.dst + base, (uint32_t)(D - base), body_chunk(P.src, v, D));
-        else if (kMode == kModeSer && P.edges)
-            st16_region<kMode>(P.dst + base, (uint32_t)(D - base), prepared_edge(P, fr[u], v, D));
     }
 }
 
@@ -767,7 +732,6 @@ __device__ __forceinline__ void general_region(const Pass& P, uint32_t f0, uint3
     auto rel = [base](uint64_t x, uint64_t hi) -> uint32_t {
         return x <= base ? 0u : (x - base >= hi ? (uint32_t)hi : (uint32_t)(x - base));
     };
-    const bool prep = kMode == kModeSer && P.edges != nullptr;
     uint32_t ro = (uint32_t)kRegion, rng = 0, kr = 0, dlo = 0, dhi = 0;
     if (lane < nf) {
         const FrameView v = frame_view<kMode>(P, f0 + lane);
@@ -799,25 +763,18 @@ __device__ __forceinline__ void general_region(const Pass& P, uint32_t f0, uint3
         const uint64_t s = base + r + d;
         ph[u] = (uint32_t)(s & 15u);
         sp[u] = P.src + (s & ~uint64_t(15));
-        if (prep && !fast[u])     // the prepared chunk of frame f0 + j (slot: before its body or not)
-            sp[u] = reinterpret_cast<const uint8_t*>(P.edges + uint64_t(f0 + j) * kEdgeSlots +
-                                                     (r < (rg & 0xffffu) ? 0 : 1));
     }
     uint4 a[kUnroll], b[kUnroll];
 #pragma unroll
-    for (int u = 0; u < kUnroll; ++u) a[u] = (fast[u] || prep) ? ld16(sp[u]) : make_uint4(0, 0, 0, 0);
+    for (int u = 0; u < kUnroll; ++u) a[u] = fast[u] ? ld16(sp[u]) : make_uint4(0, 0, 0, 0);
     // the block holding the chunk's last byte: a body byte, inside the source
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u) b[u] = fast[u] && ph[u] ? ld16(sp[u] + 16) : make_uint4(0, 0, 0, 0);
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u) {
-        uint4 o = a[u];
-        if (fast[u]) {
-            o = ph[u] ? funnel16(a[u], b[u], ph[u]) : a[u];
-            xor4(o, key[u]);
-        } else if (!prep) {
-            continue;
-        }
+        if (!fast[u]) continue;
+        uint4 o = ph[u] ? funnel16(a[u], b[u], ph[u]) : a[u];
+        xor4(o, key[u]);
         st16_region<kMode>(P.dst + base, u * (uint32_t)kSlice + lane * (uint32_t)kChunk, o);
     }
 }
@@ -842,8 +799,6 @@ __device__ __forceinline__ void tail_region(const Pass& P, uint32_t f0, uint32_t
         const FrameView v = frame_view<kMode>(P, lo);
         if (D >= v.body_start && D + kChunk <= v.body_start + v.body_len)
             store_chunk(P, D, body_chunk(P.src, v, D));
-        else if (kMode == kModeSer && P.edges)
-            store_chunk(P, D, prepared_edge(P, lo, v, D));
     }
 }
 
@@ -932,53 +887,7 @@ edge_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
     P.klass = klass;
     P.sid = sid;
     P.parent = parent;
-    P.edges = nullptr;
     edge_frame<kMode>(P, f, edge_thread_part(t));
-}
-
-// WS serialize: every frame's edge chunks, prepared for the streaming
-// kernel's region waves (kEdgeSlots, prepared_edge): one thread per frame,
-// the chunks edge_frame would have stored, into edges[] instead. Runs after
-// the plan (offsets final) and before the stream, as part of the execute.
-__global__ void __launch_bounds__(kThreads)
-edge_prep_kernel(const uint8_t* __restrict__ src, const cfws_frame_desc_t* __restrict__ desc,
-                 const uint64_t* __restrict__ offs, const uint64_t* __restrict__ total_p, uint64_t capacity,
-                 uint32_t n_frames, uint4* __restrict__ edges)
-{
-    const uint64_t f = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
-    if (f >= n_frames) return;
-    Pass P;
-    P.src = src;
-    P.dst = nullptr;
-    P.desc = desc;
-    P.status = nullptr;
-    P.offs = offs;
-    P.total = *total_p;
-    P.capacity = capacity;
-    P.n_frames = n_frames;
-    P.klass = kClassAll;
-    P.sid = 0;
-    P.parent = nullptr;
-    P.edges = nullptr;
-    const uint32_t fa = (uint32_t)f, fb = fa + 1 < n_frames ? fa + 1 : fa;
-    const FrameView va = frame_view<kModeSer>(P, fa);
-    const FrameView vb = frame_view<kModeSer>(P, fb);
-    const uint64_t o2 = fa + 2 < n_frames ? offs[fa + 2] : ~uint64_t(0);
-    const uint64_t o1 = fa + 1 < n_frames ? vb.out_off : ~uint64_t(0);
-    uint64_t hi = fa + 1 < n_frames ? vb.out_off : P.total;
-    if (hi > P.total) hi = P.total;
-    if (va.out_off >= hi) return;
-    const uint64_t be = va.body_start + va.body_len;
-    const uint64_t first = (va.out_off + 15) & ~uint64_t(15);
-    // slot 0: the chunk that starts inside the header (D < body_start)
-    if (first < hi && first < va.body_start)
-        edges[f * kEdgeSlots] = edge_chunk<kModeSer>(P, fa, first, va, vb, o1, o2);
-    // slot 1: the chunk reaching past the body end (frames are packed, so
-    // the next frame starts at be: one chunk at most)
-    uint64_t d0 = be >= 15 ? ((be - 15 + 15) & ~uint64_t(15)) : 0;
-    if (d0 < first) d0 = first;
-    if (d0 < va.body_start) d0 = (va.body_start + 15) & ~uint64_t(15);
-    if (d0 < hi) edges[f * kEdgeSlots + 1] = edge_chunk<kModeSer>(P, fa, d0, va, vb, o1, o2);
 }
 
 // Deserialize with reassembly (CFWS_DESERIALIZE_REASSEMBLE): the edge chunks
@@ -1049,8 +958,7 @@ xform_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
              const uint64_t* __restrict__ total_p, const uint64_t* __restrict__ base_p,
              uint64_t capacity, uint32_t n_frames, uint32_t klass, uint32_t sid,
              const cfws_frame_desc_t* __restrict__ parent, uint32_t edge_blocks,
-             const uint64_t* __restrict__ reasm_offs1, uint32_t edge_stride,
-             const uint4* __restrict__ edges)
+             const uint64_t* __restrict__ reasm_offs1, uint32_t edge_stride)
 {
     // Which workgroups are edge workgroups: the first edge_blocks, or (edge
     // stride s > 0) every s-th one, spread through the grid
@@ -1083,7 +991,6 @@ xform_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
     P.klass = klass;
     P.sid = sid;
     P.parent = parent;
-    P.edges = edges;
     if (has_edge_blocks(kMode) && is_edge) {
         const uint64_t t = uint64_t(eidx) * kThreads + threadIdx.x;
         if (edge_thread_frame(t) < n_frames) edge_frame<kMode>(P, edge_thread_frame(t), edge_thread_part(t));
@@ -1116,9 +1023,9 @@ xform_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
             if (base >= va.body_start && end <= va.body_start + va.body_len)
                 fast_region<kMode>(P, va, base, lane);
             else
-                two_frame_region<kMode>(P, f0, va, va, false, base, lane);   // partial body, one frame
+                two_frame_region<kMode>(P, va, va, base, lane);   // partial body, one frame
         } else if (f1 == f0 + 1 || offs[f0 + 2] >= end) {
-            two_frame_region<kMode>(P, f0, va, frame_view<kMode>(P, f0 + 1), true, base, lane);
+            two_frame_region<kMode>(P, va, frame_view<kMode>(P, f0 + 1), base, lane);
         } else {
             general_region<kMode>(P, f0, f1, base, lane);
         }
@@ -1594,14 +1501,6 @@ inline uint32_t xform_lds_bytes(int mode = -1, uint64_t frame_bytes = ~uint64_t(
     return kXformLdsDefault;
 }
 
-// WS serialize prepares its edge chunks (edge_prep_kernel) unless
-// CFWS_PREP_EDGES=0 (edge workgroups in the stream, the round-2 layout).
-inline bool prep_edges()
-{
-    static const bool v = env_knob("CFWS_PREP_EDGES", 1) != 0;
-    return v;
-}
-
 // One pass: the streaming kernel with its edge workgroups in front
 // (CFWS_EDGE_SPLIT=1: the edge chunks as a launch of their own after it, the
 // previous layout, kept for A/B).
@@ -1635,15 +1534,8 @@ void launch_streaming(const void* src, void* dst, const cfws_frame_desc_t* desc,
                       const uint64_t* total_p, const uint64_t* base_p, uint64_t regions,
                       uint64_t cap, size_t n, uint32_t klass, uint32_t sid, hipStream_t st,
                       const cfws_frame_desc_t* parent = nullptr, bool edges = true,
-                      const uint64_t* reasm_offs1 = nullptr, uint4* prep = nullptr)
+                      const uint64_t* reasm_offs1 = nullptr)
 {
-    // WS serialize with a prepared-edge buffer: the edge chunks are made by
-    // edge_prep_kernel first and stored by the region waves; no edge threads
-    if (kMode == kModeSer && prep && edges) {
-        edge_prep_kernel<<<grid_for(n, kThreads), kThreads, 0, st>>>(
-            static_cast<const uint8_t*>(src), desc, offs, total_p, cap, (uint32_t)n, prep);
-        edges = false;
-    }
     const bool split = edges && (edge_split() || !has_edge_blocks(kMode));
     const uint32_t eb = (edges && !split) ? grid_for(edge_threads(n), kThreads) : 0;
     const uint32_t sg = stream_grid(regions);
@@ -1658,7 +1550,7 @@ void launch_streaming(const void* src, void* dst, const cfws_frame_desc_t* desc,
     xform_kernel<kMode><<<eb + sg, kThreads, xform_lds_bytes(kMode, n ? cap / n : cap), st>>>(
         static_cast<const uint8_t*>(src), static_cast<uint8_t*>(dst), desc, status, offs, map,
         total_p, base_p, cap, (uint32_t)n, klass, sid, parent, eb, eb ? reasm_offs1 : nullptr,
-        stride, kMode == kModeSer ? prep : nullptr);
+        stride);
     // (a separate edge launch on a second stream, overlapping the streaming
     // kernel, measured no faster on config 5: the stream slowed by what the
     // overlap saved)
@@ -1681,8 +1573,7 @@ void launch_pass(const WsLayout& L, int p, const void* src, void* dst, const cfw
     launch_streaming<kMode>(src, dst, desc, status, ws_ptr<const uint64_t>(ws, L.offs[p]),
                             ws_ptr<const uint32_t>(ws, L.map[p]), hdr + p,
                             p == 1 ? hdr + 2 : nullptr, regions, cap, n, klass, sid, st, nullptr,
-                            edges, reasm_edges ? ws_ptr<const uint64_t>(ws, L.offs[1]) : nullptr,
-                            kMode == kModeSer && prep_edges() ? ws_ptr<uint4>(ws, L.edges) : nullptr);
+                            edges, reasm_edges ? ws_ptr<const uint64_t>(ws, L.offs[1]) : nullptr);
 }
 
 }  // namespace
