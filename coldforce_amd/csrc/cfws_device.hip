@@ -562,7 +562,7 @@ int deserialize_plan_impl(const void* d_wire, uint64_t wire_size, const uint64_t
         return set_err(CFWS_ERROR_INVALID_ARGUMENT, "unknown flags", hipSuccess);
     const WsLayout L = ws_layout(n, cap);
     if (!ws || ws_size < L.bytes) return set_err(CFWS_ERROR_WORKSPACE, "workspace too small", hipSuccess);
-    if (n > kMapFrame) return set_err(CFWS_ERROR_INVALID_ARGUMENT, "too many frames (limit 2^31 - 1)", hipSuccess);
+    if (n > 0xffffffffull) return set_err(CFWS_ERROR_INVALID_ARGUMENT, "too many frames", hipSuccess);
     hipStream_t st = static_cast<hipStream_t>(stream);
     if (n == 0) return zero_totals(L, ws, d_total, st);
     if (!d_wire || !d_index || !d_desc || !d_status)
@@ -611,7 +611,7 @@ int cfws_serialize_plan(cfws_frame_desc_t* d_desc, size_t n, uint64_t cap, uint6
     if (int rc = check_init()) return rc;
     const WsLayout L = ws_layout(n, cap);
     if (!ws || ws_size < L.bytes) return set_err(CFWS_ERROR_WORKSPACE, "workspace too small", hipSuccess);
-    if (n > kMapFrame) return set_err(CFWS_ERROR_INVALID_ARGUMENT, "too many frames (limit 2^31 - 1)", hipSuccess);
+    if (n > 0xffffffffull) return set_err(CFWS_ERROR_INVALID_ARGUMENT, "too many frames", hipSuccess);
     hipStream_t st = static_cast<hipStream_t>(stream);
     if (n == 0) return zero_totals(L, ws, d_total, st);
     if (!d_desc) return set_err(CFWS_ERROR_INVALID_ARGUMENT, "null descriptor table", hipSuccess);

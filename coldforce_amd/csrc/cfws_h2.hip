@@ -117,7 +117,7 @@ h2_finalize_kernel(cfws_frame_desc_t* __restrict__ ddesc, uint64_t* __restrict__
     const uint64_t a = lo < total ? lo : total, b = hi < total ? hi : total;
     if (b > a) {
         const uint64_t r1 = (b + kRegion - 1) / kRegion;
-        for (uint64_t r = (a + kRegion - 1) / kRegion; r < r1; ++r) map[r] = map_entry(r, lo, d);
+        for (uint64_t r = (a + kRegion - 1) / kRegion; r < r1; ++r) map[r] = (uint32_t)d;
     }
     if (d == n_max - 1) {
         map[(total + kRegion - 1) / kRegion] = (uint32_t)(n_max - 1);

@@ -84,20 +84,6 @@ __host__ __device__ constexpr bool is_ser(int mode) { return mode != kModeDeser;
 // ---------------------------------------------------------------------------
 // hdr[0] pass-0 total (clamped)   hdr[1] pass-1 total (clamped)
 // hdr[2] pass-1 output base       hdr[3] pass-0 grand total   hdr[4] pass-1 grand
-// Region-map entries: the frame holding the region's first byte, with the
-// top bit set when that frame starts exactly there. A region's last frame
-// is then its successor's entry, minus one when the successor's frame
-// starts exactly at the region's end -- read in the same round as its own
-// entry, where the frame offsets used to take a dependent round (§3.1).
-// Frame ids are therefore below 2^31.
-constexpr uint32_t kMapFrame = 0x7fffffffu;
-constexpr uint32_t kMapStartsHere = 0x80000000u;
-
-__device__ __forceinline__ uint32_t map_entry(uint64_t r, uint64_t lo, uint64_t f)
-{
-    return (uint32_t)f | (r * kRegion == lo ? kMapStartsHere : 0u);
-}
-
 struct WsLayout {
     uint64_t hdr;
     uint64_t offs[2];      // u64[n] per pass: sizes, then exclusive offsets
@@ -1021,14 +1007,13 @@ xform_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
         const uint64_t end = base + kRegion;
         // The plan writes every entry in [0, n_regions]; the clamps only keep
         // a corrupted workspace from turning into an out-of-bounds read.
-        const uint32_t m0 = region_map[r], m1 = region_map[r + 1];
-        uint32_t f0 = m0 & kMapFrame;
-        uint32_t f1 = m1 & kMapFrame;
+        uint32_t f0 = region_map[r];
+        uint32_t f1 = region_map[r + 1];
         if (f1 >= n_frames) f1 = n_frames - 1;
         if (f0 > f1) f0 = f1;
-        // region_map[r + 1] holds the NEXT region's first byte; its frame
-        // does not touch this region when it starts exactly at our end
-        if ((m1 & kMapStartsHere) && f1 > f0) --f1;
+        // region_map[r + 1] holds the NEXT region's first byte; frames that
+        // start at or after this region's end do not touch it.
+        if (f1 > f0 && offs[f0 + 1] >= end) f1 = f0;
         if (end > P.total) {                  // the pass end (a capacity cut may fall in a body)
             tail_region<kMode>(P, f0, f1, base, lane);
             continue;
@@ -1039,7 +1024,7 @@ xform_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
                 fast_region<kMode>(P, va, base, lane);
             else
                 two_frame_region<kMode>(P, va, va, base, lane);   // partial body, one frame
-        } else if (f1 == f0 + 1) {
+        } else if (f1 == f0 + 1 || offs[f0 + 2] >= end) {
             two_frame_region<kMode>(P, va, frame_view<kMode>(P, f0 + 1), base, lane);
         } else {
             general_region<kMode>(P, f0, f1, base, lane);
@@ -1276,7 +1261,7 @@ __device__ __forceinline__ void map_regions(const uint64_t* __restrict__ offs, u
     const uint64_t b = hi < total ? hi : total;
     if (b > a) {
         const uint64_t r1 = (b + kRegion - 1) / kRegion;
-        for (uint64_t r = (a + kRegion - 1) / kRegion; r < r1; ++r) map[r] = map_entry(r, lo, f);
+        for (uint64_t r = (a + kRegion - 1) / kRegion; r < r1; ++r) map[r] = (uint32_t)f;
     }
     if (f == n - 1) map[(total + kRegion - 1) / kRegion] = (uint32_t)(n - 1);
 }
@@ -1290,7 +1275,7 @@ __device__ __forceinline__ void map_range(uint64_t lo, uint64_t hi, uint64_t f, 
     const uint64_t b = hi < total ? hi : total;
     if (b > a) {
         const uint64_t r1 = (b + kRegion - 1) / kRegion;
-        for (uint64_t r = (a + kRegion - 1) / kRegion; r < r1; ++r) map[r] = map_entry(r, lo, f);
+        for (uint64_t r = (a + kRegion - 1) / kRegion; r < r1; ++r) map[r] = (uint32_t)f;
     }
 }
 

@@ -693,7 +693,7 @@ int cfws_encode_headers(cfws_frame_desc_t* d_desc, size_t n, void* d_wire, uint6
     if (int rc = check_init()) return rc;
     if (n == 0) return CFWS_OK;
     if (!d_desc || !d_wire) return set_err(CFWS_ERROR_INVALID_ARGUMENT, "null pointer", hipSuccess);
-    if (n > kMapFrame) return set_err(CFWS_ERROR_INVALID_ARGUMENT, "too many frames (limit 2^31 - 1)", hipSuccess);
+    if (n > 0xffffffffull) return set_err(CFWS_ERROR_INVALID_ARGUMENT, "too many frames", hipSuccess);
     encode_headers_kernel<<<grid_for(n, kThreads), kThreads, 0, static_cast<hipStream_t>(stream)>>>(
         d_desc, n, static_cast<uint8_t*>(d_wire), wire_capacity);
     return launch_check("encode_headers");
