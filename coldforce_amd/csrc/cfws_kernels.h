@@ -251,6 +251,15 @@ __device__ __forceinline__ uint32_t from_next_lane(uint32_t v, uint32_t last)
     return __builtin_amdgcn_update_dpp(last, v, 0x130, 0xf, 0xf, false);
 }
 
+// lane i <- lane i + 1, lane 63 <- lane 0 (DPP wave_rol:1)
+__device__ __forceinline__ uint4 from_next_lane_wrap(const uint4& v)
+{
+    return make_uint4(__builtin_amdgcn_update_dpp(0u, v.x, 0x134, 0xf, 0xf, false),
+                      __builtin_amdgcn_update_dpp(0u, v.y, 0x134, 0xf, 0xf, false),
+                      __builtin_amdgcn_update_dpp(0u, v.z, 0x134, 0xf, 0xf, false),
+                      __builtin_amdgcn_update_dpp(0u, v.w, 0x134, 0xf, 0xf, false));
+}
+
 __device__ __forceinline__ uint4 from_next_lane(const uint4& v, const uint4& last)
 {
     return make_uint4(from_next_lane(v.x, last.x), from_next_lane(v.y, last.y),

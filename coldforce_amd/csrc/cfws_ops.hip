@@ -58,15 +58,78 @@ parse_headers_kernel(const uint8_t* __restrict__ wire, uint64_t size, const uint
 // so a 64 KiB frame is 4 equal workgroups at any alignment. Stores are
 // write-through and the mask runs at 4 workgroups per CU, the unmask at 5,
 // as the streaming kernel (+0.6 % over `nt` stores and interleaved spans,
-// tools/split_ab.sh). Chunks inside the frame are one
-// 16-byte store (source funnel-shifted into place; a lane's second source
-// block comes from the next lane over DPP). The frame's first and last
-// chunk, which it may share with its neighbours, are assembled the same way
-// from the (at most two) source blocks holding their bytes and stored byte
-// by byte from registers.
+// tools/split_ab.sh). A run is straight-line buffer loads and stores over
+// descriptors clipped to it (xor_run); the frame's first and last chunk,
+// which it may share with its neighbours, are stored byte by byte from
+// registers. Round 3 took the per-lane bounds and per-store descriptor
+// work out of the slots: 1.59 / 1.42 ms -> 1.47 / 1.38 ms (mask / unmask,
+// config 2 layout, profiles/r03_split_ab/).
+#ifndef CFWS_MASK_LDS
+#define CFWS_MASK_LDS 40000
+#endif
+#ifndef CFWS_UNMASK_LDS
+#define CFWS_UNMASK_LDS 32000
+#endif
 constexpr uint32_t kPieceK = 5;
 constexpr uint32_t kSpanChunks = 64;
 constexpr uint32_t kPieceSpans = kPieceK * kWaves;
+
+// One wave's run of up to kPieceK 1 KiB spans of a frame: every lane of every
+// slot loads and stores; buffer descriptors clipped to the run and the frame
+// make the loads outside them return zeros and the stores outside them drop,
+// so there is no branch but the frame's two partial chunks. Lane l of slot k
+// reads the aligned source block at offset sd + 1024 k + 16 l of rs
+// (funnel-shifted with the next lane's block over DPP; the block after slot
+// k < 4 is lane 0 of slot k + 1, rotated into lane 63) and writes the chunk
+// at offset dd + 1024 k + 16 l of rd. kEdge: the run holds the frame's first
+// or last span, so it may start below a descriptor's base (sd or dd
+// negative) -- offsets then go out of range explicitly, never by 32-bit
+// wrap-around -- and may hold a partial chunk, stored byte by byte. Without
+// it (every other run) the slots are straight-line loads and stores: the
+// per-slot edge test alone cost the unmask 7 % (1.46 against 1.37 ms).
+template <bool kEdge>
+__device__ __forceinline__ void xor_run(__amdgpu_buffer_rsrc_t rs, __amdgpu_buffer_rsrc_t rd, int32_t sd, int32_t dd,
+                                        uint32_t ph, uint32_t kr, uint8_t* __restrict__ dst, uint64_t wb,
+                                        uint32_t cnt, uint64_t dof, uint64_t dend, uint64_t pspan0, uint64_t pspan1)
+{
+    constexpr uint64_t kSpan = kSpanChunks * 16;
+    const uint32_t lane = threadIdx.x & 63u;
+    auto off = [](int32_t o) { return kEdge ? (o < 0 ? 0x7fffffff : o) : o; };
+    u32x4 a[kPieceK], ex = {0, 0, 0, 0};
+#pragma unroll
+    for (int k = 0; k < (int)kPieceK; ++k)
+        a[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, off(sd + (int32_t)(lane * 16 + k * kSpan)), 0, 0);
+    if (ph && lane == 63) ex = __builtin_amdgcn_raw_buffer_load_b128(rs, off(sd + (int32_t)(kPieceK * kSpan)), 0, 0);
+#pragma unroll
+    for (int k = 0; k < (int)kPieceK; ++k) {
+        const uint4 A4 = make_uint4(a[k][0], a[k][1], a[k][2], a[k][3]);
+        uint4 o = A4;
+        if (ph) {
+            const uint4 L = k + 1 < (int)kPieceK
+                                ? from_next_lane_wrap(make_uint4(a[k + 1][0], a[k + 1][1], a[k + 1][2], a[k + 1][3]))
+                                : make_uint4(ex[0], ex[1], ex[2], ex[3]);
+            o = funnel16(A4, from_next_lane(A4, L), ph);
+        }
+        xor4(o, kr);
+        // write-through, as the streaming kernel's regions (sc0 sc1 nt)
+        const u32x4 v = {o.x, o.y, o.z, o.w};
+        __builtin_amdgcn_raw_buffer_store_b128(v, rd, off(dd + (int32_t)(lane * 16 + k * kSpan)), 0, 19);
+        // the frame's first and last chunk when partial (shared with its
+        // neighbours, in spans pspan0 / pspan1, ~0 when none): the frame's
+        // bytes only, one by one
+        const uint64_t span = wb + uint64_t(k);
+        if (!kEdge || (uint32_t)k >= cnt || (span != pspan0 && span != pspan1)) continue;
+        const uint64_t A = span * kSpan + lane * 16;
+        if ((A < dof && A + 16 > dof) || (A < dend && A + 16 > dend)) {
+            const uint32_t jb = A < dof ? (uint32_t)(dof - A) : 0u;
+            const uint32_t je = A + 16 <= dend ? 16u : (uint32_t)(dend - A);
+            const uint32_t ow[4] = {o.x, o.y, o.z, o.w};
+#pragma unroll
+            for (uint32_t j = 0; j < 16; ++j)
+                if (j >= jb && j < je) dst[A + j] = (uint8_t)(ow[j >> 2] >> (8 * (j & 3u)));
+        }
+    }
+}
 
 template <bool kUnmask>
 __global__ void __launch_bounds__(kThreads)
@@ -92,74 +155,45 @@ payload_xor_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
     const uint64_t used = (ns + kPieceSpans - 1) / kPieceSpans;
     // source phase against the 16-byte destination chunks: one per frame
     const uint32_t ph = (uint32_t)((so - dof) & 15u);
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t wave = threadIdx.x >> 6;
+    // wave-uniform, so the span bases and buffer descriptors stay scalar (a
+    // descriptor the compiler cannot prove uniform costs a readfirstlane loop
+    // per store)
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    // the key rotation of every 16-byte destination chunk: A - dof = -dof mod 4
+    const uint32_t kr = rotr8(key, (uint32_t)((0u - (uint32_t)dof) & 3u));
+    constexpr uint64_t kSpan = kSpanChunks * 16;
+    // the aligned source blocks holding the frame's bytes, [xs0, xs1), and
+    // the destination chunks the frame fills whole, [xd0, xd1)
+    const int64_t xs0 = (int64_t)(so & ~uint64_t(15)), xs1 = (int64_t)((so + (dend - dof) + 15) & ~uint64_t(15));
+    const uint64_t xd0 = (dof + 15) & ~uint64_t(15), xd1 = dend & ~uint64_t(15);
+    // the spans holding a partial first / last chunk (~0: none)
+    const uint64_t pspan0 = (dof & 15u) ? s0 : ~uint64_t(0), pspan1 = (dend & 15u) ? s1 - 1 : ~uint64_t(0);
     // virtual pieces p, p + pieces, ...: a frame larger than the caller's
     // max_payload_size (or a grid capped below 2^31 blocks) still gets every
     // chunk written
     for (uint64_t vp = p; vp < used; vp += pieces) {
         const uint64_t sb = s0 + ns * vp / used, se_piece = s0 + ns * (vp + 1) / used;
-        // wave w streams a contiguous run of the piece's spans
+        // wave w streams a contiguous run of the piece's spans, [wb, se)
         const uint64_t m = se_piece - sb;
         const uint64_t wb = sb + m * wave / kWaves, se = sb + m * (wave + 1) / kWaves;
-        uint4 a[kPieceK], e[kPieceK];
-        uint32_t full = 0, part = 0, own_b = 0;
-#pragma unroll
-        for (int k = 0; k < (int)kPieceK; ++k) {
-            const uint64_t span = wb + uint64_t(k);
-            const uint64_t A = (span * kSpanChunks + lane) * 16;
-            a[k] = make_uint4(0, 0, 0, 0);
-            e[k] = make_uint4(0, 0, 0, 0);
-            if (span >= se || A + 16 <= dof || A >= dend) continue;
-            // the aligned source blocks of the window this chunk funnels from
-            const int64_t w = (int64_t)so + (int64_t)A - (int64_t)dof;
-            const int64_t wa = w - (w & 15);
-            if (A >= dof && A + 16 <= dend) {
-                full |= 1u << k;
-                a[k] = ld16(src + wa);
-                // the block holding the chunk's last source byte, when the
-                // next lane does not load it: lane 63 (the span's last chunk)
-                // or a partial chunk next
-                if (ph && (lane == 63 || A + 32 > dend)) {
-                    e[k] = ld16(src + wa + 16);
-                    own_b |= 1u << k;
-                }
-            } else {
-                // the frame's first or last chunk: only the blocks that hold
-                // its bytes (wa >= 0 whenever s_lo < wa + 16)
-                part |= 1u << k;
-                const uint64_t lo = A > dof ? A : dof, hi = A + 16 < dend ? A + 16 : dend;
-                const int64_t s_lo = (int64_t)so + (int64_t)(lo - dof);
-                const int64_t s_hi = (int64_t)so + (int64_t)(hi - 1 - dof);
-                if (s_lo < wa + 16) a[k] = ld16(src + wa);
-                if (s_hi >= wa + 16) e[k] = ld16(src + wa + 16);
-            }
-        }
-#pragma unroll
-        for (int k = 0; k < (int)kPieceK; ++k) {
-            const uint4 nb = from_next_lane(a[k], e[k]);     // every lane: DPP needs the full wave
-            const uint64_t span = wb + uint64_t(k);
-            const uint64_t A = (span * kSpanChunks + lane) * 16;
-            if ((full >> k) & 1u) {
-                uint4 o = ph ? funnel16(a[k], (own_b >> k) & 1u ? e[k] : nb, ph) : a[k];
-                xor4(o, rotr8(key, (uint32_t)((A - dof) & 3u)));
-                // write-through over the span, as the streaming kernel's
-                // regions (sc0 sc1 nt)
-                const u32x4 v = {o.x, o.y, o.z, o.w};
-                const auto r = __builtin_amdgcn_make_buffer_rsrc(dst + span * kSpanChunks * 16, 0,
-                                                                 (int)(kSpanChunks * 16), 0x00020000);
-                __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)(lane * 16), 0, 19);
-            } else if ((part >> k) & 1u) {
-                uint4 o = ph ? funnel16(a[k], e[k], ph) : a[k];
-                xor4(o, rotr8(key, (uint32_t)((A - dof) & 3u)));
-                const uint32_t jb = A < dof ? (uint32_t)(dof - A) : 0u;
-                const uint32_t je = A + 16 <= dend ? 16u : (uint32_t)(dend - A);
-                const uint32_t ow[4] = {o.x, o.y, o.z, o.w};
-#pragma unroll
-                for (uint32_t j = 0; j < 16; ++j)
-                    if (j >= jb && j < je) dst[A + j] = (uint8_t)(ow[j >> 2] >> (8 * (j & 3u)));
-            }
-        }
+        const uint32_t cnt = (uint32_t)(se - wb);
+        // descriptors over the run's source blocks and whole destination
+        // chunks, clipped to the frame's (xor_run); lane l of span wb + k
+        // reads the aligned source block at vb + 1024 k + 16 l
+        const int64_t vb = (int64_t)so + (int64_t)(wb * kSpan) - (int64_t)dof - (int64_t)ph;
+        const int64_t ve = vb + (int64_t)(cnt * kSpan) + 16;
+        const int64_t ls = vb > xs0 ? vb : xs0, le = ve < xs1 ? ve : xs1;
+        const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(src) + (le > ls ? ls : 0), 0,
+                                                          le > ls ? (int)(le - ls) : 0, 0x00020000);
+        const int32_t sd = (int32_t)(vb - ls);
+        const uint64_t ds = wb * kSpan > xd0 ? wb * kSpan : xd0, de = se * kSpan < xd1 ? se * kSpan : xd1;
+        const auto rd = __builtin_amdgcn_make_buffer_rsrc(dst + (de > ds ? ds : 0), 0,
+                                                          de > ds ? (int)(de - ds) : 0, 0x00020000);
+        const int32_t ddl = (int32_t)((int64_t)(wb * kSpan) - (int64_t)ds);
+        if (sd < 0 || ddl < 0 || (pspan1 >= wb && pspan1 < se))
+            xor_run<true>(rs, rd, sd, ddl, ph, kr, dst, wb, cnt, dof, dend, pspan0, pspan1);
+        else
+            xor_run<false>(rs, rd, sd, ddl, ph, kr, dst, wb, cnt, dof, dend, pspan0, pspan1);
     }
 }
 
@@ -742,7 +776,7 @@ int launch_payload_xor(const void* src, void* dst, const cfws_frame_desc_t* d_de
         return set_err(CFWS_ERROR_INVALID_ARGUMENT, "arenas must be 16-byte aligned", hipSuccess);
     if (n > 0x7fffffffull) return set_err(CFWS_ERROR_INVALID_ARGUMENT, "too many frames", hipSuccess);
     const uint32_t pieces = payload_pieces(n, max_payload_size);
-    payload_xor_kernel<kUnmask><<<(uint32_t)(n * pieces), kThreads, kUnmask ? 32000 : 40000,
+    payload_xor_kernel<kUnmask><<<(uint32_t)(n * pieces), kThreads, kUnmask ? CFWS_UNMASK_LDS : CFWS_MASK_LDS,
                                   static_cast<hipStream_t>(stream)>>>(
         static_cast<const uint8_t*>(src), static_cast<uint8_t*>(dst), d_desc, d_status, n, pieces, cap);
     return launch_check(what);
