@@ -729,6 +729,12 @@ __device__ __forceinline__ void general_region_search(const Pass& P, uint32_t f0
 // output start, its body range, its source delta and its key rotated for
 // 16-aligned chunks. Each chunk then finds its frame by a binary search over
 // the lanes (shuffles) and loads only its source blocks.
+#ifndef CFWS_GENERAL_SCAN
+#define CFWS_GENERAL_SCAN 8
+#endif
+#ifndef CFWS_GENERAL_DIRECT
+#define CFWS_GENERAL_DIRECT 1
+#endif
 template <int kMode>
 __device__ __forceinline__ void general_region(const Pass& P, uint32_t f0, uint32_t f1, uint64_t base,
                                                uint32_t lane)
@@ -754,16 +760,37 @@ __device__ __forceinline__ void general_region(const Pass& P, uint32_t f0, uint3
     const uint8_t* sp[kUnroll];
     uint32_t ph[kUnroll], key[kUnroll];
     bool fast[kUnroll];
+    uint32_t js[kUnroll];
+    if (nf <= CFWS_GENERAL_SCAN) {
+        // few frames: count the frame starts <= r, each start read once into
+        // an SGPR (no LDS round trips; 1 KiB frames: send 1.813 -> 1.765 ms,
+        // receive 1.458 -> 1.437, profiles/r03_small_ab/)
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) js[u] = 0;
+        for (uint32_t c = 1; c < nf; ++c) {
+            const uint32_t oc = (uint32_t)__builtin_amdgcn_readlane((int)ro, (int)c);
+#pragma unroll
+            for (int u = 0; u < kUnroll; ++u)
+                js[u] += oc <= u * (uint32_t)kSlice + lane * (uint32_t)kChunk ? 1u : 0u;
+        }
+    } else {
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) {
+            const uint32_t r = u * (uint32_t)kSlice + lane * (uint32_t)kChunk;
+            uint32_t j = 0;                             // largest frame with start <= r
+#pragma unroll
+            for (uint32_t step = 32; step >= 1; step >>= 1) {
+                const uint32_t c = j + step;
+                const uint32_t oc = (uint32_t)__shfl((int)ro, (int)(c & 63u), 64);
+                if (c < nf && oc <= r) j = c;
+            }
+            js[u] = j;
+        }
+    }
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u) {
         const uint32_t r = u * (uint32_t)kSlice + lane * (uint32_t)kChunk;
-        uint32_t j = 0;                             // largest frame with start <= r
-#pragma unroll
-        for (uint32_t step = 32; step >= 1; step >>= 1) {
-            const uint32_t c = j + step;
-            const uint32_t oc = (uint32_t)__shfl((int)ro, (int)(c & 63u), 64);
-            if (c < nf && oc <= r) j = c;
-        }
+        const uint32_t j = js[u];
         const uint32_t rg = (uint32_t)__shfl((int)rng, (int)j, 64);
         const uint64_t d = (uint64_t)(uint32_t)__shfl((int)dlo, (int)j, 64) |
                            (uint64_t)(uint32_t)__shfl((int)dhi, (int)j, 64) << 32;
@@ -959,8 +986,11 @@ __host__ __device__ constexpr bool has_edge_blocks(int mode)
 #ifndef CFWS_H2SER_MIN_BLOCKS
 #define CFWS_H2SER_MIN_BLOCKS 5
 #endif
+#ifndef CFWS_XFORM_MIN_BLOCKS
+#define CFWS_XFORM_MIN_BLOCKS 5
+#endif
 template <int kMode>
-__global__ void __launch_bounds__(kThreads, kMode == kModeH2Ser ? CFWS_H2SER_MIN_BLOCKS : 5)
+__global__ void __launch_bounds__(kThreads, kMode == kModeH2Ser ? CFWS_H2SER_MIN_BLOCKS : CFWS_XFORM_MIN_BLOCKS)
 xform_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
              const cfws_frame_desc_t* __restrict__ desc, const int32_t* __restrict__ status,
              const uint64_t* __restrict__ offs, const uint32_t* __restrict__ region_map,
@@ -1020,13 +1050,25 @@ xform_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
         uint32_t f1 = region_map[r + 1];
         if (f1 >= n_frames) f1 = n_frames - 1;
         if (f0 > f1) f0 = f1;
-        // region_map[r + 1] holds the NEXT region's first byte; frames that
-        // start at or after this region's end do not touch it.
-        if (f1 > f0 && offs[f0 + 1] >= end) f1 = f0;
         if (end > P.total) {                  // the pass end (a capacity cut may fall in a body)
             tail_region<kMode>(P, f0, f1, base, lane);
             continue;
         }
+#if CFWS_GENERAL_DIRECT
+        // f0 + 1 and f0 + 2 start inside the region: a run of small frames,
+        // straight to the per-lane views without the offset round trip below
+        // (general_region ignores frames that start at or after the end).
+        // The receive only: 1 KiB frames 1.437 -> 1.385 ms, 256 B 1.758 ->
+        // 1.686; the send measured slower with it (256 B 2.74 -> 2.93 ms,
+        // profiles/r03_small_ab/)
+        if (kMode == kModeDeser && f1 >= f0 + 3) {
+            general_region<kMode>(P, f0, f1, base, lane);
+            continue;
+        }
+#endif
+        // region_map[r + 1] holds the NEXT region's first byte; frames that
+        // start at or after this region's end do not touch it.
+        if (f1 > f0 && offs[f0 + 1] >= end) f1 = f0;
         const FrameView va = frame_view<kMode>(P, f0);
         if (f0 == f1) {
             if (base >= va.body_start && end <= va.body_start + va.body_len)
