@@ -3,6 +3,7 @@
 # passes (instruction mix, wait/active cycles, levels) over
 # `bench.py --frames 4194304 --frame-size 1024`, edge chunks in a launch of
 # their own (CFWS_EDGE_SPLIT=1) so the region kernels are counted alone.
+# ARGS overrides the bench arguments (e.g. ARGS="--workload split").
 # Summary: python3 tools/pmc_kernels.py gpurun_out/$TAG
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-/root/repo}
@@ -15,5 +16,5 @@ i=0
 for C in "$P1" "$P2" "$P3"; do
   i=$((i+1))
   CFWS_EDGE_SPLIT=${EDGE_SPLIT:-1} timeout -s KILL 120 rocprofv3 --pmc $C --output-format csv -d "$OUT/p$i" -o p -- \
-    python3 $R/bench.py --frames ${FRAMES:-4194304} --frame-size ${FS:-1024} --steps 2 --warmup 1 --no-cpu-baseline > "$OUT/p$i.log" 2>&1 || exit 1
+    python3 $R/bench.py ${ARGS:---frames 4194304 --frame-size 1024} --steps 2 --warmup 1 --no-cpu-baseline > "$OUT/p$i.log" 2>&1 || exit 1
 done
