@@ -26,6 +26,7 @@ s c4 400 python3 $R/bench.py --workload config4 --no-cpu-baseline
 s c5 200 python3 $R/bench.py --workload config5 --no-cpu-baseline
 s c5_64k 200 python3 $R/bench.py --workload config5 --frame-size 65536 --no-cpu-baseline
 s fs1k 200 python3 $R/bench.py --frames 4194304 --frame-size 1024 --no-cpu-baseline
+s fs256 200 python3 $R/bench.py --frames 16777216 --frame-size 256 --no-cpu-baseline
 s split 200 python3 $R/bench.py --workload split --no-cpu-baseline
 s index 200 python3 $R/bench.py --workload index
 s accept 200 python3 $R/bench.py --workload accept
@@ -34,6 +35,7 @@ s kt 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt" -o kt
 s fetch 200 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch" -o fetch -- python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline
 s write 200 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write" -o write -- python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline
 s kt_c5 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt_c5" -o kt -- python3 $R/bench.py --workload config5 --steps 10 --warmup 2 --no-cpu-baseline
+s kt_fs1k 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt_fs1k" -o kt -- python3 $R/bench.py --frames 4194304 --frame-size 1024 --steps 10 --warmup 2 --no-cpu-baseline
 s kt_split 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt_split" -o kt -- python3 $R/bench.py --workload split --steps 10 --warmup 2 --no-cpu-baseline
 cd $R
 s config1 400 python3 $R/tools/config1_bench.py --out "$OUT/config1.jsonl" --reps 2
