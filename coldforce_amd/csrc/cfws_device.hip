@@ -250,6 +250,197 @@ deserialize_plan_reduce_kernel(const uint8_t* __restrict__ wire, uint64_t wire_s
     }
 }
 
+// Single-pass plans (plan_lookback): the reduce and apply kernels above in
+// one launch, for plans of more than kSelfScanBlocks blocks (no scan launch,
+// no second read of the sizes). A block takes kThreads x kSingleItems frames,
+// each wave a contiguous kSingleItems x 64 of them (item k, lane l: frame k * 64 + l of
+// the wave's run, so every load is coalesced): the look-back's cost is a
+// device-scope round trip per 64 blocks, and 16 K blocks of 256 frames spent
+// 232 us on it for 4 M frames. With a capacity cut the region map clips at
+// the capacity itself: a frame's range ends at or below the grand total, so
+// that is the same clip as at min(total, capacity).
+#ifndef CFWS_SINGLE_ITEMS_SER
+#define CFWS_SINGLE_ITEMS_SER 16
+#endif
+#ifndef CFWS_SINGLE_ITEMS_DESER
+#define CFWS_SINGLE_ITEMS_DESER 8
+#endif
+constexpr int kSingleItemsSer = CFWS_SINGLE_ITEMS_SER;
+constexpr int kSingleItemsDeser = CFWS_SINGLE_ITEMS_DESER;
+
+// The wave-exclusive prefixes of v[k] in frame order (k-major), and the
+// wave's total.
+template <int kSingleItems>
+__device__ __forceinline__ uint64_t wave_scan_items(const uint64_t (&v)[kSingleItems], uint64_t (&ex)[kSingleItems])
+{
+    const uint32_t lane = threadIdx.x & 63u;
+    uint64_t run = 0;
+#pragma unroll
+    for (int k = 0; k < kSingleItems; ++k) {
+        uint64_t inc = v[k];
+#pragma unroll
+        for (uint32_t o = 1; o < 64; o <<= 1) {
+            const uint64_t y = __shfl_up(inc, o, 64);
+            if (lane >= o) inc += y;
+        }
+        ex[k] = run + inc - v[k];
+        run += __shfl(inc, 63, 64);
+    }
+    return run;
+}
+
+// This block's exclusive prefix from the look-back, plus each wave's offset
+// within the block (s_wave: the waves' totals).
+__device__ __forceinline__ uint64_t single_block_prefix(uint32_t b, uint64_t wave_total, uint64_t* s_wave,
+                                                        uint64_t* s_prefix, uint32_t* look, uint64_t* agg,
+                                                        uint64_t* incl)
+{
+    const uint32_t wid = threadIdx.x >> 6;
+    if ((threadIdx.x & 63u) == 0) s_wave[wid] = wave_total;
+    __syncthreads();
+    uint64_t before = 0, all = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < kWaves; ++w) {
+        if (w < wid) before += s_wave[w];
+        all += s_wave[w];
+    }
+    if (wid == 0) {
+        const uint64_t pre = plan_lookback(b, all, look + 1, agg, incl);
+        if (threadIdx.x == 0) *s_prefix = pre;
+    }
+    __syncthreads();
+    return *s_prefix + before;
+}
+
+__global__ void __launch_bounds__(kThreads)
+serialize_plan_single_kernel(cfws_frame_desc_t* __restrict__ desc, uint64_t* __restrict__ offs, uint64_t n,
+                             uint32_t* __restrict__ look, uint64_t* __restrict__ agg,
+                             uint64_t* __restrict__ incl, uint64_t* __restrict__ hdr, uint64_t capacity,
+                             uint32_t* __restrict__ map, uint64_t* __restrict__ user_total)
+{
+    __shared__ uint64_t s_wave[kWaves];
+    __shared__ uint64_t s_prefix;
+    __shared__ uint32_t s_bid;
+    constexpr int kSingleItems = kSingleItemsSer;
+    static_assert(kSingleItems <= 16, "4-bit header sizes in one word");
+    constexpr uint64_t kSingleFrames = uint64_t(kThreads) * kSingleItems;
+    const uint32_t b = plan_ticket(look, &s_bid);
+    const uint64_t f0 = uint64_t(b) * kSingleFrames + uint64_t(threadIdx.x >> 6) * (64 * kSingleItems) +
+                        (threadIdx.x & 63u);
+    uint64_t v[kSingleItems], ex[kSingleItems];
+    uint64_t hsp = 0;                                  // 4 bits per item: header sizes (2..14)
+#pragma unroll
+    for (int k = 0; k < kSingleItems; ++k) {
+        const uint64_t f = f0 + uint64_t(k) * 64;
+        v[k] = 0;
+        if (f < n) {
+            const uint64_t len = desc[f].payload_size;
+            const uint32_t hs = header_size_of(len, desc[f].mask != 0);
+            hsp |= uint64_t(hs) << (4 * k);
+            v[k] = hs + len;
+        }
+    }
+    const uint64_t pre = single_block_prefix(b, wave_scan_items(v, ex), s_wave, &s_prefix, look, agg, incl);
+#pragma unroll
+    for (int k = 0; k < kSingleItems; ++k) {
+        const uint64_t f = f0 + uint64_t(k) * 64;
+        if (f >= n) continue;
+        const uint64_t run = pre + ex[k];
+        offs[f] = run;
+        // both descriptor fields at once, so the line is written back once
+        desc[f].wire_off = run;
+        desc[f].header_size = (uint8_t)((hsp >> (4 * k)) & 15u);
+        map_range(run, run + v[k], f, capacity, map);
+        if (f == n - 1) {
+            const uint64_t g = run + v[k], t = g < capacity ? g : capacity;
+            map[(t + kRegion - 1) / kRegion] = (uint32_t)f;
+            hdr[0] = t;
+            hdr[3] = g;
+            if (user_total) *user_total = g;
+        }
+    }
+}
+
+// deserialize_plan_reduce_kernel + deserialize_plan_apply_kernel in one
+// launch, without reassembly (its control-frame pass starts at the data
+// pass's grand total, which no block knows before the last one). The
+// descriptors are written as parsed, their payload offsets (and the
+// capacity rule's status) once the offsets are known.
+__global__ void __launch_bounds__(kThreads)
+deserialize_plan_single_kernel(const uint8_t* __restrict__ wire, uint64_t wire_size_all,
+                               const uint64_t* __restrict__ index, const uint64_t* __restrict__ ends,
+                               uint64_t n, uint64_t max_payload, uint64_t align,
+                               cfws_frame_desc_t* __restrict__ desc, int32_t* __restrict__ status,
+                               uint64_t* __restrict__ offs, uint32_t* __restrict__ look,
+                               uint64_t* __restrict__ agg, uint64_t* __restrict__ incl,
+                               uint64_t* __restrict__ hdr, uint64_t capacity, uint32_t* __restrict__ map,
+                               uint64_t* __restrict__ user_total)
+{
+    __shared__ uint64_t s_wave[kWaves];
+    __shared__ uint64_t s_prefix;
+    __shared__ uint32_t s_bid;
+    constexpr int kSingleItems = kSingleItemsDeser;
+    constexpr uint64_t kSingleFrames = uint64_t(kThreads) * kSingleItems;
+    const uint32_t b = plan_ticket(look, &s_bid);
+    const uint64_t f0 = uint64_t(b) * kSingleFrames + uint64_t(threadIdx.x >> 6) * (64 * kSingleItems) +
+                        (threadIdx.x & 63u);
+    // each descriptor is written once, whole, with its offset: the parsed
+    // fields wait in registers (wire_off, payload_size, the last word)
+    uint64_t v[kSingleItems], ex[kSingleItems], wo[kSingleItems], ps[kSingleItems], w3[kSingleItems];
+    int32_t sts[kSingleItems];
+#pragma unroll
+    for (int k = 0; k < kSingleItems; ++k) {
+        const uint64_t f = f0 + uint64_t(k) * 64;
+        v[k] = 0;
+        if (f < n) {
+            const uint64_t wire_size = ends && ends[f] < wire_size_all ? ends[f] : wire_size_all;
+            cfws_frame_desc_t d;
+            sts[k] = parse_ws_header(wire, wire_size, index[f], max_payload, d);
+            wo[k] = d.wire_off;
+            ps[k] = d.payload_size;
+            w3[k] = (uint64_t)d.mask_key | (uint64_t)d.fin << 32 | (uint64_t)d.opcode << 40 |
+                    (uint64_t)d.mask << 48 | (uint64_t)d.header_size << 56;
+            const uint64_t len = (sts[k] == CFWS_PARSE_COMPLETE) ? d.payload_size : 0;
+            v[k] = (len + align - 1) & ~(align - 1);
+        }
+    }
+    const uint64_t pre = single_block_prefix(b, wave_scan_items(v, ex), s_wave, &s_prefix, look, agg, incl);
+#pragma unroll
+    for (int k = 0; k < kSingleItems; ++k) {
+        const uint64_t f = f0 + uint64_t(k) * 64;
+        if (f >= n) continue;
+        const uint64_t run = pre + ex[k];
+        offs[f] = run;
+        uint64_t* q = reinterpret_cast<uint64_t*>(desc) + 4 * f;
+        q[0] = run;
+        q[1] = wo[k];
+        q[2] = ps[k];
+        q[3] = w3[k];
+        // the capacity rule (co_ws_frame.c:216-223), as deserialize_plan_apply_kernel
+        int32_t st = sts[k];
+        if (st == CFWS_PARSE_COMPLETE && ps[k] > 0 && run + ps[k] > capacity) st = CFWS_ERROR_OUT_OF_MEMORY;
+        status[f] = st;
+        map_range(run, run + v[k], f, capacity, map);
+        if (f == n - 1) {
+            const uint64_t g = run + v[k], t = g < capacity ? g : capacity;
+            map[(t + kRegion - 1) / kRegion] = (uint32_t)f;
+            hdr[0] = t;
+            hdr[1] = 0;
+            hdr[2] = t;
+            hdr[3] = g;
+            if (user_total) *user_total = t;
+        }
+    }
+}
+
+// Single-pass plans above kSelfScanBlocks blocks (CFWS_PLAN_SINGLE=0: the
+// reduce / scan / apply launches everywhere; A/B knob).
+bool plan_single()
+{
+    static const bool v = env_knob("CFWS_PLAN_SINGLE", 1) != 0;
+    return v;
+}
+
 // ---------------------------------------------------------------------------
 // small batches: plan and stream in one launch per direction
 // ---------------------------------------------------------------------------
@@ -574,6 +765,16 @@ int deserialize_plan_impl(const void* d_wire, uint64_t wire_size, const uint64_t
     uint64_t* part0 = ws_ptr<uint64_t>(ws, L.partials[0]);
     uint64_t* part1 = ws_ptr<uint64_t>(ws, L.partials[1]);
     const uint32_t nb = grid_for(n, kPlanBlock);
+    if (!reasm && nb > kSelfScanBlocks && plan_single()) {
+        uint32_t* look = ws_ptr<uint32_t>(ws, L.look);
+        const uint32_t sb = grid_for(n, uint64_t(kThreads) * kSingleItemsDeser);
+        if (hipMemsetAsync(look, 0, 4 * (uint64_t(sb) + 1), st) != hipSuccess)
+            return launch_check("deserialize_plan");
+        deserialize_plan_single_kernel<<<sb, kThreads, 0, st>>>(
+            static_cast<const uint8_t*>(d_wire), wire_size, d_index, d_ends, n, max_payload, align, d_desc,
+            d_status, offs0, look, part0, part1, hdr, cap, ws_ptr<uint32_t>(ws, L.map[0]), d_total);
+        return launch_check("deserialize_plan");
+    }
     deserialize_plan_reduce_kernel<<<nb, kThreads, plan_lds_bytes(), st>>>(
         static_cast<const uint8_t*>(d_wire), wire_size, d_index, d_ends, n, max_payload, align, reasm,
         d_desc, d_status, offs0, offs1, part0, part1);
@@ -620,6 +821,16 @@ int cfws_serialize_plan(cfws_frame_desc_t* d_desc, size_t n, uint64_t cap, uint6
     uint64_t* partials = ws_ptr<uint64_t>(ws, L.partials[0]);
     const uint32_t nb = grid_for(n, kPlanBlock);
     const uint32_t self_scan = nb <= kSelfScanBlocks ? 1u : 0u;
+    if (!self_scan && plan_single()) {
+        uint32_t* look = ws_ptr<uint32_t>(ws, L.look);
+        const uint32_t sb = grid_for(n, uint64_t(kThreads) * kSingleItemsSer);
+        if (hipMemsetAsync(look, 0, 4 * (uint64_t(sb) + 1), st) != hipSuccess)
+            return launch_check("serialize_plan");
+        serialize_plan_single_kernel<<<sb, kThreads, 0, st>>>(d_desc, offs, n, look, partials,
+                                                              ws_ptr<uint64_t>(ws, L.partials[1]), hdr, cap,
+                                                              ws_ptr<uint32_t>(ws, L.map[0]), d_total);
+        return launch_check("serialize_plan");
+    }
     serialize_plan_reduce_kernel<<<nb, kThreads, plan_lds_bytes(), st>>>(d_desc, offs, n, partials);
     if (!self_scan) scan_partials_kernel<<<1, kThreads, 0, st>>>(partials, nb, hdr + 3);
     serialize_plan_apply_kernel<<<nb, kThreads, plan_lds_bytes(), st>>>(d_desc, offs, n, partials, nb, self_scan,

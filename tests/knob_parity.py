@@ -9,6 +9,8 @@ tests/test_knobs.py runs this script once per setting):
   CFWS_OCC_FRAME_MAX=0  no register-limited residency for small frames
   CFWS_XFORM_LDS=N      the LDS reservation for every mode
   CFWS_PLAN_LDS=N       LDS reserved by the plan kernels
+  CFWS_PLAN_SINGLE=0    plans of > 2,048 blocks as reduce / scan / apply
+                        launches instead of the single-pass look-back
 
 Each case is checked byte for byte against the oracle. Prints "KNOB OK".
 """
@@ -63,6 +65,8 @@ def main():
         roundtrip(sizes, rng, 1, align)
     # 1 KiB frames in a large batch (spread edges, register-limited residency)
     roundtrip(np.full(20000, 1024), rng, 2, 16, opcodes=np.full(20000, 1), fins=np.ones(20000))
+    # 600 K tiny frames: plans of > 2,048 blocks (single-pass unless CFWS_PLAN_SINGLE=0)
+    roundtrip(rng.integers(0, 31, 600000), rng, 4, 1)
     # a small batch (single-launch path unless CFWS_SMALL=0)
     roundtrip(np.full(256, 1000), rng, 3, 16)
     # fragments + pings, reassembled (two passes, pass-1 capped grid)

@@ -397,3 +397,36 @@ def test_device_copy():
         assert torch.equal(dst[:n], src[:n]) and int(dst[n:].sum()) == 0, n
     with pytest.raises(cfws.CodecError):
         cfws.device_copy(src, dst, 15)
+
+
+def test_single_pass_plans_capacity_and_errors():
+    """Plans of more than 2,048 blocks take the single-pass look-back form
+    (one launch, no block-sum scan): 700 K frames of 0-40 bytes against the
+    oracle, serialize cut by the capacity (the region map, the clamped
+    total, the unclamped total reported), then deserialize the wire with
+    invalid headers sprinkled in and a capacity that fails the later frames
+    with OUT_OF_MEMORY; both the batch and the plan + execute calls."""
+    n = 700_000
+    rng = np.random.default_rng(71)
+    payload = O.fill_splitmix(1 << 16, 71, 0)
+    desc = np.zeros(n, dtype=cfws.DESC_DTYPE)
+    desc["payload_size"] = rng.integers(0, 41, n).astype(np.uint64)
+    desc["payload_off"] = rng.integers(0, (1 << 16) - 64, n).astype(np.uint64)
+    desc["fin"] = 1
+    desc["opcode"] = 2
+    desc["mask"] = (rng.random(n) < 0.5).astype(np.uint8)
+    desc["mask_key"] = rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32) * desc["mask"]
+    wire, total = check_serialize(payload, desc)
+    exp = wire[:total].copy()
+    for pe in (False, True):
+        cap = total // 2 + 3
+        got, _, tot, _ = gpu_serialize(payload, desc, capacity=cap, plan_execute=pe)
+        assert tot == total
+        assert np.array_equal(got[:cap], exp[:cap]) and (got[cap:] == 0xEE).all()
+    offs, _ = W.wire_layout(desc)
+    bad = rng.choice(n, 300, replace=False)
+    w = exp.copy()
+    w[offs[bad].astype(np.int64)] |= 0x40                 # RSV2 -> INVALID_FRAME
+    for pe in (False, True):
+        check_deserialize(w, offs, align=1, plan_execute=pe)
+        check_deserialize(w, offs, align=16, capacity=total // 3, plan_execute=pe)
