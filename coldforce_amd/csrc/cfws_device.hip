@@ -329,16 +329,22 @@ serialize_plan_single_kernel(cfws_frame_desc_t* __restrict__ desc, uint64_t* __r
                         (threadIdx.x & 63u);
     uint64_t v[kSingleItems], ex[kSingleItems];
     uint64_t hsp = 0;                                  // 4 bits per item: header sizes (2..14)
+    // every item's loads in one round (frames past n read frame n - 1's:
+    // a branch per item made it a round trip per item)
+    uint64_t len[kSingleItems];
+    uint32_t msk[kSingleItems];
+#pragma unroll
+    for (int k = 0; k < kSingleItems; ++k) {
+        const uint64_t f = f0 + uint64_t(k) * 64, fc = f < n ? f : n - 1;
+        len[k] = desc[fc].payload_size;
+        msk[k] = desc[fc].mask;
+    }
 #pragma unroll
     for (int k = 0; k < kSingleItems; ++k) {
         const uint64_t f = f0 + uint64_t(k) * 64;
-        v[k] = 0;
-        if (f < n) {
-            const uint64_t len = desc[f].payload_size;
-            const uint32_t hs = header_size_of(len, desc[f].mask != 0);
-            hsp |= uint64_t(hs) << (4 * k);
-            v[k] = hs + len;
-        }
+        const uint32_t hs = header_size_of(len[k], msk[k] != 0);
+        hsp |= uint64_t(hs) << (4 * k);
+        v[k] = f < n ? hs + len[k] : 0;
     }
     const uint64_t pre = single_block_prefix(b, wave_scan_items(v, ex), s_wave, &s_prefix, look, agg, incl);
 #pragma unroll
@@ -388,14 +394,63 @@ deserialize_plan_single_kernel(const uint8_t* __restrict__ wire, uint64_t wire_s
     // fields wait in registers (wire_off, payload_size, the last word)
     uint64_t v[kSingleItems], ex[kSingleItems], wo[kSingleItems], ps[kSingleItems], w3[kSingleItems];
     int32_t sts[kSingleItems];
+    // the loads of all items first, in two rounds (starts and ends, then
+    // every header's five dwords, clamped to the buffer's last whole dword
+    // instead of branching on the bytes available), then the parses: a
+    // header per round trip serialized the wave (24 round trips for 8 items)
+    // (frames past n load frame n - 1's entries: no branch in the round)
+    uint64_t sx[kSingleItems], sz[kSingleItems];
+#pragma unroll
+    for (int k = 0; k < kSingleItems; ++k) {
+        const uint64_t f = f0 + uint64_t(k) * 64, fc = f < n ? f : n - 1;
+        sx[k] = index[fc];
+        sz[k] = wire_size_all;
+    }
+    if (ends) {
+#pragma unroll
+        for (int k = 0; k < kSingleItems; ++k) {
+            const uint64_t f = f0 + uint64_t(k) * 64, fc = f < n ? f : n - 1;
+            const uint64_t e = ends[fc];
+            sz[k] = e < wire_size_all ? e : wire_size_all;
+        }
+    }
+    const bool clamp = wire_size_all >= 8;
+    uint32_t hw[kSingleItems][5];
+    if (clamp) {
+        const uintptr_t last = ((uintptr_t)wire + wire_size_all - 4) & ~uintptr_t(3);
+#pragma unroll
+        for (int k = 0; k < kSingleItems; ++k) {
+            const uintptr_t a0 = ((uintptr_t)wire + sx[k]) & ~uintptr_t(3);
+#pragma unroll
+            for (int j = 0; j < 5; ++j) {
+                const uintptr_t a = a0 + 4 * j < last ? a0 + 4 * j : last;
+                hw[k][j] = *reinterpret_cast<const uint32_t*>(wire + (a - (uintptr_t)wire));
+            }
+        }
+    }
 #pragma unroll
     for (int k = 0; k < kSingleItems; ++k) {
         const uint64_t f = f0 + uint64_t(k) * 64;
         v[k] = 0;
         if (f < n) {
-            const uint64_t wire_size = ends && ends[f] < wire_size_all ? ends[f] : wire_size_all;
+            const uint64_t wire_size = sz[k];
             cfws_frame_desc_t d;
-            sts[k] = parse_ws_header(wire, wire_size, index[f], max_payload, d);
+            if (clamp) {
+                const uint64_t s0 = sx[k];
+                const uint64_t avail = s0 <= wire_size ? wire_size - s0 : 0;
+                const uint32_t o = (uint32_t)(((uintptr_t)wire + s0) & 3u);
+                const uint32_t kk = avail < 14 ? (uint32_t)avail : 14u;
+                const uint32_t nd = kk ? (o + kk + 3u) >> 2 : 0u;
+                uint32_t x[5], w[4];
+#pragma unroll
+                for (uint32_t j = 0; j < 5; ++j) x[j] = j < nd ? hw[k][j] : 0u;
+#pragma unroll
+                for (uint32_t t = 0; t < 4; ++t) w[t] = __builtin_amdgcn_alignbyte(x[t + 1], x[t], o);
+                sts[k] = parse_ws_header_regs(w, avail, max_payload, d);
+                d.wire_off = s0;
+            } else {
+                sts[k] = parse_ws_header(wire, wire_size, sx[k], max_payload, d);
+            }
             wo[k] = d.wire_off;
             ps[k] = d.payload_size;
             w3[k] = (uint64_t)d.mask_key | (uint64_t)d.fin << 32 | (uint64_t)d.opcode << 40 |
