@@ -56,9 +56,9 @@ parse_headers_kernel(const uint8_t* __restrict__ wire, uint64_t size, const uint
 // evenly over the fewest pieces of at most 20 spans, each wave taking a
 // contiguous run of up to 5 (every load in flight before the first store),
 // so a 64 KiB frame is 4 equal workgroups at any alignment. Stores are
-// write-through and both run at 4 workgroups per CU (the unmask at 5 until
-// the round-3 rewrite; at 4 since: 1.377 -> 1.349 ms), as the streaming kernel (+0.6 % over `nt` stores and interleaved spans,
-// tools/split_ab.sh). A run is straight-line buffer loads and stores over
+// write-through (+0.6 % over `nt` stores and interleaved spans,
+// tools/split_ab.sh) and both run at 4 workgroups per CU (the unmask ran
+// at 5 until the round-3 rewrite; at 4 since, 1.377 -> 1.349 ms). A run is straight-line buffer loads and stores over
 // descriptors clipped to it (xor_run); the frame's first and last chunk,
 // which it may share with its neighbours, are stored byte by byte from
 // registers. Round 3 took the per-lane bounds and per-store descriptor
