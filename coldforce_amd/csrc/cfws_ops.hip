@@ -100,8 +100,7 @@ __device__ __forceinline__ void xor_run(__amdgpu_buffer_rsrc_t rs, __amdgpu_buff
     for (int k = 0; k < (int)kPieceK; ++k)
         a[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, off(sd + (int32_t)(lane * 16 + k * kSpan)), 0, 0);
     if (ph && lane == 63) ex = __builtin_amdgcn_raw_buffer_load_b128(rs, off(sd + (int32_t)(kPieceK * kSpan)), 0, 0);
-#pragma unroll
-    for (int k = 0; k < (int)kPieceK; ++k) {
+    auto slot = [&](const int k) {
         const uint4 A4 = make_uint4(a[k][0], a[k][1], a[k][2], a[k][3]);
         uint4 o = A4;
         if (ph) {
@@ -118,17 +117,28 @@ __device__ __forceinline__ void xor_run(__amdgpu_buffer_rsrc_t rs, __amdgpu_buff
         // neighbours, in spans pspan0 / pspan1, ~0 when none): the frame's
         // bytes only, one by one
         const uint64_t span = wb + uint64_t(k);
-        if (!kEdge || (uint32_t)k >= cnt || (span != pspan0 && span != pspan1)) continue;
+        if (!kEdge || (uint32_t)k >= cnt || (span != pspan0 && span != pspan1)) return;
         const uint64_t A = span * kSpan + lane * 16;
         if ((A < dof && A + 16 > dof) || (A < dend && A + 16 > dend)) {
-            const uint32_t jb = A < dof ? (uint32_t)(dof - A) : 0u;
-            const uint32_t je = A + 16 <= dend ? 16u : (uint32_t)(dend - A);
+            // sixteen unconditional byte stores through a descriptor over
+            // the span's frame bytes (wave-uniform): the ones outside drop.
+            // These stores cost the mask 6 % (1.476 against 1.384 ms with
+            // them left out, which is wrong output); neither their order
+            // in the wave, dword stores for the whole dwords, `nt` nor
+            // straight-line code over a branch per byte changed that, and
+            // write-through bytes cost 57 % (profiles/r03_split_ab/bytes/).
+            const uint64_t S = span * kSpan;
+            const uint64_t bs = dof > S ? dof : S, be = dend < S + kSpan ? dend : S + kSpan;
+            const auto rb = __builtin_amdgcn_make_buffer_rsrc(dst + bs, 0, (int)(be - bs), 0x00020000);
+            const int32_t rel = (int32_t)((int64_t)A - (int64_t)bs);
             const uint32_t ow[4] = {o.x, o.y, o.z, o.w};
 #pragma unroll
-            for (uint32_t j = 0; j < 16; ++j)
-                if (j >= jb && j < je) dst[A + j] = (uint8_t)(ow[j >> 2] >> (8 * (j & 3u)));
+            for (int32_t j = 0; j < 16; ++j)
+                __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(ow[j >> 2] >> (8 * (j & 3))), rb, off(rel + j), 0, 0);
         }
-    }
+    };
+#pragma unroll
+    for (int k = 0; k < (int)kPieceK; ++k) slot(k);
 }
 
 template <bool kUnmask>
