@@ -395,10 +395,10 @@ deserialize_plan_single_kernel(const uint8_t* __restrict__ wire, uint64_t wire_s
     uint64_t v[kSingleItems], ex[kSingleItems], wo[kSingleItems], ps[kSingleItems], w3[kSingleItems];
     int32_t sts[kSingleItems];
     // the loads of all items first, in two rounds (starts and ends, then
-    // every header's five dwords, clamped to the buffer's last whole dword
+    // every header's two blocks, clamped to the buffer's last whole block
     // instead of branching on the bytes available), then the parses: a
-    // header per round trip serialized the wave (24 round trips for 8 items)
-    // (frames past n load frame n - 1's entries: no branch in the round)
+    // header per round trip serialized the wave (24 round trips for 8
+    // items). Frames past n load frame n - 1's entries: no branch in a round.
     uint64_t sx[kSingleItems], sz[kSingleItems];
 #pragma unroll
     for (int k = 0; k < kSingleItems; ++k) {
@@ -414,18 +414,19 @@ deserialize_plan_single_kernel(const uint8_t* __restrict__ wire, uint64_t wire_s
             sz[k] = e < wire_size_all ? e : wire_size_all;
         }
     }
-    const bool clamp = wire_size_all >= 8;
-    uint32_t hw[kSingleItems][5];
-    if (clamp) {
-        const uintptr_t last = ((uintptr_t)wire + wire_size_all - 4) & ~uintptr_t(3);
+    // a 16-byte-aligned buffer: every header from the two aligned 16-byte
+    // blocks that hold it (2 loads per header instead of 5 dwords); a header
+    // whose second block is not a whole block of the buffer (the last 32
+    // bytes) is parsed by the loads of parse_ws_header instead
+    const bool b16 = ((uintptr_t)wire & 15u) == 0 && wire_size_all >= 32;
+    const uint64_t lastb = (wire_size_all - 16) & ~uint64_t(15);
+    uint4 hb0[kSingleItems], hb1[kSingleItems];
+    if (b16) {
 #pragma unroll
         for (int k = 0; k < kSingleItems; ++k) {
-            const uintptr_t a0 = ((uintptr_t)wire + sx[k]) & ~uintptr_t(3);
-#pragma unroll
-            for (int j = 0; j < 5; ++j) {
-                const uintptr_t a = a0 + 4 * j < last ? a0 + 4 * j : last;
-                hw[k][j] = *reinterpret_cast<const uint32_t*>(wire + (a - (uintptr_t)wire));
-            }
+            const uint64_t a = sx[k] & ~uint64_t(15);
+            hb0[k] = ld16(wire + (a < lastb ? a : lastb));
+            hb1[k] = ld16(wire + (a + 16 < lastb ? a + 16 : lastb));
         }
     }
 #pragma unroll
@@ -435,21 +436,15 @@ deserialize_plan_single_kernel(const uint8_t* __restrict__ wire, uint64_t wire_s
         if (f < n) {
             const uint64_t wire_size = sz[k];
             cfws_frame_desc_t d;
-            if (clamp) {
-                const uint64_t s0 = sx[k];
+            const uint64_t s0 = sx[k], a = s0 & ~uint64_t(15);
+            if (b16 && a + 16 <= lastb) {
                 const uint64_t avail = s0 <= wire_size ? wire_size - s0 : 0;
-                const uint32_t o = (uint32_t)(((uintptr_t)wire + s0) & 3u);
-                const uint32_t kk = avail < 14 ? (uint32_t)avail : 14u;
-                const uint32_t nd = kk ? (o + kk + 3u) >> 2 : 0u;
-                uint32_t x[5], w[4];
-#pragma unroll
-                for (uint32_t j = 0; j < 5; ++j) x[j] = j < nd ? hw[k][j] : 0u;
-#pragma unroll
-                for (uint32_t t = 0; t < 4; ++t) w[t] = __builtin_amdgcn_alignbyte(x[t + 1], x[t], o);
+                const uint4 W = funnel16(hb0[k], hb1[k], (uint32_t)(s0 - a));
+                const uint32_t w[4] = {W.x, W.y, W.z, W.w};
                 sts[k] = parse_ws_header_regs(w, avail, max_payload, d);
                 d.wire_off = s0;
             } else {
-                sts[k] = parse_ws_header(wire, wire_size, sx[k], max_payload, d);
+                sts[k] = parse_ws_header(wire, wire_size, s0, max_payload, d);
             }
             wo[k] = d.wire_off;
             ps[k] = d.payload_size;
