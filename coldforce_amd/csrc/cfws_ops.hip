@@ -58,12 +58,13 @@ parse_headers_kernel(const uint8_t* __restrict__ wire, uint64_t size, const uint
 // so a 64 KiB frame is 4 equal workgroups at any alignment. Stores are
 // write-through (+0.6 % over `nt` stores and interleaved spans,
 // tools/split_ab.sh) and both run at 4 workgroups per CU (the unmask ran
-// at 5 until the round-3 rewrite; at 4 since, 1.377 -> 1.349 ms). A run is straight-line buffer loads and stores over
-// descriptors clipped to it (xor_run); the frame's first and last chunk,
-// which it may share with its neighbours, are stored byte by byte from
-// registers. Round 3 took the per-lane bounds and per-store descriptor
-// work out of the slots: 1.59 / 1.42 ms -> 1.47 / 1.38 ms (mask / unmask,
-// config 2 layout, profiles/r03_split_ab/).
+// at 5 until the round-3 rewrite; at 4 since, 1.377 -> 1.349 ms). A run is
+// straight-line buffer loads and stores over descriptors clipped to it
+// (xor_run); the frame's first and last chunk, which it may share with its
+// neighbours, are written byte by byte by payload_edge_kernel after the
+// stream. Round 3 took the per-lane bounds and per-store descriptor work out
+// of the slots: 1.59 / 1.42 ms -> 1.47 / 1.38 ms (mask / unmask, config 2
+// layout, profiles/r03_split_ab/).
 #ifndef CFWS_MASK_LDS
 #define CFWS_MASK_LDS 40000
 #endif
@@ -75,22 +76,20 @@ constexpr uint32_t kSpanChunks = 64;
 constexpr uint32_t kPieceSpans = kPieceK * kWaves;
 
 // One wave's run of up to kPieceK 1 KiB spans of a frame: every lane of every
-// slot loads and stores; buffer descriptors clipped to the run and the frame
-// make the loads outside them return zeros and the stores outside them drop,
-// so there is no branch but the frame's two partial chunks. Lane l of slot k
-// reads the aligned source block at offset sd + 1024 k + 16 l of rs
+// slot loads and stores; buffer descriptors clipped to the run and to the
+// frame's whole chunks make the loads outside them return zeros and the
+// stores outside them drop, so there is no branch. Lane l of slot k reads
+// the aligned source block at offset sd + 1024 k + 16 l of rs
 // (funnel-shifted with the next lane's block over DPP; the block after slot
 // k < 4 is lane 0 of slot k + 1, rotated into lane 63) and writes the chunk
 // at offset dd + 1024 k + 16 l of rd. kEdge: the run holds the frame's first
-// or last span, so it may start below a descriptor's base (sd or dd
-// negative) -- offsets then go out of range explicitly, never by 32-bit
-// wrap-around -- and may hold a partial chunk, stored byte by byte. Without
-// it (every other run) the slots are straight-line loads and stores: the
-// per-slot edge test alone cost the unmask 7 % (1.46 against 1.37 ms).
+// span and starts below a descriptor's base (sd or dd negative), so offsets
+// go out of range explicitly, never by 32-bit wrap-around. Without it
+// (every other run) the offsets are plain: a per-slot edge test cost the
+// unmask 7 % (1.46 against 1.37 ms).
 template <bool kEdge>
 __device__ __forceinline__ void xor_run(__amdgpu_buffer_rsrc_t rs, __amdgpu_buffer_rsrc_t rd, int32_t sd, int32_t dd,
-                                        uint32_t ph, uint32_t kr, uint8_t* __restrict__ dst, uint64_t wb,
-                                        uint32_t cnt, uint64_t dof, uint64_t dend, uint64_t pspan0, uint64_t pspan1)
+                                        uint32_t ph, uint32_t kr)
 {
     constexpr uint64_t kSpan = kSpanChunks * 16;
     const uint32_t lane = threadIdx.x & 63u;
@@ -113,29 +112,6 @@ __device__ __forceinline__ void xor_run(__amdgpu_buffer_rsrc_t rs, __amdgpu_buff
         // write-through, as the streaming kernel's regions (sc0 sc1 nt)
         const u32x4 v = {o.x, o.y, o.z, o.w};
         __builtin_amdgcn_raw_buffer_store_b128(v, rd, off(dd + (int32_t)(lane * 16 + k * kSpan)), 0, 19);
-        // the frame's first and last chunk when partial (shared with its
-        // neighbours, in spans pspan0 / pspan1, ~0 when none): the frame's
-        // bytes only, one by one
-        const uint64_t span = wb + uint64_t(k);
-        if (!kEdge || (uint32_t)k >= cnt || (span != pspan0 && span != pspan1)) return;
-        const uint64_t A = span * kSpan + lane * 16;
-        if ((A < dof && A + 16 > dof) || (A < dend && A + 16 > dend)) {
-            // sixteen unconditional byte stores through a descriptor over
-            // the span's frame bytes (wave-uniform): the ones outside drop.
-            // These stores cost the mask 6 % (1.476 against 1.384 ms with
-            // them left out, which is wrong output); neither their order
-            // in the wave, dword stores for the whole dwords, `nt` nor
-            // straight-line code over a branch per byte changed that, and
-            // write-through bytes cost 57 % (profiles/r03_split_ab/bytes/).
-            const uint64_t S = span * kSpan;
-            const uint64_t bs = dof > S ? dof : S, be = dend < S + kSpan ? dend : S + kSpan;
-            const auto rb = __builtin_amdgcn_make_buffer_rsrc(dst + bs, 0, (int)(be - bs), 0x00020000);
-            const int32_t rel = (int32_t)((int64_t)A - (int64_t)bs);
-            const uint32_t ow[4] = {o.x, o.y, o.z, o.w};
-#pragma unroll
-            for (int32_t j = 0; j < 16; ++j)
-                __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(ow[j >> 2] >> (8 * (j & 3))), rb, off(rel + j), 0, 0);
-        }
     };
 #pragma unroll
     for (int k = 0; k < (int)kPieceK; ++k) slot(k);
@@ -176,8 +152,6 @@ payload_xor_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
     // the destination chunks the frame fills whole, [xd0, xd1)
     const int64_t xs0 = (int64_t)(so & ~uint64_t(15)), xs1 = (int64_t)((so + (dend - dof) + 15) & ~uint64_t(15));
     const uint64_t xd0 = (dof + 15) & ~uint64_t(15), xd1 = dend & ~uint64_t(15);
-    // the spans holding a partial first / last chunk (~0: none)
-    const uint64_t pspan0 = (dof & 15u) ? s0 : ~uint64_t(0), pspan1 = (dend & 15u) ? s1 - 1 : ~uint64_t(0);
     // virtual pieces p, p + pieces, ...: a frame larger than the caller's
     // max_payload_size (or a grid capped below 2^31 blocks) still gets every
     // chunk written
@@ -200,10 +174,10 @@ payload_xor_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
         const auto rd = __builtin_amdgcn_make_buffer_rsrc(dst + (de > ds ? ds : 0), 0,
                                                           de > ds ? (int)(de - ds) : 0, 0x00020000);
         const int32_t ddl = (int32_t)((int64_t)(wb * kSpan) - (int64_t)ds);
-        if (sd < 0 || ddl < 0 || (pspan1 >= wb && pspan1 < se))
-            xor_run<true>(rs, rd, sd, ddl, ph, kr, dst, wb, cnt, dof, dend, pspan0, pspan1);
+        if (sd < 0 || ddl < 0)
+            xor_run<true>(rs, rd, sd, ddl, ph, kr);
         else
-            xor_run<false>(rs, rd, sd, ddl, ph, kr, dst, wb, cnt, dof, dend, pspan0, pspan1);
+            xor_run<false>(rs, rd, sd, ddl, ph, kr);
     }
 }
 
@@ -761,6 +735,38 @@ int cfws_parse_headers(const void* d_wire, uint64_t wire_size, const uint64_t* d
 
 namespace {
 
+// The frames' partial first and last chunks: one thread per frame writes
+// the frame's bytes of the (at most two) 16-byte destination chunks it
+// shares with its neighbours, byte by byte, in a launch after the stream.
+// (In the stream, the edge runs' byte stores held their workgroups' slots:
+// mask 1.482 ms there against 1.404 + 0.012 here, profiles/r03_split_ab/
+// edge_kernel/.)
+template <bool kUnmask>
+__global__ void __launch_bounds__(kThreads)
+payload_edge_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                    const cfws_frame_desc_t* __restrict__ desc, const int32_t* __restrict__ status,
+                    uint64_t n, uint64_t cap)
+{
+    const uint64_t f = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
+    if (f >= n) return;
+    if (kUnmask && status && status[f] != CFWS_PARSE_COMPLETE) return;
+    const DescWords d = load_desc(desc, (uint32_t)f);
+    const uint64_t len = d.payload_size;
+    const uint64_t so = kUnmask ? d.wire_off + d.header_size() : d.payload_off;
+    const uint64_t dof = kUnmask ? d.payload_off : d.wire_off + header_size_of(len, d.mask() != 0);
+    const uint32_t key = d.mask() ? d.key() : 0u;
+    if (len == 0 || dof >= cap) return;
+    const uint64_t dend = len < cap - dof ? dof + len : cap;
+    // [dof, first whole chunk) and [last whole chunk's end, dend)
+    const uint64_t h1 = (dof + 15) & ~uint64_t(15), t0 = dend & ~uint64_t(15);
+    const uint64_t ha = dof, hb = h1 < dend ? h1 : dend;
+    const uint64_t ta = t0 > hb ? t0 : hb, tb = dend;
+    for (uint64_t x = ha; x < hb; ++x)
+        dst[x] = src[so + (x - dof)] ^ (uint8_t)(key >> (8 * ((x - dof) & 3u)));
+    for (uint64_t x = ta; x < tb; ++x)
+        dst[x] = src[so + (x - dof)] ^ (uint8_t)(key >> (8 * ((x - dof) & 3u)));
+}
+
 // Pieces per frame for the split payload ops: enough workgroups to cover the
 // largest frame (max_payload_size, at any alignment) in pieces of at most
 // kPieceSpans 1 KiB spans, capped so the grid stays under 2^31 blocks (the
@@ -789,6 +795,8 @@ int launch_payload_xor(const void* src, void* dst, const cfws_frame_desc_t* d_de
     payload_xor_kernel<kUnmask><<<(uint32_t)(n * pieces), kThreads, kUnmask ? CFWS_UNMASK_LDS : CFWS_MASK_LDS,
                                   static_cast<hipStream_t>(stream)>>>(
         static_cast<const uint8_t*>(src), static_cast<uint8_t*>(dst), d_desc, d_status, n, pieces, cap);
+    payload_edge_kernel<kUnmask><<<grid_for(n, kThreads), kThreads, 0, static_cast<hipStream_t>(stream)>>>(
+        static_cast<const uint8_t*>(src), static_cast<uint8_t*>(dst), d_desc, d_status, n, cap);
     return launch_check(what);
 }
 
