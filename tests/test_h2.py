@@ -284,9 +284,11 @@ def test_gpu_config5_digest(idx):
 @pytest.mark.gpu
 @pytest.mark.skipif(not gpu_present(), reason="needs the MI355X")
 def test_gpu_h2_roundtrip_600k_frames():
-    """600,000 small WS frames, one DATA frame each: both plans run with more
-    than 2,048 blocks (the block sums take a scan launch of their own instead
-    of the apply kernel's self-scan). Send and receive vs the oracle."""
+    """600,000 small WS frames, one DATA frame each: the plans run with more
+    than 2,048 blocks (a scan launch of their own for the block sums in the
+    H2 plans; the single-pass look-back in the WS deserialize plan the pool
+    overflow's general form runs, with per-message ends). Send and receive
+    vs the oracle, with the pool holding everything and half of it."""
     rng = np.random.default_rng(600)
     n = 600_000
     payload = O.fill_splitmix(1 << 20, 600, 0)
@@ -302,6 +304,7 @@ def test_gpu_h2_roundtrip_600k_frames():
     index = O.h2_index(exp)
     assert len(index) == n
     check_h2_deserialize(exp, index, align=1)
+    check_h2_deserialize(exp, index, align=1, pool_cap=len(exp) // 2)
 
 
 @pytest.mark.gpu
