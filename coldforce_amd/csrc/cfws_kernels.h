@@ -807,6 +807,31 @@ __device__ __forceinline__ void general_region(const Pass& P, uint32_t f0, uint3
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u) a[u] = fast[u] ? ld16(sp[u]) : make_uint4(0, 0, 0, 0);
     // the block holding the chunk's last byte: a body byte, inside the source
+    if (kMode == kModeDeser) {
+        // ... loaded by this lane only when the next lane does not hold it
+        // as its own block (the next chunk in the same frame's body): over
+        // DPP. The receive only: 256 B frames 1.69 -> 1.57 ms, 1 KiB 1.40
+        // -> 1.39; the send measured slower with it (1 KiB 1.76 -> 1.98 ms,
+        // profiles/r03_small_ab/dpp/)
+        bool own[kUnroll];
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) {
+            const uint32_t nj = from_next_lane(js[u], 0xffffffffu);
+            const uint32_t nf_ = from_next_lane(fast[u] ? 1u : 0u, 0u);
+            own[u] = fast[u] && ph[u] && !(nj == js[u] && nf_);
+        }
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) b[u] = own[u] ? ld16(sp[u] + 16) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) {
+            const uint4 nb = from_next_lane(a[u], b[u]);    // every lane: DPP needs the full wave
+            if (!fast[u]) continue;
+            uint4 o = ph[u] ? funnel16(a[u], own[u] ? b[u] : nb, ph[u]) : a[u];
+            xor4(o, key[u]);
+            st16_region<kMode>(P.dst + base, u * (uint32_t)kSlice + lane * (uint32_t)kChunk, o);
+        }
+        return;
+    }
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u) b[u] = fast[u] && ph[u] ? ld16(sp[u] + 16) : make_uint4(0, 0, 0, 0);
 #pragma unroll
