@@ -430,3 +430,52 @@ def test_single_pass_plans_capacity_and_errors():
     for pe in (False, True):
         check_deserialize(w, offs, align=1, plan_execute=pe)
         check_deserialize(w, offs, align=16, capacity=total // 3, plan_execute=pe)
+
+
+def _mixed_desc(rng, n, payload_len, lo=80, hi=2000):
+    desc = np.zeros(n, dtype=cfws.DESC_DTYPE)
+    sz = rng.integers(lo, hi + 1, n).astype(np.uint64)
+    desc["payload_size"] = sz
+    desc["payload_off"] = (rng.integers(0, payload_len - 2048, n) & ~15).astype(np.uint64)
+    desc["fin"] = (rng.random(n) < 0.8).astype(np.uint8)
+    desc["opcode"] = rng.choice([0, 1, 2, 9], n).astype(np.uint8)
+    desc["mask"] = (rng.random(n) < 0.7).astype(np.uint8)
+    desc["mask_key"] = rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32) * desc["mask"]
+    return desc
+
+
+@pytest.mark.parametrize("n", [30_000, 600_000])
+def test_serialize_mixed_small_frames(n):
+    """WS serialize of 80..2,000-byte payloads at 16-aligned source offsets
+    (the frames of the round-3 in-region edge experiment): both
+    plan forms (30 K frames: reduce + apply; 600 K: the single-pass plan),
+    masked and unmasked frames, 7- and 16-bit lengths, against the oracle;
+    then a capacity cut inside the pass, a batch whose total is a whole
+    number of 4 KiB regions (no tail region), and one 79-byte payload."""
+    rng = np.random.default_rng(n)
+    payload = O.fill_splitmix(1 << 22, n, 0)
+    desc = _mixed_desc(rng, n, 1 << 22)
+    wire, total = check_serialize(payload, desc)
+    exp = wire[:total].copy()
+    for pe in (False, True):
+        cap = total // 2 + 4101
+        got, _, tot, _ = gpu_serialize(payload, desc, capacity=cap, plan_execute=pe)
+        assert tot == total
+        assert np.array_equal(got[:cap], exp[:cap]) and (got[cap:] == 0xEE).all()
+    # total a multiple of the 4 KiB region: grow the last frames' payloads
+    d2 = desc.copy()
+    short = (-total) % 4096
+    i = n - 1
+    while short:
+        add = min(short, 2000 - int(d2[i]["payload_size"]))
+        if int(d2[i]["payload_size"]) <= 125 < int(d2[i]["payload_size"]) + add:
+            add = 125 - int(d2[i]["payload_size"])          # keep the header size
+        d2[i]["payload_size"] += add
+        short -= add
+        i -= 1
+    _, t2 = W.wire_layout(d2)
+    assert t2 % 4096 == 0
+    check_serialize(payload, d2)
+    d3 = desc.copy()
+    d3[n // 2]["payload_size"] = 79
+    check_serialize(payload, d3, plan_execute=True)
