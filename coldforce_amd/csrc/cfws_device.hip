@@ -138,11 +138,19 @@ edge_reasm_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
 // ---------------------------------------------------------------------------
 // WS plan kernels
 // ---------------------------------------------------------------------------
+// WS serialize's in-region edge chunks (general_region_ser_edges) need every
+// frame's payload at 80..2,000 bytes and 16-aligned in the payload arena.
+__device__ __forceinline__ bool ser_inreg_frame_ok(uint64_t len, uint32_t payload_off_lo)
+{
+    return len >= 80 && len <= 2000 && (payload_off_lo & 15u) == 0;
+}
+
 __global__ void __launch_bounds__(kThreads)
 serialize_plan_reduce_kernel(cfws_frame_desc_t* __restrict__ desc, uint64_t* __restrict__ vals,
-                             uint64_t n, uint64_t* __restrict__ partials)
+                             uint64_t n, uint64_t* __restrict__ partials, uint32_t* __restrict__ inreg_flag)
 {
     __shared__ uint64_t s_wave[kWaves];
+    if (blockIdx.x == 0 && threadIdx.x == 0) *inreg_flag = 0u;    // the apply kernel ORs into it
     const uint64_t b0 = uint64_t(blockIdx.x) * kPlanBlock;
     uint64_t sum = 0;
 #pragma unroll
@@ -165,7 +173,8 @@ __global__ void __launch_bounds__(kThreads)
 serialize_plan_apply_kernel(cfws_frame_desc_t* __restrict__ desc, uint64_t* __restrict__ vals,
                             uint64_t n, const uint64_t* __restrict__ partials, uint64_t nb,
                             uint32_t self_scan, uint64_t* __restrict__ hdr, uint64_t capacity,
-                            uint32_t* __restrict__ map, uint64_t* __restrict__ user_total)
+                            uint32_t* __restrict__ map, uint64_t* __restrict__ user_total,
+                            uint32_t* __restrict__ inreg_flag)
 {
     __shared__ uint64_t s_wave[kWaves];
     uint64_t prefix, g;
@@ -179,6 +188,7 @@ serialize_plan_apply_kernel(cfws_frame_desc_t* __restrict__ desc, uint64_t* __re
     const uint64_t i0 = uint64_t(blockIdx.x) * kPlanBlock + uint64_t(threadIdx.x) * kPlanItems;
     uint64_t v[kPlanItems];
     uint64_t sum = 0;
+    bool bad = false;
 #pragma unroll
     for (int k = 0; k < kPlanItems; ++k) {
         v[k] = (i0 + k < n) ? vals[i0 + k] : 0;
@@ -191,6 +201,7 @@ serialize_plan_apply_kernel(cfws_frame_desc_t* __restrict__ desc, uint64_t* __re
         const uint64_t f = i0 + k;
         if (f < n) {
             vals[f] = run;
+            bad |= !ser_inreg_frame_ok(desc[f].payload_size, (uint32_t)desc[f].payload_off);
             desc[f].wire_off = run;
             map_range(run, run + v[k], f, total, map);
             if (f == n - 1) {
@@ -202,6 +213,7 @@ serialize_plan_apply_kernel(cfws_frame_desc_t* __restrict__ desc, uint64_t* __re
         }
         run += v[k];
     }
+    if (__syncthreads_or(bad) && threadIdx.x == 0) atomicOr(inreg_flag, 1u);
 }
 
 // Header decode at index[f] against its data size (the whole buffer, or the
@@ -267,6 +279,23 @@ deserialize_plan_reduce_kernel(const uint8_t* __restrict__ wire, uint64_t wire_s
 #endif
 constexpr int kSingleItemsSer = CFWS_SINGLE_ITEMS_SER;
 constexpr int kSingleItemsDeser = CFWS_SINGLE_ITEMS_DESER;
+
+// The flag word the serialize plan leaves for the execute: 0 = in-region
+// edges (the single-pass plan found every frame qualifying), else not. It
+// sits after the single-pass plan's ticket and block flags, inside the
+// look area (>= 64 words, and >= n / 256 + 1).
+uint32_t* ser_inreg_flag(const WsLayout& L, const void* ws, uint64_t n)
+{
+    return ws_ptr<uint32_t>(ws, L.look) + grid_for(n, uint64_t(kThreads) * kSingleItemsSer) + 1;
+}
+
+// CFWS_SER_INREG=0: the edge workgroups write every serialize edge chunk
+// (A/B knob).
+bool ser_inreg()
+{
+    static const bool v = env_knob("CFWS_SER_INREG", 1) != 0;
+    return v;
+}
 
 // The wave-exclusive prefixes of v[k] in frame order (k-major), and the
 // wave's total.
@@ -339,6 +368,7 @@ serialize_plan_single_kernel(cfws_frame_desc_t* __restrict__ desc, uint64_t* __r
         len[k] = desc[fc].payload_size;
         msk[k] = desc[fc].mask;
     }
+    bool bad = false;                                  // a frame outside ser_inreg_frame_ok
 #pragma unroll
     for (int k = 0; k < kSingleItems; ++k) {
         const uint64_t f = f0 + uint64_t(k) * 64;
@@ -353,9 +383,12 @@ serialize_plan_single_kernel(cfws_frame_desc_t* __restrict__ desc, uint64_t* __r
         if (f >= n) continue;
         const uint64_t run = pre + ex[k];
         offs[f] = run;
+        const uint32_t hs = (uint32_t)((hsp >> (4 * k)) & 15u);
+        // (the payload offset read here, not with the sizes: 276 VGPRs there)
+        bad |= !ser_inreg_frame_ok(v[k] - hs, (uint32_t)desc[f].payload_off);
         // both descriptor fields at once, so the line is written back once
         desc[f].wire_off = run;
-        desc[f].header_size = (uint8_t)((hsp >> (4 * k)) & 15u);
+        desc[f].header_size = (uint8_t)hs;
         map_range(run, run + v[k], f, capacity, map);
         if (f == n - 1) {
             const uint64_t g = run + v[k], t = g < capacity ? g : capacity;
@@ -365,6 +398,9 @@ serialize_plan_single_kernel(cfws_frame_desc_t* __restrict__ desc, uint64_t* __r
             if (user_total) *user_total = g;
         }
     }
+    // in-region edges only when every frame qualifies (look[gridDim.x + 1],
+    // zeroed with the tickets)
+    if (__syncthreads_or(bad) && threadIdx.x == 0) atomicOr(look + gridDim.x + 1, 1u);
 }
 
 // deserialize_plan_reduce_kernel + deserialize_plan_apply_kernel in one
@@ -874,18 +910,19 @@ int cfws_serialize_plan(cfws_frame_desc_t* d_desc, size_t n, uint64_t cap, uint6
     if (!self_scan && plan_single()) {
         uint32_t* look = ws_ptr<uint32_t>(ws, L.look);
         const uint32_t sb = grid_for(n, uint64_t(kThreads) * kSingleItemsSer);
-        if (hipMemsetAsync(look, 0, 4 * (uint64_t(sb) + 1), st) != hipSuccess)
+        if (hipMemsetAsync(look, 0, 4 * (uint64_t(sb) + 2), st) != hipSuccess)
             return launch_check("serialize_plan");
         serialize_plan_single_kernel<<<sb, kThreads, 0, st>>>(d_desc, offs, n, look, partials,
                                                               ws_ptr<uint64_t>(ws, L.partials[1]), hdr, cap,
                                                               ws_ptr<uint32_t>(ws, L.map[0]), d_total);
         return launch_check("serialize_plan");
     }
-    serialize_plan_reduce_kernel<<<nb, kThreads, plan_lds_bytes(), st>>>(d_desc, offs, n, partials);
+    serialize_plan_reduce_kernel<<<nb, kThreads, plan_lds_bytes(), st>>>(d_desc, offs, n, partials,
+                                                                         ser_inreg_flag(L, ws, n));
     if (!self_scan) scan_partials_kernel<<<1, kThreads, 0, st>>>(partials, nb, hdr + 3);
     serialize_plan_apply_kernel<<<nb, kThreads, plan_lds_bytes(), st>>>(d_desc, offs, n, partials, nb, self_scan,
                                                         hdr, cap, ws_ptr<uint32_t>(ws, L.map[0]),
-                                                        d_total);
+                                                        d_total, ser_inreg_flag(L, ws, n));
     return launch_check("serialize_plan");
 }
 
@@ -900,7 +937,8 @@ int cfws_serialize_execute(const void* d_payload, const cfws_frame_desc_t* d_des
         return set_err(CFWS_ERROR_INVALID_ARGUMENT, "arenas must be 16-byte aligned", hipSuccess);
     const WsLayout L = ws_layout(n, cap);
     launch_pass<kModeSer>(L, 0, d_payload, d_wire, d_desc, nullptr, ws, cap, n, kClassAll,
-                      static_cast<hipStream_t>(stream));
+                          static_cast<hipStream_t>(stream), 0, true, false,
+                          ser_inreg() ? ser_inreg_flag(L, ws, n) : nullptr);
     return launch_check("serialize_execute");
 }
 

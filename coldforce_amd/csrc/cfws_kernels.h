@@ -738,9 +738,150 @@ __device__ __forceinline__ void general_region_search(const Pass& P, uint32_t f0
 #ifndef CFWS_GENERAL_DIRECT
 #define CFWS_GENERAL_DIRECT 1
 #endif
+// WS serialize, in-region edge chunks (`inreg`: the plan found every frame
+// with an 80..2,000-byte payload at a 16-aligned source offset; see
+// ser_inreg_frame_ok). Such frames are longer than a chunk, so a chunk that
+// is not inside one body holds exactly one frame's header bytes, with frame
+// j's body tail before them and the header frame's body head after them;
+// and no region holding a boundary is fast_region or two_frame_region (two
+// frames of <= 2,014 wire bytes cannot cover 4 KiB). Each part comes from
+// registers the region already holds: the header words from the frames'
+// views, the body tail from the lane's own source blocks, the body head from
+// the next chunk's first block (that chunk lies inside the same body, whose
+// source is 16-aligned, so its block A is the body's first source block).
+// The chunk is stored in the same instruction as its segment's body chunks:
+// no edge workgroup touches it and no 64-byte segment is written in two
+// parts. 1 KiB frames: send 1.77 -> 1.59 ms; 256 B: 2.71-2.89
+// -> 1.83 ms (profiles/r03_inreg_ab/v2/). The first form, a full two-frame
+// assembly per chunk (masks and funnels per part, six shuffles per slot),
+// was slower than the edge workgroups (profiles/r03_inreg_ab/).
+__device__ __forceinline__ uint4 readlane4(const uint4& v, int l)
+{
+    return make_uint4((uint32_t)__builtin_amdgcn_readlane((int)v.x, l), (uint32_t)__builtin_amdgcn_readlane((int)v.y, l),
+                      (uint32_t)__builtin_amdgcn_readlane((int)v.z, l), (uint32_t)__builtin_amdgcn_readlane((int)v.w, l));
+}
+
+// The 128-bit value v shifted up by `sh` bytes (0 <= sh < 16), as two 64-bit halves.
+__device__ __forceinline__ uint4 shl_bytes(uint64_t lo, uint64_t hi, uint32_t sh)
+{
+    const uint32_t b = 8u * (sh & 7u);
+    const uint64_t l1 = b ? lo << b : lo;
+    const uint64_t h1 = b ? (hi << b) | (lo >> (64u - b)) : hi;
+    const uint64_t L = sh < 8 ? l1 : 0, H = sh < 8 ? h1 : l1;
+    return make_uint4((uint32_t)L, (uint32_t)(L >> 32), (uint32_t)H, (uint32_t)(H >> 32));
+}
+
+// general_region's send with in-region edge chunks (see above): every chunk
+// of the region, body or edge, in one store round. js/fast/ph/sp/key are the
+// chunks' frame lanes, classification, source phase, source block and
+// rotated key; the lane's frame (lane < nf): ro/rng/dlo/dhi as in
+// general_region, its header as words (h0, h1: <= 8 bytes, zero past pre),
+// hm = its header start relative to the region (16-bit signed) | pre << 16,
+// tk its key. A non-fast chunk holds exactly one frame's header bytes: frame
+// j's (the chunk starts before j's body) or j + 1's; it is
+//   [j's body tail] [the header, at q = header start - chunk] [the body head,
+//   the header's frame's first source block, at q + pre]
+// each part a shift of words and none masked but the tail.
+__device__ __forceinline__ void general_region_ser_edges(const Pass& P, uint64_t base, uint32_t lane, uint32_t nf,
+                                                        const uint32_t (&js)[kUnroll], const bool (&fast)[kUnroll],
+                                                        const uint32_t (&ph)[kUnroll],
+                                                        const uint8_t* const (&sp)[kUnroll],
+                                                        const uint32_t (&key)[kUnroll], uint32_t rng,
+                                                        uint32_t dlo, uint32_t dhi, uint32_t h0, uint32_t h1,
+                                                        uint32_t hm, uint32_t tk)
+{
+    const uint4 z = make_uint4(0, 0, 0, 0);
+    auto hstart = [](uint32_t m) { return (int)(int16_t)(m & 0xffffu); };
+    bool tl[kUnroll], ob[kUnroll];
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+        const uint32_t r = u * (uint32_t)kSlice + lane * (uint32_t)kChunk;
+        const uint32_t rg = (uint32_t)__shfl((int)rng, (int)js[u], 64);
+        const uint32_t bs = rg & 0xffffu, be = rg >> 16;
+        tl[u] = !fast[u] && r >= bs && r < be;                 // frame j's body tail
+        const uint32_t cnt = be - r < 16u ? be - r : 16u;
+        ob[u] = (fast[u] && ph[u]) || (tl[u] && ph[u] + cnt > 16u);
+    }
+    // The region's last chunk takes a body head from the next region's first
+    // chunk: loaded here by lane 63.
+    uint4 hx = z;
+    {
+        const int R = (int)(kRegion - kChunk);
+        const uint32_t jl = (uint32_t)__builtin_amdgcn_readlane((int)js[kUnroll - 1], 63);
+        const uint32_t ml = (uint32_t)__builtin_amdgcn_readlane((int)hm, (int)jl);
+        const int bsl = hstart(ml) + (int)(ml >> 16);
+        int h = -1, bsh = 0;
+        if (R < bsl && bsl < R + 16) {
+            h = (int)jl;
+            bsh = bsl;
+        } else if (jl + 1 < nf) {
+            const uint32_t mn = (uint32_t)__builtin_amdgcn_readlane((int)hm, (int)jl + 1);
+            const int bsn = hstart(mn) + (int)(mn >> 16);
+            if (bsn < R + 16) {
+                h = (int)jl + 1;
+                bsh = bsn;
+            }
+        }
+        // a vector load from a full 64-bit VGPR address (as a wave-uniform
+        // address it became a scalar load with the delta's low word as a
+        // 32-bit SOFFSET, which does not carry: the block came back wrong)
+        if (h >= 0 && lane == 63) {
+            const uint64_t d = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)dlo, h) |
+                               (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)dhi, h) << 32;
+            uint64_t addr = reinterpret_cast<uint64_t>(P.src) + base + (uint64_t)bsh + d;
+            asm volatile("" : "+v"(addr));
+            hx = ld16(reinterpret_cast<const uint8_t*>(addr));
+        }
+    }
+    uint4 a[kUnroll], b[kUnroll];
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) a[u] = fast[u] || tl[u] ? ld16(sp[u]) : z;
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) b[u] = ob[u] ? ld16(sp[u] + 16) : z;
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+        const int R = (int)(u * (uint32_t)kSlice + lane * (uint32_t)kChunk);
+        const uint32_t j = js[u], jn = j + 1 < nf ? j + 1 : j;
+        // the header's frame, and its values with every lane active
+        const uint32_t rg = (uint32_t)__shfl((int)rng, (int)j, 64);
+        const uint32_t hf = R < (int)(rg & 0xffffu) ? j : jn;
+        const uint32_t mf = (uint32_t)__shfl((int)hm, (int)hf, 64);
+        const uint32_t x0 = (uint32_t)__shfl((int)h0, (int)hf, 64);
+        const uint32_t x1 = (uint32_t)__shfl((int)h1, (int)hf, 64);
+        const uint32_t kf = (uint32_t)__shfl((int)tk, (int)hf, 64);
+        const uint4 N = from_next_lane(a[u], u + 1 < kUnroll ? readlane4(a[u + 1 < kUnroll ? u + 1 : u], 0) : hx);
+        uint4 o = ph[u] ? funnel16(a[u], b[u], ph[u]) : a[u];
+        xor4(o, key[u]);
+        if (!fast[u]) {
+            const int q = hstart(mf) - R;                 // -7 .. 15
+            const int s = q + (int)(mf >> 16);            // 1 .. 23
+            const uint64_t Hv = (uint64_t)x0 | (uint64_t)x1 << 32;
+            // the tail: bytes [0, q) of o
+            const uint32_t t = q > 0 ? (uint32_t)q : 0u;
+            const uint64_t ml = t >= 8 ? ~0ull : (t ? (1ull << (8 * t)) - 1 : 0ull);
+            const uint64_t mh = t > 8 ? (1ull << (8 * (t - 8))) - 1 : 0ull;
+            uint4 w = make_uint4(o.x & (uint32_t)ml, o.y & (uint32_t)(ml >> 32), o.z & (uint32_t)mh,
+                                 o.w & (uint32_t)(mh >> 32));
+            // the header at q
+            const uint4 Hs = q >= 0 ? shl_bytes(Hv, 0, (uint32_t)q)
+                                    : make_uint4((uint32_t)(Hv >> (8 * -q)), (uint32_t)(Hv >> (8 * -q) >> 32), 0u, 0u);
+            w = or4(w, Hs);
+            // the body head at s
+            if (s < 16) {
+                uint4 W = N;
+                xor4(W, kf);
+                w = or4(w, shl_bytes((uint64_t)W.x | (uint64_t)W.y << 32, (uint64_t)W.z | (uint64_t)W.w << 32,
+                                     (uint32_t)s));
+            }
+            o = w;
+        }
+        st16_region<kModeSer>(P.dst + base, (uint32_t)R, o);
+    }
+}
+
 template <int kMode>
 __device__ __forceinline__ void general_region(const Pass& P, uint32_t f0, uint32_t f1, uint64_t base,
-                                               uint32_t lane)
+                                               uint32_t lane, bool inreg = false)
 {
     const uint32_t nf = f1 - f0 + 1;
     if (nf > 64) {
@@ -750,7 +891,7 @@ __device__ __forceinline__ void general_region(const Pass& P, uint32_t f0, uint3
     auto rel = [base](uint64_t x, uint64_t hi) -> uint32_t {
         return x <= base ? 0u : (x - base >= hi ? (uint32_t)hi : (uint32_t)(x - base));
     };
-    uint32_t ro = (uint32_t)kRegion, rng = 0, kr = 0, dlo = 0, dhi = 0;
+    uint32_t ro = (uint32_t)kRegion, rng = 0, kr = 0, dlo = 0, dhi = 0, h0 = 0, h1 = 0, hm = 0, tk = 0;
     if (lane < nf) {
         const FrameView v = frame_view<kMode>(P, f0 + lane);
         ro = rel(v.out_off, kRegion);
@@ -759,6 +900,13 @@ __device__ __forceinline__ void general_region(const Pass& P, uint32_t f0, uint3
         dlo = (uint32_t)delta;
         dhi = (uint32_t)(delta >> 32);
         kr = rotr8(v.key, (uint32_t)(base - v.body_start) & 3u);
+        if (kMode == kModeSer && inreg) {
+            const uint4 H = ws_header_words(v.body_len, v.hb, v.key);
+            h0 = H.x;
+            h1 = H.y;
+            hm = ((uint32_t)(v.out_off - base) & 0xffffu) | v.pre << 16;
+            tk = v.key;
+        }
     }
     const uint8_t* sp[kUnroll];
     uint32_t ph[kUnroll], key[kUnroll];
@@ -802,6 +950,10 @@ __device__ __forceinline__ void general_region(const Pass& P, uint32_t f0, uint3
         const uint64_t s = base + r + d;
         ph[u] = (uint32_t)(s & 15u);
         sp[u] = P.src + (s & ~uint64_t(15));
+    }
+    if (kMode == kModeSer && inreg) {
+        general_region_ser_edges(P, base, lane, nf, js, fast, ph, sp, key, rng, dlo, dhi, h0, h1, hm, tk);
+        return;
     }
     uint4 a[kUnroll], b[kUnroll];
 #pragma unroll
@@ -891,7 +1043,7 @@ __device__ __forceinline__ uint32_t edge_thread_part(uint64_t t) { return (uint3
 // The edge chunks of frame f in pass P (part 0: before the body; part 1:
 // reaching past the body end).
 template <int kMode>
-__device__ __forceinline__ void edge_frame(const Pass& P, uint64_t f, uint32_t part)
+__device__ __forceinline__ void edge_frame(const Pass& P, uint64_t f, uint32_t part, uint64_t dmin = 0)
 {
     // Everything the chunks need that depends on f alone is loaded up front
     // (frame f and f + 1's descriptors, statuses, offsets): one memory round
@@ -908,7 +1060,8 @@ __device__ __forceinline__ void edge_frame(const Pass& P, uint64_t f, uint32_t p
     if (lo >= hi) return;
     const FrameView& v = va;
     const uint64_t be = v.body_start + v.body_len;
-    const uint64_t first = (lo + 15) & ~uint64_t(15);
+    uint64_t first = (lo + 15) & ~uint64_t(15);
+    if (first < dmin) first = dmin;                   // chunks below dmin: written in-region
     if (part == 0) {
         // chunks before the body (headers): D < body_start
         for (uint64_t D = first; D < hi && D < v.body_start; D += 16)
@@ -1025,7 +1178,8 @@ xform_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
              const uint64_t* __restrict__ total_p, const uint64_t* __restrict__ base_p,
              uint64_t capacity, uint32_t n_frames, uint32_t klass, uint32_t sid,
              const cfws_frame_desc_t* __restrict__ parent, uint32_t edge_blocks,
-             const uint64_t* __restrict__ reasm_offs1, uint32_t edge_stride)
+             const uint64_t* __restrict__ reasm_offs1, uint32_t edge_stride,
+             const uint32_t* __restrict__ inreg_flag)
 {
     // Which workgroups are edge workgroups: the first edge_blocks, or (edge
     // stride s > 0) every s-th one, spread through the grid
@@ -1058,9 +1212,21 @@ xform_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
     P.klass = klass;
     P.sid = sid;
     P.parent = parent;
+    // WS serialize with in-region edges (the plan's ser_inreg flag clear):
+    // the general regions write every edge chunk below the tail region.
+    const bool inreg = kMode == kModeSer && inreg_flag && *inreg_flag == 0;
     if (has_edge_blocks(kMode) && is_edge) {
         const uint64_t t = uint64_t(eidx) * kThreads + threadIdx.x;
-        if (edge_thread_frame(t) < n_frames) edge_frame<kMode>(P, edge_thread_frame(t), edge_thread_part(t));
+        const uint64_t f = edge_thread_frame(t);
+        if (f >= n_frames) return;
+        uint64_t dmin = 0;
+        if (inreg) {
+            // only the tail region's chunks are left (tail_region writes
+            // body chunks only); the frames before its first have none
+            dmin = P.total / kRegion * kRegion;
+            if (dmin >= P.total || f < region_map[dmin / kRegion]) return;
+        }
+        edge_frame<kMode>(P, f, edge_thread_part(t), dmin);
         return;
     }
     const uint64_t n_regions = (P.total + kRegion - 1) / kRegion;
@@ -1106,7 +1272,7 @@ xform_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
         } else if (f1 == f0 + 1 || offs[f0 + 2] >= end) {
             two_frame_region<kMode>(P, va, frame_view<kMode>(P, f0 + 1), base, lane);
         } else {
-            general_region<kMode>(P, f0, f1, base, lane);
+            general_region<kMode>(P, f0, f1, base, lane, inreg);
         }
     }
 }
@@ -1683,7 +1849,7 @@ void launch_streaming(const void* src, void* dst, const cfws_frame_desc_t* desc,
                       const uint64_t* total_p, const uint64_t* base_p, uint64_t regions,
                       uint64_t cap, size_t n, uint32_t klass, uint32_t sid, hipStream_t st,
                       const cfws_frame_desc_t* parent = nullptr, bool edges = true,
-                      const uint64_t* reasm_offs1 = nullptr)
+                      const uint64_t* reasm_offs1 = nullptr, const uint32_t* inreg_flag = nullptr)
 {
     const bool split = edges && (edge_split() || !has_edge_blocks(kMode));
     const uint32_t eb = (edges && !split) ? grid_for(edge_threads(n), kThreads) : 0;
@@ -1699,7 +1865,7 @@ void launch_streaming(const void* src, void* dst, const cfws_frame_desc_t* desc,
     xform_kernel<kMode><<<eb + sg, kThreads, xform_lds_bytes(kMode, n ? cap / n : cap), st>>>(
         static_cast<const uint8_t*>(src), static_cast<uint8_t*>(dst), desc, status, offs, map,
         total_p, base_p, cap, (uint32_t)n, klass, sid, parent, eb, eb ? reasm_offs1 : nullptr,
-        stride);
+        stride, split ? nullptr : inreg_flag);
     // (a separate edge launch on a second stream, overlapping the streaming
     // kernel, measured no faster on config 5: the stream slowed by what the
     // overlap saved)
@@ -1711,7 +1877,8 @@ void launch_streaming(const void* src, void* dst, const cfws_frame_desc_t* desc,
 template <int kMode>
 void launch_pass(const WsLayout& L, int p, const void* src, void* dst, const cfws_frame_desc_t* desc,
                  const int32_t* status, const void* ws, uint64_t cap, size_t n, uint32_t klass,
-                 hipStream_t st, uint32_t sid = 0, bool edges = true, bool reasm_edges = false)
+                 hipStream_t st, uint32_t sid = 0, bool edges = true, bool reasm_edges = false,
+                 const uint32_t* inreg_flag = nullptr)
 {
     const uint64_t* hdr = ws_ptr<const uint64_t>(ws, L.hdr);
     // Pass 1 (reassembly: control frames, <= 125-byte payloads each) is
@@ -1722,7 +1889,8 @@ void launch_pass(const WsLayout& L, int p, const void* src, void* dst, const cfw
     launch_streaming<kMode>(src, dst, desc, status, ws_ptr<const uint64_t>(ws, L.offs[p]),
                             ws_ptr<const uint32_t>(ws, L.map[p]), hdr + p,
                             p == 1 ? hdr + 2 : nullptr, regions, cap, n, klass, sid, st, nullptr,
-                            edges, reasm_edges ? ws_ptr<const uint64_t>(ws, L.offs[1]) : nullptr);
+                            edges, reasm_edges ? ws_ptr<const uint64_t>(ws, L.offs[1]) : nullptr,
+                            inreg_flag);
 }
 
 }  // namespace

@@ -445,13 +445,16 @@ def _mixed_desc(rng, n, payload_len, lo=80, hi=2000):
 
 
 @pytest.mark.parametrize("n", [30_000, 600_000])
-def test_serialize_mixed_small_frames(n):
-    """WS serialize of 80..2,000-byte payloads at 16-aligned source offsets
-    (the frames of the round-3 in-region edge experiment): both
-    plan forms (30 K frames: reduce + apply; 600 K: the single-pass plan),
-    masked and unmasked frames, 7- and 16-bit lengths, against the oracle;
-    then a capacity cut inside the pass, a batch whose total is a whole
-    number of 4 KiB regions (no tail region), and one 79-byte payload."""
+def test_serialize_in_region_edges(n):
+    """WS serialize with in-region edge chunks (every payload 80..2,000 bytes
+    at a 16-aligned source offset: general_region_ser_edges writes each edge
+    chunk with its segment): both plan forms (30 K frames: reduce + apply;
+    600 K: the single-pass plan), masked and unmasked frames, 7- and 16-bit
+    lengths, against the oracle; then a capacity cut inside the pass (the
+    tail region's edge chunks stay with the edge workgroups), a batch whose
+    total is a whole number of 4 KiB regions (no tail region), and the same
+    frames with one 79-byte payload (the plan's flag off: edge workgroups
+    write every edge chunk)."""
     rng = np.random.default_rng(n)
     payload = O.fill_splitmix(1 << 22, n, 0)
     desc = _mixed_desc(rng, n, 1 << 22)
