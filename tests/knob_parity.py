@@ -10,6 +10,7 @@ tests/test_knobs.py runs this script once per setting):
   CFWS_XFORM_LDS=N      the LDS reservation for every mode
   CFWS_PLAN_LDS=N       LDS reserved by the plan kernels
   CFWS_PLAN_SINGLE=0    plans of > 2,048 blocks as reduce / scan / apply
+  CFWS_SER_INREG=0      WS serialize edge chunks always by edge workgroups
                         launches instead of the single-pass look-back
 
 Each case is checked byte for byte against the oracle. Prints "KNOB OK".
@@ -28,16 +29,19 @@ from coldforce_amd import cfws  # noqa: E402
 from coldforce_amd import workloads as W  # noqa: E402
 
 
-def roundtrip(sizes, rng, seed, align, flags=0, opcodes=None, fins=None):
+def roundtrip(sizes, rng, seed, align, flags=0, opcodes=None, fins=None, aligned=False):
     n = len(sizes)
     desc = np.zeros(n, dtype=cfws.DESC_DTYPE)
     desc["payload_size"] = sizes
-    desc["payload_off"] = np.concatenate([[0], np.cumsum(sizes[:-1])]) + 5
+    if aligned:          # 16-aligned payloads (the in-region send edges' condition)
+        desc["payload_off"] = np.concatenate([[0], np.cumsum((sizes[:-1] + 15) // 16 * 16)])
+    else:
+        desc["payload_off"] = np.concatenate([[0], np.cumsum(sizes[:-1])]) + 5
     desc["fin"] = fins if fins is not None else rng.integers(0, 2, n)
     desc["opcode"] = opcodes if opcodes is not None else rng.choice([0, 1, 2, 9, 10], n)
     desc["mask"] = rng.integers(0, 2, n)
     desc["mask_key"] = cfws.draw_mask_keys(n, desc["mask"], seed=seed)
-    payload_np = O.fill_splitmix(int(sizes.sum()) + 32, 0x5EED + seed, 0)
+    payload_np = O.fill_splitmix(int(desc["payload_off"][-1]) + int(sizes[-1]) + 32, 0x5EED + seed, 0)
     exp_wire, _ = O.serialize_batch(payload_np, desc.view(O.DESC_DTYPE))
     payload = torch.from_numpy(payload_np).cuda()
     offs, total = W.wire_layout(desc)
@@ -67,6 +71,11 @@ def main():
     roundtrip(np.full(20000, 1024), rng, 2, 16, opcodes=np.full(20000, 1), fins=np.ones(20000))
     # 600 K tiny frames: plans of > 2,048 blocks (single-pass unless CFWS_PLAN_SINGLE=0)
     roundtrip(rng.integers(0, 31, 600000), rng, 4, 1)
+    # 80..2,000-byte payloads at 16-aligned offsets: in-region send edge chunks
+    # unless CFWS_SER_INREG=0 or CFWS_EDGE_SPLIT=1 (reduce + apply plan, then
+    # the single-pass plan)
+    roundtrip(rng.integers(80, 2001, 20000), rng, 5, 16, aligned=True)
+    roundtrip(rng.integers(80, 200, 600000), rng, 6, 1, aligned=True)
     # a small batch (single-launch path unless CFWS_SMALL=0)
     roundtrip(np.full(256, 1000), rng, 3, 16)
     # fragments + pings, reassembled (two passes, pass-1 capped grid)

@@ -16,6 +16,7 @@ KNOBS = [
     {"CFWS_EDGE_ORDER": "1", "CFWS_OCC_FRAME_MAX": "0", "CFWS_PLAN_LDS": "8192"},
     {"CFWS_GRID": "300", "CFWS_XFORM_LDS": "0"},
     {"CFWS_PLAN_SINGLE": "0"},
+    {"CFWS_SER_INREG": "0"},
 ]
 
 
