@@ -738,6 +738,7 @@ __device__ __forceinline__ void general_region_search(const Pass& P, uint32_t f0
 #ifndef CFWS_GENERAL_DIRECT
 #define CFWS_GENERAL_DIRECT 1
 #endif
+
 // WS serialize, in-region edge chunks (`inreg`: the plan found every frame
 // with an 80..2,000-byte payload at a 16-aligned source offset; see
 // ser_inreg_frame_ok). Such frames are longer than a chunk, so a chunk that
@@ -1138,6 +1139,64 @@ __device__ __forceinline__ void reasm_edge_frame(const uint8_t* __restrict__ src
     edge_frame<kModeDeser>(P, f, part);
 }
 
+// The streaming regions of one launch (the waves of the non-edge
+// workgroups, one 4 KiB region each per grid stride). kInreg: WS serialize
+// with in-region edge chunks (general_region_ser_edges).
+template <int kMode, bool kInreg>
+__device__ __forceinline__ void region_loop(const Pass& P, const uint64_t* __restrict__ offs,
+                                            const uint32_t* __restrict__ region_map, uint32_t n_frames,
+                                            uint32_t edge_blocks, uint32_t sidx)
+{
+    const uint64_t n_regions = (P.total + kRegion - 1) / kRegion;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t stride = uint64_t(gridDim.x - edge_blocks) * kWaves;
+
+    for (uint64_t r = uint64_t(sidx) * kWaves + wave; r < n_regions;
+         r += stride) {
+        const uint64_t base = r * kRegion;
+        const uint64_t end = base + kRegion;
+        // The plan writes every entry in [0, n_regions]; the clamps only keep
+        // a corrupted workspace from turning into an out-of-bounds read.
+        uint32_t f0 = region_map[r];
+        uint32_t f1 = region_map[r + 1];
+        if (f1 >= n_frames) f1 = n_frames - 1;
+        if (f0 > f1) f0 = f1;
+        if (end > P.total) {                  // the pass end (a capacity cut may fall in a body)
+            tail_region<kMode>(P, f0, f1, base, lane);
+            continue;
+        }
+#if CFWS_GENERAL_DIRECT
+        // f0 + 1 and f0 + 2 start inside the region: a run of small frames,
+        // straight to the per-lane views without the offset round trip below
+        // (general_region ignores frames that start at or after the end).
+        // The receive, and the in-region send: 1 KiB frames receive 1.437 ->
+        // 1.385 ms, 256 B 1.758 -> 1.686; in-region send 1 KiB 1.58 -> 1.54,
+        // 256 B 1.81-1.83 -> 1.69-1.70 (profiles/r03_inreg_ab/v3/); the send
+        // with edge workgroups measured slower with it (256 B 2.74 -> 2.93
+        // ms, profiles/r03_small_ab/)
+        if ((kMode == kModeDeser || kInreg) && f1 >= f0 + 3) {
+            general_region<kMode>(P, f0, f1, base, lane, kInreg);
+            continue;
+        }
+#endif
+        // region_map[r + 1] holds the NEXT region's first byte; frames that
+        // start at or after this region's end do not touch it.
+        if (f1 > f0 && offs[f0 + 1] >= end) f1 = f0;
+        const FrameView va = frame_view<kMode>(P, f0);
+        if (f0 == f1) {
+            if (base >= va.body_start && end <= va.body_start + va.body_len)
+                fast_region<kMode>(P, va, base, lane);
+            else
+                two_frame_region<kMode>(P, va, va, base, lane);   // partial body, one frame
+        } else if (f1 == f0 + 1 || offs[f0 + 2] >= end) {
+            two_frame_region<kMode>(P, va, frame_view<kMode>(P, f0 + 1), base, lane);
+        } else {
+            general_region<kMode>(P, f0, f1, base, lane, kInreg);
+        }
+    }
+}
+
 // WS serialize / deserialize and the fused WS-over-HTTP/2 send carry their
 // edge chunks in the streaming launch. The send's edge code spills 12 bytes
 // per lane there (96 VGPRs, 5 waves per SIMD, the residency the LDS
@@ -1229,52 +1288,13 @@ xform_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
         edge_frame<kMode>(P, f, edge_thread_part(t), dmin);
         return;
     }
-    const uint64_t n_regions = (P.total + kRegion - 1) / kRegion;
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint64_t stride = uint64_t(gridDim.x - edge_blocks) * kWaves;
-
-    for (uint64_t r = uint64_t(sidx) * kWaves + wave; r < n_regions;
-         r += stride) {
-        const uint64_t base = r * kRegion;
-        const uint64_t end = base + kRegion;
-        // The plan writes every entry in [0, n_regions]; the clamps only keep
-        // a corrupted workspace from turning into an out-of-bounds read.
-        uint32_t f0 = region_map[r];
-        uint32_t f1 = region_map[r + 1];
-        if (f1 >= n_frames) f1 = n_frames - 1;
-        if (f0 > f1) f0 = f1;
-        if (end > P.total) {                  // the pass end (a capacity cut may fall in a body)
-            tail_region<kMode>(P, f0, f1, base, lane);
-            continue;
-        }
-#if CFWS_GENERAL_DIRECT
-        // f0 + 1 and f0 + 2 start inside the region: a run of small frames,
-        // straight to the per-lane views without the offset round trip below
-        // (general_region ignores frames that start at or after the end).
-        // The receive only: 1 KiB frames 1.437 -> 1.385 ms, 256 B 1.758 ->
-        // 1.686; the send measured slower with it (256 B 2.74 -> 2.93 ms,
-        // profiles/r03_small_ab/)
-        if (kMode == kModeDeser && f1 >= f0 + 3) {
-            general_region<kMode>(P, f0, f1, base, lane);
-            continue;
-        }
-#endif
-        // region_map[r + 1] holds the NEXT region's first byte; frames that
-        // start at or after this region's end do not touch it.
-        if (f1 > f0 && offs[f0 + 1] >= end) f1 = f0;
-        const FrameView va = frame_view<kMode>(P, f0);
-        if (f0 == f1) {
-            if (base >= va.body_start && end <= va.body_start + va.body_len)
-                fast_region<kMode>(P, va, base, lane);
-            else
-                two_frame_region<kMode>(P, va, va, base, lane);   // partial body, one frame
-        } else if (f1 == f0 + 1 || offs[f0 + 2] >= end) {
-            two_frame_region<kMode>(P, va, frame_view<kMode>(P, f0 + 1), base, lane);
-        } else {
-            general_region<kMode>(P, f0, f1, base, lane, inreg);
-        }
-    }
+    // the region loop, instantiated apart for the in-region send so that the
+    // other loops' code stays as it was (config 3's send lost 6 % when one
+    // loop carried both)
+    if (kMode == kModeSer && inreg)
+        region_loop<kMode, true>(P, offs, region_map, n_frames, edge_blocks, sidx);
+    else
+        region_loop<kMode, false>(P, offs, region_map, n_frames, edge_blocks, sidx);
 }
 
 // ---------------------------------------------------------------------------
