@@ -106,27 +106,34 @@ def effective_cpus() -> int:
 
 def cpu_baseline(frame_size: int, seconds: float):
     """Reference codec (oracle/_ref, compiled from coldforce's own sources at
-    -O2) when it was built, else the clean-room port; timed on this host on
-    1 .. nproc threads, a 1/8/16/32/64/nproc sweep at -O2
-    and the as-shipped -O0 at 1 and nproc threads. `value` is the
-    fastest point of the sweep (see below), `cores` its thread count."""
+    -O2) when it was built, else the clean-room port; timed on this host
+    (SURVEY.md 8(d)): a sweep over 1/8/16/32/64 threads up to the CPUs the
+    job's cgroup grants (effective_cpus) plus nproc, at -O2, and the
+    as-shipped -O0 at 1 and the best thread count. `value` is the fastest
+    point of the sweep, `cores` its thread count.
+
+    Only the combined rate (mask + unmask payload bytes over the time of
+    both) is reported. The per-frame loop alternates a mask phase (bound by
+    glibc's random() lock) and an unmask phase of a few ms each, so under a
+    CPU quota a phase timed alone can run on time the other phase left
+    unspent, and a split rate would overstate what the host sustains."""
     import oracle
     kind = "reference" if oracle.ref_lib("O2") is not None else "port"
     cpus = host_cpus()
+    eff = effective_cpus()
 
     def frames_for(threads):
         return max(256, 64 * threads)
 
     def rate(k, threads, target_s):
-        """GiB/s of payload (mask + unmask) of `k` on `threads` over ~target_s."""
+        """(payload bytes of one direction, seconds of mask + unmask, iters)."""
         n = frames_for(threads)
         oracle.cpu_bench(n, frame_size, threads, 1, k)          # first touch of the heaps
         m1, u1 = oracle.cpu_bench(n, frame_size, threads, 2, k)
         it = max(1, int(math.ceil(2 * target_s / max(m1 + u1, 1e-3))))
         if it > 1:
             m1, u1 = oracle.cpu_bench(n, frame_size, threads, it, k)
-        payload = n * frame_size * it
-        return payload, m1, u1, it
+        return n * frame_size * it, m1 + u1, it
 
     # the sweep first (short samples), then the main sample on the thread
     # count that ran fastest: on a shared box the job's cgroup can grant far
@@ -134,51 +141,61 @@ def cpu_baseline(frame_size: int, seconds: float):
     # serialise on glibc's random() lock, so nproc threads can be the
     # slowest choice; every point is reported
     sweep = []
-    for t in sorted({1, 8, 16, 32, 64, cpus}):
-        if t > cpus:
+    for t in sorted({1, 8, 16, 32, 64, eff, cpus}):
+        if t > cpus or (t > eff and t != cpus):
             continue
-        p, m1, u1, _ = rate(kind, t, 1.5)
-        sweep.append({"threads": t, "gibs": round(2 * p / (m1 + u1) / GIB, 3),
-                      "mask_gibs": round(p / m1 / GIB, 3), "unmask_gibs": round(p / u1 / GIB, 3)})
+        p, sec, _ = rate(kind, t, 1.5)
+        sweep.append({"threads": t, "gibs": round(2 * p / sec / GIB, 3)})
     best = max(sweep, key=lambda r: r["gibs"])["threads"]
-    payload, ms, us, iters = rate(kind, best, seconds)
+    payload, sec, iters = rate(kind, best, seconds)
     as_shipped = {}
     if kind == "reference":
-        for t in sorted({1, best, cpus}):
-            p, m1, u1, _ = rate("reference_O0", t, 1.5)
-            as_shipped[str(t)] = round(2 * p / (m1 + u1) / GIB, 3)
-    p, m1, u1, _ = rate("port", 1, 1.5)
+        for t in sorted({1, best}):
+            p, s0, _ = rate("reference_O0", t, 1.5)
+            as_shipped[str(t)] = round(2 * p / s0 / GIB, 3)
+    p, s1, _ = rate("port", 1, 1.5)
     n = frames_for(best)
     return {
-        "value": round(2 * payload / (ms + us) / GIB, 3),
+        "value": round(2 * payload / sec / GIB, 3),
         "unit": "GiB/s",
         "cores": best,
         "kind": kind,
-        "sample": (f"{n} x {frame_size // 1024} KiB binary frames x {iters} iters, per-frame "
+        "sample": (f"{n} x {size_label(frame_size)} binary frames x {iters} iters, per-frame "
                    f"co_ws_frame_serialize(mask) + co_ws_frame_deserialize"
                    f"{' (reference -O2, oracle/_ref)' if kind == 'reference' else ' (port, -O2)'},"
-                   f" {best} threads (the fastest of the sweep over 1..nproc = {cpus}), each on a "
-                   f"contiguous frame range"),
-        "mask_gibs": round(payload / ms / GIB, 3),
-        "unmask_gibs": round(payload / us / GIB, 3),
-        "seconds": round(ms + us, 2),
+                   f" {best} threads (the fastest of the sweep; cgroup grants {eff} of nproc = "
+                   f"{cpus}), each on a contiguous frame range; mask and unmask timed as one "
+                   f"combined rate"),
+        "seconds": round(sec, 2),
         "nproc": cpus,
+        "effective_cpus": eff,
         "scaling_O2": sweep,
         "as_shipped_O0": as_shipped,
-        "port_O2_1_thread": round(2 * p / (m1 + u1) / GIB, 3),
+        "port_O2_1_thread": round(2 * p / s1 / GIB, 3),
         "cgroup_cpu_max": cgroup_cpu_limit(),
     }
 
 
-def load_traffic(kernel: str):
-    """HBM bytes per launch from the committed PMC pass (profiles/), if any."""
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    try:
-        with open(path) as f:
-            data = json.load(f)
-        return data.get(kernel, {}).get("hbm_bytes_per_launch")
-    except (OSError, ValueError):
-        return None
+def size_label(n: int) -> str:
+    """64 KiB, 1 KiB, 256 B, 16376 B: the frame size as the workload names it."""
+    return f"{n // 1024} KiB" if n >= 1024 and n % 1024 == 0 else f"{n} B"
+
+
+def load_traffic(kernel: str, workload: str):
+    """HBM bytes per launch of `kernel` from the committed PMC summary taken
+    on exactly this workload (profiles/pmc_traffic*.json, written by
+    tools/pmc_summary.py with its "workload" key), or None when no PMC pass
+    has been run on it."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_traffic*.json"))):
+        try:
+            with open(path) as f:
+                data = json.load(f)
+        except (OSError, ValueError):
+            continue
+        if data.get("workload") == workload:
+            return data.get(kernel, {}).get("hbm_bytes_per_launch")
+    return None
 
 
 def bench_h2(args, rank, world, dev):
@@ -661,6 +678,9 @@ def main():
     achieved = alg_bytes / (dom_ms * 1e-3) / 1e9
     kernel_symbol = ("xform_kernel<0>" if dom_name == "serialize_execute"   # kModeSer
                      else "xform_kernel<1>")                                 # kModeDeser
+    # the PMC summary a traffic figure may come from: the same workload only
+    traffic_key = (f"config2:{F}x{fs}" if args.workload == "config2" else
+                   "config3" if args.workload == "config3" else f"config4:{F}x{fs}")
     rows = shard.gather_floats([local, arena_bytes, ser_ms, de_ms, alg_bytes], dev)
     total_payload = 2.0 * sum(r[1] for r in rows) * args.steps
     line = {
@@ -677,7 +697,7 @@ def main():
         "dtype": "u8",
         "data": "synthetic (splitmix64 payloads, glibc random() mask keys as co_ws_frame_serialize draws them)",
         "config": {
-            "workload": (f"config2: {F} binary frames x {fs // 1024} KiB per GPU, client-mask "
+            "workload": (f"config2: {F} binary frames x {size_label(fs)} per GPU, client-mask "
                          f"(serialize) then server-unmask (deserialize), device resident"
                          if args.workload == "config2" else
                          f"config4: shard {rank} of 8 of the 8 M x 64 KiB batch ({F} frames, "
@@ -699,7 +719,7 @@ def main():
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": load_traffic(kernel_symbol) if args.workload == "config2" else None,
+            "traffic": load_traffic(kernel_symbol, traffic_key),
             "algorithmic_bytes_per_launch": alg_bytes,
             "avg_launch_ms": round(dom_ms, 4),
         },

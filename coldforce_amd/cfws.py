@@ -47,7 +47,7 @@ BATCH_SYMBOLS = (
     "cfws_serialize_plan", "cfws_serialize_execute", "cfws_serialize_batch",
     "cfws_deserialize_plan", "cfws_deserialize_execute", "cfws_deserialize_batch",
     "cfws_xor_mask", "cfws_draw_mask_keys", "cfws_draw_mask_keys_seeded",
-    "cfws_release_thread_resources",
+    "cfws_release_thread_resources", "cfws_set_dropin_gpu_min", "cfws_dropin_gpu_min",
     "cfws_fill_splitmix", "cfws_pipeline_create", "cfws_pipeline_destroy",
     "cfws_pipeline_serialize", "cfws_pipeline_deserialize", "cfws_pipeline_receive",
     "cfws_h2_serialize_workspace_size", "cfws_h2_serialize_batch",
@@ -135,6 +135,8 @@ def lib(path: str = LIB_PATH) -> C.CDLL:
         "cfws_device_copy": ([_vp, _vp, _u64, _vp], C.c_int),
         "cfws_bind_thread_device": ([C.c_int], C.c_int),
         "cfws_thread_device": ([], C.c_int),
+        "cfws_set_dropin_gpu_min": ([_sz], None),
+        "cfws_dropin_gpu_min": ([], _sz),
         "cfws_fill_splitmix": ([_vp, _u64, _u64, _u64, _vp], C.c_int),
         "cfws_h2_serialize_workspace_size": ([_sz, _u64, _u64, _u32], _sz),
         "cfws_h2_serialize_batch": ([_vp, _vp, _sz, _u32, _u32, _vp, _u64, _vp, _u64, _vp, _vp,

@@ -46,18 +46,12 @@ struct ThreadDevice {
     size_t host_cap = 0;
     bool zc_warm = false;          // first zero-copy frame done
     bool dma_warm = false;         // first DMA-path frame done
-    // the frame service (frames up to kCfwsServiceMax): a resident kernel on
-    // svc_stream polling the mailbox; both in mapped pinned host memory
-    uint64_t* mbox = nullptr;      // host address (cfws_internal.h: request, done, stop)
-    uint64_t* mbox_dev = nullptr;
-    uint8_t* svc_buf = nullptr;    // kCfwsServiceMax bytes, the frame is XORed here in place
-    uint8_t* svc_buf_dev = nullptr;
-    hipStream_t svc_stream = nullptr;
-    uint32_t seq = 0;              // last request the service finished
-    bool svc_running = false;      // a service kernel was launched and may still run
+    // the frame service (frames up to service_max()): this thread's slot in
+    // its device's service, and the seq of its last request there
+    int svc_slot = -1;
+    uint32_t seq = 0;
     bool svc_warm = false;         // first service frame done
-    double svc_last = 0;           // when the last request finished (steady clock, s)
-    bool holds() const { return stream || buf || host || mbox; }
+    bool holds() const { return stream || buf || host || svc_slot >= 0; }
 };
 
 // Device policy and per-device resource pool: cfws_devpolicy.h. The pool is
@@ -218,20 +212,22 @@ private:
     char* saved_ = nullptr;
 };
 
-// dst[i] = src[i] ^ key[i % 4] for a host buffer, through the device.
 // ---- the frame service ---------------------------------------------------
-// A masked frame of at most kCfwsServiceMax bytes (64 KiB) is XORed by a
-// resident kernel (dropin_service_kernel, cfws_ops.hip): the host copies
-// the frame into a mapped pinned buffer, posts one 64-bit request word
-// (key, length, seq) and spins on the done word, which the kernel writes
-// after its stores are released to system scope. No launch, no completion
-// signal per frame: config 1's 1 KiB frames go from a launch + synchronise
-// round trip to a PCIe round trip. The kernel exits
-// by itself after an idle spell (CFWS_DROPIN_SERVICE_IDLE_US, default 2000)
-// and is relaunched on the next frame; it is only ever relaunched after
-// hipStreamQuery has seen the previous one finish, so at most one kernel
-// serves a mailbox. CFWS_DROPIN_SERVICE=0 sends every frame through the
-// launch path instead.
+// A masked frame of at most service_max() bytes is XORed by a resident
+// kernel (dropin_service_kernel, cfws_ops.hip) that serves every calling
+// thread on its device: the thread copies the frame into its slot's mapped
+// pinned buffer, posts one 64-bit request word (key, length, seq) and spins
+// on its done word, which the kernel writes after its stores are released
+// to system scope. No launch and no completion signal per frame (DESIGN.md
+// section 6). One kernel per device, whatever the number of threads: with
+// GPU_MAX_HW_QUEUES = 4 the process's streams share hardware queues, and a
+// resident kernel per thread would queue other threads' launches behind
+// itself. The kernel ends after an idle spell (CFWS_DROPIN_SERVICE_IDLE_US,
+// default 2,000) or after CFWS_DROPIN_SERVICE_LIFE_US in all (default
+// 10,000: the longest a launch sharing its queue waits); the next request,
+// or a waiting thread that sees the exit word, launches it again. A thread
+// beyond the 64 slots, or one whose slot was given up after a timeout, takes
+// the launch path. CFWS_DROPIN_SERVICE=0 sends every frame there.
 bool service_enabled()
 {
     static const bool v = [] {
@@ -256,13 +252,22 @@ size_t service_max()
     return v;
 }
 
+double env_us(const char* name, double dflt, double lo)
+{
+    const char* s = getenv(name);
+    const double us = s && *s ? strtod(s, nullptr) : dflt;
+    return (us < lo ? lo : us) * 1e-6;
+}
+
 double service_idle_s()
 {
-    static const double v = [] {
-        const char* s = getenv("CFWS_DROPIN_SERVICE_IDLE_US");
-        const double us = s && *s ? strtod(s, nullptr) : 2000.0;
-        return (us < 50.0 ? 50.0 : us) * 1e-6;
-    }();
+    static const double v = env_us("CFWS_DROPIN_SERVICE_IDLE_US", 2000.0, 50.0);
+    return v;
+}
+
+double service_life_s()
+{
+    static const double v = env_us("CFWS_DROPIN_SERVICE_LIFE_US", 10000.0, 200.0);
     return v;
 }
 
@@ -271,125 +276,221 @@ double now_s()
     return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
-// Every mailbox ever created, so that process exit can tell the kernels to
-// stop (a plain host store each; no HIP call at exit).
-struct MailboxRegistry {
-    std::mutex mu;
-    std::vector<uint64_t*> boxes;
+// One per device, created by the first thread that needs it, never freed
+// (no HIP call at exit: the process-exit hook only sets the stop word).
+struct ServiceDevice {
+    std::mutex mu;                         // launches; slot allocation
+    uint64_t* ctl = nullptr;               // control page, host address
+    uint64_t* ctl_dev = nullptr;
+    uint8_t* bufs = nullptr;               // kCfwsServiceSlots x kCfwsServiceMax
+    uint8_t* bufs_dev = nullptr;
+    hipStream_t stream = nullptr;
+    uint64_t idle_ticks = 0, life_ticks = 0;
+    std::atomic<uint64_t> launched{0};     // generation of the last launch
+    uint64_t free_slots = ~0ull;           // under mu
+    uint64_t lost_slots = 0;               // given up after a timeout: never reused
+    bool failed = false;                   // set-up failed: launch path only
 };
 
-MailboxRegistry& mailboxes()
+std::mutex& services_mutex()
 {
-    static MailboxRegistry* r = new MailboxRegistry;
-    return *r;
+    static std::mutex* mu = new std::mutex;
+    return *mu;
 }
+
+ServiceDevice* g_services[kPoolDevices];   // under services_mutex()
 
 void stop_all_services()
 {
-    MailboxRegistry& r = mailboxes();
-    std::lock_guard<std::mutex> lock(r.mu);
-    for (uint64_t* m : r.boxes) __atomic_store_n(&m[2], uint64_t(1), __ATOMIC_RELEASE);
+    std::lock_guard<std::mutex> lock(services_mutex());
+    for (ServiceDevice* sd : g_services)
+        if (sd && sd->ctl) __atomic_store_n(&sd->ctl[kCfwsServiceStopWord], uint64_t(1), __ATOMIC_RELEASE);
 }
 
-bool service_setup(ThreadDevice& t_dev, int dev)
+// The device's service, set up on first use; nullptr when that failed.
+ServiceDevice* service_device(int dev)
 {
-    if (t_dev.mbox) return true;
+    std::lock_guard<std::mutex> lock(services_mutex());
+    ServiceDevice*& sd = g_services[dev];
+    if (sd) return sd->failed ? nullptr : sd;
+    sd = new ServiceDevice;
     CurrentDevice on(dev);
     void* m = nullptr;
     void* b = nullptr;
-    if (hipHostMalloc(&m, 4096, hipHostMallocMapped) != hipSuccess ||
-        hipHostMalloc(&b, kCfwsServiceMax, hipHostMallocMapped) != hipSuccess) {
-        fprintf(stderr, "cfws: frame service: hipHostMalloc failed\n");
-        if (m) (void)hipHostFree(m);
-        if (b) (void)hipHostFree(b);
-        return false;
-    }
     void* md = nullptr;
     void* bd = nullptr;
-    if (hipHostGetDevicePointer(&md, m, 0) != hipSuccess || hipHostGetDevicePointer(&bd, b, 0) != hipSuccess ||
-        hipStreamCreateWithFlags(&t_dev.svc_stream, hipStreamNonBlocking) != hipSuccess) {
-        fprintf(stderr, "cfws: frame service: mapping or stream failed\n");
-        (void)hipHostFree(m);
-        (void)hipHostFree(b);
-        t_dev.svc_stream = nullptr;
-        return false;
+    if (hipHostMalloc(&m, kCfwsServiceCtlBytes, hipHostMallocMapped) != hipSuccess ||
+        hipHostMalloc(&b, size_t(kCfwsServiceSlots) * kCfwsServiceMax, hipHostMallocMapped) != hipSuccess ||
+        hipHostGetDevicePointer(&md, m, 0) != hipSuccess || hipHostGetDevicePointer(&bd, b, 0) != hipSuccess ||
+        hipStreamCreateWithFlags(&sd->stream, hipStreamNonBlocking) != hipSuccess) {
+        fprintf(stderr, "cfws: frame service set-up on device %d failed; frames take the launch path\n", dev);
+        if (m) (void)hipHostFree(m);
+        if (b) (void)hipHostFree(b);
+        sd->failed = true;
+        return nullptr;
     }
-    memset(m, 0, 4096);
-    t_dev.mbox = static_cast<uint64_t*>(m);
-    t_dev.mbox_dev = static_cast<uint64_t*>(md);
-    t_dev.svc_buf = static_cast<uint8_t*>(b);
-    t_dev.svc_buf_dev = static_cast<uint8_t*>(bd);
-    t_dev.seq = 0;
-    t_dev.svc_running = false;
-    static std::once_flag exit_hook;
-    std::call_once(exit_hook, [] { atexit(stop_all_services); });
-    MailboxRegistry& r = mailboxes();
-    std::lock_guard<std::mutex> lock(r.mu);
-    r.boxes.push_back(t_dev.mbox);
-    return true;
-}
-
-bool service_launch(ThreadDevice& t_dev, int dev)
-{
+    memset(m, 0, kCfwsServiceCtlBytes);
+    sd->ctl = static_cast<uint64_t*>(m);
+    sd->ctl_dev = static_cast<uint64_t*>(md);
+    sd->bufs = static_cast<uint8_t*>(b);
+    sd->bufs_dev = static_cast<uint8_t*>(bd);
     int rate_khz = 0;
     if (hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess || rate_khz <= 0)
         rate_khz = 100000;
-    const uint64_t idle_ticks = (uint64_t)(service_idle_s() * 1e3 * (double)rate_khz);
-    __atomic_store_n(&t_dev.mbox[2], uint64_t(0), __ATOMIC_RELEASE);
+    sd->idle_ticks = (uint64_t)(service_idle_s() * 1e3 * (double)rate_khz);
+    sd->life_ticks = (uint64_t)(service_life_s() * 1e3 * (double)rate_khz);
+    static std::once_flag exit_hook;
+    std::call_once(exit_hook, [] { atexit(stop_all_services); });
+    return sd;
+}
+
+// Is the last launched kernel still serving? It has ended once it wrote its
+// generation to the exit word (after that it touches no slot).
+bool service_running(ServiceDevice& sd)
+{
+    const uint64_t g = sd.launched.load(std::memory_order_acquire);
+    return g != 0 && __atomic_load_n(&sd.ctl[kCfwsServiceExitWord], __ATOMIC_ACQUIRE) != g;
+}
+
+// Launches the next generation unless one is serving. Any thread may call;
+// one launches.
+bool service_ensure_running(ServiceDevice& sd, int dev)
+{
+    if (service_running(sd)) return true;
+    std::lock_guard<std::mutex> lock(sd.mu);
+    if (service_running(sd)) return true;
+    const uint64_t g = sd.launched.load(std::memory_order_relaxed) + 1;
     CurrentDevice on(dev);
-    if (cfws_internal_service_launch(t_dev.mbox_dev, t_dev.svc_buf_dev, idle_ticks, t_dev.seq, t_dev.svc_stream) !=
-        CFWS_OK)
+    if (cfws_internal_service_launch(sd.ctl_dev, sd.bufs_dev, g, sd.idle_ticks, sd.life_ticks, sd.stream) != CFWS_OK) {
+        fprintf(stderr, "cfws: frame service launch failed: %s\n", cfws_last_error());
         return false;
-    t_dev.svc_running = true;
+    }
+    sd.launched.store(g, std::memory_order_release);
     return true;
 }
 
-// Has the service kernel finished (idled out)? hipStreamQuery on its stream.
-bool service_finished(ThreadDevice& t_dev)
+int service_take_slot(ServiceDevice& sd)
 {
-    const hipError_t e = hipStreamQuery(t_dev.svc_stream);
-    if (e == hipErrorNotReady) return false;
-    if (e != hipSuccess) fprintf(stderr, "cfws: frame service: %s\n", hipGetErrorString(e));
-    return true;
+    std::lock_guard<std::mutex> lock(sd.mu);
+    if (!sd.free_slots) return -1;
+    const int s = __builtin_ctzll(sd.free_slots);
+    sd.free_slots &= sd.free_slots - 1;
+    return s;
 }
 
-bool service_xor(ThreadDevice& t_dev, int dev, const uint8_t* src, uint8_t* dst, size_t n, uint32_t key)
+void service_give_slot(int dev, int s)
 {
-    if (!service_setup(t_dev, dev)) return false;
-    // the kernel idles out service_idle_s() after its last request: well
-    // inside that, it is still polling; past half of it, ask the stream
-    if (t_dev.svc_running && now_s() - t_dev.svc_last > 0.5 * service_idle_s() && service_finished(t_dev))
-        t_dev.svc_running = false;
-    memcpy(t_dev.svc_buf, src, n);
-    uint32_t seq = (t_dev.seq + 1) & 0xffffu;
+    if (dev < 0 || dev >= kPoolDevices || s < 0) return;
+    ServiceDevice* sd = nullptr;
+    {
+        std::lock_guard<std::mutex> lock(services_mutex());
+        sd = g_services[dev];
+    }
+    if (!sd) return;
+    std::lock_guard<std::mutex> lock(sd->mu);
+    if (!(sd->lost_slots >> s & 1)) sd->free_slots |= 1ull << s;
+}
+
+// 1: done; 0: no slot or no service here (the caller takes the launch
+// path); -1: failed.
+int service_xor(ThreadDevice& t_dev, int dev, const uint8_t* src, uint8_t* dst, size_t n, uint32_t key)
+{
+    ServiceDevice* sd = service_device(dev);
+    if (!sd) return 0;
+    if (t_dev.svc_slot < 0) {
+        t_dev.svc_slot = service_take_slot(*sd);
+        if (t_dev.svc_slot < 0) return 0;
+        t_dev.seq = (uint32_t)(__atomic_load_n(&sd->ctl[kCfwsServiceDoneWord + t_dev.svc_slot], __ATOMIC_ACQUIRE) >> 48);
+    }
+    const int s = t_dev.svc_slot;
+    uint8_t* buf = sd->bufs + (size_t)s * kCfwsServiceMax;
+    memcpy(buf, src, n);
+    const uint32_t seq = (t_dev.seq + 1) & 0xffffu;
     const uint64_t word = (uint64_t)key | ((uint64_t)(n - 1) << 32) | ((uint64_t)seq << 48);
-    __atomic_store_n(&t_dev.mbox[0], word, __ATOMIC_RELEASE);
-    if (!t_dev.svc_running && !service_launch(t_dev, dev)) return false;
+    __atomic_store_n(&sd->ctl[kCfwsServiceReqWord + s], word, __ATOMIC_RELEASE);
+    t_dev.seq = seq;               // posted: never reused for another frame
+    if (!service_ensure_running(*sd, dev)) return -1;
+    const uint64_t* done = &sd->ctl[kCfwsServiceDoneWord + s];
     const double t0 = now_s();
     for (uint64_t spin = 1;; ++spin) {
-        if ((uint32_t)(__atomic_load_n(&t_dev.mbox[1], __ATOMIC_ACQUIRE) >> 48) == seq) break;
-        if ((spin & 1023u) == 0) {
-            const double dt = now_s() - t0;
-            if (dt > 5.0) {
-                fprintf(stderr, "cfws: frame service: no answer in 5 s\n");
-                return false;
+        if ((uint32_t)(__atomic_load_n(done, __ATOMIC_ACQUIRE) >> 48) == seq) break;
+        if ((spin & 255u) == 0) {
+            // the kernel may have ended (idle or lifetime) without taking
+            // the request: launch the next one
+            if (!service_ensure_running(*sd, dev)) return -1;
+            if (now_s() - t0 > 5.0) {
+                // give the slot up for good: the request stays posted, and a
+                // later kernel may still XOR that buffer
+                fprintf(stderr, "cfws: frame service: no answer in 5 s (slot %d given up)\n", s);
+                {
+                    std::lock_guard<std::mutex> lock(sd->mu);
+                    sd->lost_slots |= 1ull << s;
+                }
+                t_dev.svc_slot = -1;
+                return -1;
             }
-            // an exit that raced the request: relaunch once the old kernel
-            // has finished (never two kernels on one mailbox)
-            if (dt > 20e-6 && service_finished(t_dev) &&
-                (uint32_t)(__atomic_load_n(&t_dev.mbox[1], __ATOMIC_ACQUIRE) >> 48) != seq &&
-                !service_launch(t_dev, dev))
-                return false;
         }
         __builtin_ia32_pause();
     }
-    t_dev.seq = seq;
-    t_dev.svc_last = now_s();
-    memcpy(dst, t_dev.svc_buf, n);
-    return true;
+    memcpy(dst, buf, n);
+    return 1;
 }
 
 std::atomic<bool> g_runtime_up{false};   // the HIP runtime has been initialised by us
+
+// ---- the size policy --------------------------------------------------------
+// Below CFWS_DROPIN_GPU_MIN bytes (cfws_set_dropin_gpu_min at run time) a
+// masked payload is XORed on the calling thread: a frame that small costs
+// less there than one PCIe round trip to the device (SURVEY.md section 7:
+// the socket-driven per-frame API is latency-bound; profiles/r04_dropin_lat
+// has both sides measured). At or above it, the device paths below run. The
+// policy still needs the device: the first masked frame of the process
+// initialises it, and without a gfx950 agent every masked frame fails, on
+// both sides of the threshold, as before. The batch ABI (include/cfws.h) has
+// no host path at any size.
+std::atomic<size_t> g_gpu_min{[] {
+    const char* s = getenv("CFWS_DROPIN_GPU_MIN");
+    return s && *s ? (size_t)strtoull(s, nullptr, 10) : (size_t)CFWS_DROPIN_GPU_MIN_DEFAULT;
+}()};
+std::atomic<bool> g_device_ok{false};     // a gfx950 device answered cfws_init
+
+// dst[i] = src[i] ^ key[i % 4] (key byte j = bits 8j..8j+7), 16 bytes per
+// step on two 64-bit words (the compiler keeps them in one SSE register).
+void host_xor(const uint8_t* src, uint8_t* dst, size_t n, uint32_t key)
+{
+    const uint64_t k = (uint64_t)key | (uint64_t)key << 32;
+    size_t i = 0;
+    for (; i + 16 <= n; i += 16) {
+        uint64_t a, b;
+        memcpy(&a, src + i, 8);
+        memcpy(&b, src + i + 8, 8);
+        a ^= k;
+        b ^= k;
+        memcpy(dst + i, &a, 8);
+        memcpy(dst + i + 8, &b, 8);
+    }
+    for (; i < n; ++i) dst[i] = (uint8_t)(src[i] ^ (key >> (8 * (i & 3u))));
+}
+
+bool device_xor(const uint8_t* src, uint8_t* dst, size_t n, uint32_t key);
+
+bool payload_xor(const uint8_t* src, uint8_t* dst, size_t n, uint32_t key)
+{
+    if (n >= g_gpu_min.load(std::memory_order_relaxed)) return device_xor(src, dst, n, key);
+    if (!g_device_ok.load(std::memory_order_acquire)) {
+        RandomStateGuard keep_random_stream;
+        if (!g_runtime_up.load(std::memory_order_acquire)) keep_random_stream.engage();
+        const int dev = target_device();
+        if ((dev < 0 ? cfws_init() : cfws_init_device(dev)) != CFWS_OK || dev < 0) {
+            fprintf(stderr, "cfws: drop-in has no usable device (%s)\n", cfws_last_error());
+            return false;
+        }
+        g_runtime_up.store(true, std::memory_order_release);
+        g_device_ok.store(true, std::memory_order_release);
+    }
+    host_xor(src, dst, n, key);
+    return true;
+}
 
 bool device_xor(const uint8_t* src, uint8_t* dst, size_t n, uint32_t key)
 {
@@ -406,17 +507,18 @@ bool device_xor(const uint8_t* src, uint8_t* dst, size_t n, uint32_t key)
     ThreadDevice& t_dev = tdev(dev);
     if (service_enabled() && n <= service_max()) {
         if (!t_dev.svc_warm) keep_random_stream.engage();
-        if (!service_xor(t_dev, dev, src, dst, n, key)) return false;
-        t_dev.svc_warm = true;
-        return true;
+        const int r = service_xor(t_dev, dev, src, dst, n, key);
+        if (r < 0) return false;
+        if (r > 0) {
+            t_dev.svc_warm = true;
+            return true;
+        }
     }
     const bool zero_copy = n <= zero_copy_max();
     if (!t_dev.stream || (zero_copy ? (!t_dev.zc_warm || t_dev.host_cap < n) : (!t_dev.dma_warm || t_dev.cap < n)))
         keep_random_stream.engage();
-    {
-        CurrentDevice on(dev);
-        if (zero_copy ? !host_stage(t_dev, n) : !device_stage(t_dev, n)) return false;
-    }
+    CurrentDevice on(dev);         // held across the launch and the synchronize
+    if (zero_copy ? !host_stage(t_dev, n) : !device_stage(t_dev, n)) return false;
     hipStream_t st = t_dev.stream;
     if (zero_copy) {
         memcpy(t_dev.host, src, n);
@@ -497,7 +599,7 @@ bool co_ws_frame_serialize(bool fin, uint8_t opcode, bool mask, const void* data
     const uint32_t hs = encode_header(fin, opcode, mask, key, n, out);
     if (n > 0) {
         if (mask) {
-            if (!device_xor(static_cast<const uint8_t*>(data), out + hs, n, key)) return false;
+            if (!payload_xor(static_cast<const uint8_t*>(data), out + hs, n, key)) return false;
         } else {
             memcpy(out + hs, data, n);
         }
@@ -545,7 +647,7 @@ int co_ws_frame_deserialize(co_ws_frame_t* frame, const uint8_t* data, const siz
         if (!payload) return CO_WS_ERROR_OUT_OF_MEMORY;
         payload[n] = 0;
         if (mask) {
-            if (!device_xor(data + p, payload, static_cast<size_t>(n), key)) {
+            if (!payload_xor(data + p, payload, static_cast<size_t>(n), key)) {
                 free(payload);
                 return CO_WS_ERROR_OUT_OF_MEMORY;
             }
@@ -627,23 +729,7 @@ int cfws_draw_mask_keys_seeded(uint32_t seed, size_t n, const uint8_t* mask_flag
 void cfws_release_thread_resources(void)
 {
     ThreadDevice& t_dev = t_slot.current();
-    if (t_dev.mbox) {
-        __atomic_store_n(&t_dev.mbox[2], uint64_t(1), __ATOMIC_RELEASE);
-        if (t_dev.svc_stream) (void)hipStreamSynchronize(t_dev.svc_stream);
-        {
-            MailboxRegistry& r = mailboxes();
-            std::lock_guard<std::mutex> lock(r.mu);
-            for (auto& m : r.boxes)
-                if (m == t_dev.mbox) {
-                    m = r.boxes.back();
-                    r.boxes.pop_back();
-                    break;
-                }
-        }
-        (void)hipHostFree(t_dev.mbox);
-        if (t_dev.svc_buf) (void)hipHostFree(t_dev.svc_buf);
-        if (t_dev.svc_stream) (void)hipStreamDestroy(t_dev.svc_stream);
-    }
+    if (t_dev.svc_slot >= 0) service_give_slot(t_dev.device, t_dev.svc_slot);
     if (t_dev.buf) (void)hipFree(t_dev.buf);
     if (t_dev.host) (void)hipHostFree(t_dev.host);
     if (t_dev.stream) (void)hipStreamDestroy(t_dev.stream);
@@ -661,5 +747,8 @@ int cfws_bind_thread_device(int device)
 }
 
 int cfws_thread_device(void) { return target_device(); }
+
+void cfws_set_dropin_gpu_min(size_t bytes) { g_gpu_min.store(bytes, std::memory_order_relaxed); }
+size_t cfws_dropin_gpu_min(void) { return g_gpu_min.load(std::memory_order_relaxed); }
 
 }  // extern "C"

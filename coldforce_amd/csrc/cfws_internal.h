@@ -18,16 +18,30 @@ uint64_t cfws_internal_h2_grand_total_offset(uint64_t n_h2, uint64_t pool_cap, u
 int cfws_internal_copy_out(const void* d_src, void* dev_dst, uint64_t n, void* stream);
 
 // The drop-in's frame service (cfws_ops.hip, used by cfws_frame.cpp): one
-// resident workgroup that polls a mailbox in mapped host memory and XORs
-// each posted frame in place in a mapped host buffer, so a masked frame
-// costs no kernel launch and no completion signal. Mailbox words (u64):
-//   [0] request: key (bits 0-31) | n - 1 (bits 32-47) | seq (bits 48-63)
-//   [1] done:    seq of the last finished request (bits 48-63)
-//   [2] stop:    non-zero ends the kernel
-// The kernel also ends after idle_ticks of the wall clock without a request
-// (every wave reaches that exit). last_seq: the seq done before this launch.
+// resident workgroup per device that serves every calling thread of the
+// process. Each thread owns a slot: a request word and a done word in the
+// control page, and a kCfwsServiceMax-byte buffer; all in mapped host
+// memory. The thread copies its frame into its buffer and posts the request
+// word; the kernel XORs the buffer in place and writes the done word. No
+// launch and no completion signal per frame. Control page words (u64):
+//   [kCfwsServiceStopWord]   non-zero ends the kernel
+//   [kCfwsServiceExitWord]   the generation of the last launch that ended
+//   [kCfwsServiceReqWord + s]  slot s request: key (bits 0-31) | n - 1
+//                            (bits 32-47) | seq (bits 48-63)
+//   [kCfwsServiceDoneWord + s] slot s done: seq of its last finished
+//                            request (bits 48-63)
+// The kernel ends by itself after idle_ticks of the wall clock without a
+// request or after life_ticks in all (every wave reaches that exit) and
+// then writes `gen` to the exit word; requests it did not take stay posted
+// for the next launch.
 constexpr uint32_t kCfwsServiceMax = 65536;       // largest frame the service takes
-extern "C" int cfws_internal_service_launch(uint64_t* dev_mbox, uint8_t* dev_buf, uint64_t idle_ticks,
-                                            uint32_t last_seq, void* stream);
+constexpr uint32_t kCfwsServiceSlots = 64;        // calling threads per device
+constexpr uint32_t kCfwsServiceStopWord = 0;
+constexpr uint32_t kCfwsServiceExitWord = 1;
+constexpr uint32_t kCfwsServiceReqWord = 16;      // 64 words: bytes 128-639
+constexpr uint32_t kCfwsServiceDoneWord = 96;     // 64 words: bytes 768-1279
+constexpr uint32_t kCfwsServiceCtlBytes = 4096;
+extern "C" int cfws_internal_service_launch(uint64_t* dev_ctl, uint8_t* dev_bufs, uint64_t gen,
+                                            uint64_t idle_ticks, uint64_t life_ticks, void* stream);
 
 #endif

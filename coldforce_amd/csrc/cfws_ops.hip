@@ -265,79 +265,145 @@ stream_copy_kernel(const u32x4* __restrict__ src, u32x4* __restrict__ dst, uint6
 }
 
 // The drop-in's frame service (cfws_internal.h): the XOR of a masked frame
-// (co_ws_frame.c:93-97 / :234-242) without a launch per frame. One
-// workgroup of 1,024 threads; thread 0 polls the request word with
-// system-scope loads (s_sleep between polls), the workgroup XORs the frame
-// in place in the mapped host buffer (16-byte chunks, all of a 64 KiB frame
-// in flight at once; the buffer is 16-byte aligned: 4 KiB frames took one
-// round with 256 threads, 64 KiB four, 27 us), every thread releases its
-// stores at system scope, then
-// thread 0 publishes the seq in the done word. Exit: the stop word, or
-// idle_ticks without a request.
-constexpr uint32_t kServiceThreads = 1024;         // 16 KiB per round of loads
+// (co_ws_frame.c:93-97 / :234-242) without a launch per frame, for every
+// calling thread of a process on one device. One workgroup of 16 waves:
+//   * wave 0 dispatches: lane s polls slot s's request word with one
+//     coalesced system-scope load per round (all 64 slots' words in 512
+//     contiguous bytes of mapped host memory, s_sleep between rounds), and
+//     hands each new request to an idle worker wave through LDS;
+//   * waves 1-15 serve: a worker XORs its slot's buffer in place (16-byte
+//     chunks, up to 16 KiB of loads in flight per round, each a PCIe round
+//     trip), releases its stores at system scope and writes the slot's done
+//     word, so up to 15 threads' frames are in flight at once.
+// The kernel ends (a) when the stop word is set, (b) after idle_ticks of the
+// wall clock without a request, or (c) after life_ticks in all, so that a
+// stream sharing its hardware queue never waits behind it for longer
+// (GPU_MAX_HW_QUEUES = 4: streams share queues); requests still pending
+// then are served by the next launch. After every wave has left the loop,
+// thread 0 writes the launch's generation to the exit word: from then on
+// this kernel touches no slot, and the host may launch the next one.
+constexpr uint32_t kServiceThreads = 1024;
+constexpr uint32_t kServiceWorkers = kServiceThreads / 64 - 1;     // 15
+constexpr uint32_t kServiceRound = 16;             // chunks per lane per round (16 KiB per wave)
+static_assert(kCfwsServiceSlots == 64, "wave 0's lanes poll the slots");
+
+__device__ __forceinline__ uint64_t sys_load(const uint64_t* p)
+{
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__device__ __forceinline__ void sys_store(uint64_t* p, uint64_t v)
+{
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// One frame of n bytes at buf, XORed in place by one wave (chunk c at 16c:
+// key phase 0 for every chunk).
+__device__ __forceinline__ void service_xor_frame(uint8_t* buf, uint32_t n, uint32_t key, uint32_t lane)
+{
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");      // the frame's bytes, written by the host
+    const uint32_t nv = n / 16;
+    u32x4* b = reinterpret_cast<u32x4*>(buf);
+    for (uint32_t c0 = 0; c0 < nv; c0 += 64 * kServiceRound) {
+        u32x4 v[kServiceRound];
+#pragma unroll
+        for (uint32_t k = 0; k < kServiceRound; ++k) {
+            const uint32_t c = c0 + k * 64 + lane;
+            if (c < nv) v[k] = b[c];
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < kServiceRound; ++k) {
+            const uint32_t c = c0 + k * 64 + lane;
+            if (c < nv) b[c] = v[k] ^ key;
+        }
+    }
+    if (lane < n - nv * 16) {                          // the 0-15 tail bytes
+        const uint32_t i = nv * 16 + lane;
+        buf[i] = (uint8_t)(buf[i] ^ (key >> (8 * (i & 3u))));
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");      // the stores, before the done word
+}
 
 __global__ void __launch_bounds__(kServiceThreads)
-dropin_service_kernel(uint64_t* mbox, uint8_t* buf, uint64_t idle_ticks, uint32_t last_seq)
+dropin_service_kernel(uint64_t* ctl, uint8_t* bufs, uint64_t gen, uint64_t idle_ticks, uint64_t life_ticks)
 {
-    __shared__ uint64_t s_req;
+    // per worker: its slot + 1 (0 = idle) and the request word; the
+    // dispatcher writes the word, then the slot; the worker clears the slot
+    // once the done word is out
+    __shared__ uint64_t s_job[kServiceWorkers];
+    __shared__ uint32_t s_busy[kServiceWorkers];
     __shared__ uint32_t s_exit;
-    uint32_t last = last_seq & 0xffffu;
-    for (;;) {
-        if (threadIdx.x == 0) {
-            const uint64_t t0 = (uint64_t)wall_clock64();
-            uint32_t ex = 1;
-            uint64_t w = 0;
-            for (;;) {
-                w = __hip_atomic_load(&mbox[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                if ((uint32_t)(w >> 48) != last) {
-                    ex = 0;
-                    break;
+    const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+    if (threadIdx.x < kServiceWorkers) s_busy[threadIdx.x] = 0;
+    if (threadIdx.x == 0) s_exit = 0;
+    __syncthreads();
+    uint64_t* req = ctl + kCfwsServiceReqWord;
+    uint64_t* done = ctl + kCfwsServiceDoneWord;
+    if (wv == 0) {
+        // lane s: the seq last handed out for slot s (its done word at
+        // launch: every earlier request of the slot was finished)
+        uint32_t handed = (uint32_t)(sys_load(&done[lane]) >> 48);
+        const uint64_t t_start = (uint64_t)wall_clock64();
+        uint64_t t_last = t_start;
+        for (;;) {
+            const uint64_t now = (uint64_t)wall_clock64();
+            const bool retiring = sys_load(&ctl[kCfwsServiceStopWord]) != 0 || now - t_start > life_ticks;
+            if (!retiring) {
+                const uint64_t w = sys_load(&req[lane]);
+                uint64_t pend = __ballot((uint32_t)(w >> 48) != handed);
+                if (pend) t_last = now;
+                // each new request to an idle worker; a slot's next request
+                // comes only after its done word, so a slot is never on two
+                // workers (checked anyway)
+                while (pend) {
+                    const uint32_t s = (uint32_t)__builtin_ctzll(pend);
+                    pend &= pend - 1;
+                    uint32_t pick = kServiceWorkers;
+                    bool held = false;
+                    for (uint32_t k = 0; k < kServiceWorkers; ++k) {
+                        const uint32_t b = __hip_atomic_load(&s_busy[k], __ATOMIC_RELAXED,
+                                                             __HIP_MEMORY_SCOPE_WORKGROUP);
+                        held |= b == s + 1;
+                        if (b == 0 && pick == kServiceWorkers) pick = k;
+                    }
+                    if (held || pick == kServiceWorkers) continue;     // next round
+                    const uint64_t ws = __shfl(w, (int)s);
+                    if (lane == 0) {
+                        s_job[pick] = ws;
+                        __hip_atomic_store(&s_busy[pick], s + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    }
+                    if (lane == s) handed = (uint32_t)(ws >> 48);
                 }
-                if (__hip_atomic_load(&mbox[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0) break;
-                if ((uint64_t)wall_clock64() - t0 > idle_ticks) break;
-                __builtin_amdgcn_s_sleep(2);
             }
-            s_req = w;
-            s_exit = ex;
+            bool busy = false;
+            for (uint32_t k = 0; k < kServiceWorkers; ++k)
+                busy |= __hip_atomic_load(&s_busy[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 0;
+            // the workers finish the frames they hold before the kernel ends
+            if (!busy && (retiring || now - t_last > idle_ticks)) break;
+            __builtin_amdgcn_s_sleep(2);
         }
-        __syncthreads();
-        if (s_exit) break;
-        const uint64_t w = s_req;
-        const uint32_t key = (uint32_t)w;
-        const uint32_t n = (uint32_t)((w >> 32) & 0xffffu) + 1u;
-        const uint32_t nv = n / 16;
-        // wave w takes chunks [256 w, 256 w + 256) (4 KiB, 4 per lane), all
-        // of them in flight at once (each load is a PCIe round trip); waves
-        // past the frame skip the work and the fence, so a 1 KiB frame costs
-        // one wave's release, not sixteen
-        const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u;
-        const uint32_t c0 = wv * 256u;
-        if (c0 < nv || (c0 == nv && n > nv * 16)) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");   // the frame's bytes, written by the host
-            u32x4 v[4];
-#pragma unroll
-            for (uint32_t k = 0; k < 4; ++k) {
-                const uint32_t c = c0 + k * 64 + lane;
-                if (c < nv) v[k] = reinterpret_cast<const u32x4*>(buf)[c];
+        if (lane == 0) __hip_atomic_store(&s_exit, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    } else {
+        const uint32_t me = wv - 1;
+        for (;;) {
+            const uint32_t b = __hip_atomic_load(&s_busy[me], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (b == 0) {
+                if (__hip_atomic_load(&s_exit, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
+                __builtin_amdgcn_s_sleep(1);
+                continue;
             }
-#pragma unroll
-            for (uint32_t k = 0; k < 4; ++k) {
-                const uint32_t c = c0 + k * 64 + lane;
-                if (c < nv) reinterpret_cast<u32x4*>(buf)[c] = v[k] ^ key;    // chunk at 16c: phase 0
+            const uint32_t s = b - 1;
+            const uint64_t j = s_job[me];
+            const uint32_t n = (uint32_t)((j >> 32) & 0xffffu) + 1u;
+            service_xor_frame(bufs + (uint64_t)s * kCfwsServiceMax, n, (uint32_t)j, lane);
+            if (lane == 0) {
+                sys_store(&done[s], j & 0xffff000000000000ull);
+                __hip_atomic_store(&s_busy[me], 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
             }
-            // the tail bytes, by the wave whose span holds them
-            if (nv / 256 == wv && lane < n - nv * 16) {
-                const uint32_t i = nv * 16 + lane;
-                buf[i] = (uint8_t)(buf[i] ^ (key >> (8 * (i & 3u))));
-            }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");   // this wave's stores, before the done word
         }
-        __syncthreads();
-        last = (uint32_t)(w >> 48);
-        if (threadIdx.x == 0) __hip_atomic_store(&mbox[1], (uint64_t)last << 48, __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_SYSTEM);
-        __syncthreads();                                   // s_req / s_exit are rewritten next round
     }
+    __syncthreads();
+    if (threadIdx.x == 0) sys_store(&ctl[kCfwsServiceExitWord], gen);
 }
 
 __device__ __forceinline__ uint64_t splitmix64(uint64_t seed, uint64_t i)
@@ -831,12 +897,11 @@ int cfws_xor_mask(const void* d_src, void* d_dst, uint64_t n, uint32_t key, uint
     return launch_check("xor_mask");
 }
 
-int cfws_internal_service_launch(uint64_t* dev_mbox, uint8_t* dev_buf, uint64_t idle_ticks, uint32_t last_seq,
-                                 void* stream)
+int cfws_internal_service_launch(uint64_t* dev_ctl, uint8_t* dev_bufs, uint64_t gen, uint64_t idle_ticks,
+                                 uint64_t life_ticks, void* stream)
 {
-    static_assert(4 * kServiceThreads * 16 >= kCfwsServiceMax, "one round of loads covers a frame");
-    dropin_service_kernel<<<1, kServiceThreads, 0, static_cast<hipStream_t>(stream)>>>(dev_mbox, dev_buf,
-                                                                                     idle_ticks, last_seq);
+    dropin_service_kernel<<<1, kServiceThreads, 0, static_cast<hipStream_t>(stream)>>>(dev_ctl, dev_bufs, gen,
+                                                                                     idle_ticks, life_ticks);
     return launch_check("dropin_service");
 }
 

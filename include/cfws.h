@@ -417,6 +417,20 @@ void cfws_release_thread_resources(void);
 int cfws_bind_thread_device(int device);
 int cfws_thread_device(void);
 
+/* Size policy of the drop-in co_ws_frame_* calls (cfws_frame.cpp). A masked
+ * payload of fewer than `bytes` bytes is XORed on the calling thread, where
+ * one small frame costs less than a round trip to the device (SURVEY.md §7:
+ * the per-frame path is latency-bound; DESIGN.md §6.2 has the measured
+ * crossover); larger payloads run on the device. The policy never runs
+ * without the device: the first masked frame initialises it, and with no
+ * gfx950 agent every masked frame fails at any size. Default
+ * CFWS_DROPIN_GPU_MIN_DEFAULT, or the CFWS_DROPIN_GPU_MIN environment
+ * variable read at load; 0 sends every masked frame to the device.
+ * Process-wide. The batch ABI above has no host path at any size. */
+#define CFWS_DROPIN_GPU_MIN_DEFAULT 65536
+void cfws_set_dropin_gpu_min(size_t bytes);
+size_t cfws_dropin_gpu_min(void);
+
 /* ---- streaming device copy ------------------------------------------------
  * d_dst[i] = d_src[i], i < n: a bare HBM stream (the bench's copy ceiling,
  * the read + write shape of the codec without its frames). Pointers and n

@@ -64,6 +64,50 @@ int ref_deserialize(const unsigned char* data, unsigned long long size,
     return r;
 }
 
+/* n equal frames of fs payload bytes taken back to back from `arena`, each
+ * through co_ws_frame_serialize into a fresh byte array (co_ws_send's call,
+ * co_ws_client.c:443-449), the wire appended to `out`. Keys come from the
+ * reference's own random() draws (co_ws_frame.c:93-97). Returns the wire
+ * byte count, -1 if a serialize failed, -2 if `cap` is too small. */
+long long ref_serialize_run(const unsigned char* arena, unsigned long long n,
+                            unsigned long long fs, int fin, unsigned char opcode, int mask,
+                            unsigned char* out, unsigned long long cap)
+{
+    unsigned long long total = 0;
+    for (unsigned long long i = 0; i < n; ++i) {
+        long long w = ref_serialize(fin, opcode, mask, arena + i * fs, fs, out + total, cap - total);
+        if (w < 0) return w;
+        total += (unsigned long long)w;
+    }
+    return (long long)total;
+}
+
+/* The receive loop's walk (co_ws_server.c:107-169) over data[0, size): each
+ * frame through co_ws_frame_deserialize, its unmasked payload appended to
+ * `out`. Returns the frame count, or -(1 + k) when frame k did not decode
+ * COMPLETE, or -(1 << 40) if `cap` is too small. */
+long long ref_deserialize_run(const unsigned char* data, unsigned long long size,
+                              unsigned char* out, unsigned long long cap,
+                              unsigned long long* out_len)
+{
+    size_t index = 0;
+    unsigned long long used = 0;
+    long long k = 0;
+    while (index < size) {
+        co_ws_frame_t* f = co_ws_frame_create();
+        int r = co_ws_frame_deserialize(f, data, (size_t)size, &index);
+        if (r != CO_WS_PARSE_COMPLETE) { co_ws_frame_destroy(f); return -(1 + k); }
+        size_t n = (size_t)f->header.payload_size;
+        if (used + n > cap) { co_ws_frame_destroy(f); return -(1LL << 40); }
+        if (n) memcpy(out + used, f->payload_data, n);
+        used += n;
+        co_ws_frame_destroy(f);
+        ++k;
+    }
+    *out_len = used;
+    return k;
+}
+
 /* The receive loop of co_ws_server_on_tcp_receive_ready (co_ws_server.c
  * :107-169) around the reference's own co_ws_frame_deserialize, over
  * data[0, size) from receive index `begin`: the callbacks are replaced by

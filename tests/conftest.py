@@ -12,6 +12,8 @@ if ROOT not in sys.path:
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) device")
+    config.addinivalue_line("markers", "host_policy: keeps the drop-in's default size policy "
+                            "(tests/test_gpu_dropin.py)")
 
 
 def golden(name):

@@ -49,14 +49,15 @@ def _read_line(proc: subprocess.Popen, timeout: float) -> str:
 
 
 def run_echo(build: str, mode: str, frames: int, payload: int = 1024, window: int = 64, seed: int = 1,
-             port: int | None = None, capture_dir: str | None = None, timeout: float = 300.0) -> dict:
+             port: int | None = None, capture_dir: str | None = None, timeout: float = 300.0,
+             env: dict | None = None) -> dict:
     """One server process + one client process of `build` in `mode` ("ws" or
     "h2"). Returns the client's and server's JSON lines, return codes, stderr
     tails and, with capture_dir, the paths of each side's sent bytes."""
     exe = BUILDS[build]
     port = port or free_port()
-    env_s = dict(os.environ)
-    env_c = dict(os.environ)
+    env_s = dict(os.environ, **(env or {}))
+    env_c = dict(os.environ, **(env or {}))
     cap = {}
     if capture_dir:
         os.makedirs(capture_dir, exist_ok=True)

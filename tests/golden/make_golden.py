@@ -14,6 +14,9 @@ Fixtures (inputs + expected outputs):
                         size limits, concatenated frames, non-minimal lengths
   keys.json             mask-key stream after srandom(seed)
   batch_digests.json    SHA-256 of whole serialized batches (config 2 full size)
+  small_batch_digests.json  SHA-256 of the wire and of the reference's own
+                        deserialize output for the small-frame batches the
+                        bench quotes (4 M x 1 KiB TEXT, 16 M x 256 B BINARY)
   handshake_cases.json  Sec-WebSocket-Accept keys (co_sha1.c + co_base64.c)
   index_cases.json      receive-loop frame indexing (co_ws_server.c:107-169 around
                         the reference's co_ws_frame_deserialize): frame starts,
@@ -186,6 +189,43 @@ def batch_digest(R, n_frames, frame_size, payload_seed, key_seed, chunk=1024):
     return dict(n_frames=n_frames, frame_size=frame_size, payload_seed=payload_seed,
                 key_seed=key_seed, fin=True, opcode=2, mask=True, wire_len=total,
                 wire_sha256=h.hexdigest(), payload_sha256=hp.hexdigest())
+
+
+def small_batch_digest(R, n_frames, frame_size, payload_seed, key_seed, opcode, chunk=1 << 16):
+    """n_frames x frame_size frames through the reference, in C
+    (ref_serialize_run: co_ws_frame_serialize per frame, one byte array per
+    frame as co_ws_send does), then the concatenated wire walked back
+    through co_ws_frame_deserialize (ref_deserialize_run: the receive loop);
+    SHA-256 of the wire and of the reference's unmasked payloads."""
+    import ctypes as C
+    ser, de = R.ref_serialize_run, R.ref_deserialize_run
+    ser.argtypes = [C.c_void_p, C.c_ulonglong, C.c_ulonglong, C.c_int, C.c_ubyte, C.c_int,
+                    C.c_void_p, C.c_ulonglong]
+    ser.restype = C.c_longlong
+    de.argtypes = [C.c_void_p, C.c_ulonglong, C.c_void_p, C.c_ulonglong,
+                   C.POINTER(C.c_ulonglong)]
+    de.restype = C.c_longlong
+    hw, hp, ha = hashlib.sha256(), hashlib.sha256(), hashlib.sha256()
+    total = 0
+    O.srandom(R, key_seed)
+    wire = np.empty(chunk * (frame_size + 14), np.uint8)
+    back = np.empty(chunk * frame_size, np.uint8)
+    for c0 in range(0, n_frames, chunk):
+        c = min(n_frames, c0 + chunk) - c0
+        arena = O.splitmix_words(payload_seed, c0 * frame_size // 8, c * frame_size // 8).view(np.uint8)
+        ha.update(arena.tobytes())
+        w = ser(arena.ctypes.data, c, frame_size, 1, opcode, 1, wire.ctypes.data, wire.size)
+        assert w > 0, w
+        hw.update(wire[:w].tobytes())
+        total += w
+        used = C.c_ulonglong(0)
+        k = de(wire.ctypes.data, w, back.ctypes.data, back.size, C.byref(used))
+        assert k == c and used.value == c * frame_size, (k, used.value)
+        hp.update(back[:used.value].tobytes())
+    assert ha.hexdigest() == hp.hexdigest()
+    return dict(n_frames=n_frames, frame_size=frame_size, payload_seed=payload_seed,
+                key_seed=key_seed, fin=True, opcode=opcode, mask=True, wire_len=total,
+                wire_sha256=hw.hexdigest(), payload_sha256=hp.hexdigest())
 
 
 def zipf_digest(R, target, seed, key_seed, ping_every=0):
@@ -372,6 +412,13 @@ def handshake_cases(R):
     return [dict(key_hex=k.hex(), accept=O.ref_ws_accept_key(R, k)) for k in keys]
 
 
+def small_batches(R):
+    # the bench's payload / key seeds (bench.py PAYLOAD_SEED, KEY_SEED);
+    # 1 KiB as TEXT (config 1's frames), 256 B as BINARY
+    return [small_batch_digest(R, 4 << 20, 1024, 0x5EED0002, 2, 1),
+            small_batch_digest(R, 16 << 20, 256, 0x5EED0002, 2, 2)]
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--skip-full", action="store_true", help="skip the 4 GiB config-2 digest")
@@ -382,6 +429,9 @@ def main():
     assert R is not None, "oracle/_ref not built (needs /root/reference)"
     if a.only == "index":
         dump("index_cases.json", index_cases(R))
+        return
+    if a.only == "small":
+        dump("small_batch_digests.json", small_batches(R))
         return
     if a.only == "handshake":
         dump("handshake_cases.json", handshake_cases(R))
@@ -406,6 +456,8 @@ def main():
     dump("h2_digests.json", h2d)
     dump("index_cases.json", index_cases(R))
     dump("handshake_cases.json", handshake_cases(R))
+    if not a.skip_full:
+        dump("small_batch_digests.json", small_batches(R))
 
 
 if __name__ == "__main__":

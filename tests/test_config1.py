@@ -144,11 +144,15 @@ def test_dropin_build_fails_loudly_without_device():
 # GPU: the drop-in under the reference's callers
 # ---------------------------------------------------------------------------
 @pytest.mark.gpu
+@pytest.mark.parametrize("policy", ["default", "device"])
 @pytest.mark.parametrize("mode", ["ws", "h2"])
-def test_dropin_echo_wire_identical_to_stock(mode, tmp_path):
+def test_dropin_echo_wire_identical_to_stock(mode, policy, tmp_path):
     """Config 1 (100 k masked 1 KiB TEXT frames after srandom(1)) through the
     reference's callers: the drop-in build's wire equals the stock build's
-    byte for byte in both directions, and every echo checks."""
+    byte for byte in both directions, and every echo checks. Under the
+    default size policy the 1 KiB payloads are XORed on the calling thread;
+    with CFWS_DROPIN_GPU_MIN=0 every one goes through the device (the frame
+    service)."""
     _need("stock")
     _need("cfws")
     frames = 100_000
@@ -156,7 +160,8 @@ def test_dropin_echo_wire_identical_to_stock(mode, tmp_path):
     out = {}
     for build in ("stock", "cfws"):
         r = run_echo(build, mode, frames, PAYLOAD, window=64, seed=1, port=port,
-                     capture_dir=str(tmp_path / build), timeout=240)
+                     capture_dir=str(tmp_path / build), timeout=240,
+                     env={"CFWS_DROPIN_GPU_MIN": "0"} if policy == "device" else None)
         _ok(r, frames)
         out[build] = r
     for side in ("client", "server"):
@@ -169,14 +174,17 @@ def test_dropin_echo_wire_identical_to_stock(mode, tmp_path):
     if dst:
         with open(dst, "a") as f:
             for build in ("stock", "cfws"):
-                f.write(json.dumps({"test": "wire_identical", "build": build, **out[build]["client"]}) + "\n")
+                f.write(json.dumps({"test": "wire_identical", "build": build, "mode": mode,
+                                    "policy": policy, **out[build]["client"]}) + "\n")
 
 
 @pytest.mark.gpu
 def test_dropin_echo_small_frames_and_binary_sizes(tmp_path):
     """Frame sizes around the header-length boundaries through the real
     callers (125/126 B, 65,535/65,536 B) are checked by every echo; the wire
-    equals the stock build's."""
+    equals the stock build's. 65,535 B is the last size the default size
+    policy XORs on the calling thread, 65,536 B the first it sends to the
+    device."""
     _need("stock")
     _need("cfws")
     for payload, frames in ((125, 2000), (126, 2000), (65535, 200), (65536, 200)):

@@ -268,6 +268,56 @@ def test_config2_full_size_digest():
     _roundtrip_digest(g, full=True)
 
 
+def _sha_device(t: "torch.Tensor", n: int) -> str:
+    h = hashlib.sha256()
+    step = 1 << 28
+    for o in range(0, n, step):
+        h.update(t[o:min(n, o + step)].cpu().numpy().tobytes())
+    return h.hexdigest()
+
+
+@pytest.mark.parametrize("which", [0, 1], ids=["4M_x_1KiB_text", "16M_x_256B_binary"])
+def test_small_frame_reference_digests(which):
+    """The small-frame batches the bench quotes (4,194,304 x 1 KiB TEXT and
+    16,777,216 x 256 B BINARY, the bench's seeds) through the bench's own
+    calls: serialize plan + execute (single-pass look-back plan, in-region
+    send edges) and deserialize plan + execute at 16-byte slots. The wire's
+    SHA-256 equals the reference's co_ws_frame_serialize output
+    (co_ws_frame.c:21-119, compiled in place, tests/golden/make_golden.py
+    small_batch_digest), and the unmasked payloads' SHA-256 equals what the
+    reference's co_ws_frame_deserialize walk (co_ws_frame.c:121-247) returned
+    from that wire."""
+    g = golden("small_batch_digests.json")[which]
+    n, fs = g["n_frames"], g["frame_size"]
+    desc = W.uniform_batch(n, fs, g["key_seed"], opcode=g["opcode"])
+    offs, total = W.wire_layout(desc)
+    assert total == g["wire_len"]
+    payload = torch.empty(n * fs, dtype=torch.uint8, device="cuda")
+    cfws.fill_splitmix(payload, g["payload_seed"])
+    d_t = cfws.desc_to_device(desc)
+    wire = torch.full((W.round16(total),), 0xEE, dtype=torch.uint8, device="cuda")
+    ws = cfws.workspace(n, wire.numel())
+    tot = torch.zeros(1, dtype=torch.int64, device="cuda")
+    cfws.serialize_plan(d_t, wire.numel(), tot, ws)
+    cfws.serialize_execute(payload, d_t, wire, ws)
+    torch.cuda.synchronize()
+    assert tot.item() == total
+    assert _sha_device(wire, total) == g["wire_sha256"]
+    del ws
+    idx = torch.from_numpy(offs.astype(np.int64)).cuda()
+    back = torch.full((n * fs + 64,), 0xEE, dtype=torch.uint8, device="cuda")
+    desc_de = torch.empty((n, 32), dtype=torch.uint8, device="cuda")
+    status = torch.full((n,), 99, dtype=torch.int32, device="cuda")
+    ws = cfws.workspace(n, back.numel())
+    ptot = torch.zeros(1, dtype=torch.int64, device="cuda")
+    cfws.deserialize_plan(wire, total, idx, desc_de, status, back.numel(), ptot, ws, align=16)
+    cfws.deserialize_execute(wire, desc_de, status, back, ws)
+    torch.cuda.synchronize()
+    assert ptot.item() == n * fs and bool((status == 0).all())
+    assert _sha_device(back, n * fs) == g["payload_sha256"]
+    assert torch.equal(back[:n * fs], payload)
+
+
 def _roundtrip_digest(g, full=False):
     n, fs = g["n_frames"], g["frame_size"]
     desc = W.uniform_batch(n, fs, g["key_seed"])

@@ -26,6 +26,18 @@ def device():
     cfws.init()
 
 
+@pytest.fixture(autouse=True)
+def device_policy(request):
+    """Every masked frame to the device (CFWS_DROPIN_GPU_MIN = 0) unless a
+    test asks for the size policy's default (marker `host_policy`)."""
+    L = cfws.lib()
+    saved = L.cfws_dropin_gpu_min()
+    if request.node.get_closest_marker("host_policy") is None:
+        L.cfws_set_dropin_gpu_min(0)
+    yield
+    L.cfws_set_dropin_gpu_min(saved)
+
+
 def test_serialize_golden_cases():
     import ctypes
     libc = ctypes.CDLL(None)
@@ -120,7 +132,7 @@ def _fnv1a(b: bytes) -> int:
     return h
 
 
-@pytest.mark.parametrize("zc_max", [None, "0", "1000", "service_off"])
+@pytest.mark.parametrize("zc_max", [None, "0", "1000", "service_off", "policy_default"])
 def test_link_level_dropin_harness(zc_max):
     """oracle/_ref/dropin_link: a C program built against coldforce's own
     headers (co_ws_frame.h, co_ws_config.h, co_byte_array.h) and the
@@ -137,7 +149,10 @@ def test_link_level_dropin_harness(zc_max):
     env = dict(os.environ)
     env.pop("CFWS_DROPIN_ZC_MAX", None)
     env.pop("CFWS_DROPIN_SERVICE", None)
-    if zc_max == "service_off":
+    env["CFWS_DROPIN_GPU_MIN"] = "0"
+    if zc_max == "policy_default":
+        env.pop("CFWS_DROPIN_GPU_MIN")            # < 64 KiB on the calling thread
+    elif zc_max == "service_off":
         env["CFWS_DROPIN_SERVICE"] = "0"          # every frame through the launch path
     elif zc_max is not None:
         env["CFWS_DROPIN_ZC_MAX"] = zc_max
@@ -292,3 +307,104 @@ def test_frame_service_idle_relaunch_and_seq_wrap():
         ok, got = cfws.frame_serialize(True, 2, True, data)
         O.srandom(L, 77)
         assert ok and got == O.ref_serialize(L, True, 2, True, data)
+
+
+@pytest.mark.host_policy
+def test_size_policy_both_sides():
+    """The drop-in's size policy (cfws_set_dropin_gpu_min): payloads below the
+    threshold are XORed on the calling thread, at or above it on the device;
+    the wire and the decoded payloads equal the reference's on both sides,
+    at the default threshold and at moved ones (0: all device; huge: all
+    host), for sizes around the 16-byte step and the threshold itself."""
+    import ctypes
+    libc = ctypes.CDLL(None)
+    L = cfws.lib()
+    Lo = O.lib()
+    default = L.cfws_dropin_gpu_min()
+    assert default == 65536
+    rng = random.Random(12)
+    for gmin in (default, 0, 1000, 1 << 40):
+        L.cfws_set_dropin_gpu_min(gmin)
+        for n in (1, 3, 15, 16, 17, 999, 1000, 1001, 4096, 65535, 65536, 65537, 300000):
+            data = rng.randbytes(n)
+            libc.srandom(n + gmin % 1000)
+            ok, w = cfws.frame_serialize(True, 2, True, data)
+            assert ok
+            O.srandom(Lo, n + gmin % 1000)
+            assert w == O.ref_serialize(Lo, True, 2, True, data), (gmin, n)
+            assert cfws.frame_deserialize(w) == O.ref_deserialize(Lo, w), (gmin, n)
+
+
+def test_service_many_threads_streaming():
+    """16 threads on one device each stream masked frames through the frame
+    service for 300 ms (1 KiB and 16 KiB frames alternating, deserialize of
+    oracle-built frames plus serialize checked against the oracle's
+    serialization under the key it drew), while a 17th thread sends 100 KiB
+    frames through the launch path: the service kernel never idles out, it
+    ends at its lifetime (CFWS_DROPIN_SERVICE_LIFE_US, 10 ms) and is
+    relaunched under load, every frame is correct, and no call waits
+    anywhere near the 5 s timeout (the largest per-frame time is reported
+    and bounded)."""
+    import threading
+    import time
+    Lo = O.lib()
+    frames = []
+    for n in (1024, 16384, 100_000):
+        data = random.Random(n).randbytes(n)
+        O.srandom(Lo, n)
+        frames.append((O.ref_serialize(Lo, True, 2, True, data), data))
+    errors, counts, worst = [], {}, {}
+    t_end = time.perf_counter() + 0.3
+
+    def run(k):
+        try:
+            c, slow = 0, 0.0
+            big = k == 16
+            while time.perf_counter() < t_end:
+                w, data = frames[2] if big else frames[c % 2]
+                t0 = time.perf_counter()
+                r = cfws.frame_deserialize(w)
+                slow = max(slow, time.perf_counter() - t0)
+                assert r["rc"] == 0 and r["payload"] == data + b"\0", (k, c)
+                if not big:
+                    ok, s = cfws.frame_serialize(True, 1, True, data)
+                    assert ok
+                    key = int.from_bytes(s[len(s) - len(data) - 4:len(s) - len(data)], "little")
+                    assert s == O.serialize_keyed(True, 1, True, key, data), (k, c)
+                c += 1
+            counts[k], worst[k] = c, slow
+        except Exception as e:          # reported from the main thread
+            errors.append(e)
+
+    ts = [threading.Thread(target=run, args=(k,)) for k in range(17)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errors, errors
+    print("frames per thread", counts, "worst per-frame s", {k: round(v, 4) for k, v in worst.items()})
+    assert all(counts[k] > 20 for k in range(17)), counts
+    assert max(worst.values()) < 1.0, worst
+
+
+def test_service_idle_gap_keeps_random_stream():
+    """Two masked frames serialized after one srandom(), with a pause longer
+    than the service's idle timeout between them (the second frame finds the
+    kernel gone and relaunches it): both wires equal the reference's for the
+    same seed, so nothing on the relaunch path consumed random()."""
+    import ctypes
+    import time
+    libc = ctypes.CDLL(None)
+    Lo = O.lib()
+    datas = [random.Random(k).randbytes(n) for k, n in enumerate((1024, 20000, 77))]
+    cfws.frame_serialize(True, 2, True, b"warm")        # service set up outside the seeded run
+    time.sleep(0.02)
+    libc.srandom(4321)
+    got = []
+    for d in datas:
+        ok, w = cfws.frame_serialize(True, 2, True, d)
+        assert ok
+        got.append(w)
+        time.sleep(0.02)                                 # > CFWS_DROPIN_SERVICE_IDLE_US (2 ms)
+    O.srandom(Lo, 4321)
+    assert got == [O.ref_serialize(Lo, True, 2, True, d) for d in datas]
