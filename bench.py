@@ -611,15 +611,25 @@ def main():
     tot_ser = torch.zeros(1, dtype=torch.int64, device=dev)
     tot_de = torch.zeros(1, dtype=torch.int64, device=dev)
 
+    # batches of small frames (<= 512 B of wire per frame on average, no
+    # reassembly) deserialize in one call: cfws_deserialize_batch runs the
+    # fused plan + copy kernel there (deserialize_plan_single_kernel<true>),
+    # so the timed kernel is that launch; other batches plan, then execute
+    fused_de = flags == 0 and F > 1024 and wire_total // F <= 512     # kFusedAvgMax (cfws_device.hip)
+
     def step(ev=None):
         cfws.serialize_plan(desc_ser, wire.numel(), tot_ser, ws_ser)
         if ev: ev[0].record()
         cfws.serialize_execute(payload, desc_ser, wire, ws_ser)
         if ev: ev[1].record()
-        cfws.deserialize_plan(wire, wire_total, index, desc_de, status, back.numel(), tot_de,
-                              ws_de, align=16, flags=flags)
-        if ev: ev[2].record()
-        cfws.deserialize_execute(wire, desc_de, status, back, ws_de, flags=flags)
+        if fused_de:
+            if ev: ev[2].record()
+            cfws.deserialize(wire, wire_total, index, back, desc_de, status, ws_de, tot_de, align=16)
+        else:
+            cfws.deserialize_plan(wire, wire_total, index, desc_de, status, back.numel(), tot_de,
+                                  ws_de, align=16, flags=flags)
+            if ev: ev[2].record()
+            cfws.deserialize_execute(wire, desc_de, status, back, ws_de, flags=flags)
         if ev: ev[3].record()
 
     for _ in range(args.warmup):
@@ -677,6 +687,7 @@ def main():
     dom_ms = max(ser_ms, de_ms)
     achieved = alg_bytes / (dom_ms * 1e-3) / 1e9
     kernel_symbol = ("xform_kernel<0>" if dom_name == "serialize_execute"   # kModeSer
+                     else "deserialize_plan_single_kernel<true>" if fused_de  # fused plan + copy
                      else "xform_kernel<1>")                                 # kModeDeser
     # the PMC summary a traffic figure may come from: the same workload only
     traffic_key = (f"config2:{F}x{fs}" if args.workload == "config2" else

@@ -271,8 +271,16 @@ deserialize_plan_reduce_kernel(const uint8_t* __restrict__ wire, uint64_t wire_s
 // 232 us on it for 4 M frames. With a capacity cut the region map clips at
 // the capacity itself: a frame's range ends at or below the grand total, so
 // that is the same clip as at min(total, capacity).
+// The serialize plan reads every descriptor whole and writes it back whole
+// (CFWS_SER_PLAN_FULL, default; 8 frames per thread for the registers): a
+// descriptor line then leaves L2 fully written, and the payload offset is
+// not fetched a second time. 0: the sizes first, the payload offset after
+// the look-back, two fields written (16 frames per thread).
+#ifndef CFWS_SER_PLAN_FULL
+#define CFWS_SER_PLAN_FULL 0
+#endif
 #ifndef CFWS_SINGLE_ITEMS_SER
-#define CFWS_SINGLE_ITEMS_SER 16
+#define CFWS_SINGLE_ITEMS_SER (CFWS_SER_PLAN_FULL ? 8 : 16)
 #endif
 #ifndef CFWS_SINGLE_ITEMS_DESER
 #define CFWS_SINGLE_ITEMS_DESER 8
@@ -362,13 +370,29 @@ serialize_plan_single_kernel(cfws_frame_desc_t* __restrict__ desc, uint64_t* __r
     // a branch per item made it a round trip per item)
     uint64_t len[kSingleItems];
     uint32_t msk[kSingleItems];
+    bool bad = false;                                  // a frame outside ser_inreg_frame_ok
+#if CFWS_SER_PLAN_FULL
+    uint64_t poff[kSingleItems], w3[kSingleItems];
+#pragma unroll
+    for (int k = 0; k < kSingleItems; ++k) {
+        const uint64_t f = f0 + uint64_t(k) * 64, fc = f < n ? f : n - 1;
+        const DescWords d = load_desc(desc, (uint32_t)fc);
+        poff[k] = d.payload_off;
+        len[k] = d.payload_size;
+        w3[k] = d.w3;
+        msk[k] = d.mask();
+    }
+#pragma unroll
+    for (int k = 0; k < kSingleItems; ++k)
+        bad |= f0 + uint64_t(k) * 64 < n && !ser_inreg_frame_ok(len[k], (uint32_t)poff[k]);
+#else
 #pragma unroll
     for (int k = 0; k < kSingleItems; ++k) {
         const uint64_t f = f0 + uint64_t(k) * 64, fc = f < n ? f : n - 1;
         len[k] = desc[fc].payload_size;
         msk[k] = desc[fc].mask;
     }
-    bool bad = false;                                  // a frame outside ser_inreg_frame_ok
+#endif
 #pragma unroll
     for (int k = 0; k < kSingleItems; ++k) {
         const uint64_t f = f0 + uint64_t(k) * 64;
@@ -384,11 +408,20 @@ serialize_plan_single_kernel(cfws_frame_desc_t* __restrict__ desc, uint64_t* __r
         const uint64_t run = pre + ex[k];
         offs[f] = run;
         const uint32_t hs = (uint32_t)((hsp >> (4 * k)) & 15u);
+#if CFWS_SER_PLAN_FULL
+        // the whole descriptor: the line leaves L2 fully written
+        uint64_t* q = reinterpret_cast<uint64_t*>(desc) + 4 * f;
+        q[0] = poff[k];
+        q[1] = run;
+        q[2] = len[k];
+        q[3] = (w3[k] & ~(uint64_t(0xff) << 56)) | uint64_t(hs) << 56;
+#else
         // (the payload offset read here, not with the sizes: 276 VGPRs there)
         bad |= !ser_inreg_frame_ok(v[k] - hs, (uint32_t)desc[f].payload_off);
         // both descriptor fields at once, so the line is written back once
         desc[f].wire_off = run;
         desc[f].header_size = (uint8_t)hs;
+#endif
         map_range(run, run + v[k], f, capacity, map);
         if (f == n - 1) {
             const uint64_t g = run + v[k], t = g < capacity ? g : capacity;
@@ -403,12 +436,158 @@ serialize_plan_single_kernel(cfws_frame_desc_t* __restrict__ desc, uint64_t* __r
     if (__syncthreads_or(bad) && threadIdx.x == 0) atomicOr(look + gridDim.x + 1, 1u);
 }
 
+// ---- the fused deserialize: plan and copy in one pass ------------------------
+// For batches of small frames at 16-byte slots (cfws_deserialize_batch),
+// each block of the single-pass plan copies its own frames once their
+// offsets are known, so the header lines the plan reads are the lines the
+// copy streams next (one pass over the wire instead of two: the plan alone
+// re-read 0.5 GB of 128-byte lines for 4 M x 1 KiB frames, 2.2 GB for
+// 16 M x 256 B). Wave w copies the frames it parsed (item k, lane l: frame
+// k * 64 + l of its run). Per item, the wave's largest slot sets how many
+// frames share one wave-instruction: groups of G lanes (G x 16 bytes >= the
+// slot), one frame per group; items with a slot over 1 KiB go frame by
+// frame, 1 KiB per instruction. A lane's chunk is its frame's source block
+// funnel-shifted with the next lane's block over DPP (the lane loads the
+// next block itself at its group's end), XORed with the key (each chunk
+// starts at a payload index that is a multiple of 16, so the key needs no
+// rotation) and masked past the payload: every slot byte below the pass
+// total is written once, payload or zero, as the plan + execute write it.
+#ifndef CFWS_FUSED_UNROLL
+#define CFWS_FUSED_UNROLL 4
+#endif
+#ifndef CFWS_FUSED_MIN_BLOCKS
+#define CFWS_FUSED_MIN_BLOCKS 5
+#endif
+constexpr int kFusedUnroll = CFWS_FUSED_UNROLL;   // rounds of loads in flight per wave
+
+__device__ __forceinline__ void fused_store(uint8_t* __restrict__ out, uint64_t D, uint64_t total, uint4 o)
+{
+    if (D + 16 <= total) {
+        st16(out + D, o);
+    } else {
+        for (uint32_t j = 0; D + j < total; ++j) {
+            const uint32_t w = j < 4 ? o.x : (j < 8 ? o.y : (j < 12 ? o.z : o.w));
+            out[D + j] = (uint8_t)(w >> (8 * (j & 3)));
+        }
+    }
+}
+
+// One round of every lane's chunk: frame info by lane (fl: the lane of
+// the wave holding the frame), chunk c of it. Loads issued, returned in
+// A / E for fused_finish.
+struct FusedChunk {
+    uint64_t D, s;
+    uint32_t need, nbytes, key, c;
+};
+
+__device__ __forceinline__ void fused_item(const uint8_t* __restrict__ wire, uint8_t* __restrict__ out,
+                                           uint64_t total, uint64_t run, uint64_t src, uint32_t len,
+                                           uint32_t nb, uint32_t key, uint32_t lane)
+{
+    // wave-wide largest slot
+    uint32_t m = nb;
+#pragma unroll
+    for (uint32_t o = 32; o >= 1; o >>= 1) {
+        const uint32_t y = (uint32_t)__shfl_xor((int)m, o, 64);
+        m = y > m ? y : m;
+    }
+    const uint4 z = make_uint4(0, 0, 0, 0);
+    if (m == 0) return;
+    if (m <= 1024) {
+        // G lanes per frame (G x 16 >= m), P = 64 / G frames per round
+        uint32_t G = 1;
+        while (G * 16 < m) G <<= 1;
+        const uint32_t P = 64 / G, g = lane / G, c = lane % G;
+        for (uint32_t r0 = 0; r0 < G; r0 += kFusedUnroll) {
+            uint4 A[kFusedUnroll], E[kFusedUnroll];
+            FusedChunk q[kFusedUnroll];
+            bool nl[kFusedUnroll];
+#pragma unroll
+            for (int u = 0; u < kFusedUnroll; ++u) {
+                const uint32_t r = r0 + u;
+                const int fl = (int)((r < G ? r : 0) * P + g);
+                const uint64_t runj = __shfl(run, fl, 64), srcj = __shfl(src, fl, 64);
+                const uint32_t lenj = (uint32_t)__shfl((int)len, fl, 64);
+                const uint32_t nbj = r < G ? (uint32_t)__shfl((int)nb, fl, 64) : 0u;
+                q[u].key = (uint32_t)__shfl((int)key, fl, 64);
+                q[u].D = runj + 16 * c;
+                q[u].s = srcj + 16 * c;
+                q[u].nbytes = 16 * c < nbj ? (uint32_t)(nbj - 16 * c < 16 ? nbj - 16 * c : 16) : 0u;
+                q[u].need = q[u].nbytes && 16 * c < lenj ? (uint32_t)(lenj - 16 * c < 16 ? lenj - 16 * c : 16) : 0u;
+                nl[u] = c + 1 < G && 16 * (c + 1) < lenj;          // the next lane loads the next block
+                const uint32_t ph = (uint32_t)(q[u].s & 15u);
+                A[u] = q[u].need ? ld16(wire + (q[u].s & ~uint64_t(15))) : z;
+                E[u] = q[u].need && ph && !nl[u] && ph + q[u].need > 16
+                           ? ld16(wire + (q[u].s & ~uint64_t(15)) + 16) : z;
+            }
+#pragma unroll
+            for (int u = 0; u < kFusedUnroll; ++u) {
+                const uint4 nb4 = from_next_lane(A[u], E[u]);      // every lane: DPP needs the full wave
+                if (!q[u].nbytes) continue;
+                const uint32_t ph = (uint32_t)(q[u].s & 15u);
+                uint4 o = z;
+                if (q[u].need) {
+                    o = ph ? funnel16(A[u], nl[u] ? nb4 : E[u], ph) : A[u];
+                    xor4(o, q[u].key);
+                    if (q[u].need < 16) o = and4(o, byte_range(0, q[u].need));
+                }
+                fused_store(out, q[u].D, total, o);
+            }
+        }
+        return;
+    }
+    // items with a slot over 1 KiB: frame by frame, wave-uniform
+    for (int j = 0; j < 64; ++j) {
+        const uint64_t nbj = (uint32_t)__builtin_amdgcn_readlane((int)nb, j);
+        if (nbj == 0) continue;
+        const uint64_t runj = __shfl(run, j, 64), srcj = __shfl(src, j, 64);
+        const uint64_t lenj = (uint32_t)__builtin_amdgcn_readlane((int)len, j);
+        const uint32_t kj = (uint32_t)__shfl((int)key, j, 64);
+        const uint32_t ph = (uint32_t)(srcj & 15u);
+        for (uint64_t c0 = 0; c0 < nbj; c0 += 64 * 16 * kFusedUnroll) {
+            uint4 A[kFusedUnroll], E[kFusedUnroll];
+            uint32_t need[kFusedUnroll];
+            bool nl[kFusedUnroll];
+#pragma unroll
+            for (int u = 0; u < kFusedUnroll; ++u) {
+                const uint64_t k0 = c0 + (uint64_t)u * 1024 + 16 * lane;
+                need[u] = k0 < lenj ? (uint32_t)(lenj - k0 < 16 ? lenj - k0 : 16) : 0u;
+                nl[u] = lane != 63 && k0 + 16 < lenj;
+                const uint64_t s = srcj + k0;
+                A[u] = need[u] ? ld16(wire + (s & ~uint64_t(15))) : z;
+                E[u] = need[u] && ph && !nl[u] && ph + need[u] > 16 ? ld16(wire + (s & ~uint64_t(15)) + 16) : z;
+            }
+#pragma unroll
+            for (int u = 0; u < kFusedUnroll; ++u) {
+                const uint4 nb4 = from_next_lane(A[u], E[u]);
+                const uint64_t k0 = c0 + (uint64_t)u * 1024 + 16 * lane;
+                if (k0 >= nbj) continue;
+                uint4 o = z;
+                if (need[u]) {
+                    o = ph ? funnel16(A[u], nl[u] ? nb4 : E[u], ph) : A[u];
+                    xor4(o, kj);
+                    if (need[u] < 16) o = and4(o, byte_range(0, need[u]));
+                }
+                fused_store(out, runj + k0, total, o);
+            }
+        }
+    }
+}
+
 // deserialize_plan_reduce_kernel + deserialize_plan_apply_kernel in one
 // launch, without reassembly (its control-frame pass starts at the data
 // pass's grand total, which no block knows before the last one). The
 // descriptors are written as parsed, their payload offsets (and the
-// capacity rule's status) once the offsets are known.
-__global__ void __launch_bounds__(kThreads)
+// capacity rule's status) once the offsets are known. kCopy: the fused
+// deserialize (above): each block then copies its frames into `out`; no
+// offsets or region map are written (no execute follows).
+#ifndef CFWS_FUSED_ITEMS
+#define CFWS_FUSED_ITEMS 2
+#endif
+constexpr int kFusedItems = CFWS_FUSED_ITEMS;   // frames per thread in the fused form (registers)
+
+template <bool kCopy>
+__global__ void __launch_bounds__(kThreads, kCopy ? CFWS_FUSED_MIN_BLOCKS : 1)
 deserialize_plan_single_kernel(const uint8_t* __restrict__ wire, uint64_t wire_size_all,
                                const uint64_t* __restrict__ index, const uint64_t* __restrict__ ends,
                                uint64_t n, uint64_t max_payload, uint64_t align,
@@ -416,12 +595,13 @@ deserialize_plan_single_kernel(const uint8_t* __restrict__ wire, uint64_t wire_s
                                uint64_t* __restrict__ offs, uint32_t* __restrict__ look,
                                uint64_t* __restrict__ agg, uint64_t* __restrict__ incl,
                                uint64_t* __restrict__ hdr, uint64_t capacity, uint32_t* __restrict__ map,
-                               uint64_t* __restrict__ user_total)
+                               uint64_t* __restrict__ user_total, uint8_t* __restrict__ out = nullptr,
+                               const uint64_t* __restrict__ grand = nullptr)
 {
     __shared__ uint64_t s_wave[kWaves];
     __shared__ uint64_t s_prefix;
     __shared__ uint32_t s_bid;
-    constexpr int kSingleItems = kSingleItemsDeser;
+    constexpr int kSingleItems = kCopy ? kFusedItems : kSingleItemsDeser;
     constexpr uint64_t kSingleFrames = uint64_t(kThreads) * kSingleItems;
     const uint32_t b = plan_ticket(look, &s_bid);
     const uint64_t f0 = uint64_t(b) * kSingleFrames + uint64_t(threadIdx.x >> 6) * (64 * kSingleItems) +
@@ -491,12 +671,17 @@ deserialize_plan_single_kernel(const uint8_t* __restrict__ wire, uint64_t wire_s
         }
     }
     const uint64_t pre = single_block_prefix(b, wave_scan_items(v, ex), s_wave, &s_prefix, look, agg, incl);
+    // kCopy: what the copy needs per item, compact (the parse's arrays die here)
+    uint64_t c_run[kSingleItems], c_src[kSingleItems];
+    uint32_t c_len[kSingleItems], c_nb[kSingleItems], c_key[kSingleItems];
 #pragma unroll
     for (int k = 0; k < kSingleItems; ++k) {
         const uint64_t f = f0 + uint64_t(k) * 64;
+        c_run[k] = c_src[k] = 0;
+        c_len[k] = c_nb[k] = c_key[k] = 0;
         if (f >= n) continue;
         const uint64_t run = pre + ex[k];
-        offs[f] = run;
+        if (!kCopy) offs[f] = run;
         uint64_t* q = reinterpret_cast<uint64_t*>(desc) + 4 * f;
         q[0] = run;
         q[1] = wo[k];
@@ -506,10 +691,23 @@ deserialize_plan_single_kernel(const uint8_t* __restrict__ wire, uint64_t wire_s
         int32_t st = sts[k];
         if (st == CFWS_PARSE_COMPLETE && ps[k] > 0 && run + ps[k] > capacity) st = CFWS_ERROR_OUT_OF_MEMORY;
         status[f] = st;
-        map_range(run, run + v[k], f, capacity, map);
+        if (kCopy) {
+            // slot bytes below the capacity (every slot ends at or below the
+            // grand total, so that is the pass total's cut); the payload
+            // only for a frame still COMPLETE, zeros otherwise
+            const uint64_t end = run + v[k] < capacity ? run + v[k] : capacity;
+            const uint64_t nbk = end > run ? end - run : 0;
+            c_run[k] = run;
+            c_src[k] = wo[k] + (w3[k] >> 56);
+            c_nb[k] = nbk < 0xffffffffull ? (uint32_t)nbk : 0xffffffffu;
+            c_len[k] = st == CFWS_PARSE_COMPLETE ? (uint32_t)(ps[k] < nbk ? ps[k] : nbk) : 0u;
+            c_key[k] = (w3[k] >> 48) & 0xffu ? (uint32_t)w3[k] : 0u;
+        } else {
+            map_range(run, run + v[k], f, capacity, map);
+        }
         if (f == n - 1) {
             const uint64_t g = run + v[k], t = g < capacity ? g : capacity;
-            map[(t + kRegion - 1) / kRegion] = (uint32_t)f;
+            if (!kCopy) map[(t + kRegion - 1) / kRegion] = (uint32_t)f;
             hdr[0] = t;
             hdr[1] = 0;
             hdr[2] = t;
@@ -517,6 +715,27 @@ deserialize_plan_single_kernel(const uint8_t* __restrict__ wire, uint64_t wire_s
             if (user_total) *user_total = t;
         }
     }
+    if (!kCopy) return;
+    // the copy: every slot byte below the pass total min(grand total,
+    // capacity), cut at the capacity itself (above)
+    (void)grand;
+    const uint32_t lane = threadIdx.x & 63u;
+#pragma unroll
+    for (int k = 0; k < kSingleItems; ++k)
+        fused_item(wire, out, capacity, c_run[k], c_src[k], c_len[k], c_nb[k], c_key[k], lane);
+}
+
+// The fused deserialize (deserialize_plan_single_kernel<true>) for batches
+// of more than kSmallFrames frames averaging at most kFusedAvgMax wire
+// bytes (CFWS_FUSED_DESER=0: plan + execute; A/B knob). A block copies its
+// own frames, so a batch mixing a few huge frames into small ones would
+// leave those to single waves: the average keeps such batches on the
+// region stream.
+constexpr uint64_t kFusedAvgMax = 512;
+bool fused_deser()
+{
+    static const bool v = env_knob("CFWS_FUSED_DESER", 1) != 0;
+    return v;
 }
 
 // Single-pass plans above kSelfScanBlocks blocks (CFWS_PLAN_SINGLE=0: the
@@ -856,7 +1075,7 @@ int deserialize_plan_impl(const void* d_wire, uint64_t wire_size, const uint64_t
         const uint32_t sb = grid_for(n, uint64_t(kThreads) * kSingleItemsDeser);
         if (hipMemsetAsync(look, 0, 4 * (uint64_t(sb) + 1), st) != hipSuccess)
             return launch_check("deserialize_plan");
-        deserialize_plan_single_kernel<<<sb, kThreads, 0, st>>>(
+        deserialize_plan_single_kernel<false><<<sb, kThreads, 0, st>>>(
             static_cast<const uint8_t*>(d_wire), wire_size, d_index, d_ends, n, max_payload, align, d_desc,
             d_status, offs0, look, part0, part1, hdr, cap, ws_ptr<uint32_t>(ws, L.map[0]), d_total);
         return launch_check("deserialize_plan");
@@ -1015,6 +1234,23 @@ int cfws_deserialize_batch(const void* d_wire, uint64_t wire_size, const uint64_
             d_desc, d_status, static_cast<uint8_t*>(d_payload), cap,
             ws_ptr<uint64_t>(ws, ws_layout(n, cap).hdr), d_total);
         return launch_check("deserialize_batch(small)");
+    }
+    // small frames at 16-byte (or wider) slots: the fused plan + copy
+    if (fused_deser() && flags == 0 && align >= 16 && align <= 4096 && (align & (align - 1)) == 0 &&
+        n > kSmallFrames && n <= 0xffffffffull && wire_size / n <= kFusedAvgMax && check_init() == CFWS_OK &&
+        d_wire && d_index && d_desc && d_status && ws && ws_size >= ws_layout(n, cap).bytes &&
+        (cap == 0 || (d_payload && !misaligned(d_payload, d_wire)))) {
+        const WsLayout L = ws_layout(n, cap);
+        hipStream_t st = static_cast<hipStream_t>(stream);
+        uint32_t* look = ws_ptr<uint32_t>(ws, L.look);
+        const uint32_t sb = grid_for(n, uint64_t(kThreads) * kFusedItems);
+        if (hipMemsetAsync(look, 0, 4 * (uint64_t(sb) + 1), st) != hipSuccess)
+            return launch_check("deserialize_batch(fused)");
+        deserialize_plan_single_kernel<true><<<sb, kThreads, 0, st>>>(
+            static_cast<const uint8_t*>(d_wire), wire_size, d_index, nullptr, n, max_payload, align, d_desc,
+            d_status, nullptr, look, ws_ptr<uint64_t>(ws, L.partials[0]), ws_ptr<uint64_t>(ws, L.partials[1]),
+            ws_ptr<uint64_t>(ws, L.hdr), cap, nullptr, d_total, static_cast<uint8_t*>(d_payload));
+        return launch_check("deserialize_batch(fused)");
     }
     if (int rc = cfws_deserialize_plan(d_wire, wire_size, d_index, n, max_payload, align, flags,
                                        d_desc, d_status, cap, d_total, ws, ws_size, stream))

@@ -141,10 +141,12 @@ __device__ __forceinline__ uint64_t data_frames_of(uint64_t W, uint64_t S)
 
 __global__ void __launch_bounds__(kThreads)
 h2_ser_plan_reduce_kernel(cfws_frame_desc_t* __restrict__ desc, uint64_t n, uint64_t S,
-                          uint64_t* __restrict__ partials_w, uint64_t* __restrict__ partials_k)
+                          uint64_t* __restrict__ partials_w, uint64_t* __restrict__ partials_k,
+                          uint32_t* __restrict__ inreg_flag)
 {
     __shared__ uint64_t s_wave[kWaves];
     const uint64_t f = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
+    if (f == 0) *inreg_flag = 0;                         // the apply kernel ORs misses in
     uint64_t w = 0, k = 0;
     if (f < n) {
         const uint64_t len = desc[f].payload_size;
@@ -173,7 +175,7 @@ h2_ser_plan_apply_kernel(cfws_frame_desc_t* __restrict__ desc, uint64_t n, uint6
                          uint64_t nb, uint32_t self_scan, uint64_t* __restrict__ hdr, uint64_t capacity,
                          uint64_t n_max, cfws_frame_desc_t* __restrict__ ddesc,
                          uint64_t* __restrict__ doffs, uint32_t* __restrict__ map,
-                         uint64_t* __restrict__ user_total)
+                         uint64_t* __restrict__ user_total, uint32_t* __restrict__ inreg_flag)
 {
     __shared__ uint64_t s_wave[kWaves];
     uint64_t pre_w, pre_k, gw, gk;
@@ -209,24 +211,29 @@ h2_ser_plan_apply_kernel(cfws_frame_desc_t* __restrict__ desc, uint64_t n, uint6
             // h_in of them header; stored as the send pass reads it
             // (frame_view<kModeH2Ser>): body source offset and length, key
             // rotated to the body's first payload index, bytes before the
-            // body (9 + h_in), END_STREAM; the WS frame in wire_off, s0 in
-            // opcode (the output offset is doffs[d])
+            // body (9 + h_in), END_STREAM; for the first slice (h_in > 0:
+            // with S >= 64 the whole WS header, s0 = 0) the WS header's
+            // fields: payload size in wire_off, byte 0 in opcode, the mask
+            // bit (the output offset is doffs[d])
             const uint64_t s0 = j * S;
             const uint64_t len = (j + 1 < k) ? S : w - s0;
             const uint64_t h_in = s0 < hs ? (hs - s0 < len ? hs - s0 : len) : 0;
             const uint64_t q = s0 + h_in - hs;           // payload index of the body start
             cfws_frame_desc_t e;
             e.payload_off = wd.payload_off + q;
-            e.wire_off = f;
+            e.wire_off = h_in ? wd.payload_size : 0;
             e.payload_size = len - h_in;
             e.mask_key = wd.mask() ? rotr8(wd.key(), (uint32_t)(q & 3u)) : 0u;
             e.fin = (j + 1 == k) ? 1 : 0;
-            e.opcode = h_in ? (uint8_t)s0 : 0;
-            e.mask = 0;
+            e.opcode = h_in ? (uint8_t)((wd.opcode() | (wd.fin() ? 0x80u : 0u)) & 0xffu) : 0;
+            e.mask = h_in && wd.mask() ? 1 : 0;
             e.header_size = (uint8_t)(9 + h_in);
             ddesc[d] = e;
             const uint64_t out = 9 * d + w0 + s0;
             doffs[d] = out;
+            // the send's in-region edge chunks need every DATA frame but the
+            // stream's last to span a region and more (two_frame_region)
+            if (9 + len < kRegion + 32 && d + 1 < gk) atomicOr(inreg_flag, 1u);
             // DATA frames lie back to back: this one ends where d + 1 starts
             map_range(out, out + 9 + len, d, total, map);
         }
@@ -669,6 +676,18 @@ extern "C" {
 
 namespace {
 
+// CFWS_H2_INREG=1: the fused send's two-frame regions write the edge chunks
+// of a batch whose DATA frames (all but the last) span more than a region
+// (two_frame_region<kModeH2Ser, true>). Off by default: on config 5 it cut
+// the sub-64-byte write requests from 160 K to 47 K per launch and the
+// wave-cycles by 8.6 %, yet the step ran 0.5-1.5 % slower on the same box
+// (profiles/r04/h2_inreg_ab/). Parity-tested both ways.
+bool h2_inreg()
+{
+    static const bool v = env_knob("CFWS_H2_INREG", 0) != 0;
+    return v;
+}
+
 struct H2SerLayout {
     uint64_t ser;        // WS serialize workspace
     uint64_t hdr;        // [0] wrapped total (clamped) [3] DATA-frame count
@@ -770,6 +789,9 @@ int cfws_h2_serialize_batch(const void* d_payload, cfws_frame_desc_t* d_desc, si
     cfws_frame_desc_t* ddesc = ws_ptr<cfws_frame_desc_t>(ws, L.ddesc);
     uint64_t* doffs = ws_ptr<uint64_t>(ws, L.doffs);
     uint32_t* map = ws_ptr<uint32_t>(ws, L.map);
+    // clear: every DATA frame but the last spans more than a region, and
+    // the send's two-frame regions write the edge chunks (kEdges)
+    uint32_t* inreg = reinterpret_cast<uint32_t*>(hdr + 8);
     if (fused) {
         // WS layout + DATA frames + region map in two launches (three above
         // kSelfScanBlocks blocks)
@@ -777,10 +799,11 @@ int cfws_h2_serialize_batch(const void* d_payload, cfws_frame_desc_t* d_desc, si
         const uint32_t self_scan = nb <= kSelfScanBlocks ? 1u : 0u;
         uint64_t* pw = ws_ptr<uint64_t>(ws, WL.partials[0]);
         uint64_t* pk = ws_ptr<uint64_t>(ws, WL.partials[1]);
-        h2_ser_plan_reduce_kernel<<<nb, kThreads, 0, st>>>(d_desc, n, S, pw, pk);
+        h2_ser_plan_reduce_kernel<<<nb, kThreads, 0, st>>>(d_desc, n, S, pw, pk, inreg);
         if (!self_scan) scan_partials2_kernel<<<2, kThreads, 0, st>>>(pw, pk, nb, hdr + 4, hdr + 5);
         h2_ser_plan_apply_kernel<<<nb, kThreads, 0, st>>>(d_desc, n, S, pw, pk, nb, self_scan, hdr,
-                                                         h2_cap, L.n_max, ddesc, doffs, map, d_h2_total);
+                                                         h2_cap, L.n_max, ddesc, doffs, map, d_h2_total,
+                                                         inreg);
     } else {
         if (int rc = cfws_serialize_batch(d_payload, d_desc, n, d_wire, wire_cap, nullptr, ws, WL.bytes,
                                           stream))
@@ -798,7 +821,8 @@ int cfws_h2_serialize_batch(const void* d_payload, cfws_frame_desc_t* d_desc, si
     // 3. the DATA frames: 9-byte header + slice, one streaming pass
     if (h2_cap && fused)
         launch_streaming<kModeH2Ser>(d_payload, d_h2, ddesc, nullptr, doffs, map, hdr, nullptr,
-                                     L.regions, h2_cap, L.n_max, kClassAll, stream_id, st, d_desc);
+                                     L.regions, h2_cap, L.n_max, kClassAll, stream_id, st, d_desc, true,
+                                     nullptr, h2_inreg() ? inreg : nullptr);
     else if (h2_cap)
         launch_streaming<kModeH2Wrap>(d_wire, d_h2, ddesc, nullptr, doffs, map, hdr, nullptr,
                                       L.regions, h2_cap, L.n_max, kClassAll, stream_id, st);

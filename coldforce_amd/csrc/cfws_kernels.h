@@ -176,8 +176,8 @@ struct FrameView {
     uint32_t key;   // 0 when the frame is not masked: XOR becomes a copy
     uint32_t pre;
     uint32_t hb;    // serialize: header byte 0 | mask bit << 8; DATA: flags
-    uint32_t aux;   // kModeH2Ser: the parent WS frame (its header bytes come from it)
-    uint32_t s0;    // kModeH2Ser: the slice's first byte within the WS frame
+    uint32_t whb;   // kModeH2Ser, a WS frame's first slice: its WS header byte 0 | mask bit << 8
+    uint64_t wlen;  // kModeH2Ser, a WS frame's first slice: the WS payload size
 };
 
 // Byte r < pre of a serialize frame's header, from its view (co_ws_frame.c:34-91).
@@ -201,19 +201,21 @@ __device__ __forceinline__ FrameView frame_view(const Pass& P, uint32_t f)
     v.key = d.mask() ? d.key() : 0u;
     v.out_off = P.offs[f];
     v.hb = 0;
-    v.aux = 0;
-    v.s0 = 0;
+    v.whb = 0;
+    v.wlen = 0;
     if (kMode == kModeH2Ser) {
         // one DATA frame as h2_ser_plan_apply_kernel laid it out: body
         // source offset and length, rotated key, 9 + h_in bytes before the
-        // body (0: an unused slot), END_STREAM, the WS frame, s0
+        // body (0: an unused slot), END_STREAM, and for a WS frame's first
+        // slice (h_in > 0: the whole WS header, max_frame_size >= 64) the
+        // WS header's fields: no load of the WS frame's descriptor
         v.pre = d.header_size();
         v.body_len = d.payload_size;
         v.src_off = d.payload_off;
         v.key = d.key();
         v.hb = d.fin() ? 0x1u : 0u;                      // DATA flags: END_STREAM
-        v.aux = (uint32_t)d.wire_off;
-        v.s0 = d.opcode();                             // only read when pre > 9 (s0 < 14)
+        v.whb = d.opcode() | (d.mask() ? 0x100u : 0u);
+        v.wlen = d.wire_off;
     } else if (is_ser(kMode)) {
         v.pre = d.header_size();
         v.body_len = d.payload_size;
@@ -291,10 +293,15 @@ __device__ __forceinline__ void st16(uint8_t* p, uint4 o)
 #ifndef CFWS_STORE_AUX_RECV
 #define CFWS_STORE_AUX_RECV 19
 #endif
+#ifndef CFWS_STORE_AUX_H2SER
+#define CFWS_STORE_AUX_H2SER 0
+#endif
 template <int kMode>
 __device__ __forceinline__ void st16_region(uint8_t* rb, uint32_t off, uint4 o)
 {
-    constexpr int aux = kMode == kModeDeser ? CFWS_STORE_AUX_RECV : (kMode == kModeSer ? CFWS_STORE_AUX_SER : 0);
+    constexpr int aux = kMode == kModeDeser ? CFWS_STORE_AUX_RECV
+                      : kMode == kModeSer ? CFWS_STORE_AUX_SER
+                      : kMode == kModeH2Ser ? CFWS_STORE_AUX_H2SER : 0;
     if (aux == 0) {
         st16(rb + off, o);
     } else {
@@ -347,13 +354,12 @@ __device__ __forceinline__ uint32_t header_byte_of(const Pass& P, const FrameVie
     if (kMode == kModeH2Wrap) return h2_header_byte((uint32_t)v.body_len, v.hb, P.sid, r);
     if (kMode == kModeH2Ser) {
         if (r < 9) return h2_header_byte(v.pre - 9u + (uint32_t)v.body_len, v.hb, P.sid, r);
-        // the WS frame's header (co_ws_frame.c:34-91)
-        const DescWords w = load_desc(P.parent, v.aux);
+        // the WS frame's header (co_ws_frame.c:34-91), from the slice's fields
         FrameView wv;
-        wv.body_len = w.payload_size;
-        wv.key = w.mask() ? w.key() : 0u;
-        wv.hb = ((w.opcode() | (w.fin() ? 0x80u : 0u)) & 0xffu) | (w.mask() ? 0x100u : 0u);
-        return view_header_byte(wv, r - 9u + v.s0);
+        wv.body_len = v.wlen;
+        wv.key = v.key;                                 // the first slice: rotated by 0
+        wv.hb = v.whb;
+        return view_header_byte(wv, r - 9u);
     }
     return view_header_byte(v, r);
 }
@@ -515,11 +521,7 @@ __device__ __forceinline__ HeaderWords header_words(const Pass& P, const FrameVi
         const uint32_t len = v.pre - 9u + (uint32_t)v.body_len;
         const uint32_t sid = P.sid & 0x7fffffffu;
         uint4 w = z;
-        if (v.pre > 9u) {
-            const DescWords p = load_desc(P.parent, v.aux);
-            const uint32_t hb = ((p.opcode() | (p.fin() ? 0x80u : 0u)) & 0xffu) | (p.mask() ? 0x100u : 0u);
-            w = funnel16(ws_header_words(p.payload_size, hb, p.mask() ? p.key() : 0u), z, v.s0 & 15u);
-        }
+        if (v.pre > 9u) w = ws_header_words(v.wlen, v.whb, v.key);
         HeaderWords h;
         h.lo.x = (len >> 16 & 0xffu) | (len >> 8 & 0xffu) << 8 | (len & 0xffu) << 16;
         h.lo.y = (v.hb & 0xffu) | (sid >> 24 & 0xffu) << 8 | (sid >> 16 & 0xffu) << 16 |
@@ -646,7 +648,20 @@ __device__ __forceinline__ void fast_region(const Pass& P, const FrameView& v, u
 // edge_kernel. As in fast_region, a lane's block B comes from the next lane
 // over DPP when that lane loads it (same frame, chunk inside the body);
 // otherwise (lane 63, the last chunk before a body end) the lane loads it.
-template <int kMode>
+//
+// kEdges (the fused HTTP/2 send when its plan found every DATA frame but the
+// last at least kRegion + 32 bytes long, h2_ser_plan_apply_kernel): the
+// region's edge chunks too, assembled from registers and stored in the same
+// instruction as their segment's body chunks, so no edge workgroup writes
+// them and no 64-byte segment leaves L2 in two parts. With
+// such frames a region holds at most one header, vb's (the frames are back
+// to back: va's body ends where vb starts), and an edge chunk at r is
+//   [va's body tail: bytes < q] [vb's header at q = vb.out_off - r]
+//   [vb's body head from q + pre on]
+// (va == vb: the header started at or before the region; no tail). The
+// header words and the body's first 16 masked bytes are wave-uniform,
+// computed once per region; the tail is the lane's own source blocks.
+template <int kMode, bool kEdges = false>
 __device__ __forceinline__ void two_frame_region(const Pass& P, const FrameView& va,
                                                  const FrameView& vb, uint64_t base, uint32_t lane)
 {
@@ -668,7 +683,11 @@ __device__ __forceinline__ void two_frame_region(const Pass& P, const FrameView&
     const uint32_t krA = rotr8(va.key, (uint32_t)(base - va.body_start) & 3u);
     const uint32_t krB = rotr8(vb.key, (uint32_t)(base - vb.body_start) & 3u);
     const uint8_t* sp[kUnroll];
-    bool fast[kUnroll], own[kUnroll], hi[kUnroll];
+    bool fast[kUnroll], own[kUnroll], hi[kUnroll], tl[kUnroll];
+    // kEdges: vb's header start relative to the region (va == vb: <= 0)
+    const bool twof = kEdges && vb.out_off != va.out_off;
+    const int64_t hs64 = (int64_t)vb.out_off - (int64_t)base;
+    const int hs = hs64 < -64 ? -64 : (hs64 > (int64_t)kRegion ? (int)kRegion : (int)hs64);
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u) {
         const uint32_t r = u * (uint32_t)kSlice + lane * (uint32_t)kChunk;
@@ -678,22 +697,65 @@ __device__ __forceinline__ void two_frame_region(const Pass& P, const FrameView&
         // the next lane's chunk loads block sp + 16 iff it is in the same
         // frame and inside the body
         const bool next_loads = lane != 63 && (r + 16 >= ob) == hi[u] && r + 32 <= hi_;
-        own[u] = fast[u] && (hi[u] ? phB : phA) != 0 && !next_loads;
+        // kEdges: the chunk holding va's body tail (and vb's header start)
+        tl[u] = twof && !fast[u] && (int)r < hs;
+        own[u] = (fast[u] && (hi[u] ? phB : phA) != 0 && !next_loads) ||
+                 (tl[u] && phA + (uint32_t)(hs - (int)r) > 16u);
         sp[u] = P.src + (((hi[u] ? sB : sA) + r) & ~uint64_t(15));
     }
     uint4 a[kUnroll], e[kUnroll];
 #pragma unroll
-    for (int u = 0; u < kUnroll; ++u) a[u] = fast[u] ? ld16(sp[u]) : make_uint4(0, 0, 0, 0);
+    for (int u = 0; u < kUnroll; ++u) a[u] = fast[u] || tl[u] ? ld16(sp[u]) : make_uint4(0, 0, 0, 0);
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u) e[u] = own[u] ? ld16(sp[u] + 16) : make_uint4(0, 0, 0, 0);
+    // kEdges: vb's header words and its body's first 16 bytes, masked
+    // (every lane loads the same two blocks; a full 64-bit VGPR address, see
+    // general_region_ser_edges)
+    HeaderWords H = {};
+    uint4 W0 = make_uint4(0, 0, 0, 0);
+    if (kEdges) {
+        H = header_words<kMode>(P, vb);
+        uint64_t addr = reinterpret_cast<uint64_t>(P.src) + (vb.src_off & ~uint64_t(15));
+        asm volatile("" : "+v"(addr));
+        const uint8_t* p0 = reinterpret_cast<const uint8_t*>(addr);
+        const uint32_t ph0 = (uint32_t)(vb.src_off & 15u);
+        // only blocks that hold a body byte (the stream's last frame may be
+        // short when the pass ends on a region boundary)
+        if (vb.body_len > 0) W0 = ld16(p0);
+        if (ph0) W0 = funnel16(W0, vb.body_len > 16 - ph0 ? ld16(p0 + 16) : make_uint4(0, 0, 0, 0), ph0);
+        xor4(W0, vb.key);
+    }
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u) {
         const uint4 nb = from_next_lane(a[u], e[u]);     // every lane: DPP needs the full wave
+        const uint32_t R = u * (uint32_t)kSlice + lane * (uint32_t)kChunk;
+        if (kEdges && !fast[u]) {
+            const uint4 z = make_uint4(0, 0, 0, 0);
+            const int q = hs - (int)R;                   // vb's header byte 0 at chunk byte q
+            const int pre = (int)vb.pre;
+            uint4 o = z;
+            if (tl[u]) {                                 // va's body tail: bytes [0, q)
+                uint4 t = phA ? funnel16(a[u], e[u], phA) : a[u];
+                xor4(t, krA);
+                o = and4(t, byte_range(0, (uint32_t)(q < 16 ? q : 16)));
+            }
+            if (q < 16 && q + pre > 0) {                 // the header: bytes [q, q + pre)
+                uint4 Hs;
+                if (q >= 0) Hs = q == 0 ? H.lo : funnel16(z, H.lo, 16u - (uint32_t)q);
+                else Hs = -q < 16 ? funnel16(H.lo, H.hi, (uint32_t)-q) : funnel16(H.hi, z, (uint32_t)(-q - 16));
+                o = or4(o, and4(Hs, byte_range(q > 0 ? (uint32_t)q : 0u,
+                                               q + pre < 16 ? (uint32_t)(q + pre) : 16u)));
+            }
+            const int s = q + pre;                       // vb's body head: bytes [s, 16)
+            if (s > 0 && s < 16) o = or4(o, funnel16(z, W0, 16u - (uint32_t)s));
+            st16_region<kMode>(P.dst + base, R, o);
+            continue;
+        }
         if (!fast[u]) continue;
         const uint32_t ph = hi[u] ? phB : phA;
         uint4 o = ph ? funnel16(a[u], own[u] ? e[u] : nb, ph) : a[u];
         xor4(o, hi[u] ? krB : krA);
-        st16_region<kMode>(P.dst + base, u * (uint32_t)kSlice + lane * (uint32_t)kChunk, o);
+        st16_region<kMode>(P.dst + base, R, o);
     }
 }
 
@@ -1175,7 +1237,7 @@ __device__ __forceinline__ void region_loop(const Pass& P, const uint64_t* __res
         // 256 B 1.81-1.83 -> 1.69-1.70 (profiles/r03_inreg_ab/v3/); the send
         // with edge workgroups measured slower with it (256 B 2.74 -> 2.93
         // ms, profiles/r03_small_ab/)
-        if ((kMode == kModeDeser || kInreg) && f1 >= f0 + 3) {
+        if ((kMode == kModeDeser || (kInreg && kMode == kModeSer)) && f1 >= f0 + 3) {
             general_region<kMode>(P, f0, f1, base, lane, kInreg);
             continue;
         }
@@ -1184,13 +1246,14 @@ __device__ __forceinline__ void region_loop(const Pass& P, const uint64_t* __res
         // start at or after this region's end do not touch it.
         if (f1 > f0 && offs[f0 + 1] >= end) f1 = f0;
         const FrameView va = frame_view<kMode>(P, f0);
+        constexpr bool kEdges = kInreg && kMode == kModeH2Ser;   // edge chunks in-region
         if (f0 == f1) {
             if (base >= va.body_start && end <= va.body_start + va.body_len)
                 fast_region<kMode>(P, va, base, lane);
             else
-                two_frame_region<kMode>(P, va, va, base, lane);   // partial body, one frame
+                two_frame_region<kMode, kEdges>(P, va, va, base, lane);   // partial body, one frame
         } else if (f1 == f0 + 1 || offs[f0 + 2] >= end) {
-            two_frame_region<kMode>(P, va, frame_view<kMode>(P, f0 + 1), base, lane);
+            two_frame_region<kMode, kEdges>(P, va, frame_view<kMode>(P, f0 + 1), base, lane);
         } else {
             general_region<kMode>(P, f0, f1, base, lane, kInreg);
         }
@@ -1271,9 +1334,11 @@ xform_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
     P.klass = klass;
     P.sid = sid;
     P.parent = parent;
-    // WS serialize with in-region edges (the plan's ser_inreg flag clear):
-    // the general regions write every edge chunk below the tail region.
-    const bool inreg = kMode == kModeSer && inreg_flag && *inreg_flag == 0;
+    // In-region edge chunks (the plan's flag word clear): WS serialize of
+    // 80..2,000-byte frames (the general regions write them) and the fused
+    // HTTP/2 send of DATA frames >= kRegion + 32 bytes (the two-frame
+    // regions write them): every edge chunk below the tail region.
+    const bool inreg = (kMode == kModeSer || kMode == kModeH2Ser) && inreg_flag && *inreg_flag == 0;
     if (has_edge_blocks(kMode) && is_edge) {
         const uint64_t t = uint64_t(eidx) * kThreads + threadIdx.x;
         const uint64_t f = edge_thread_frame(t);
@@ -1291,7 +1356,7 @@ xform_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
     // the region loop, instantiated apart for the in-region send so that the
     // other loops' code stays as it was (config 3's send lost 6 % when one
     // loop carried both)
-    if (kMode == kModeSer && inreg)
+    if ((kMode == kModeSer || kMode == kModeH2Ser) && inreg)
         region_loop<kMode, true>(P, offs, region_map, n_frames, edge_blocks, sidx);
     else
         region_loop<kMode, false>(P, offs, region_map, n_frames, edge_blocks, sidx);

@@ -269,22 +269,25 @@ stream_copy_kernel(const u32x4* __restrict__ src, u32x4* __restrict__ dst, uint6
 // calling thread of a process on one device. One workgroup of 16 waves:
 //   * wave 0 dispatches: lane s polls slot s's request word with one
 //     coalesced system-scope load per round (all 64 slots' words in 512
-//     contiguous bytes of mapped host memory, s_sleep between rounds), and
-//     hands each new request to an idle worker wave through LDS;
-//   * waves 1-15 serve: a worker XORs its slot's buffer in place (16-byte
-//     chunks, up to 16 KiB of loads in flight per round, each a PCIe round
-//     trip), releases its stores at system scope and writes the slot's done
-//     word, so up to 15 threads' frames are in flight at once.
+//     contiguous bytes of mapped host memory, s_sleep between rounds),
+//     cuts each new frame into 4 KiB pieces and hands the pieces to idle
+//     worker waves through LDS;
+//   * waves 1-15 serve: a worker XORs its piece of its slot's buffer in
+//     place (4 chunks per lane, all loads in flight at once, each a PCIe
+//     round trip) and releases its stores at system scope; the worker that
+//     finishes a frame's last piece writes the slot's done word. A 64 KiB
+//     frame is 16 pieces on 15 workers; frames of several threads share
+//     them.
 // The kernel ends (a) when the stop word is set, (b) after idle_ticks of the
 // wall clock without a request, or (c) after life_ticks in all, so that a
 // stream sharing its hardware queue never waits behind it for longer
-// (GPU_MAX_HW_QUEUES = 4: streams share queues); requests still pending
-// then are served by the next launch. After every wave has left the loop,
-// thread 0 writes the launch's generation to the exit word: from then on
-// this kernel touches no slot, and the host may launch the next one.
+// (GPU_MAX_HW_QUEUES = 4: streams share queues); requests not yet taken stay
+// posted for the next launch. After every wave has left the loop, thread 0
+// writes the launch's generation to the exit word: from then on this kernel
+// touches no slot, and the host may launch the next one.
 constexpr uint32_t kServiceThreads = 1024;
 constexpr uint32_t kServiceWorkers = kServiceThreads / 64 - 1;     // 15
-constexpr uint32_t kServiceRound = 16;             // chunks per lane per round (16 KiB per wave)
+constexpr uint32_t kServicePiece = 4096;           // bytes per piece: 4 chunks per lane
 static_assert(kCfwsServiceSlots == 64, "wave 0's lanes poll the slots");
 
 __device__ __forceinline__ uint64_t sys_load(const uint64_t* p)
@@ -297,88 +300,92 @@ __device__ __forceinline__ void sys_store(uint64_t* p, uint64_t v)
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// One frame of n bytes at buf, XORed in place by one wave (chunk c at 16c:
-// key phase 0 for every chunk).
-__device__ __forceinline__ void service_xor_frame(uint8_t* buf, uint32_t n, uint32_t key, uint32_t lane)
+// Piece p of a frame of n bytes at buf, XORed in place by one wave (chunk c
+// at 16c: key phase 0 for every chunk); the frame's 0-15 tail bytes by the
+// wave of its last piece.
+__device__ __forceinline__ void service_xor_piece(uint8_t* buf, uint32_t n, uint32_t key, uint32_t p, uint32_t lane)
 {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");      // the frame's bytes, written by the host
-    const uint32_t nv = n / 16;
+    constexpr uint32_t kPer = kServicePiece / 16 / 64;
+    const uint32_t nv = n / 16, c0 = p * (kServicePiece / 16);
     u32x4* b = reinterpret_cast<u32x4*>(buf);
-    for (uint32_t c0 = 0; c0 < nv; c0 += 64 * kServiceRound) {
-        u32x4 v[kServiceRound];
+    u32x4 v[kPer];
 #pragma unroll
-        for (uint32_t k = 0; k < kServiceRound; ++k) {
-            const uint32_t c = c0 + k * 64 + lane;
-            if (c < nv) v[k] = b[c];
-        }
-#pragma unroll
-        for (uint32_t k = 0; k < kServiceRound; ++k) {
-            const uint32_t c = c0 + k * 64 + lane;
-            if (c < nv) b[c] = v[k] ^ key;
-        }
+    for (uint32_t k = 0; k < kPer; ++k) {
+        const uint32_t c = c0 + k * 64 + lane;
+        if (c < nv) v[k] = b[c];
     }
-    if (lane < n - nv * 16) {                          // the 0-15 tail bytes
+#pragma unroll
+    for (uint32_t k = 0; k < kPer; ++k) {
+        const uint32_t c = c0 + k * 64 + lane;
+        if (c < nv) b[c] = v[k] ^ key;
+    }
+    if ((n - 1) / kServicePiece == p && lane < n - nv * 16) {
         const uint32_t i = nv * 16 + lane;
         buf[i] = (uint8_t)(buf[i] ^ (key >> (8 * (i & 3u))));
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");      // the stores, before the done word
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");      // the stores, before the piece counts as done
 }
 
 __global__ void __launch_bounds__(kServiceThreads)
 dropin_service_kernel(uint64_t* ctl, uint8_t* bufs, uint64_t gen, uint64_t idle_ticks, uint64_t life_ticks)
 {
-    // per worker: its slot + 1 (0 = idle) and the request word; the
-    // dispatcher writes the word, then the slot; the worker clears the slot
-    // once the done word is out
-    __shared__ uint64_t s_job[kServiceWorkers];
-    __shared__ uint32_t s_busy[kServiceWorkers];
+    // per worker: its job (slot + 1 | piece << 8; 0 = idle), written by the
+    // dispatcher, cleared by the worker; per slot: its request word and the
+    // pieces not yet finished (the worker that takes it to 0 writes done)
+    __shared__ uint32_t s_job[kServiceWorkers];
+    __shared__ uint64_t s_word[kCfwsServiceSlots];
+    __shared__ uint32_t s_left[kCfwsServiceSlots];
     __shared__ uint32_t s_exit;
     const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u;
-    if (threadIdx.x < kServiceWorkers) s_busy[threadIdx.x] = 0;
+    if (threadIdx.x < kServiceWorkers) s_job[threadIdx.x] = 0;
     if (threadIdx.x == 0) s_exit = 0;
     __syncthreads();
     uint64_t* req = ctl + kCfwsServiceReqWord;
     uint64_t* done = ctl + kCfwsServiceDoneWord;
     if (wv == 0) {
-        // lane s: the seq last handed out for slot s (its done word at
-        // launch: every earlier request of the slot was finished)
+        // lane s: the seq last taken for slot s (its done word at launch:
+        // every earlier request of the slot was finished), and the pieces of
+        // the slot's current frame still to hand out: [next, npieces)
         uint32_t handed = (uint32_t)(sys_load(&done[lane]) >> 48);
+        uint32_t next = 0, npieces = 0;
         const uint64_t t_start = (uint64_t)wall_clock64();
         uint64_t t_last = t_start;
         for (;;) {
             const uint64_t now = (uint64_t)wall_clock64();
             const bool retiring = sys_load(&ctl[kCfwsServiceStopWord]) != 0 || now - t_start > life_ticks;
-            if (!retiring) {
+            // a slot takes a new request only when its frame is all handed
+            // out; a retiring kernel takes none
+            if (!retiring && next == npieces) {
                 const uint64_t w = sys_load(&req[lane]);
-                uint64_t pend = __ballot((uint32_t)(w >> 48) != handed);
-                if (pend) t_last = now;
-                // each new request to an idle worker; a slot's next request
-                // comes only after its done word, so a slot is never on two
-                // workers (checked anyway)
-                while (pend) {
-                    const uint32_t s = (uint32_t)__builtin_ctzll(pend);
-                    pend &= pend - 1;
-                    uint32_t pick = kServiceWorkers;
-                    bool held = false;
-                    for (uint32_t k = 0; k < kServiceWorkers; ++k) {
-                        const uint32_t b = __hip_atomic_load(&s_busy[k], __ATOMIC_RELAXED,
-                                                             __HIP_MEMORY_SCOPE_WORKGROUP);
-                        held |= b == s + 1;
-                        if (b == 0 && pick == kServiceWorkers) pick = k;
-                    }
-                    if (held || pick == kServiceWorkers) continue;     // next round
-                    const uint64_t ws = __shfl(w, (int)s);
-                    if (lane == 0) {
-                        s_job[pick] = ws;
-                        __hip_atomic_store(&s_busy[pick], s + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    }
-                    if (lane == s) handed = (uint32_t)(ws >> 48);
+                if ((uint32_t)(w >> 48) != handed) {
+                    // its previous frame is finished: the host posts the next
+                    // request only after that frame's done word
+                    const uint32_t n = (uint32_t)((w >> 32) & 0xffffu) + 1u;
+                    handed = (uint32_t)(w >> 48);
+                    next = 0;
+                    npieces = (n + kServicePiece - 1) / kServicePiece;
+                    s_word[lane] = w;
+                    s_left[lane] = npieces;
+                    t_last = now;
                 }
             }
-            bool busy = false;
+            // hand out pieces, lowest slot first, to idle workers
+            for (uint32_t k = 0; k < kServiceWorkers; ++k) {
+                uint64_t want = __ballot(next < npieces);
+                if (!want) break;
+                if (__hip_atomic_load(&s_job[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 0) continue;
+                const uint32_t s = (uint32_t)__builtin_ctzll(want);
+                const uint32_t p = (uint32_t)__shfl((int)next, (int)s);
+                if (lane == 0)
+                    __hip_atomic_store(&s_job[k], (s + 1) | p << 8, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (lane == s) ++next;
+            }
+            bool busy = __ballot(next < npieces) != 0;
             for (uint32_t k = 0; k < kServiceWorkers; ++k)
-                busy |= __hip_atomic_load(&s_busy[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 0;
-            // the workers finish the frames they hold before the kernel ends
+                busy |= __hip_atomic_load(&s_job[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 0;
+            // the workers finish the pieces they hold, and every handed-out
+            // frame is completed, before the kernel ends
             if (!busy && (retiring || now - t_last > idle_ticks)) break;
             __builtin_amdgcn_s_sleep(2);
         }
@@ -386,19 +393,21 @@ dropin_service_kernel(uint64_t* ctl, uint8_t* bufs, uint64_t gen, uint64_t idle_
     } else {
         const uint32_t me = wv - 1;
         for (;;) {
-            const uint32_t b = __hip_atomic_load(&s_busy[me], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-            if (b == 0) {
+            const uint32_t j = __hip_atomic_load(&s_job[me], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (j == 0) {
                 if (__hip_atomic_load(&s_exit, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
                 __builtin_amdgcn_s_sleep(1);
                 continue;
             }
-            const uint32_t s = b - 1;
-            const uint64_t j = s_job[me];
-            const uint32_t n = (uint32_t)((j >> 32) & 0xffffu) + 1u;
-            service_xor_frame(bufs + (uint64_t)s * kCfwsServiceMax, n, (uint32_t)j, lane);
+            const uint32_t s = (j & 0xffu) - 1, p = j >> 8;
+            const uint64_t w = s_word[s];
+            const uint32_t n = (uint32_t)((w >> 32) & 0xffffu) + 1u;
+            service_xor_piece(bufs + (uint64_t)s * kCfwsServiceMax, n, (uint32_t)w, p, lane);
             if (lane == 0) {
-                sys_store(&done[s], j & 0xffff000000000000ull);
-                __hip_atomic_store(&s_busy[me], 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                // the last piece of the frame: its done word
+                if (__hip_atomic_fetch_sub(&s_left[s], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP) == 1u)
+                    sys_store(&done[s], w & 0xffff000000000000ull);
+                __hip_atomic_store(&s_job[me], 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
             }
         }
     }

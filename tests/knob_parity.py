@@ -60,6 +60,26 @@ def roundtrip(sizes, rng, seed, align, flags=0, opcodes=None, fins=None, aligned
     assert np.array_equal(out[:e_tot].cpu().numpy(), e_out[:e_tot]), "deserialize != oracle"
 
 
+def h2_send(sizes, rng, S=16384):
+    n = len(sizes)
+    payload = O.fill_splitmix(1 << 20, 17, 0)
+    d = np.zeros(n, dtype=O.DESC_DTYPE)
+    d["payload_size"] = sizes
+    d["payload_off"] = rng.integers(0, (1 << 20) - 60000, n).astype(np.uint64)
+    d["mask"] = (rng.random(n) < .8).astype(np.uint8)
+    d["mask_key"] = rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32) * d["mask"]
+    d["fin"], d["opcode"] = 1, 2
+    exp, _ = O.h2_serialize_batch(payload, d, 9, S)
+    pay = torch.from_numpy(payload).cuda()
+    _, wtotal = W.wire_layout(d)
+    wire = torch.empty(W.round16(wtotal) + 16, dtype=torch.uint8, device="cuda")
+    h2 = torch.empty(cfws.h2_wrapped_bound(wire.numel(), n, S), dtype=torch.uint8, device="cuda")
+    tot = cfws.h2_serialize(pay, cfws.desc_to_device(d), wire, h2, 9, S)
+    torch.cuda.synchronize()
+    assert int(tot.item()) == len(exp)
+    assert np.array_equal(h2[:len(exp)].cpu().numpy(), exp), "h2 send != oracle"
+
+
 def main():
     cfws.init()
     rng = np.random.default_rng(11)
@@ -76,6 +96,9 @@ def main():
     # the single-pass plan)
     roundtrip(rng.integers(80, 2001, 20000), rng, 5, 16, aligned=True)
     roundtrip(rng.integers(80, 200, 600000), rng, 6, 1, aligned=True)
+    # WebSocket over HTTP/2, DATA frames all over 4 KiB + 32: the fused
+    # send's in-region edge chunks unless CFWS_H2_INREG=0 or CFWS_EDGE_SPLIT=1
+    h2_send(rng.integers(4200, 60000, 1500), rng)
     # a small batch (single-launch path unless CFWS_SMALL=0)
     roundtrip(np.full(256, 1000), rng, 3, 16)
     # fragments + pings, reassembled (two passes, pass-1 capped grid)

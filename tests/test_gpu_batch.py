@@ -316,6 +316,13 @@ def test_small_frame_reference_digests(which):
     assert ptot.item() == n * fs and bool((status == 0).all())
     assert _sha_device(back, n * fs) == g["payload_sha256"]
     assert torch.equal(back[:n * fs], payload)
+    # the one-call form (256 B frames: the fused plan + copy kernel)
+    back.fill_(0xEE)
+    status.fill_(99)
+    _, st2, ptot2 = cfws.deserialize(wire, total, idx, back, desc_de, status, ws, align=16)
+    torch.cuda.synchronize()
+    assert ptot2.item() == n * fs and bool((st2 == 0).all())
+    assert _sha_device(back, n * fs) == g["payload_sha256"]
 
 
 def _roundtrip_digest(g, full=False):
@@ -532,3 +539,45 @@ def test_serialize_in_region_edges(n):
     d3 = desc.copy()
     d3[n // 2]["payload_size"] = 79
     check_serialize(payload, d3, plan_execute=True)
+
+
+@pytest.mark.parametrize("align", [16, 64, 4096])
+def test_fused_deserialize_mixed_and_errors(align):
+    """The fused deserialize (cfws_deserialize_batch on > 1,024 frames of
+    <= 512 B average wire: deserialize_plan_single_kernel<true>, plan and
+    copy in one pass) against the oracle and against plan + execute: frames
+    of 0-40 bytes (64 frames per wave-instruction), 100-1,024 bytes, some
+    of 1-9 KiB (frame by frame), masked and unmasked; invalid headers
+    sprinkled in, a truncated last frame (MORE_DATA), a payload limit
+    (TOO_BIG), and capacities that cut a slot and fail the frames past it
+    with OUT_OF_MEMORY (their in-capacity slot bytes written as zeros)."""
+    rng = np.random.default_rng(align)
+    n = 120_000
+    payload = O.fill_splitmix(1 << 16, align, 0)
+    desc = np.zeros(n, dtype=cfws.DESC_DTYPE)
+    kind = rng.random(n)
+    sz = np.where(kind < 0.6, rng.integers(0, 41, n),
+                  np.where(kind < 0.97, rng.integers(100, 1025, n), rng.integers(1025, 9000, n)))
+    desc["payload_size"] = sz.astype(np.uint64)
+    desc["payload_off"] = rng.integers(0, (1 << 16) - 9000, n).astype(np.uint64)
+    desc["fin"] = 1
+    desc["opcode"] = rng.choice([0, 1, 2, 9], n).astype(np.uint8)
+    desc["mask"] = (rng.random(n) < 0.7).astype(np.uint8)
+    desc["mask_key"] = rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32) * desc["mask"]
+    exp_wire, d2 = O.serialize_batch(payload, desc.view(O.DESC_DTYPE))
+    offs = d2["wire_off"].astype(np.uint64)
+    w = exp_wire.copy()
+    bad = rng.choice(n - 1, 200, replace=False)
+    w[offs[bad].astype(np.int64)] |= 0x40                      # RSV2 -> INVALID_FRAME
+    w = w[:len(w) - 3]                                          # the last frame: MORE_DATA
+    assert len(w) // n <= 512                                   # the fused form's batches
+    out, d, st, tot = check_deserialize(w, offs, align=align)
+    assert (st == O.ERROR_INVALID_FRAME).sum() >= 200 and st[-1] == O.PARSE_MORE_DATA
+    ref = gpu_deserialize(w, offs, align=align, plan_execute=True)
+    assert tot == ref[3] and np.array_equal(out[:tot], ref[0][:tot])
+    check_deserialize(w, offs, align=align, max_payload=700)              # TOO_BIG
+    for cap in (tot // 3 + 5, tot // 2):
+        o2, _, s2, t2 = check_deserialize(w, offs, align=align, capacity=cap)
+        assert (s2 == O.ERROR_OUT_OF_MEMORY).any() and t2 == cap
+        r2 = gpu_deserialize(w, offs, align=align, capacity=cap, plan_execute=True)
+        assert np.array_equal(o2[:cap], r2[0][:cap]) and (o2[cap:] == 0xEE).all()

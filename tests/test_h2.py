@@ -125,6 +125,69 @@ def test_gpu_h2_serialize_random(S):
     assert bad.size == 0, bad[:10]
 
 
+def _units(d, S):
+    """Output lengths of the DATA frames the send makes (9 + slice)."""
+    out = []
+    for n, m in zip(d["payload_size"], d["mask"]):
+        w = int(n) + O.header_size(int(n), bool(m))
+        k = 1 if w <= S else -(-w // S)
+        out += [9 + min(S, w - j * S) for j in range(k)]
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not gpu_present(), reason="needs the MI355X")
+@pytest.mark.parametrize("S,case", [(16384, "mixed"), (16384, "last_short"), (5000, "mixed"),
+                                    (16384, "cut"), (4200, "mixed")])
+def test_gpu_h2_send_in_region_edges(S, case):
+    """The fused send's in-region edge chunks (two_frame_region<kModeH2Ser,
+    kEdges>): every DATA frame but the stream's last spans more than a 4 KiB
+    region and a 32-byte margin (the plan's flag), so the two-frame regions
+    assemble each boundary's chunks -- the previous body's tail, the DATA +
+    WS header at any offset, the next body's head -- in registers. Random
+    payload sizes (7/16/64-bit WS lengths, masked and unmasked, unaligned
+    sources, WS frames split into several DATA frames), a short last frame,
+    and a capacity cut inside the stream, against the oracle (pinned to the
+    reference's co_http2_frame.c + co_ws_frame.c)."""
+    rng = random.Random(S * 31 + len(case))
+    payload = O.fill_splitmix(1 << 22, S, 0)
+    d = []
+    while len(d) < 1500:
+        sz = rng.choice([rng.randrange(4200, 16300), rng.randrange(4200, 40000), 65535, 65536,
+                         rng.randrange(66000, 200000)])
+        m = rng.random() < .8
+        w = sz + O.header_size(sz, m)
+        k = 1 if w <= S else -(-w // S)
+        if 9 + w - (k - 1) * S < 4096 + 32:
+            continue
+        d.append((rng.randrange(0, (1 << 22) - sz), 0, sz, rng.getrandbits(32) if m else 0,
+                  rng.random() < .6, rng.choice([0, 1, 2, 9]), m, 0))
+    if case == "last_short":
+        d.append((77, 0, 10, 0x1234567, True, 2, True, 0))
+    d = np.array(d, dtype=O.DESC_DTYPE)
+    units = _units(d, S)
+    assert min(units[:-1]) >= 4096 + 32          # the plan's flag is clear
+    exp, _ = O.h2_serialize_batch(payload, d, 7, S)
+    if case != "cut":
+        got, t = gpu_h2_serialize(payload, d, 7, S)
+        assert t == len(exp)
+        bad = np.nonzero(got != exp)[0]
+        assert bad.size == 0, (bad.size, bad[:10])
+        return
+    torch, cfws = _gpu()
+    from coldforce_amd import workloads as W
+    pay = torch.from_numpy(payload).cuda()
+    _, wtotal = W.wire_layout(d)
+    wire = torch.empty(W.round16(wtotal) + 16, dtype=torch.uint8, device="cuda")
+    for cap in (len(exp) // 2 + 4101, len(exp) // 3 // 4096 * 4096):
+        h2 = torch.full((cap + 4096,), 0xEE, dtype=torch.uint8, device="cuda")
+        tot = cfws.h2_serialize(pay, cfws.desc_to_device(d), wire, h2[:cap], 7, S)
+        torch.cuda.synchronize()
+        assert int(tot.item()) == len(exp)
+        got = h2.cpu().numpy()
+        assert np.array_equal(got[:cap], exp[:cap]) and (got[cap:] == 0xEE).all(), cap
+
+
 @pytest.mark.gpu
 @pytest.mark.skipif(not gpu_present(), reason="needs the MI355X")
 def test_gpu_h2_wrap_golden():

@@ -17,6 +17,7 @@ KNOBS = [
     {"CFWS_GRID": "300", "CFWS_XFORM_LDS": "0"},
     {"CFWS_PLAN_SINGLE": "0"},
     {"CFWS_SER_INREG": "0"},
+    {"CFWS_H2_INREG": "1"},
 ]
 
 

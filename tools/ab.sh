@@ -13,7 +13,7 @@ for round in 1 2; do
     for lds in ${LDS:-default}; do
       if [ "$lds" = default ]; then unset CFWS_XFORM_LDS; else export CFWS_XFORM_LDS=$lds; fi
       CFWS_LIB=$PWD/$lib timeout -k 10 300 python bench.py --steps 20 --warmup 3 \
-          --no-cpu-baseline --workload ${WL:-config2} \
+          --no-cpu-baseline --workload ${WL:-config2} $ARGS \
           > "$OUT/${v}_lds${lds}_r$round.json" 2> "$OUT/${v}_lds${lds}_r$round.err" || { echo "variant $v lds $lds failed"; exit 1; }
     done
   done

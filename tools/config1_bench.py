@@ -23,7 +23,9 @@ def main():
     ap.add_argument("--latency-frames", type=int, default=20_000)
     ap.add_argument("--payload", type=int, default=1024)
     ap.add_argument("--modes", default="ws,h2")
-    ap.add_argument("--builds", default="stock,cfws")
+    ap.add_argument("--builds", default="stock,cfws,cfws:device",
+                    help="cfws:device = the drop-in build with CFWS_DROPIN_GPU_MIN=0 (every "
+                         "masked payload to the device)")
     ap.add_argument("--windows", default="64,1")
     a = ap.parse_args()
     with open(a.out, "a") as f:
@@ -32,10 +34,12 @@ def main():
                 frames = a.frames if window > 1 else a.latency_frames
                 for rep in range(a.reps):
                     port = free_port()
-                    for build in a.builds.split(","):
+                    for spec in a.builds.split(","):
+                        build, _, pol = spec.partition(":")
+                        env = {"CFWS_DROPIN_GPU_MIN": "0"} if pol == "device" else None
                         r = run_echo(build, mode, frames, a.payload, window=window, seed=1, port=port,
-                                     timeout=600)
-                        line = {"build": build, "rep": rep, "client_rc": r["client_rc"],
+                                     timeout=600, env=env)
+                        line = {"build": spec, "rep": rep, "client_rc": r["client_rc"],
                                 **(r["client"] or {"mode": mode, "window": window, "error": r["client_err"]})}
                         f.write(json.dumps(line) + "\n")
                         f.flush()

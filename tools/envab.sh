@@ -9,7 +9,7 @@ for round in 1 2; do
   i=0
   for e in "${SETS[@]}"; do
     name=$(echo "$e" | tr ' =' '_-')
-    env $e timeout -k 10 300 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --workload ${WL:-config2} \
+    env $e timeout -k 10 300 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --workload ${WL:-config2} $ARGS \
         > "$OUT/${name}_r$round.json" 2> "$OUT/${name}_r$round.err" || { echo "set $e failed"; exit 1; }
     i=$((i+1))
   done

@@ -18,6 +18,10 @@ step() {  # name limit cmd...
   echo "== $name rc=$rc $(date +%T)"
   tail -3 "$OUT/$name.log"
   if [ $rc -ge 124 ] || [ $rc -gt 128 ]; then echo "STOP after $name (rc=$rc)"; exit $rc; fi
+  # a device fault reported as a Python exception (rc 1): stop too
+  if grep -q -E "illegal memory access|Memory access fault|hipErrorIllegalAddress|HSA_STATUS_ERROR" "$OUT/$name.log"; then
+    echo "STOP after $name (device fault)"; exit 3
+  fi
   return 0
 }
 pmc() {  # name workload-args... ; counters in $C
@@ -31,13 +35,26 @@ for s in "$@"; do
     split) step split 200 python3 $R/bench.py --workload split --no-cpu-baseline ;;
     c5) step c5 200 python3 $R/bench.py --workload config5 --no-cpu-baseline ;;
     c3) step c3 200 python3 $R/bench.py --workload config3 --no-cpu-baseline ;;
+    fs256) step fs256 200 python3 $R/bench.py --frames 16777216 --frame-size 256 --no-cpu-baseline ;;
+    kstats_fs256) step kstats_fs256 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kstats_fs256" -o ks -- python3 $R/bench.py --frames 16777216 --frame-size 256 --steps 10 --warmup 3 --no-cpu-baseline ;;
     fs1k) step fs1k 200 python3 $R/bench.py --frames 4194304 --frame-size 1024 --no-cpu-baseline ;;
     config1) step config1 400 python3 $R/tools/config1_bench.py --out "$OUT/config1.jsonl" --reps 2 ;;
+    dropin) step dropin 400 env TAG=$TAG bash $R/tools/dropin_lat.sh ;;
     kstats) step kstats 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kstats" -o ks -- python3 $R/bench.py --steps 10 --warmup 3 --no-cpu-baseline ;;
     kstats_c5) step kstats_c5 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kstats_c5" -o ks -- python3 $R/bench.py --workload config5 --steps 10 --warmup 3 --no-cpu-baseline ;;
     kstats_fs1k) step kstats_fs1k 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kstats_fs1k" -o ks -- python3 $R/bench.py --frames 4194304 --frame-size 1024 --steps 10 --warmup 3 --no-cpu-baseline ;;
     kstats_split) step kstats_split 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kstats_split" -o ks -- python3 $R/bench.py --workload split --steps 10 --warmup 3 --no-cpu-baseline ;;
     list) step list 60 rocprofv3 -L ;;
+    prof_c2) step prof_c2 400 env TAG=$TAG/prof_c2 bash $R/tools/profile.sh ;;
+    prof_fs1k) step prof_fs1k 400 env TAG=$TAG/prof_fs1k ARGS="--frames 4194304 --frame-size 1024" bash $R/tools/profile.sh ;;
+    prof_fs256) step prof_fs256 400 env TAG=$TAG/prof_fs256 ARGS="--frames 16777216 --frame-size 256" bash $R/tools/profile.sh ;;
+    ab) step ab 600 env TAG=$TAG/ab bash $R/tools/ab.sh ;;
+    envab) step envab 600 env TAG=$TAG/envab bash $R/tools/envab.sh ;;
+    pmc_c5ab)
+      for v in 1 0; do
+        step pmc_c5ab_wr$v 120 env CFWS_H2_INREG=$v rocprofv3 --pmc TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum --output-format csv -d "$OUT/pmc_c5ab_wr$v" -o pmc -- python3 $R/bench.py --workload config5 --steps 2 --warmup 1 --no-cpu-baseline
+        step pmc_c5ab_sq$v 120 env CFWS_H2_INREG=$v rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_BUSY_CYCLES --output-format csv -d "$OUT/pmc_c5ab_sq$v" -o pmc -- python3 $R/bench.py --workload config5 --steps 2 --warmup 1 --no-cpu-baseline
+      done ;;
     pmc)
       C="SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_BUSY_CYCLES"
       pmc sq_c2 && pmc sq_c5 --workload config5
