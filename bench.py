@@ -265,7 +265,7 @@ def bench_h2(args, rank, world, dev):
 
 def bench_split(args, rank, world, dev):
     """Config 2 through the split ops of include/cfws.h: cfws_encode_headers
-    + cfws_mask_batch (send), cfws_parse_headers + cfws_unmask_batch
+    + cfws_mask_batch_packed (send), cfws_parse_headers + cfws_unmask_batch
     (receive), per step; wire offsets laid out by the host."""
     import numpy as np
     import torch
@@ -287,9 +287,13 @@ def bench_split(args, rank, world, dev):
     # the receive side's payload layout: the frame index x frame size
     pay_off = torch.from_numpy((np.arange(F, dtype=np.uint64) * np.uint64(fs)).view(np.int64)).to(dev)
 
+    # cfws_mask_batch_packed (the frames are packed back to back);
+    # CFWS_BENCH_SPLIT_PACKED=0: cfws_mask_batch (A/B)
+    packed = os.environ.get("CFWS_BENCH_SPLIT_PACKED", "1") != "0"
+
     def step():
         cfws.encode_headers(d_t, wire)
-        cfws.mask_batch(payload, d_t, wire, fs)
+        cfws.mask_batch(payload, d_t, wire, fs, packed=packed)   # the frames are packed back to back
         cfws.parse_headers(wire, wire_total, idx, pd_t, st_t)
         pd_t.view(torch.int64)[:, 0] = pay_off
         cfws.unmask_batch(wire, pd_t, st_t, back, fs)
@@ -309,7 +313,7 @@ def bench_split(args, rank, world, dev):
             "value": round(2.0 * F * fs * world * args.steps / elapsed / GIB, 2), "unit": "GiB/s",
             "n_gpus": world, "steps": args.steps, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "config": {"workload": f"split: {F} binary frames x {fs} B per GPU: encode_headers + "
-                                   f"mask_batch, then parse_headers + unmask_batch"},
+                                   f"mask_batch_packed, then parse_headers + unmask_batch"},
             "per_gpu": per_gpu_rows(rows, args.steps), "verified": ok}
     if rank == 0:
         print(json.dumps(line), flush=True)

@@ -54,7 +54,8 @@ BATCH_SYMBOLS = (
     "cfws_h2_deserialize_workspace_size", "cfws_h2_deserialize_batch",
     "cfws_index_frames", "cfws_index_workspace_size", "cfws_index_frames_batch",
     "cfws_ws_accept_keys_batch", "cfws_encode_headers", "cfws_parse_headers",
-    "cfws_mask_batch", "cfws_unmask_batch", "cfws_copy_to_host", "cfws_mapped_device_pointer",
+    "cfws_mask_batch", "cfws_mask_batch_packed", "cfws_unmask_batch", "cfws_copy_to_host",
+    "cfws_mapped_device_pointer",
     "cfws_pipeline_set_d2h", "cfws_graph_serialize", "cfws_graph_deserialize", "cfws_graph_launch",
     "cfws_graph_destroy", "cfws_pipeline_h2_serialize", "cfws_pipeline_h2_deserialize",
 )
@@ -115,6 +116,7 @@ def lib(path: str = LIB_PATH) -> C.CDLL:
         "cfws_encode_headers": ([_vp, _sz, _vp, _u64, _vp], C.c_int),
         "cfws_parse_headers": ([_vp, _u64, _vp, _sz, _u64, _vp, _vp, _vp], C.c_int),
         "cfws_mask_batch": ([_vp, _vp, _sz, _u64, _vp, _u64, _vp], C.c_int),
+        "cfws_mask_batch_packed": ([_vp, _vp, _sz, _u64, _vp, _u64, _vp], C.c_int),
         "cfws_unmask_batch": ([_vp, _vp, _vp, _sz, _u64, _vp, _u64, _vp], C.c_int),
         "cfws_copy_to_host": ([_vp, _vp, _u64, _vp], C.c_int),
         "cfws_pipeline_set_d2h": ([_vp, C.c_int], C.c_int),
@@ -459,10 +461,13 @@ def parse_headers(wire_t, wire_size: int, index_t, desc_t, status_t,
 
 
 def mask_batch(payload_t, desc_t, wire_t, max_payload_size: int, wire_capacity: int | None = None,
-               stream=None) -> None:
+               stream=None, packed: bool = False) -> None:
+    """cfws_mask_batch, or with packed=True cfws_mask_batch_packed (frames
+    back to back, headers as cfws_encode_headers writes them)."""
     cap = wire_t.numel() if wire_capacity is None else wire_capacity
-    _check(lib().cfws_mask_batch(_p(payload_t), _p(desc_t), desc_t.shape[0], max_payload_size,
-                                 _p(wire_t), cap, _stream(stream)), "cfws_mask_batch")
+    fn = lib().cfws_mask_batch_packed if packed else lib().cfws_mask_batch
+    _check(fn(_p(payload_t), _p(desc_t), desc_t.shape[0], max_payload_size, _p(wire_t), cap,
+              _stream(stream)), "cfws_mask_batch")
 
 
 def unmask_batch(wire_t, desc_t, status_t, payload_t, max_payload_size: int,

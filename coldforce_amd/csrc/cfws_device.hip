@@ -277,7 +277,7 @@ deserialize_plan_reduce_kernel(const uint8_t* __restrict__ wire, uint64_t wire_s
 // not fetched a second time. 0: the sizes first, the payload offset after
 // the look-back, two fields written (16 frames per thread).
 #ifndef CFWS_SER_PLAN_FULL
-#define CFWS_SER_PLAN_FULL 0
+#define CFWS_SER_PLAN_FULL 1
 #endif
 #ifndef CFWS_SINGLE_ITEMS_SER
 #define CFWS_SINGLE_ITEMS_SER (CFWS_SER_PLAN_FULL ? 8 : 16)
@@ -472,12 +472,11 @@ __device__ __forceinline__ void fused_store(uint8_t* __restrict__ out, uint64_t 
     }
 }
 
-// One round of every lane's chunk: frame info by lane (fl: the lane of
-// the wave holding the frame), chunk c of it. Loads issued, returned in
-// A / E for fused_finish.
+// One lane's chunk in a round: its destination D and source s, the bytes
+// of the slot it writes (nbytes) and of those the payload (need), the key.
 struct FusedChunk {
     uint64_t D, s;
-    uint32_t need, nbytes, key, c;
+    uint32_t need, nbytes, key;
 };
 
 __device__ __forceinline__ void fused_item(const uint8_t* __restrict__ wire, uint8_t* __restrict__ out,
@@ -581,6 +580,26 @@ __device__ __forceinline__ void fused_item(const uint8_t* __restrict__ wire, uin
 // capacity rule's status) once the offsets are known. kCopy: the fused
 // deserialize (above): each block then copies its frames into `out`; no
 // offsets or region map are written (no execute follows).
+// How the deserialize plans load the two 16-byte blocks around a header
+// (A/B knob, CFWS_HDR_LOAD): 0 plain loads; 1 non-temporal; 2 sc0 sc1 nt
+// (system-coherent streaming: the L2 may fetch only the sectors asked for).
+#ifndef CFWS_HDR_LOAD
+#define CFWS_HDR_LOAD 0
+#endif
+__device__ __forceinline__ uint4 ld16_hdr(const uint8_t* p)
+{
+#if CFWS_HDR_LOAD == 1
+    const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+    return make_uint4(v.x, v.y, v.z, v.w);
+#elif CFWS_HDR_LOAD == 2
+    u32x4 v;
+    asm volatile("global_load_dwordx4 %0, %1, off sc0 sc1 nt\n\ts_waitcnt vmcnt(0)" : "=v"(v) : "v"(p) : "memory");
+    return make_uint4(v.x, v.y, v.z, v.w);
+#else
+    return ld16(p);
+#endif
+}
+
 #ifndef CFWS_FUSED_ITEMS
 #define CFWS_FUSED_ITEMS 2
 #endif
@@ -595,8 +614,7 @@ deserialize_plan_single_kernel(const uint8_t* __restrict__ wire, uint64_t wire_s
                                uint64_t* __restrict__ offs, uint32_t* __restrict__ look,
                                uint64_t* __restrict__ agg, uint64_t* __restrict__ incl,
                                uint64_t* __restrict__ hdr, uint64_t capacity, uint32_t* __restrict__ map,
-                               uint64_t* __restrict__ user_total, uint8_t* __restrict__ out = nullptr,
-                               const uint64_t* __restrict__ grand = nullptr)
+                               uint64_t* __restrict__ user_total, uint8_t* __restrict__ out = nullptr)
 {
     __shared__ uint64_t s_wave[kWaves];
     __shared__ uint64_t s_prefix;
@@ -641,8 +659,8 @@ deserialize_plan_single_kernel(const uint8_t* __restrict__ wire, uint64_t wire_s
 #pragma unroll
         for (int k = 0; k < kSingleItems; ++k) {
             const uint64_t a = sx[k] & ~uint64_t(15);
-            hb0[k] = ld16(wire + (a < lastb ? a : lastb));
-            hb1[k] = ld16(wire + (a + 16 < lastb ? a + 16 : lastb));
+            hb0[k] = ld16_hdr(wire + (a < lastb ? a : lastb));
+            hb1[k] = ld16_hdr(wire + (a + 16 < lastb ? a + 16 : lastb));
         }
     }
 #pragma unroll
@@ -718,7 +736,6 @@ deserialize_plan_single_kernel(const uint8_t* __restrict__ wire, uint64_t wire_s
     if (!kCopy) return;
     // the copy: every slot byte below the pass total min(grand total,
     // capacity), cut at the capacity itself (above)
-    (void)grand;
     const uint32_t lane = threadIdx.x & 63u;
 #pragma unroll
     for (int k = 0; k < kSingleItems; ++k)

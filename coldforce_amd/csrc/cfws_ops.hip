@@ -87,9 +87,20 @@ constexpr uint32_t kPieceSpans = kPieceK * kWaves;
 // go out of range explicitly, never by 32-bit wrap-around. Without it
 // (every other run) the offsets are plain: a per-slot edge test cost the
 // unmask 7 % (1.46 against 1.37 ms).
-template <bool kEdge>
+// A packed mask's boundary chunks (cfws_mask_batch_packed): the chunks from
+// the one holding frame f's header start up to its first whole payload
+// chunk, [c0, c0 + 16 nbc), hold frame f - 1's payload tail, f's header,
+// then f's payload head. The tail and the header are wave-uniform words
+// (T.lo, T.hi: bytes [0, 32) from c0; zero from pre = dof - c0 on); the
+// payload head is the lane's own chunk, which is right from dof on.
+struct PackedHead {
+    uint64_t c0 = 0, dof = 0;
+    uint4 lo = {0, 0, 0, 0}, hi = {0, 0, 0, 0};
+};
+
+template <bool kEdge, bool kPacked = false>
 __device__ __forceinline__ void xor_run(__amdgpu_buffer_rsrc_t rs, __amdgpu_buffer_rsrc_t rd, int32_t sd, int32_t dd,
-                                        uint32_t ph, uint32_t kr)
+                                        uint32_t ph, uint32_t kr, uint64_t wbase = 0, const PackedHead* ph_ = nullptr)
 {
     constexpr uint64_t kSpan = kSpanChunks * 16;
     const uint32_t lane = threadIdx.x & 63u;
@@ -109,6 +120,14 @@ __device__ __forceinline__ void xor_run(__amdgpu_buffer_rsrc_t rs, __amdgpu_buff
             o = funnel16(A4, from_next_lane(A4, L), ph);
         }
         xor4(o, kr);
+        if (kPacked) {
+            const uint64_t D = wbase + (uint64_t)k * kSpan + lane * 16;
+            if (D >= ph_->c0 && D < ph_->dof) {
+                const uint32_t q = (uint32_t)(ph_->dof - D < 16 ? ph_->dof - D : 16);   // bytes before the payload
+                const uint4 T = D == ph_->c0 ? ph_->lo : ph_->hi;
+                o = or4(and4(o, byte_range(q, 16)), and4(T, byte_range(0, q)));
+            }
+        }
         // write-through, as the streaming kernel's regions (sc0 sc1 nt)
         const u32x4 v = {o.x, o.y, o.z, o.w};
         __builtin_amdgcn_raw_buffer_store_b128(v, rd, off(dd + (int32_t)(lane * 16 + k * kSpan)), 0, 19);
@@ -117,11 +136,28 @@ __device__ __forceinline__ void xor_run(__amdgpu_buffer_rsrc_t rs, __amdgpu_buff
     for (int k = 0; k < (int)kPieceK; ++k) slot(k);
 }
 
+// cfws_mask_batch_packed: frame g's boundary chunks (PackedHead) are written
+// whole by g's first run when g - 1's payload ends exactly where g's header
+// starts (checked here, not trusted), g's payload has at least 16 bytes and
+// g - 1's at least 16 (so a boundary chunk holds one tail and one header),
+// and the chunks end inside the capacity; otherwise payload_edge_kernel
+// writes g's head bytes and g - 1's tail bytes one by one, as unpacked.
+__device__ __forceinline__ bool packed_inrun(const cfws_frame_desc_t* __restrict__ desc, uint64_t g, uint64_t n,
+                                             uint64_t cap)
+{
+    if (g == 0 || g >= n) return false;
+    const DescWords a = load_desc(desc, (uint32_t)(g - 1)), b = load_desc(desc, (uint32_t)g);
+    const uint64_t aend = a.wire_off + header_size_of(a.payload_size, a.mask() != 0) + a.payload_size;
+    const uint64_t bdof = b.wire_off + header_size_of(b.payload_size, b.mask() != 0);
+    return aend == b.wire_off && a.payload_size >= 16 && b.payload_size >= 16 &&
+           ((bdof + 15) & ~uint64_t(15)) <= cap;
+}
+
 template <bool kUnmask>
 __global__ void __launch_bounds__(kThreads)
 payload_xor_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
                    const cfws_frame_desc_t* __restrict__ desc, const int32_t* __restrict__ status,
-                   uint64_t n, uint32_t pieces, uint64_t cap)
+                   uint64_t n, uint32_t pieces, uint64_t cap, uint32_t packed)
 {
     const uint64_t f = blockIdx.x / pieces;
     const uint32_t p = blockIdx.x % pieces;
@@ -133,10 +169,38 @@ payload_xor_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
     const uint64_t dof = kUnmask ? d.payload_off : d.wire_off + header_size_of(len, d.mask() != 0);
     const uint32_t key = d.mask() ? d.key() : 0u;
     if (len == 0 || dof >= cap) return;
+    // the packed mask: this frame's boundary chunks in its first run
+    PackedHead H;
+    const bool inrun = !kUnmask && packed && packed_inrun(desc, f, n, cap);
+    if (inrun) {
+        const DescWords a = load_desc(desc, (uint32_t)(f - 1));
+        H.c0 = d.wire_off & ~uint64_t(15);
+        H.dof = dof;
+        const uint32_t t = (uint32_t)(d.wire_off - H.c0);             // f - 1's tail bytes
+        const uint4 z = make_uint4(0, 0, 0, 0);
+        // the header (co_ws_frame.c:34-91) at byte t of the 32-byte window
+        const uint32_t hb = ((d.opcode() | (d.fin() ? 0x80u : 0u)) & 0xffu) | (d.mask() ? 0x100u : 0u);
+        const uint4 Hd = ws_header_words(len, hb, key);
+        H.lo = t ? funnel16(z, Hd, 16u - t) : Hd;
+        H.hi = t ? funnel16(Hd, z, 16u - t) : z;
+        if (t) {
+            // f - 1's last t payload bytes, masked with its key
+            const uint64_t ts = a.payload_off + a.payload_size - t;       // their source
+            uint64_t addr = reinterpret_cast<uint64_t>(src) + (ts & ~uint64_t(15));
+            asm volatile("" : "+v"(addr));
+            const uint8_t* sp = reinterpret_cast<const uint8_t*>(addr);
+            const uint32_t tph = (uint32_t)(ts & 15u);
+            uint4 T = ld16(sp);
+            if (tph + t > 16) T = funnel16(T, ld16(sp + 16), tph);
+            else if (tph) T = funnel16(T, z, tph);
+            xor4(T, a.mask() ? rotr8(a.key(), (uint32_t)((a.payload_size - t) & 3u)) : 0u);
+            H.lo = or4(H.lo, and4(T, byte_range(0, t)));
+        }
+    }
     const uint64_t dend = len < cap - dof ? dof + len : cap;
     // 1 KiB spans of the destination arena (dst is 16-byte aligned; spans
     // count from it) holding the frame
-    const uint64_t s0 = dof / (16 * kSpanChunks), s1 = (dend - 1) / (16 * kSpanChunks) + 1;
+    const uint64_t s0 = (inrun ? H.c0 : dof) / (16 * kSpanChunks), s1 = (dend - 1) / (16 * kSpanChunks) + 1;
     const uint64_t ns = s1 - s0;
     const uint64_t used = (ns + kPieceSpans - 1) / kPieceSpans;
     // source phase against the 16-byte destination chunks: one per frame
@@ -151,7 +215,7 @@ payload_xor_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
     // the aligned source blocks holding the frame's bytes, [xs0, xs1), and
     // the destination chunks the frame fills whole, [xd0, xd1)
     const int64_t xs0 = (int64_t)(so & ~uint64_t(15)), xs1 = (int64_t)((so + (dend - dof) + 15) & ~uint64_t(15));
-    const uint64_t xd0 = (dof + 15) & ~uint64_t(15), xd1 = dend & ~uint64_t(15);
+    const uint64_t xd0 = inrun ? H.c0 : (dof + 15) & ~uint64_t(15), xd1 = dend & ~uint64_t(15);
     // virtual pieces p, p + pieces, ...: a frame larger than the caller's
     // max_payload_size (or a grid capped below 2^31 blocks) still gets every
     // chunk written
@@ -174,7 +238,9 @@ payload_xor_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
         const auto rd = __builtin_amdgcn_make_buffer_rsrc(dst + (de > ds ? ds : 0), 0,
                                                           de > ds ? (int)(de - ds) : 0, 0x00020000);
         const int32_t ddl = (int32_t)((int64_t)(wb * kSpan) - (int64_t)ds);
-        if (sd < 0 || ddl < 0)
+        if (inrun && wb * kSpan < ((dof + 15) & ~uint64_t(15)))
+            xor_run<true, true>(rs, rd, sd, ddl, ph, kr, wb * kSpan, &H);
+        else if (sd < 0 || ddl < 0)
             xor_run<true>(rs, rd, sd, ddl, ph, kr);
         else
             xor_run<false>(rs, rd, sd, ddl, ph, kr);
@@ -820,11 +886,14 @@ template <bool kUnmask>
 __global__ void __launch_bounds__(kThreads)
 payload_edge_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
                     const cfws_frame_desc_t* __restrict__ desc, const int32_t* __restrict__ status,
-                    uint64_t n, uint64_t cap)
+                    uint64_t n, uint64_t cap, uint32_t packed)
 {
     const uint64_t f = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
     if (f >= n) return;
     if (kUnmask && status && status[f] != CFWS_PARSE_COMPLETE) return;
+    // the packed mask: bytes a boundary chunk written in-run carries are done
+    const bool head_done = !kUnmask && packed && packed_inrun(desc, f, n, cap);
+    const bool tail_done = !kUnmask && packed && packed_inrun(desc, f + 1, n, cap);
     const DescWords d = load_desc(desc, (uint32_t)f);
     const uint64_t len = d.payload_size;
     const uint64_t so = kUnmask ? d.wire_off + d.header_size() : d.payload_off;
@@ -836,10 +905,12 @@ payload_edge_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
     const uint64_t h1 = (dof + 15) & ~uint64_t(15), t0 = dend & ~uint64_t(15);
     const uint64_t ha = dof, hb = h1 < dend ? h1 : dend;
     const uint64_t ta = t0 > hb ? t0 : hb, tb = dend;
-    for (uint64_t x = ha; x < hb; ++x)
-        dst[x] = src[so + (x - dof)] ^ (uint8_t)(key >> (8 * ((x - dof) & 3u)));
-    for (uint64_t x = ta; x < tb; ++x)
-        dst[x] = src[so + (x - dof)] ^ (uint8_t)(key >> (8 * ((x - dof) & 3u)));
+    if (!head_done)
+        for (uint64_t x = ha; x < hb; ++x)
+            dst[x] = src[so + (x - dof)] ^ (uint8_t)(key >> (8 * ((x - dof) & 3u)));
+    if (!tail_done)
+        for (uint64_t x = ta; x < tb; ++x)
+            dst[x] = src[so + (x - dof)] ^ (uint8_t)(key >> (8 * ((x - dof) & 3u)));
 }
 
 // Pieces per frame for the split payload ops: enough workgroups to cover the
@@ -858,7 +929,7 @@ uint32_t payload_pieces(size_t n, uint64_t max_payload_size)
 template <bool kUnmask>
 int launch_payload_xor(const void* src, void* dst, const cfws_frame_desc_t* d_desc,
                        const int32_t* d_status, size_t n, uint64_t max_payload_size, uint64_t cap,
-                       void* stream, const char* what)
+                       void* stream, const char* what, uint32_t packed = 0)
 {
     if (int rc = check_init()) return rc;
     if (n == 0 || cap == 0) return CFWS_OK;
@@ -869,9 +940,9 @@ int launch_payload_xor(const void* src, void* dst, const cfws_frame_desc_t* d_de
     const uint32_t pieces = payload_pieces(n, max_payload_size);
     payload_xor_kernel<kUnmask><<<(uint32_t)(n * pieces), kThreads, kUnmask ? CFWS_UNMASK_LDS : CFWS_MASK_LDS,
                                   static_cast<hipStream_t>(stream)>>>(
-        static_cast<const uint8_t*>(src), static_cast<uint8_t*>(dst), d_desc, d_status, n, pieces, cap);
+        static_cast<const uint8_t*>(src), static_cast<uint8_t*>(dst), d_desc, d_status, n, pieces, cap, packed);
     payload_edge_kernel<kUnmask><<<grid_for(n, kThreads), kThreads, 0, static_cast<hipStream_t>(stream)>>>(
-        static_cast<const uint8_t*>(src), static_cast<uint8_t*>(dst), d_desc, d_status, n, cap);
+        static_cast<const uint8_t*>(src), static_cast<uint8_t*>(dst), d_desc, d_status, n, cap, packed);
     return launch_check(what);
 }
 
@@ -884,6 +955,13 @@ int cfws_mask_batch(const void* d_payload, const cfws_frame_desc_t* d_desc, size
 {
     return launch_payload_xor<false>(d_payload, d_wire, d_desc, nullptr, n, max_payload_size,
                                      wire_capacity, stream, "mask_batch");
+}
+
+int cfws_mask_batch_packed(const void* d_payload, const cfws_frame_desc_t* d_desc, size_t n,
+                           uint64_t max_payload_size, void* d_wire, uint64_t wire_capacity, void* stream)
+{
+    return launch_payload_xor<false>(d_payload, d_wire, d_desc, nullptr, n, max_payload_size,
+                                     wire_capacity, stream, "mask_batch_packed", 1u);
 }
 
 int cfws_unmask_batch(const void* d_wire, const cfws_frame_desc_t* d_desc, const int32_t* d_status,

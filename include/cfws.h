@@ -172,6 +172,19 @@ int cfws_parse_headers(const void* d_wire, uint64_t wire_size, const uint64_t* d
 int cfws_mask_batch(const void* d_payload, const cfws_frame_desc_t* d_desc, size_t n_frames,
                     uint64_t max_payload_size, void* d_wire, uint64_t wire_capacity,
                     void* stream);
+/* cfws_mask_batch for frames the caller packed back to back (frame i's
+ * header starts where frame i - 1's payload ends, as one co_byte_array of
+ * sequential co_ws_frame_serialize calls lays them out) whose headers are
+ * the bytes cfws_encode_headers writes. Same result bytes; the 16-byte
+ * chunks a frame shares with its neighbour's payload and its own header are
+ * then written whole, header bytes included (rewritten with the values
+ * cfws_encode_headers wrote), instead of byte by byte after the stream
+ * (DESIGN.md §3.8). Each adjacency is checked on the device: a boundary that
+ * is not packed, or whose payloads are shorter than 16 bytes, is written as
+ * by cfws_mask_batch. */
+int cfws_mask_batch_packed(const void* d_payload, const cfws_frame_desc_t* d_desc, size_t n_frames,
+                           uint64_t max_payload_size, void* d_wire, uint64_t wire_capacity,
+                           void* stream);
 int cfws_unmask_batch(const void* d_wire, const cfws_frame_desc_t* d_desc, const int32_t* d_status,
                       size_t n_frames, uint64_t max_payload_size, void* d_payload,
                       uint64_t payload_capacity, void* stream);

@@ -104,7 +104,7 @@ def dev():
 
 
 def gpu_encode_mask(payload, desc, wire_len, fill=0xA5, capacity=None, max_payload=None,
-                    headers=True):
+                    headers=True, packed=False):
     torch = _torch()
     from coldforce_amd import cfws
     pay = torch.from_numpy(payload).cuda()
@@ -114,7 +114,7 @@ def gpu_encode_mask(payload, desc, wire_len, fill=0xA5, capacity=None, max_paylo
     if headers:
         cfws.encode_headers(d_t, wire, cap)
     mp = int(desc["payload_size"].max()) if max_payload is None else max_payload
-    cfws.mask_batch(pay, d_t, wire, mp, cap)
+    cfws.mask_batch(pay, d_t, wire, mp, cap, packed=packed)
     torch.cuda.synchronize()
     return wire.cpu().numpy(), cfws.desc_from_device(d_t)
 
@@ -147,6 +147,38 @@ def test_encode_mask_packed_equals_serialize(dev):
     d["wire_off"] = d_exp["wire_off"]
     got, _ = gpu_encode_mask(payload, d, len(wire) + 16)
     assert np.array_equal(got[:len(wire)], wire)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", [12, 13])
+def test_mask_packed(dev, seed):
+    """cfws_mask_batch_packed: frames packed back to back (the serialize
+    layout) of every size class -- 0-15-byte payloads whose boundaries fall
+    back to byte stores, 16-31, 1 KiB, 64 KiB, 16- and 64-bit lengths,
+    masked and unmasked -- give the serialize wire exactly, as do capacity
+    cuts inside a boundary chunk and inside a payload; a batch with gaps
+    (not packed) equals cfws_mask_batch's bytes, gaps untouched."""
+    rng = random.Random(seed)
+    payload = O.fill_splitmix(1 << 21, seed)
+    desc = random_frames(rng, 3000, len(payload), sizes=[0, 1, 5, 15, 16, 17, 31, 32, 100, 125, 126,
+                                                          1000, 1024, 4095, 65535, 65536, 70000])
+    wire, d_exp = O.serialize_batch(payload, desc)
+    d = desc.copy()
+    d["wire_off"] = d_exp["wire_off"]
+    got, _ = gpu_encode_mask(payload, d, len(wire) + 16, packed=True)
+    bad = np.nonzero(got[:len(wire)] != wire)[0]
+    assert bad.size == 0, f"{bad.size} bytes differ, first at {bad[:8]}"
+    assert (got[len(wire):] == 0xA5).all()
+    for cap in (len(wire) // 2 + 7, len(wire) // 3 // 16 * 16, int(d["wire_off"][1500]) + 5):
+        got, _ = gpu_encode_mask(payload, d, len(wire) + 16, capacity=cap, packed=True)
+        exp = np.full(len(wire) + 16, 0xA5, np.uint8)
+        O.mask_batch(payload, O.encode_headers(d, exp, cap), exp, cap)
+        assert np.array_equal(got, exp), cap
+    d["wire_off"], total = scattered_wire_offsets(rng, desc)
+    got, _ = gpu_encode_mask(payload, d, total + 64, packed=True)
+    exp = np.full(total + 64, 0xA5, np.uint8)
+    O.mask_batch(payload, O.encode_headers(d, exp), exp)
+    assert np.array_equal(got, exp)
 
 
 @pytest.mark.gpu
