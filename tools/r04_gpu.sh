@@ -44,6 +44,10 @@ for s in "$@"; do
     kstats_c5) step kstats_c5 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kstats_c5" -o ks -- python3 $R/bench.py --workload config5 --steps 10 --warmup 3 --no-cpu-baseline ;;
     kstats_fs1k) step kstats_fs1k 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kstats_fs1k" -o ks -- python3 $R/bench.py --frames 4194304 --frame-size 1024 --steps 10 --warmup 3 --no-cpu-baseline ;;
     kstats_split) step kstats_split 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kstats_split" -o ks -- python3 $R/bench.py --workload split --steps 10 --warmup 3 --no-cpu-baseline ;;
+    knobs_fused) step knobs_fused 600 python3 -u -m pytest $R/tests/test_knobs.py -m gpu -x -v -k FUSED --timeout 300 --timeout-method thread ;;
+    envab_fs1k) step envab_fs1k 600 env TAG=$TAG/envab_fs1k ARGS="--frames 4194304 --frame-size 1024" bash $R/tools/envab.sh ;;
+    envab_fs256) step envab_fs256 600 env TAG=$TAG/envab_fs256 ARGS="--frames 16777216 --frame-size 256" bash $R/tools/envab.sh ;;
+    kstats_staged) step kstats_staged 200 env CFWS_FUSED_DESER=2 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kstats_staged" -o ks -- python3 $R/bench.py --frames 4194304 --frame-size 1024 --steps 10 --warmup 3 --no-cpu-baseline ;;
     list) step list 60 rocprofv3 -L ;;
     prof_c2) step prof_c2 400 env TAG=$TAG/prof_c2 bash $R/tools/profile.sh ;;
     prof_fs1k) step prof_fs1k 400 env TAG=$TAG/prof_fs1k ARGS="--frames 4194304 --frame-size 1024" bash $R/tools/profile.sh ;;
