@@ -619,14 +619,8 @@ def main():
     # reassembly) deserialize in one call: cfws_deserialize_batch runs the
     # fused plan + copy kernel there (deserialize_plan_single_kernel<true>),
     # so the timed kernel is that launch; other batches plan, then execute
-    # (CFWS_FUSED_DESER=2, an A/B: the LDS-staged form, up to ~1 KiB frames)
-    fused_mode = os.environ.get("CFWS_FUSED_DESER", "1")
-    avg = wire_total // F
-    win = int(os.environ.get("CFWS_STAGED_WINDOW_KIB", "72"))
-    win = 72 if win >= 72 else 36 if win >= 36 else 18
-    min_frames = {72: 64, 36: 32, 18: 16}[win]                          # staged_kernel()
-    staged = fused_mode == "2" and min_frames * (avg + avg // 16 + 16) + 32 <= win * 1024
-    fused_de = flags == 0 and F > 1024 and (staged or (fused_mode != "0" and avg <= 512))  # kFusedAvgMax
+    fused_de = (flags == 0 and F > 1024 and wire_total // F <= 512      # kFusedAvgMax (cfws_device.hip)
+                and os.environ.get("CFWS_FUSED_DESER", "1") != "0")
 
     def step(ev=None):
         cfws.serialize_plan(desc_ser, wire.numel(), tot_ser, ws_ser)
@@ -698,7 +692,6 @@ def main():
     dom_ms = max(ser_ms, de_ms)
     achieved = alg_bytes / (dom_ms * 1e-3) / 1e9
     kernel_symbol = ("xform_kernel<0>" if dom_name == "serialize_execute"   # kModeSer
-                     else "deserialize_staged_kernel" if staged and fused_de  # staged through LDS
                      else "deserialize_plan_single_kernel<true>" if fused_de  # fused plan + copy
                      else "xform_kernel<1>")                                 # kModeDeser
     # the PMC summary a traffic figure may come from: the same workload only

@@ -726,199 +726,6 @@ deserialize_plan_single_kernel(const uint8_t* __restrict__ wire, uint64_t wire_s
         fused_item(wire, out, capacity, c_run[k], c_src[k], c_len[k], c_nb[k], c_key[k], lane);
 }
 
-// ---- the staged fused deserialize ---------------------------------------------
-// The fused form above reads every header line twice (parse, then copy: by
-// then the line has left L2). Here a block of kF frames first copies the
-// wire window its frames lie in -- from its first frame start --
-// into LDS with coalesced 16-byte loads (every byte read once), parses the
-// headers from LDS, takes its prefix by the look-back, writes descriptors
-// and statuses as the plan does, and then its four waves copy the frames'
-// payloads from LDS to their 16-byte slots, frames interleaved over the
-// waves (the block's output is one contiguous range). A block whose frames
-// do not all lie in its window (scattered index, a larger frame) parses and
-// copies from the wire instead: the same bytes, read twice.
-// CFWS_FUSED_DESER=2 selects it (A/B); kF by the batch's wire bytes per
-// frame so that kF frames fill the window.
-// windows of 72, 36 or 18 KiB (CFWS_STAGED_WINDOW_KIB, an A/B): 2, 4 or 7
-// blocks per CU in its 160 KiB of LDS
-
-// 16 wire bytes starting at byte r of the staged window (r + 32 <= staged bytes)
-__device__ __forceinline__ uint4 stage16(const uint4* s_stage, uint64_t r)
-{
-    const uint32_t c = (uint32_t)(r >> 4), ph = (uint32_t)(r & 15u);
-    const uint4 A = s_stage[c];
-    return ph ? funnel16(A, s_stage[c + 1], ph) : A;
-}
-
-template <int kF, int kWinK>
-__global__ void __launch_bounds__(kThreads, kWinK >= 72 ? 2 : (kWinK >= 36 ? 4 : 7))
-deserialize_staged_kernel(const uint8_t* __restrict__ wire, uint64_t wire_size,
-                          const uint64_t* __restrict__ index, uint64_t n, uint64_t max_payload,
-                          uint64_t align, uint32_t stage_len, cfws_frame_desc_t* __restrict__ desc,
-                          int32_t* __restrict__ status, uint32_t* __restrict__ look,
-                          uint64_t* __restrict__ agg, uint64_t* __restrict__ incl,
-                          uint64_t* __restrict__ hdr, uint64_t capacity, uint64_t* __restrict__ user_total,
-                          uint8_t* __restrict__ out)
-{
-    static_assert(kF <= kThreads && (kF & (kF - 1)) == 0, "one frame per thread");
-    constexpr uint32_t kChunks = uint32_t(kWinK) * 1024 / 16;
-    __shared__ uint4 s_stage[kChunks + 2];
-    __shared__ uint64_t s_run[kF], s_src[kF], s_len[kF], s_nb[kF];
-    __shared__ uint32_t s_key[kF];
-    __shared__ uint64_t s_wave[kWaves];
-    __shared__ uint64_t s_prefix, s_max;
-    __shared__ uint32_t s_bid, s_miss;
-    const uint32_t b = plan_ticket(look, &s_bid);
-    const uint32_t t = threadIdx.x, lane = t & 63u, wid = t >> 6;
-    const uint64_t f0 = (uint64_t)b * kF, f = f0 + t;
-    const bool mine = t < (uint32_t)kF && f < n;
-    // 1. the window: from the block's first frame start (16-aligned down) to
-    //    the next block's first frame start (the block's end when the frames
-    //    are contiguous; 16-aligned up), at most stage_len bytes, clipped to
-    //    the 16-byte blocks that hold wire bytes
-    const uint64_t lo = index[f0 < n ? f0 : n - 1] & ~uint64_t(15);
-    const uint64_t nx = f0 + kF < n ? index[f0 + kF] : wire_size;
-    const uint64_t wend = (wire_size + 15) & ~uint64_t(15);
-    uint64_t whi = nx > lo ? (nx + 15) & ~uint64_t(15) : lo + stage_len;
-    if (whi > lo + stage_len) whi = lo + stage_len;
-    if (whi > wend) whi = wend;
-    if (whi < lo) whi = lo;
-    const uint32_t nst = (uint32_t)((whi - lo) / 16);
-    const uint64_t idx = mine ? index[f] : 0;
-    if (t == 0) {
-        s_miss = 0;
-        s_max = 0;
-    }
-    constexpr uint32_t kBatch = 9;                       // loads in flight per thread
-    for (uint32_t c0 = 0; c0 < nst; c0 += kThreads * kBatch) {
-        uint4 v[kBatch];
-#pragma unroll
-        for (uint32_t k = 0; k < kBatch; ++k) {
-            const uint32_t c = c0 + k * kThreads + t;
-            if (c < nst) v[k] = ld16(wire + lo + 16ull * c);
-        }
-#pragma unroll
-        for (uint32_t k = 0; k < kBatch; ++k) {
-            const uint32_t c = c0 + k * kThreads + t;
-            if (c < nst) s_stage[c] = v[k];
-        }
-    }
-    if (t < 2) s_stage[nst + t] = make_uint4(0, 0, 0, 0);   // the funnel's block past the end
-    __syncthreads();
-    // 2. my frame's header: from the window when its 16 bytes lie inside
-    //    it, else from the wire (the plan's own parse)
-    cfws_frame_desc_t d = {};
-    int32_t st = CFWS_PARSE_MORE_DATA;
-    uint64_t v = 0;
-    if (mine) {
-        if (idx >= lo && idx + 16 <= whi) {
-            const uint64_t avail = idx <= wire_size ? wire_size - idx : 0;
-            const uint4 W = stage16(s_stage, idx - lo);
-            const uint32_t w[4] = {W.x, W.y, W.z, W.w};
-            st = parse_ws_header_regs(w, avail, max_payload, d);
-            d.wire_off = idx;
-        } else {
-            st = parse_ws_header(wire, wire_size, idx, max_payload, d);
-        }
-        const uint64_t len = st == CFWS_PARSE_COMPLETE ? d.payload_size : 0;
-        v = (len + align - 1) & ~(align - 1);
-    }
-    // 3. the block's prefix: scan + look-back
-    uint64_t tot;
-    const uint64_t ex = block_exclusive_scan(v, s_wave, &tot);
-    if (wid == 0) {
-        const uint64_t pre = plan_lookback(b, tot, look + 1, agg, incl);
-        if (t == 0) s_prefix = pre;
-    }
-    __syncthreads();
-    const uint64_t pre = s_prefix;
-    // 4. descriptors and statuses (deserialize_plan_single_kernel's writes)
-    if (mine) {
-        const uint64_t run = pre + ex;
-        uint64_t* q = reinterpret_cast<uint64_t*>(desc) + 4 * f;
-        q[0] = run;
-        q[1] = d.wire_off;
-        q[2] = d.payload_size;
-        q[3] = (uint64_t)d.mask_key | (uint64_t)d.fin << 32 | (uint64_t)d.opcode << 40 |
-               (uint64_t)d.mask << 48 | (uint64_t)d.header_size << 56;
-        int32_t s2 = st;
-        if (s2 == CFWS_PARSE_COMPLETE && d.payload_size > 0 && run + d.payload_size > capacity)
-            s2 = CFWS_ERROR_OUT_OF_MEMORY;
-        status[f] = s2;
-        if (f == n - 1) {
-            const uint64_t g = run + v, tt = g < capacity ? g : capacity;
-            hdr[0] = tt;
-            hdr[1] = 0;
-            hdr[2] = tt;
-            hdr[3] = g;
-            if (user_total) *user_total = tt;
-        }
-        // the copy's table: slot bytes below the capacity, the payload of a
-        // frame still COMPLETE (zeros otherwise)
-        const uint64_t end = run + v < capacity ? run + v : capacity;
-        const uint64_t nb = end > run ? end - run : 0;
-        const uint64_t ln = s2 == CFWS_PARSE_COMPLETE ? (d.payload_size < nb ? d.payload_size : nb) : 0;
-        const uint64_t src = d.wire_off + d.header_size;
-        s_run[t] = ex;
-        s_src[t] = src;
-        s_len[t] = ln;
-        s_nb[t] = nb;
-        s_key[t] = d.mask ? d.mask_key : 0u;
-        if (ln && (src < lo || src + ln > whi)) atomicOr(&s_miss, 1u);
-        if (nb) atomicMax(reinterpret_cast<unsigned long long*>(&s_max), (unsigned long long)nb);
-    } else if (t < (uint32_t)kF) {
-        s_run[t] = tot;
-        s_nb[t] = 0;
-        s_len[t] = 0;
-        s_src[t] = 0;
-        s_key[t] = 0;
-    }
-    __syncthreads();
-    // 5. the copy: frames in groups of P per wave-instruction (G lanes each,
-    //    G x 16 bytes >= the block's largest slot), groups interleaved over
-    //    the waves; slots over 1 KiB frame by frame
-    const uint64_t m = s_max;
-    if (m == 0) return;
-    const bool miss = s_miss != 0;
-    const uint4 z = make_uint4(0, 0, 0, 0);
-    auto chunk = [&](uint32_t j, uint64_t k) -> uint4 {  // payload bytes [k, k + 16) of frame j
-        const uint64_t L = s_len[j];
-        if (k >= L) return z;
-        const uint64_t sp = s_src[j] + k;
-        uint4 o;
-        if (!miss) {
-            o = stage16(s_stage, sp - lo);
-        } else {
-            const uint8_t* a = wire + (sp & ~uint64_t(15));
-            const uint32_t ph = (uint32_t)(sp & 15u);
-            o = ld16(a);
-            if (ph && ph + (L - k < 16 ? L - k : 16) > 16) o = funnel16(o, ld16(a + 16), ph);
-            else if (ph) o = funnel16(o, z, ph);
-        }
-        xor4(o, s_key[j]);
-        if (L - k < 16) o = and4(o, byte_range(0, (uint32_t)(L - k)));
-        return o;
-    };
-    if (m <= 1024) {
-        uint32_t G = 1;
-        while (G * 16 < m) G <<= 1;
-        const uint32_t P = 64 / G, g = lane / G, c = lane % G;
-        for (uint32_t q = wid; q * P < (uint32_t)kF; q += kWaves) {
-            const uint32_t j = q * P + g;
-            if (j >= (uint32_t)kF) continue;
-            const uint64_t nb = s_nb[j];
-            if (16ull * c >= nb) continue;
-            fused_store(out, pre + s_run[j] + 16ull * c, capacity, chunk(j, 16ull * c));
-        }
-    } else {
-        for (uint32_t j = wid; j < (uint32_t)kF; j += kWaves) {
-            const uint64_t nb = s_nb[j];
-            for (uint64_t k = 16ull * lane; k < nb; k += 1024)
-                fused_store(out, pre + s_run[j] + k, capacity, chunk(j, k));
-        }
-    }
-}
-
 // The fused deserialize (deserialize_plan_single_kernel<true>) for batches
 // of more than kSmallFrames frames averaging at most kFusedAvgMax wire
 // bytes (CFWS_FUSED_DESER=0: plan + execute; A/B knob). A block copies its
@@ -930,40 +737,6 @@ bool fused_deser()
 {
     static const bool v = env_knob("CFWS_FUSED_DESER", 1) != 0;
     return v;
-}
-
-int fused_deser_mode()
-{
-    static const int v = (int)env_knob("CFWS_FUSED_DESER", 1);
-    return v;
-}
-
-// The staged form's kernel for a batch of `avg` wire bytes per frame: as
-// many frames per block as fill the window (null: none fits; the staged
-// form is not used).
-using StagedFn = void (*)(const uint8_t*, uint64_t, const uint64_t*, uint64_t, uint64_t, uint64_t, uint32_t,
-                          cfws_frame_desc_t*, int32_t*, uint32_t*, uint64_t*, uint64_t*, uint64_t*, uint64_t,
-                          uint64_t*, uint8_t*);
-StagedFn staged_kernel(uint64_t avg, uint32_t* frames, uint32_t* window)
-{
-    static const int w = (int)env_knob("CFWS_STAGED_WINDOW_KIB", 72);
-    const uint64_t per = avg + avg / 16 + 16;          // a margin for uneven frames
-    const uint32_t W = w >= 72 ? 72 : (w >= 36 ? 36 : 18);
-    *window = W * 1024;
-    auto fits = [&](uint32_t fr) { return fr * per + 32 <= uint64_t(W) * 1024; };
-    if (W == 72) {
-        if (fits(128)) return *frames = 128, deserialize_staged_kernel<128, 72>;
-        if (fits(64)) return *frames = 64, deserialize_staged_kernel<64, 72>;
-    } else if (W == 36) {
-        if (fits(128)) return *frames = 128, deserialize_staged_kernel<128, 36>;
-        if (fits(64)) return *frames = 64, deserialize_staged_kernel<64, 36>;
-        if (fits(32)) return *frames = 32, deserialize_staged_kernel<32, 36>;
-    } else {
-        if (fits(64)) return *frames = 64, deserialize_staged_kernel<64, 18>;
-        if (fits(32)) return *frames = 32, deserialize_staged_kernel<32, 18>;
-        if (fits(16)) return *frames = 16, deserialize_staged_kernel<16, 18>;
-    }
-    return nullptr;
 }
 
 // Single-pass plans above kSelfScanBlocks blocks (CFWS_PLAN_SINGLE=0: the
@@ -1462,31 +1235,6 @@ int cfws_deserialize_batch(const void* d_wire, uint64_t wire_size, const uint64_
             d_desc, d_status, static_cast<uint8_t*>(d_payload), cap,
             ws_ptr<uint64_t>(ws, ws_layout(n, cap).hdr), d_total);
         return launch_check("deserialize_batch(small)");
-    }
-    // small frames at 16-byte (or wider) slots, staged through LDS (A/B mode 2)
-    uint32_t sfr = 0, slen = 0;
-    const StagedFn kfn = fused_deser_mode() == 2 && n ? staged_kernel(wire_size / n, &sfr, &slen) : nullptr;
-    if (kfn && flags == 0 && align >= 16 && align <= 4096 &&
-        ((uintptr_t)d_wire & 15u) == 0 &&
-        (align & (align - 1)) == 0 && n > kSmallFrames && n <= 0xffffffffull && check_init() == CFWS_OK &&
-        d_wire && d_index && d_desc && d_status && ws && ws_size >= ws_layout(n, cap).bytes &&
-        (cap == 0 || (d_payload && !misaligned(d_payload, d_wire)))) {
-        // its blocks (n / 64 at most) outnumber the layout's scan blocks: the
-        // look-back's flags and sums go in the per-frame offsets' areas,
-        // which this path leaves unused (8 n bytes each)
-        const WsLayout L = ws_layout(n, cap);
-        hipStream_t st = static_cast<hipStream_t>(stream);
-        const uint32_t sb = grid_for(n, sfr);
-        uint32_t* look = ws_ptr<uint32_t>(ws, L.offs[1]);
-        uint64_t* agg = ws_ptr<uint64_t>(ws, L.offs[0]);
-        uint64_t* incl = agg + (uint64_t(sb) + 1);
-        static_assert(kSmallFrames >= 64, "2 (n / 64 + 1) sums fit 8 n bytes");
-        if (hipMemsetAsync(look, 0, 4 * (uint64_t(sb) + 1), st) != hipSuccess)
-            return launch_check("deserialize_batch(staged)");
-        kfn<<<sb, kThreads, 0, st>>>(static_cast<const uint8_t*>(d_wire), wire_size, d_index, n, max_payload,
-                                     align, slen, d_desc, d_status, look, agg, incl,
-                                     ws_ptr<uint64_t>(ws, L.hdr), cap, d_total, static_cast<uint8_t*>(d_payload));
-        return launch_check("deserialize_batch(staged)");
     }
     // small frames at 16-byte (or wider) slots: the fused plan + copy
     if (fused_deser() && flags == 0 && align >= 16 && align <= 4096 && (align & (align - 1)) == 0 &&

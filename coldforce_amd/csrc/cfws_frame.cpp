@@ -507,8 +507,9 @@ bool device_xor(const uint8_t* src, uint8_t* dst, size_t n, uint32_t key)
     ThreadDevice& t_dev = tdev(dev);
     if (service_enabled() && n <= service_max()) {
         if (!t_dev.svc_warm) keep_random_stream.engage();
+        // a service that failed (launch error, or a request that timed out:
+        // its slot is retired) leaves the frame to the launch path below
         const int r = service_xor(t_dev, dev, src, dst, n, key);
-        if (r < 0) return false;
         if (r > 0) {
             t_dev.svc_warm = true;
             return true;

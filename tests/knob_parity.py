@@ -12,8 +12,8 @@ tests/test_knobs.py runs this script once per setting):
   CFWS_PLAN_SINGLE=0    plans of > 2,048 blocks as reduce / scan / apply
   CFWS_SER_INREG=0      WS serialize edge chunks always by edge workgroups
                         launches instead of the single-pass look-back
-  CFWS_FUSED_DESER=0/2  small-frame deserialize as plan + execute / staged
-                        through LDS (1, the default: the fused plan + copy)
+  CFWS_FUSED_DESER=0    small-frame deserialize as plan + execute (1, the
+                        default: the fused plan + copy)
 
 Each case is checked byte for byte against the oracle. Prints "KNOB OK".
 """
@@ -101,15 +101,15 @@ def main():
     # WebSocket over HTTP/2, DATA frames all over 4 KiB + 32: the fused
     # send's in-region edge chunks unless CFWS_H2_INREG=0 or CFWS_EDGE_SPLIT=1
     h2_send(rng.integers(4200, 60000, 1500), rng)
-    # small frames at 16-byte slots: the fused deserialize (CFWS_FUSED_DESER=1:
-    # <= 512 wire bytes per frame; 2: staged through LDS; 0: plan + execute)
+    # small frames at 16-byte slots: the fused deserialize (<= 512 wire bytes
+    # per frame; CFWS_FUSED_DESER=0: plan + execute)
     roundtrip(rng.integers(0, 600, 200000), rng, 7, 16)
     if "CFWS_FUSED_DESER" in os.environ:
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         import test_gpu_batch as T
         for align in (16, 64):
             T.test_fused_deserialize_mixed_and_errors(align)
-        # frame starts out of order (every window misses) and reversed
+        # frame starts out of order and reversed
         import random
         w, _ = T.wire_stream(random.Random(8), 30000, sizes=list(range(0, 1000, 7)))
         offs, consumed = O.index_frames(w, 40000)

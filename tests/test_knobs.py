@@ -19,8 +19,6 @@ KNOBS = [
     {"CFWS_SER_INREG": "0"},
     {"CFWS_H2_INREG": "1"},
     {"CFWS_FUSED_DESER": "0"},
-    {"CFWS_FUSED_DESER": "2"},
-    {"CFWS_FUSED_DESER": "2", "CFWS_STAGED_WINDOW_KIB": "18"},
 ]
 
 
