@@ -3,6 +3,8 @@
 # line (and through torch.distributed.run), rocprof kernel stats and PMC
 # HBM traffic for the headline, the other workloads' bench lines, config 1
 # and the drop-in latency. Every GPU step has its own time limit.
+# usage: tools/r04_final.sh [A|B]   (A: suite, smoke, bench lines; B: the rest;
+# none: both -- longer than one gpurun call allows)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 R=$PWD
@@ -20,10 +22,14 @@ s() {  # name limit cmd...
     echo "STOP after $name (device fault)"; exit 3
   fi
 }
+PART=${1:-AB}
+if [[ $PART == *A* ]]; then
 s pytest 900 python3 -u -m pytest $R/tests -m gpu -v --timeout 300 --timeout-method thread
 s smoke 300 python3 -c "import sys; sys.path.insert(0, '$R'); import __graft_entry__ as g; g.smoke(); print('__SMOKE_OK__')"
 s bench 400 python3 $R/bench.py
 s bench_torchrun 400 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29533 $R/bench.py --gpus 1 --no-cpu-baseline
+fi
+if [[ $PART == *B* ]]; then
 s c3 200 python3 $R/bench.py --workload config3 --no-cpu-baseline
 s c4 400 python3 $R/bench.py --workload config4 --no-cpu-baseline
 s c5 200 python3 $R/bench.py --workload config5 --no-cpu-baseline
@@ -44,4 +50,5 @@ s kt_split 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt_
 cd $R
 s config1 400 python3 $R/tools/config1_bench.py --out "$OUT/config1.jsonl" --reps 2
 TAG=${TAG:-r04final} s dropin 300 bash $R/tools/dropin_lat.sh
+fi
 echo "== done $(date +%T)"
