@@ -619,8 +619,8 @@ def main():
     # reassembly) deserialize in one call: cfws_deserialize_batch runs the
     # fused plan + copy kernel there (deserialize_plan_single_kernel<true>),
     # so the timed kernel is that launch; other batches plan, then execute
-    fused_de = (flags == 0 and F > 1024 and wire_total // F <= 512      # kFusedAvgMax (cfws_device.hip)
-                and os.environ.get("CFWS_FUSED_DESER", "1") != "0")
+    fused_de = (flags == 0 and F > 1024 and os.environ.get("CFWS_FUSED_DESER", "1") != "0"
+                and wire_total // F <= int(os.environ.get("CFWS_FUSED_AVG_MAX", "512")))  # fused_avg_max()
 
     def step(ev=None):
         cfws.serialize_plan(desc_ser, wire.numel(), tot_ser, ws_ser)

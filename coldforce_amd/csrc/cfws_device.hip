@@ -333,8 +333,7 @@ __device__ __forceinline__ uint64_t wave_scan_items(const uint64_t (&v)[kSingleI
 // This block's exclusive prefix from the look-back, plus each wave's offset
 // within the block (s_wave: the waves' totals).
 __device__ __forceinline__ uint64_t single_block_prefix(uint32_t b, uint64_t wave_total, uint64_t* s_wave,
-                                                        uint64_t* s_prefix, uint32_t* look, uint64_t* agg,
-                                                        uint64_t* incl)
+                                                        uint64_t* s_prefix, uint32_t* look)
 {
     const uint32_t wid = threadIdx.x >> 6;
     if ((threadIdx.x & 63u) == 0) s_wave[wid] = wave_total;
@@ -346,7 +345,7 @@ __device__ __forceinline__ uint64_t single_block_prefix(uint32_t b, uint64_t wav
         all += s_wave[w];
     }
     if (wid == 0) {
-        const uint64_t pre = plan_lookback(b, all, look + 1, agg, incl);
+        const uint64_t pre = plan_lookback(b, all, look_states(look));
         if (threadIdx.x == 0) *s_prefix = pre;
     }
     __syncthreads();
@@ -355,8 +354,7 @@ __device__ __forceinline__ uint64_t single_block_prefix(uint32_t b, uint64_t wav
 
 __global__ void __launch_bounds__(kThreads)
 serialize_plan_single_kernel(cfws_frame_desc_t* __restrict__ desc, uint64_t* __restrict__ offs, uint64_t n,
-                             uint32_t* __restrict__ look, uint64_t* __restrict__ agg,
-                             uint64_t* __restrict__ incl, uint64_t* __restrict__ hdr, uint64_t capacity,
+                             uint32_t* __restrict__ look, uint64_t* __restrict__ hdr, uint64_t capacity,
                              uint32_t* __restrict__ map, uint64_t* __restrict__ user_total)
 {
     __shared__ uint64_t s_wave[kWaves];
@@ -404,7 +402,7 @@ serialize_plan_single_kernel(cfws_frame_desc_t* __restrict__ desc, uint64_t* __r
         hsp |= uint64_t(hs) << (4 * k);
         v[k] = f < n ? hs + len[k] : 0;
     }
-    const uint64_t pre = single_block_prefix(b, wave_scan_items(v, ex), s_wave, &s_prefix, look, agg, incl);
+    const uint64_t pre = single_block_prefix(b, wave_scan_items(v, ex), s_wave, &s_prefix, look);
 #pragma unroll
     for (int k = 0; k < kSingleItems; ++k) {
         const uint64_t f = f0 + uint64_t(k) * 64;
@@ -596,7 +594,6 @@ deserialize_plan_single_kernel(const uint8_t* __restrict__ wire, uint64_t wire_s
                                uint64_t n, uint64_t max_payload, uint64_t align,
                                cfws_frame_desc_t* __restrict__ desc, int32_t* __restrict__ status,
                                uint64_t* __restrict__ offs, uint32_t* __restrict__ look,
-                               uint64_t* __restrict__ agg, uint64_t* __restrict__ incl,
                                uint64_t* __restrict__ hdr, uint64_t capacity, uint32_t* __restrict__ map,
                                uint64_t* __restrict__ user_total, uint8_t* __restrict__ out = nullptr)
 {
@@ -672,7 +669,7 @@ deserialize_plan_single_kernel(const uint8_t* __restrict__ wire, uint64_t wire_s
             v[k] = (len + align - 1) & ~(align - 1);
         }
     }
-    const uint64_t pre = single_block_prefix(b, wave_scan_items(v, ex), s_wave, &s_prefix, look, agg, incl);
+    const uint64_t pre = single_block_prefix(b, wave_scan_items(v, ex), s_wave, &s_prefix, look);
     // kCopy: what the copy needs per item, compact (the parse's arrays die here)
     uint64_t c_run[kSingleItems], c_src[kSingleItems];
     uint32_t c_len[kSingleItems], c_nb[kSingleItems], c_key[kSingleItems];
@@ -727,15 +724,20 @@ deserialize_plan_single_kernel(const uint8_t* __restrict__ wire, uint64_t wire_s
 }
 
 // The fused deserialize (deserialize_plan_single_kernel<true>) for batches
-// of more than kSmallFrames frames averaging at most kFusedAvgMax wire
-// bytes (CFWS_FUSED_DESER=0: plan + execute; A/B knob). A block copies its
-// own frames, so a batch mixing a few huge frames into small ones would
-// leave those to single waves: the average keeps such batches on the
-// region stream.
-constexpr uint64_t kFusedAvgMax = 512;
+// of more than kSmallFrames frames averaging at most fused_avg_max() wire
+// bytes (CFWS_FUSED_DESER=0: plan + execute; CFWS_FUSED_AVG_MAX: the
+// average, 512 by default; A/B knobs). A block copies its own frames, so a
+// batch mixing a few huge frames into small ones would leave those to
+// single waves: the average keeps such batches on the region stream.
 bool fused_deser()
 {
     static const bool v = env_knob("CFWS_FUSED_DESER", 1) != 0;
+    return v;
+}
+
+uint64_t fused_avg_max()
+{
+    static const uint64_t v = (uint64_t)env_knob("CFWS_FUSED_AVG_MAX", 512);
     return v;
 }
 
@@ -1074,11 +1076,11 @@ int deserialize_plan_impl(const void* d_wire, uint64_t wire_size, const uint64_t
     if (!reasm && nb > kSelfScanBlocks && plan_single()) {
         uint32_t* look = ws_ptr<uint32_t>(ws, L.look);
         const uint32_t sb = grid_for(n, uint64_t(kThreads) * kSingleItemsDeser);
-        if (hipMemsetAsync(look, 0, 4 * (uint64_t(sb) + 1), st) != hipSuccess)
+        if (hipMemsetAsync(look, 0, look_bytes(sb), st) != hipSuccess)
             return launch_check("deserialize_plan");
         deserialize_plan_single_kernel<false><<<sb, kThreads, 0, st>>>(
             static_cast<const uint8_t*>(d_wire), wire_size, d_index, d_ends, n, max_payload, align, d_desc,
-            d_status, offs0, look, part0, part1, hdr, cap, ws_ptr<uint32_t>(ws, L.map[0]), d_total);
+            d_status, offs0, look, hdr, cap, ws_ptr<uint32_t>(ws, L.map[0]), d_total);
         return launch_check("deserialize_plan");
     }
     deserialize_plan_reduce_kernel<<<nb, kThreads, plan_lds_bytes(), st>>>(
@@ -1130,10 +1132,9 @@ int cfws_serialize_plan(cfws_frame_desc_t* d_desc, size_t n, uint64_t cap, uint6
     if (!self_scan && plan_single()) {
         uint32_t* look = ws_ptr<uint32_t>(ws, L.look);
         const uint32_t sb = grid_for(n, uint64_t(kThreads) * kSingleItemsSer);
-        if (hipMemsetAsync(look, 0, 4 * (uint64_t(sb) + 2), st) != hipSuccess)
+        if (hipMemsetAsync(look, 0, look_bytes(sb), st) != hipSuccess)
             return launch_check("serialize_plan");
-        serialize_plan_single_kernel<<<sb, kThreads, 0, st>>>(d_desc, offs, n, look, partials,
-                                                              ws_ptr<uint64_t>(ws, L.partials[1]), hdr, cap,
+        serialize_plan_single_kernel<<<sb, kThreads, 0, st>>>(d_desc, offs, n, look, hdr, cap,
                                                               ws_ptr<uint32_t>(ws, L.map[0]), d_total);
         return launch_check("serialize_plan");
     }
@@ -1238,19 +1239,19 @@ int cfws_deserialize_batch(const void* d_wire, uint64_t wire_size, const uint64_
     }
     // small frames at 16-byte (or wider) slots: the fused plan + copy
     if (fused_deser() && flags == 0 && align >= 16 && align <= 4096 && (align & (align - 1)) == 0 &&
-        n > kSmallFrames && n <= 0xffffffffull && wire_size / n <= kFusedAvgMax && check_init() == CFWS_OK &&
+        n > kSmallFrames && n <= 0xffffffffull && wire_size / n <= fused_avg_max() && check_init() == CFWS_OK &&
         d_wire && d_index && d_desc && d_status && ws && ws_size >= ws_layout(n, cap).bytes &&
         (cap == 0 || (d_payload && !misaligned(d_payload, d_wire)))) {
         const WsLayout L = ws_layout(n, cap);
         hipStream_t st = static_cast<hipStream_t>(stream);
         uint32_t* look = ws_ptr<uint32_t>(ws, L.look);
         const uint32_t sb = grid_for(n, uint64_t(kThreads) * kFusedItems);
-        if (hipMemsetAsync(look, 0, 4 * (uint64_t(sb) + 1), st) != hipSuccess)
+        if (hipMemsetAsync(look, 0, look_bytes(sb), st) != hipSuccess)
             return launch_check("deserialize_batch(fused)");
         deserialize_plan_single_kernel<true><<<sb, kThreads, 0, st>>>(
             static_cast<const uint8_t*>(d_wire), wire_size, d_index, nullptr, n, max_payload, align, d_desc,
-            d_status, nullptr, look, ws_ptr<uint64_t>(ws, L.partials[0]), ws_ptr<uint64_t>(ws, L.partials[1]),
-            ws_ptr<uint64_t>(ws, L.hdr), cap, nullptr, d_total, static_cast<uint8_t*>(d_payload));
+            d_status, nullptr, look, ws_ptr<uint64_t>(ws, L.hdr), cap, nullptr, d_total,
+            static_cast<uint8_t*>(d_payload));
         return launch_check("deserialize_batch(fused)");
     }
     if (int rc = cfws_deserialize_plan(d_wire, wire_size, d_index, n, max_payload, align, flags,

@@ -97,6 +97,11 @@ struct WsLayout {
 
 inline uint64_t align_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
 
+// The single-pass plans' look area for sb blocks (plan_lookback): the u32
+// ticket and flag words, then a u64 word per block from this u32 index.
+__host__ __device__ inline uint64_t look_state_index(uint64_t sb) { return (sb + 3) & ~uint64_t(1); }
+__host__ __device__ inline uint64_t look_bytes(uint64_t sb) { return 4 * look_state_index(sb) + 8 * (sb + 1); }
+
 WsLayout ws_layout(uint64_t n, uint64_t capacity)
 {
     WsLayout L;
@@ -109,7 +114,7 @@ WsLayout ws_layout(uint64_t n, uint64_t capacity)
     for (int p = 0; p < 2; ++p) { L.partials[p] = at; at = align_up(at + 8 * (L.scan_blocks + 1), 256); }
     for (int p = 0; p < 2; ++p) { L.map[p] = at; at = align_up(at + 4 * (L.regions + 2), 256); }
     L.look = at;
-    at = align_up(at + 4 * (L.scan_blocks + 1), 256);
+    at = align_up(at + look_bytes(L.scan_blocks), 256);
     L.bytes = at;
     return L;
 }
@@ -1633,17 +1638,29 @@ __device__ __forceinline__ void prefix_from_partials(const uint64_t* __restrict_
 // A plan of many blocks scans its block sums with a decoupled look-back
 // instead of a scan launch and a second pass over the frames: each block
 // takes a ticket (so every lower ticket is already running), publishes its
-// sum (flag 1, agg[b]), finds its exclusive prefix from the flags and values
-// of the blocks below it, 64 at a time, and publishes the inclusive prefix
-// (flag 2, incl[b]). agg and incl are written once each, before their flag,
-// and read after it, so a reader never mixes them. Every access is a
-// device-scope atomic (coherent across the XCDs' L2s by itself); the order
-// between a value and its flag comes from waiting for the value's store
-// before the flag's is issued, and from issuing a value's load only after
-// its flag has arrived. (Release / acquire fences would write back and
-// invalidate the whole L2 at each publish and each poll: measured 2 ms per
-// plan on 16 K blocks.) The flags and the ticket are zeroed before the
-// launch.
+// sum (flag 1), finds its exclusive prefix from the words of the blocks
+// below it, 64 at a time, and publishes the inclusive prefix (flag 2). A
+// block's flag and value are one 64-bit word (value << 2 | flag), stored and
+// loaded whole by device-scope atomics (coherent across the XCDs' L2s by
+// themselves), so a reader never sees a flag without its value and nothing
+// has to be ordered: a publish is one store the block does not wait for, a
+// poll one load. (The first form kept flags and values apart: each publish
+// waited for its value's store before the flag's, and each poll loaded the
+// value after the flag -- two more round trips per block, which under a
+// saturated memory system bound the plans by look-back latency. Release /
+// acquire fences would write back and invalidate the whole L2 at each
+// publish and each poll: measured 2 ms per plan on 16 K blocks.)
+//
+// The words live in the workspace's look area after the u32 ticket (word
+// 0), the u32 flag words 1..sb + 1 that some plans leave for their execute,
+// and padding to 8 bytes (look_state_index, look_bytes); all of it is zeroed
+// before the launch.
+
+__device__ __forceinline__ uint64_t* look_states(uint32_t* look)
+{
+    return reinterpret_cast<uint64_t*>(look + look_state_index(gridDim.x));
+}
+
 __device__ __forceinline__ uint32_t plan_ticket(uint32_t* look, uint32_t* s_bid)
 {
     if (threadIdx.x == 0) *s_bid = __hip_atomic_fetch_add(look, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1651,51 +1668,40 @@ __device__ __forceinline__ uint32_t plan_ticket(uint32_t* look, uint32_t* s_bid)
     return *s_bid;
 }
 
-__device__ __forceinline__ void plan_publish(uint32_t* flag, uint64_t* val, uint64_t v, uint32_t f)
-{
-    __hip_atomic_store(val, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __builtin_amdgcn_s_waitcnt(0x0f70);              // vmcnt(0): the value is stored
-    __hip_atomic_store(flag, f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
 // Wave 0 of block b (every lane): b's exclusive prefix, after publishing
 // `total` as b's sum; then b's inclusive prefix is published. Blocks below
 // b that have not published yet (flag 0) hold a lower ticket, so they are
 // running and publish without waiting on anyone.
-__device__ __forceinline__ uint64_t plan_lookback(uint32_t b, uint64_t total, uint32_t* flags,
-                                                  uint64_t* agg, uint64_t* incl)
+__device__ __forceinline__ uint64_t plan_lookback(uint32_t b, uint64_t total, uint64_t* state)
 {
     const uint32_t lane = threadIdx.x & 63u;
     if (b == 0) {
-        if (lane == 0) plan_publish(&flags[0], &incl[0], total, 2u);
+        if (lane == 0) __hip_atomic_store(&state[0], total << 2 | 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return 0;
     }
-    if (lane == 0) plan_publish(&flags[b], &agg[b], total, 1u);
+    if (lane == 0) __hip_atomic_store(&state[b], total << 2 | 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     uint64_t excl = 0;
     int64_t hi = (int64_t)b - 1;                      // window [hi - 63, hi], lane l: hi - l
     while (true) {
         const int64_t i = hi - (int64_t)lane;
-        uint32_t fl = 2u;
-        uint64_t v = 0;
+        uint64_t w = 2u;                              // below block 0: an inclusive 0
         if (i >= 0) {
             do {
-                fl = __hip_atomic_load(&flags[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (fl == 0u) __builtin_amdgcn_s_sleep(2);
-            } while (fl == 0u);
-            v = fl == 2u ? __hip_atomic_load(&incl[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                         : __hip_atomic_load(&agg[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                w = __hip_atomic_load(&state[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if ((w & 3u) == 0u) __builtin_amdgcn_s_sleep(2);
+            } while ((w & 3u) == 0u);
         }
         // the nearest inclusive prefix (lowest lane) ends the walk
-        const uint64_t pm = __ballot(fl == 2u);
+        const uint64_t pm = __ballot((w & 3u) == 2u);
         const uint32_t stop = pm ? (uint32_t)__builtin_ctzll(pm) : 64u;
-        uint64_t c = lane <= stop ? v : 0;
+        uint64_t c = lane <= stop ? w >> 2 : 0;
 #pragma unroll
         for (uint32_t o = 32; o >= 1; o >>= 1) c += __shfl_xor(c, o, 64);
         excl += c;
         if (pm) break;
         hi -= 64;
     }
-    if (lane == 0) plan_publish(&flags[b], &incl[b], excl + total, 2u);
+    if (lane == 0) __hip_atomic_store(&state[b], (excl + total) << 2 | 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return excl;
 }
 

@@ -53,6 +53,8 @@ for s in "$@"; do
     prof_fs1k) step prof_fs1k 400 env TAG=$TAG/prof_fs1k ARGS="--frames 4194304 --frame-size 1024" bash $R/tools/profile.sh ;;
     prof_fs256) step prof_fs256 400 env TAG=$TAG/prof_fs256 ARGS="--frames 16777216 --frame-size 256" bash $R/tools/profile.sh ;;
     ab) step ab 600 env TAG=$TAG/ab bash $R/tools/ab.sh ;;
+    ab_fs1k) step ab_fs1k 600 env TAG=$TAG/ab_fs1k ARGS="--frames 4194304 --frame-size 1024" bash $R/tools/ab.sh ;;
+    ab_fs256) step ab_fs256 600 env TAG=$TAG/ab_fs256 ARGS="--frames 16777216 --frame-size 256" bash $R/tools/ab.sh ;;
     envab) step envab 600 env TAG=$TAG/envab bash $R/tools/envab.sh ;;
     pmc_c5ab)
       for v in 1 0; do
