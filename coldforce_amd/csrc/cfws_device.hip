@@ -582,6 +582,25 @@ __device__ __forceinline__ void fused_item(const uint8_t* __restrict__ wire, uin
 // capacity rule's status) once the offsets are known. kCopy: the fused
 // deserialize (above): each block then copies its frames into `out`; no
 // offsets or region map are written (no execute follows).
+// The plan's header loads: one unaligned 16-byte load per header (1) or the
+// two aligned blocks that hold it (0), plain or non-temporal
+// (CFWS_PLAN_HDR_NT).
+#ifndef CFWS_PLAN_HDR_U
+#define CFWS_PLAN_HDR_U 1
+#endif
+#ifndef CFWS_PLAN_HDR_NT
+#define CFWS_PLAN_HDR_NT 0
+#endif
+#if CFWS_PLAN_HDR_U
+__device__ __forceinline__ uint4 ld16u(const uint8_t* p)
+{
+    typedef uint32_t u32x4u __attribute__((ext_vector_type(4), aligned(1)));
+    const u32x4u v = CFWS_PLAN_HDR_NT ? __builtin_nontemporal_load(reinterpret_cast<const u32x4u*>(p))
+                                      : *reinterpret_cast<const u32x4u*>(p);
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+#endif
+
 #ifndef CFWS_FUSED_ITEMS
 #define CFWS_FUSED_ITEMS 2
 #endif
@@ -629,6 +648,20 @@ deserialize_plan_single_kernel(const uint8_t* __restrict__ wire, uint64_t wire_s
             sz[k] = e < wire_size_all ? e : wire_size_all;
         }
     }
+#if CFWS_PLAN_HDR_U
+    // every header from one 16-byte load at its first byte (unaligned: the
+    // part's unaligned access mode; one request, or two when the 16 bytes
+    // cross a line), clamped to the buffer's last 16 bytes instead of
+    // branching on the bytes available; a header with fewer than 16 bytes
+    // after it in the buffer is parsed by the loads of parse_ws_header
+    const bool b16 = wire_size_all >= 16;
+    const uint64_t lastu = wire_size_all - 16;
+    uint4 hw[kSingleItems];
+    if (b16) {
+#pragma unroll
+        for (int k = 0; k < kSingleItems; ++k) hw[k] = ld16u(wire + (sx[k] < lastu ? sx[k] : lastu));
+    }
+#else
     // a 16-byte-aligned buffer: every header from the two aligned 16-byte
     // blocks that hold it (2 loads per header instead of 5 dwords); a header
     // whose second block is not a whole block of the buffer (the last 32
@@ -644,6 +677,7 @@ deserialize_plan_single_kernel(const uint8_t* __restrict__ wire, uint64_t wire_s
             hb1[k] = ld16(wire + (a + 16 < lastb ? a + 16 : lastb));
         }
     }
+#endif
 #pragma unroll
     for (int k = 0; k < kSingleItems; ++k) {
         const uint64_t f = f0 + uint64_t(k) * 64;
@@ -651,10 +685,17 @@ deserialize_plan_single_kernel(const uint8_t* __restrict__ wire, uint64_t wire_s
         if (f < n) {
             const uint64_t wire_size = sz[k];
             cfws_frame_desc_t d;
-            const uint64_t s0 = sx[k], a = s0 & ~uint64_t(15);
+            const uint64_t s0 = sx[k];
+#if CFWS_PLAN_HDR_U
+            if (b16 && s0 <= lastu) {
+                const uint64_t avail = s0 <= wire_size ? wire_size - s0 : 0;
+                const uint4 W = hw[k];
+#else
+            const uint64_t a = s0 & ~uint64_t(15);
             if (b16 && a + 16 <= lastb) {
                 const uint64_t avail = s0 <= wire_size ? wire_size - s0 : 0;
                 const uint4 W = funnel16(hb0[k], hb1[k], (uint32_t)(s0 - a));
+#endif
                 const uint32_t w[4] = {W.x, W.y, W.z, W.w};
                 sts[k] = parse_ws_header_regs(w, avail, max_payload, d);
                 d.wire_off = s0;
