@@ -46,7 +46,7 @@ def parse():
     ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--frames", type=int, default=65536, help="frames per GPU")
     ap.add_argument("--frame-size", type=int, default=65536)
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
