@@ -220,6 +220,49 @@ def test_deserialize_reassemble(plan_execute):
     check_deserialize(wire, starts, flags=1, capacity=len(wire) // 3)
 
 
+@pytest.mark.parametrize("shift", [0, 3, 13])
+def test_plan_any_wire_alignment(shift):
+    """The receive plan reads each header with one unaligned 16-byte load
+    (deserialize_plan_single_kernel, > 2,048 plan blocks), so it takes a wire
+    at any byte address: 600,000 frames of 0-300 bytes (7-bit and 16-bit
+    lengths, masked and not) planned from a wire shifted by `shift` bytes,
+    with invalid headers and a truncated last frame, against the oracle's
+    descriptors, statuses and total."""
+    rng = np.random.default_rng(shift + 40)
+    n = 600_000
+    payload = O.fill_splitmix(1 << 16, shift, 0)
+    desc = np.zeros(n, dtype=cfws.DESC_DTYPE)
+    desc["payload_size"] = rng.integers(0, 301, n).astype(np.uint64)
+    desc["payload_off"] = rng.integers(0, (1 << 16) - 400, n).astype(np.uint64)
+    desc["fin"] = 1
+    desc["opcode"] = rng.choice([1, 2, 9], n).astype(np.uint8)
+    desc["mask"] = (rng.random(n) < 0.6).astype(np.uint8)
+    desc["mask_key"] = rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32) * desc["mask"]
+    exp_wire, d2 = O.serialize_batch(payload, desc.view(O.DESC_DTYPE))
+    offs = d2["wire_off"].astype(np.uint64)
+    w = exp_wire.copy()
+    w[offs[rng.choice(n - 1, 100, replace=False)].astype(np.int64)] |= 0x20      # an RSV bit -> INVALID_FRAME
+    w = w[:len(w) - 2]                                                          # MORE_DATA at the end
+    buf = torch.from_numpy(np.concatenate([np.zeros(shift, np.uint8), w, np.zeros(16, np.uint8)])).cuda()
+    wt = buf[shift:]
+    assert (wt.data_ptr() - buf.data_ptr()) == shift
+    idx = torch.from_numpy(offs.astype(np.int64)).cuda()
+    cap = len(w) + 16 * n
+    ws = cfws.workspace(n, cap)
+    d_t = torch.empty((n, 32), dtype=torch.uint8, device="cuda")
+    st_t = torch.empty(n, dtype=torch.int32, device="cuda")
+    tot = torch.zeros(1, dtype=torch.int64, device="cuda")
+    cfws.deserialize_plan(wt, len(w), idx, d_t, st_t, cap, tot, ws, align=16)
+    torch.cuda.synchronize()
+    _, e_d, e_st, e_tot = O.deserialize_batch(w, offs, align=16, capacity=cap)
+    assert int(tot.item()) == e_tot
+    st = st_t.cpu().numpy()
+    assert np.array_equal(st, e_st) and (st == O.ERROR_INVALID_FRAME).sum() >= 100
+    d = cfws.desc_from_device(d_t)
+    for f in ("payload_off", "wire_off", "payload_size", "mask_key", "fin", "opcode", "mask", "header_size"):
+        assert np.array_equal(d[f], e_d[f]), f
+
+
 def test_deserialize_error_frames():
     rng = random.Random(7)
     wire, _ = wire_stream(rng, 200)
