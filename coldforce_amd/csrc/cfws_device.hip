@@ -272,19 +272,14 @@ deserialize_plan_reduce_kernel(const uint8_t* __restrict__ wire, uint64_t wire_s
 // the capacity itself: a frame's range ends at or below the grand total, so
 // that is the same clip as at min(total, capacity).
 // The serialize plan reads every descriptor whole and writes it back whole
-// (CFWS_SER_PLAN_FULL, default; 8 frames per thread for the registers): a
-// descriptor line then leaves L2 fully written, and the payload offset is
-// not fetched a second time. 0: the sizes first, the payload offset after
-// the look-back, two fields written (16 frames per thread). At 16 M x 256 B
-// the full form reads 0.54 GB per plan instead of 1.08 and writes the same
-// 0.68 GB, in the same time (328 against 331 us): the plan is bound by its
-// look-back latency at 2 waves per SIMD, not by its traffic
-// (profiles/r04/plan_ab.json).
-#ifndef CFWS_SER_PLAN_FULL
-#define CFWS_SER_PLAN_FULL 1
-#endif
+// (8 frames per thread for the registers): a descriptor line then leaves L2
+// fully written, and the payload offset is not fetched a second time. The
+// round-4 A/B against reading the sizes first and writing two fields after
+// the look-back (16 frames per thread): at 16 M x 256 B 0.54 GB read per plan
+// instead of 1.08, the same 0.68 GB written, the same time (328 against
+// 331 us; profiles/r04/plan_ab.json).
 #ifndef CFWS_SINGLE_ITEMS_SER
-#define CFWS_SINGLE_ITEMS_SER (CFWS_SER_PLAN_FULL ? 8 : 16)
+#define CFWS_SINGLE_ITEMS_SER 8
 #endif
 #ifndef CFWS_SINGLE_ITEMS_DESER
 #define CFWS_SINGLE_ITEMS_DESER 8
@@ -373,7 +368,6 @@ serialize_plan_single_kernel(cfws_frame_desc_t* __restrict__ desc, uint64_t* __r
     uint64_t len[kSingleItems];
     uint32_t msk[kSingleItems];
     bool bad = false;                                  // a frame outside ser_inreg_frame_ok
-#if CFWS_SER_PLAN_FULL
     uint64_t poff[kSingleItems], w3[kSingleItems];
 #pragma unroll
     for (int k = 0; k < kSingleItems; ++k) {
@@ -387,14 +381,6 @@ serialize_plan_single_kernel(cfws_frame_desc_t* __restrict__ desc, uint64_t* __r
 #pragma unroll
     for (int k = 0; k < kSingleItems; ++k)
         bad |= f0 + uint64_t(k) * 64 < n && !ser_inreg_frame_ok(len[k], (uint32_t)poff[k]);
-#else
-#pragma unroll
-    for (int k = 0; k < kSingleItems; ++k) {
-        const uint64_t f = f0 + uint64_t(k) * 64, fc = f < n ? f : n - 1;
-        len[k] = desc[fc].payload_size;
-        msk[k] = desc[fc].mask;
-    }
-#endif
 #pragma unroll
     for (int k = 0; k < kSingleItems; ++k) {
         const uint64_t f = f0 + uint64_t(k) * 64;
@@ -410,20 +396,12 @@ serialize_plan_single_kernel(cfws_frame_desc_t* __restrict__ desc, uint64_t* __r
         const uint64_t run = pre + ex[k];
         offs[f] = run;
         const uint32_t hs = (uint32_t)((hsp >> (4 * k)) & 15u);
-#if CFWS_SER_PLAN_FULL
         // the whole descriptor: the line leaves L2 fully written
         uint64_t* q = reinterpret_cast<uint64_t*>(desc) + 4 * f;
         q[0] = poff[k];
         q[1] = run;
         q[2] = len[k];
         q[3] = (w3[k] & ~(uint64_t(0xff) << 56)) | uint64_t(hs) << 56;
-#else
-        // (the payload offset read here, not with the sizes: 276 VGPRs there)
-        bad |= !ser_inreg_frame_ok(v[k] - hs, (uint32_t)desc[f].payload_off);
-        // both descriptor fields at once, so the line is written back once
-        desc[f].wire_off = run;
-        desc[f].header_size = (uint8_t)hs;
-#endif
         map_range(run, run + v[k], f, capacity, map);
         if (f == n - 1) {
             const uint64_t g = run + v[k], t = g < capacity ? g : capacity;
@@ -582,24 +560,14 @@ __device__ __forceinline__ void fused_item(const uint8_t* __restrict__ wire, uin
 // capacity rule's status) once the offsets are known. kCopy: the fused
 // deserialize (above): each block then copies its frames into `out`; no
 // offsets or region map are written (no execute follows).
-// The plan's header loads: one unaligned 16-byte load per header (1) or the
-// two aligned blocks that hold it (0), plain or non-temporal
-// (CFWS_PLAN_HDR_NT).
-#ifndef CFWS_PLAN_HDR_U
-#define CFWS_PLAN_HDR_U 1
-#endif
-#ifndef CFWS_PLAN_HDR_NT
-#define CFWS_PLAN_HDR_NT 0
-#endif
-#if CFWS_PLAN_HDR_U
+// One unaligned 16-byte load (the part's unaligned access mode): the
+// receive plan's header loads.
 __device__ __forceinline__ uint4 ld16u(const uint8_t* p)
 {
     typedef uint32_t u32x4u __attribute__((ext_vector_type(4), aligned(1)));
-    const u32x4u v = CFWS_PLAN_HDR_NT ? __builtin_nontemporal_load(reinterpret_cast<const u32x4u*>(p))
-                                      : *reinterpret_cast<const u32x4u*>(p);
+    const u32x4u v = *reinterpret_cast<const u32x4u*>(p);
     return make_uint4(v.x, v.y, v.z, v.w);
 }
-#endif
 
 #ifndef CFWS_FUSED_ITEMS
 #define CFWS_FUSED_ITEMS 2
@@ -629,8 +597,7 @@ deserialize_plan_single_kernel(const uint8_t* __restrict__ wire, uint64_t wire_s
     uint64_t v[kSingleItems], ex[kSingleItems], wo[kSingleItems], ps[kSingleItems], w3[kSingleItems];
     int32_t sts[kSingleItems];
     // the loads of all items first, in two rounds (starts and ends, then
-    // every header's two blocks, clamped to the buffer's last whole block
-    // instead of branching on the bytes available), then the parses: a
+    // every header's 16 bytes, below), then the parses: a
     // header per round trip serialized the wave (24 round trips for 8
     // items). Frames past n load frame n - 1's entries: no branch in a round.
     uint64_t sx[kSingleItems], sz[kSingleItems];
@@ -648,7 +615,6 @@ deserialize_plan_single_kernel(const uint8_t* __restrict__ wire, uint64_t wire_s
             sz[k] = e < wire_size_all ? e : wire_size_all;
         }
     }
-#if CFWS_PLAN_HDR_U
     // every header from one 16-byte load at its first byte (unaligned: the
     // part's unaligned access mode; one request, or two when the 16 bytes
     // cross a line), clamped to the buffer's last 16 bytes instead of
@@ -661,23 +627,6 @@ deserialize_plan_single_kernel(const uint8_t* __restrict__ wire, uint64_t wire_s
 #pragma unroll
         for (int k = 0; k < kSingleItems; ++k) hw[k] = ld16u(wire + (sx[k] < lastu ? sx[k] : lastu));
     }
-#else
-    // a 16-byte-aligned buffer: every header from the two aligned 16-byte
-    // blocks that hold it (2 loads per header instead of 5 dwords); a header
-    // whose second block is not a whole block of the buffer (the last 32
-    // bytes) is parsed by the loads of parse_ws_header instead
-    const bool b16 = ((uintptr_t)wire & 15u) == 0 && wire_size_all >= 32;
-    const uint64_t lastb = (wire_size_all - 16) & ~uint64_t(15);
-    uint4 hb0[kSingleItems], hb1[kSingleItems];
-    if (b16) {
-#pragma unroll
-        for (int k = 0; k < kSingleItems; ++k) {
-            const uint64_t a = sx[k] & ~uint64_t(15);
-            hb0[k] = ld16(wire + (a < lastb ? a : lastb));
-            hb1[k] = ld16(wire + (a + 16 < lastb ? a + 16 : lastb));
-        }
-    }
-#endif
 #pragma unroll
     for (int k = 0; k < kSingleItems; ++k) {
         const uint64_t f = f0 + uint64_t(k) * 64;
@@ -686,16 +635,9 @@ deserialize_plan_single_kernel(const uint8_t* __restrict__ wire, uint64_t wire_s
             const uint64_t wire_size = sz[k];
             cfws_frame_desc_t d;
             const uint64_t s0 = sx[k];
-#if CFWS_PLAN_HDR_U
             if (b16 && s0 <= lastu) {
                 const uint64_t avail = s0 <= wire_size ? wire_size - s0 : 0;
                 const uint4 W = hw[k];
-#else
-            const uint64_t a = s0 & ~uint64_t(15);
-            if (b16 && a + 16 <= lastb) {
-                const uint64_t avail = s0 <= wire_size ? wire_size - s0 : 0;
-                const uint4 W = funnel16(hb0[k], hb1[k], (uint32_t)(s0 - a));
-#endif
                 const uint32_t w[4] = {W.x, W.y, W.z, W.w};
                 sts[k] = parse_ws_header_regs(w, avail, max_payload, d);
                 d.wire_off = s0;

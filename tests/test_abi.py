@@ -60,8 +60,12 @@ def test_workspace_size_host_only():
     L.cfws_workspace_size.restype = ctypes.c_size_t
     L.cfws_workspace_size.argtypes = [ctypes.c_size_t, ctypes.c_uint64]
     a = L.cfws_workspace_size(65536, 1 << 32)
-    # two passes x (per-frame offsets (8 B) + one u32 per 4 KiB output region) + fixed part
-    assert 2 * (65536 * 8 + (1 << 32) // 4096 * 4) <= a < 2 * (65536 * 8 + (1 << 32) // 4096 * 4) + 8192
+    # two passes x (per-frame offsets (8 B) + one u32 per 4 KiB output region)
+    # + per plan block (256 frames) two u64 sums and the look-back's u32 + u64
+    # words + a fixed part
+    per_pass = 65536 * 8 + (1 << 32) // 4096 * 4
+    blocks = 65536 // 256
+    assert 2 * per_pass <= a < 2 * per_pass + blocks * (2 * 8 + 12) + 8192
     assert L.cfws_workspace_size(0, 0) > 0
 
 
