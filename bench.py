@@ -240,10 +240,14 @@ def bench_h2(args, rank, world, dev):
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         st, md, ms, ptot, m = step()
     torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
     local = time.perf_counter() - t0
     elapsed = shard.max_over_ranks(local, dev)
     rows = shard.gather_floats([local, F * fs], dev)
@@ -301,10 +305,14 @@ def bench_split(args, rank, world, dev):
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
     torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
     local = time.perf_counter() - t0
     elapsed = shard.max_over_ranks(local, dev)
     rows = shard.gather_floats([local, F * fs], dev)
@@ -560,10 +568,18 @@ def main():
     rank, local_rank, world = shard.world()
     if args.gpus != world and world == 1 and args.gpus > 1:
         sys.exit("bench.py: --gpus > 1 needs torchrun (one process per GPU)")
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    # CFWS_BENCH_REHEARSE=1: more ranks than GPUs (ranks share devices,
+    # bookkeeping collectives over gloo) -- a check of the multi-rank path on
+    # a smaller box, not a measurement
+    rehearse = os.environ.get("CFWS_BENCH_REHEARSE") == "1"
+    gpu = local_rank % torch.cuda.device_count() if rehearse else local_rank
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
     cfws.init()
 
     F, fs = args.frames, args.frame_size

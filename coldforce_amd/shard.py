@@ -80,6 +80,13 @@ def zipf_shard(bytes_per_rank: int, rank: int, world_size: int, seed: int, key_s
     return d, local, base
 
 
+def _coll_device(device):
+    """Where a bookkeeping collective's tensor lives: the rank's GPU under
+    RCCL, the host under gloo (a multi-rank rehearsal on fewer GPUs)."""
+    import torch.distributed as dist
+    return "cpu" if dist.get_backend() == "gloo" else device
+
+
 def gather_floats(values, device=None) -> list[list[float]]:
     """Every rank's `values` (a few floats: timings, byte counts), rank order.
     Bookkeeping only; the data path has no collective."""
@@ -87,7 +94,7 @@ def gather_floats(values, device=None) -> list[list[float]]:
     import torch.distributed as dist
     if not (dist.is_available() and dist.is_initialized()):
         return [list(map(float, values))]
-    t = torch.tensor(list(values), dtype=torch.float64, device=device)
+    t = torch.tensor(list(values), dtype=torch.float64, device=_coll_device(device))
     out = [torch.empty_like(t) for _ in range(dist.get_world_size())]
     dist.all_gather(out, t)
     return [[float(x) for x in o.tolist()] for o in out]
@@ -98,7 +105,7 @@ def max_over_ranks(value: float, device=None) -> float:
     import torch.distributed as dist
     if not (dist.is_available() and dist.is_initialized()):
         return value
-    t = torch.tensor([value], dtype=torch.float64, device=device)
+    t = torch.tensor([value], dtype=torch.float64, device=_coll_device(device))
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
@@ -108,7 +115,7 @@ def sum_over_ranks(value: float, device=None) -> float:
     import torch.distributed as dist
     if not (dist.is_available() and dist.is_initialized()):
         return value
-    t = torch.tensor([value], dtype=torch.float64, device=device)
+    t = torch.tensor([value], dtype=torch.float64, device=_coll_device(device))
     dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return float(t.item())
 
