@@ -277,10 +277,9 @@ deserialize_plan_reduce_kernel(const uint8_t* __restrict__ wire, uint64_t wire_s
 // round-4 A/B against reading the sizes first and writing two fields after
 // the look-back (16 frames per thread): at 16 M x 256 B 0.54 GB read per plan
 // instead of 1.08, the same 0.68 GB written, the same time (328 against
-// 331 us; profiles/r04/plan_ab.json).
-#ifndef CFWS_SER_PLAN_LITE
-#define CFWS_SER_PLAN_LITE 0
-#endif
+// 331 us; profiles/r04/plan_ab.json); with the packed look-back, the two-field
+// form at 4, 8 or 16 frames per thread (down to 122 VGPRs, 4 waves per SIMD)
+// was 0.2-1.9 % slower per step at 256 B and 1 KiB (profiles/r04/plan_lite_ab.json).
 #ifndef CFWS_SINGLE_ITEMS_SER
 #define CFWS_SINGLE_ITEMS_SER 8
 #endif
@@ -371,16 +370,6 @@ serialize_plan_single_kernel(cfws_frame_desc_t* __restrict__ desc, uint64_t* __r
     uint64_t len[kSingleItems];
     uint32_t msk[kSingleItems];
     bool bad = false;                                  // a frame outside ser_inreg_frame_ok
-#if CFWS_SER_PLAN_LITE
-#pragma unroll
-    for (int k = 0; k < kSingleItems; ++k) {
-        const uint64_t f = f0 + uint64_t(k) * 64, fc = f < n ? f : n - 1;
-        const DescWords d = load_desc(desc, (uint32_t)fc);
-        len[k] = d.payload_size;
-        msk[k] = d.mask();
-        bad |= f < n && !ser_inreg_frame_ok(d.payload_size, (uint32_t)d.payload_off);
-    }
-#else
     uint64_t poff[kSingleItems], w3[kSingleItems];
 #pragma unroll
     for (int k = 0; k < kSingleItems; ++k) {
@@ -394,7 +383,6 @@ serialize_plan_single_kernel(cfws_frame_desc_t* __restrict__ desc, uint64_t* __r
 #pragma unroll
     for (int k = 0; k < kSingleItems; ++k)
         bad |= f0 + uint64_t(k) * 64 < n && !ser_inreg_frame_ok(len[k], (uint32_t)poff[k]);
-#endif
 #pragma unroll
     for (int k = 0; k < kSingleItems; ++k) {
         const uint64_t f = f0 + uint64_t(k) * 64;
@@ -410,17 +398,12 @@ serialize_plan_single_kernel(cfws_frame_desc_t* __restrict__ desc, uint64_t* __r
         const uint64_t run = pre + ex[k];
         offs[f] = run;
         const uint32_t hs = (uint32_t)((hsp >> (4 * k)) & 15u);
-#if CFWS_SER_PLAN_LITE
-        desc[f].wire_off = run;
-        desc[f].header_size = (uint8_t)hs;
-#else
         // the whole descriptor: the line leaves L2 fully written
         uint64_t* q = reinterpret_cast<uint64_t*>(desc) + 4 * f;
         q[0] = poff[k];
         q[1] = run;
         q[2] = len[k];
         q[3] = (w3[k] & ~(uint64_t(0xff) << 56)) | uint64_t(hs) << 56;
-#endif
         map_range(run, run + v[k], f, capacity, map);
         if (f == n - 1) {
             const uint64_t g = run + v[k], t = g < capacity ? g : capacity;
