@@ -493,27 +493,23 @@ h2_msg_parse_kernel(const uint8_t* __restrict__ h2, const cfws_frame_desc_t* __r
 // any message, or of a message whose frame did not parse COMPLETE, are
 // empty units at the matching layout position (offsets stay monotone and
 // the pass zero-fills what the layout does not cover).
-__device__ __forceinline__ uint64_t h2_unit(const cfws_frame_desc_t* __restrict__ pdesc,
-                                            const int32_t* __restrict__ h2_status,
-                                            const uint64_t* __restrict__ poff,
-                                            const uint64_t* __restrict__ msg_id, uint64_t d,
-                                            uint64_t n_msg, const uint64_t* __restrict__ starts,
-                                            const cfws_frame_desc_t* __restrict__ mdesc,
-                                            const int32_t* __restrict__ mstatus,
-                                            const uint64_t* __restrict__ hdr, cfws_frame_desc_t& u)
+// DATA frame d of message m (descriptor M, status ms, pooled start s_m);
+// `past`: the layout's end, the output offset of a frame in no message.
+__device__ __forceinline__ uint64_t h2_unit_of(const cfws_frame_desc_t* __restrict__ pdesc,
+                                               const int32_t* __restrict__ h2_status,
+                                               const uint64_t* __restrict__ poff, uint64_t d, bool in_msg,
+                                               uint64_t s_m, const cfws_frame_desc_t& M, int32_t ms,
+                                               uint64_t past, cfws_frame_desc_t& u)
 {
-    const uint64_t m = msg_id[d];
     u = {};
-    uint64_t out = hdr[3];                             // past the last message
-    if (m < n_msg) {
-        const cfws_frame_desc_t M = mdesc[m];
-        const int32_t ms = mstatus[m];
+    uint64_t out = past;
+    if (in_msg) {
         const uint64_t hs = M.header_size;
         // the message's layout span: payload_size when it parsed (an OOM
         // frame keeps its layout), else nothing
         const uint64_t span = (ms == CFWS_PARSE_COMPLETE || ms == CFWS_ERROR_OUT_OF_MEMORY)
                                   ? M.payload_size : 0;
-        const uint64_t a = poff[d] - starts[m];
+        const uint64_t a = poff[d] - s_m;
         const uint64_t dl = h2_status[d] == CFWS_H2_PARSE_COMPLETE ? pdesc[d].payload_size : 0;
         const uint64_t b = a + dl;
         const uint64_t qa = a > hs ? (a - hs < span ? a - hs : span) : 0;
@@ -528,6 +524,28 @@ __device__ __forceinline__ uint64_t h2_unit(const cfws_frame_desc_t* __restrict_
         }
     }
     return out;
+}
+
+__device__ __forceinline__ uint64_t h2_unit(const cfws_frame_desc_t* __restrict__ pdesc,
+                                            const int32_t* __restrict__ h2_status,
+                                            const uint64_t* __restrict__ poff,
+                                            const uint64_t* __restrict__ msg_id, uint64_t d,
+                                            uint64_t n_msg, const uint64_t* __restrict__ starts,
+                                            const cfws_frame_desc_t* __restrict__ mdesc,
+                                            const int32_t* __restrict__ mstatus,
+                                            const uint64_t* __restrict__ hdr, cfws_frame_desc_t& u)
+{
+    const uint64_t m = msg_id[d];
+    const bool in_msg = m < n_msg;
+    cfws_frame_desc_t M = {};
+    int32_t ms = CFWS_PARSE_MORE_DATA;
+    uint64_t s_m = 0;
+    if (in_msg) {
+        M = mdesc[m];
+        ms = mstatus[m];
+        s_m = starts[m];
+    }
+    return h2_unit_of(pdesc, h2_status, poff, d, in_msg, s_m, M, ms, hdr[3], u);
 }
 
 // One thread per DATA frame: its unit, and the region map of the payload
@@ -561,6 +579,97 @@ h2_units_kernel(const cfws_frame_desc_t* __restrict__ pdesc, const int32_t* __re
     if (d == n - 1) map[(total + kRegion - 1) / kRegion] = (uint32_t)(n - 1);
 }
 
+
+// deserialize_plan_apply_kernel (one message per thread, no reassembly) and
+// h2_units_kernel in one launch (CFWS_H2_UNITS_MERGED, default): the
+// thread of message m lays it out (payload offset, the capacity rule, the
+// message map, the totals), then writes the units of m's DATA frames
+// [first[m], first[m + 1]) -- all from values it holds: a frame's unit
+// needs only its message's descriptor, and the last frame's unit ends
+// where message m + 1's layout starts, m's offset + its aligned size. The
+// frames after the last END_STREAM (in no message) go to the threads in
+// turn. One launch less on the receive (config 5: 7 plan kernels -> 6).
+__global__ void __launch_bounds__(kThreads)
+h2_msg_apply_units_kernel(cfws_frame_desc_t* __restrict__ mdesc, int32_t* __restrict__ mstatus,
+                          uint64_t* __restrict__ vals, uint64_t n, const uint64_t* __restrict__ partials,
+                          uint64_t nb, uint32_t self_scan, uint64_t* __restrict__ hdr, uint64_t capacity,
+                          uint32_t* __restrict__ mmap, uint64_t* __restrict__ user_total,
+                          const cfws_frame_desc_t* __restrict__ pdesc, const int32_t* __restrict__ h2_status,
+                          const uint64_t* __restrict__ poff, const uint64_t* __restrict__ n_msg_p,
+                          const uint64_t* __restrict__ starts, const uint64_t* __restrict__ first,
+                          cfws_frame_desc_t* __restrict__ udesc, int32_t* __restrict__ ustatus,
+                          uint64_t* __restrict__ uoffs, uint32_t* __restrict__ umap,
+                          const uint64_t* __restrict__ pooled_p, uint64_t pool_cap,
+                          uint64_t* __restrict__ pass_total)
+{
+    static_assert(kPlanItems == 1, "one message per thread");
+    __shared__ uint64_t s_wave[kWaves];
+    uint64_t pre, g;
+    if (self_scan) {
+        prefix_from_partials(partials, nb, blockIdx.x, s_wave, pre, g);
+    } else {
+        pre = partials[blockIdx.x];
+        g = hdr[3];
+    }
+    const uint64_t t = g < capacity ? g : capacity;
+    const uint64_t m = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
+    const uint64_t v = m < n ? vals[m] : 0;
+    uint64_t tot;
+    const uint64_t run = block_exclusive_scan(v, s_wave, &tot) + pre;
+    const uint64_t n_msg = *n_msg_p;
+    cfws_frame_desc_t M = {};
+    int32_t ms = CFWS_PARSE_MORE_DATA;
+    if (m < n) {
+        // deserialize_plan_apply_kernel's row m
+        vals[m] = run;
+        M = mdesc[m];
+        M.payload_off = run;
+        mdesc[m].payload_off = run;
+        ms = mstatus[m];
+        if (ms == CFWS_PARSE_COMPLETE && M.payload_size > 0 && run + M.payload_size > capacity) {
+            ms = CFWS_ERROR_OUT_OF_MEMORY;
+            mstatus[m] = ms;
+        }
+        map_range(run, run + v, m, t, mmap);
+        if (m == n - 1) {
+            mmap[(t + kRegion - 1) / kRegion] = (uint32_t)m;
+            hdr[0] = t;
+            hdr[1] = 0;
+            hdr[2] = t;
+            if (self_scan) hdr[3] = g;
+            if (user_total) *user_total = t;
+        }
+    }
+    if (m == 0) *pass_total = *pooled_p <= pool_cap ? t : 0;
+    // the units of message m's DATA frames
+    if (m < n_msg) {
+        const uint64_t d0 = first[m], d1 = m + 1 < n_msg ? first[m + 1] : (n_msg < n ? first[n_msg] : n);
+        const uint64_t s_m = starts[m];
+        const uint64_t next = m + 1 < n_msg ? run + v : g;    // where the next unit starts
+        cfws_frame_desc_t u, u1;
+        uint64_t lo = d0 < d1 ? h2_unit_of(pdesc, h2_status, poff, d0, true, s_m, M, ms, g, u) : 0;
+        for (uint64_t d = d0; d < d1; ++d) {
+            const uint64_t hi = d + 1 < d1 ? h2_unit_of(pdesc, h2_status, poff, d + 1, true, s_m, M, ms, g, u1)
+                                           : next;
+            udesc[d] = u;
+            ustatus[d] = CFWS_PARSE_COMPLETE;
+            uoffs[d] = lo;
+            map_range(lo, hi, d, t, umap);
+            lo = hi;
+            u = u1;
+        }
+    }
+    // frames in no message: empty units at the layout's end
+    const uint64_t tail0 = n_msg < n ? first[n_msg] : n;
+    for (uint64_t d = tail0 + m; d < n; d += uint64_t(gridDim.x) * kThreads) {
+        cfws_frame_desc_t e = {};
+        udesc[d] = e;
+        ustatus[d] = CFWS_PARSE_COMPLETE;
+        uoffs[d] = g;
+        map_range(g, g, d, t, umap);
+    }
+    if (m == 0 && n > 0) umap[(t + kRegion - 1) / kRegion] = (uint32_t)(n - 1);
+}
 
 }  // namespace
 
@@ -682,6 +791,14 @@ namespace {
 // the sub-64-byte write requests from 160 K to 47 K per launch and the
 // wave-cycles by 8.6 %, yet the step ran 0.5-1.5 % slower on the same box
 // (profiles/r04/h2_inreg_ab/). Parity-tested both ways.
+// CFWS_H2_UNITS_MERGED=0: the receive's message layout and its payload-pass
+// units as two launches (A/B knob)
+bool h2_units_merged()
+{
+    static const bool v = env_knob("CFWS_H2_UNITS_MERGED", 1) != 0;
+    return v;
+}
+
 bool h2_inreg()
 {
     static const bool v = env_knob("CFWS_H2_INREG", 0) != 0;
@@ -908,10 +1025,6 @@ int cfws_h2_deserialize_batch(const void* d_h2, uint64_t h2_size, const uint64_t
                                                 max_payload, align, d_msg_desc, d_msg_status, offs0,
                                                 first, part0);
     if (!m_self) scan_partials_kernel<<<1, kThreads, 0, st>>>(part0, mb, hdr + 3);
-    deserialize_plan_apply_kernel<<<mb, kThreads, 0, st>>>(
-        d_msg_desc, d_msg_status, offs0, ws_ptr<uint64_t>(wsd, WL.offs[1]), n, part0,
-        ws_ptr<uint64_t>(wsd, WL.partials[1]), mb, m_self, hdr, payload_cap, 0,
-        ws_ptr<uint32_t>(wsd, WL.map[0]), ws_ptr<uint32_t>(wsd, WL.map[1]), d_payload_total);
     // 3. one payload-pass unit per DATA frame, and the pass's region map
     cfws_frame_desc_t* udesc = ws_ptr<cfws_frame_desc_t>(ws, L.udesc);
     int32_t* ustatus = ws_ptr<int32_t>(ws, L.ustatus);
@@ -920,9 +1033,20 @@ int cfws_h2_deserialize_batch(const void* d_h2, uint64_t h2_size, const uint64_t
     // the pass's total, or 0 when the pool overflows (it then stores nothing;
     // the general form below does the call's work once)
     uint64_t* pass_total = ws_ptr<uint64_t>(ws, L.pass_total);
-    h2_units_kernel<<<grid_for(n, kThreads), kThreads, 0, st>>>(
-        pdesc, d_h2_status, poffs, es, n, n_msg_d, starts, d_msg_desc, d_msg_status, hdr, udesc,
-        ustatus, uoffs, umap, phdr + 3, pool_cap, pass_total);
+    if (h2_units_merged()) {
+        h2_msg_apply_units_kernel<<<mb, kThreads, 0, st>>>(
+            d_msg_desc, d_msg_status, offs0, n, part0, mb, m_self, hdr, payload_cap,
+            ws_ptr<uint32_t>(wsd, WL.map[0]), d_payload_total, pdesc, d_h2_status, poffs, n_msg_d, starts,
+            first, udesc, ustatus, uoffs, umap, phdr + 3, pool_cap, pass_total);
+    } else {
+        deserialize_plan_apply_kernel<<<mb, kThreads, 0, st>>>(
+            d_msg_desc, d_msg_status, offs0, ws_ptr<uint64_t>(wsd, WL.offs[1]), n, part0,
+            ws_ptr<uint64_t>(wsd, WL.partials[1]), mb, m_self, hdr, payload_cap, 0,
+            ws_ptr<uint32_t>(wsd, WL.map[0]), ws_ptr<uint32_t>(wsd, WL.map[1]), d_payload_total);
+        h2_units_kernel<<<grid_for(n, kThreads), kThreads, 0, st>>>(
+            pdesc, d_h2_status, poffs, es, n, n_msg_d, starts, d_msg_desc, d_msg_status, hdr, udesc,
+            ustatus, uoffs, umap, phdr + 3, pool_cap, pass_total);
+    }
     if (payload_cap)
         launch_streaming<kModeDeser>(d_h2, d_payload, udesc, ustatus, uoffs, umap, pass_total, nullptr,
                                      WL.regions, payload_cap, n, kClassAll, 0, st);

@@ -14,6 +14,8 @@ tests/test_knobs.py runs this script once per setting):
                         launches instead of the single-pass look-back
   CFWS_FUSED_DESER=0    small-frame deserialize as plan + execute (1, the
                         default: the fused plan + copy)
+  CFWS_H2_UNITS_MERGED=0  the HTTP/2 receive's message layout and payload
+                        units as two launches (1, the default: one)
 
 Each case is checked byte for byte against the oracle. Prints "KNOB OK".
 """
@@ -117,6 +119,13 @@ def main():
         perm = np.random.default_rng(9).permutation(len(offs))
         T.check_deserialize(w, offs[perm], align=16)
         T.check_deserialize(w, offs[::-1].copy(), align=16)
+    if "CFWS_H2_UNITS_MERGED" in os.environ:
+        # the HTTP/2 receive with its message layout and units as two launches
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import test_h2 as T2
+        T2.test_gpu_h2_roundtrip_random(16384)
+        T2.test_gpu_h2_deserialize_headers_across_data_frames(13)
+        T2.test_gpu_h2_rows_past_message_count_are_empty(2)
     # a small batch (single-launch path unless CFWS_SMALL=0)
     roundtrip(np.full(256, 1000), rng, 3, 16)
     # fragments + pings, reassembled (two passes, pass-1 capped grid)

@@ -19,6 +19,7 @@ KNOBS = [
     {"CFWS_SER_INREG": "0"},
     {"CFWS_H2_INREG": "1"},
     {"CFWS_FUSED_DESER": "0"},
+    {"CFWS_H2_UNITS_MERGED": "0"},
 ]
 
 
