@@ -1640,7 +1640,8 @@ __device__ __forceinline__ void prefix_from_partials(const uint64_t* __restrict_
 // takes a ticket (so every lower ticket is already running), publishes its
 // sum (flag 1), finds its exclusive prefix from the words of the blocks
 // below it, 64 at a time, and publishes the inclusive prefix (flag 2). A
-// block's flag and value are one 64-bit word (value << 2 | flag), stored and
+// block's flag and value are one 64-bit word (value << 2 | flag: sums below
+// 2^62 bytes, far above any arena), stored and
 // loaded whole by device-scope atomics (coherent across the XCDs' L2s by
 // themselves), so a reader never sees a flag without its value and nothing
 // has to be ordered: a publish is one store the block does not wait for, a
