@@ -302,6 +302,33 @@ def test_gpu_h2_deserialize_headers_across_data_frames(S):
 
 @pytest.mark.gpu
 @pytest.mark.skipif(not gpu_present(), reason="needs the MI355X")
+@pytest.mark.parametrize("cut", [1, 2, 3])
+def test_gpu_h2_stream_without_end_stream(cut):
+    """Streams whose last messages never see END_STREAM: their DATA frames
+    are in no message (h2_msg_apply_units_kernel hands them to the threads
+    in turn as empty units). `cut` DATA frames of a 40,000-byte message's
+    three are kept: 1 and 2 leave no message at all (n_messages 0) after
+    a run of complete ones (3: the last message is whole)."""
+    rng = random.Random(cut)
+    payload = O.fill_splitmix(1 << 17, cut, 0)
+    d = np.zeros(1, dtype=O.DESC_DTYPE)
+    d[0] = (100, 0, 40000, rng.getrandbits(32), 1, 2, 1, 0)
+    h2, _ = O.h2_serialize_batch(payload, d, 1, 16384)
+    index = O.h2_index(h2)
+    assert len(index) == 3
+    end = int(index[cut]) if cut < 3 else len(h2)
+    alone = h2[:end].copy()
+    got = check_h2_deserialize(alone, O.h2_index(alone))
+    assert got["n_msg"] == (1 if cut == 3 else 0)
+    # the same after 300 whole messages of mixed sizes
+    head, hidx = _h2_case(cut + 50, 300)
+    both = np.concatenate([head, alone])
+    got = check_h2_deserialize(both, O.h2_index(both))
+    assert got["n_msg"] == 300 + (1 if cut == 3 else 0)
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not gpu_present(), reason="needs the MI355X")
 @pytest.mark.parametrize("idx", [0, 1, 2, 3])
 def test_gpu_config5_digest(idx):
     """Config 5 batches (16,376 B and 64 KiB frames, 1,024 and 65,536 of
