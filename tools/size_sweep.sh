@@ -5,7 +5,7 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 OUT=gpurun_out/${TAG:-size_sweep}; mkdir -p "$OUT"
 for fs in 256 512 1024 2048 4096 16384 65536 262144 1048576; do
-  timeout -k 10 300 python bench.py --frames $((4294967296 / fs)) --frame-size $fs --steps 10 --warmup 2 \
+  timeout -k 10 300 python bench.py --frames $((4294967296 / fs)) --frame-size $fs --steps 20 --warmup 10 \
       --no-cpu-baseline > "$OUT/fs$fs.json" 2> "$OUT/fs$fs.err" || { echo "fs $fs failed"; exit 1; }
 done
 timeout -k 10 300 python bench.py --workload config3 --no-cpu-baseline > "$OUT/config3.json" 2> "$OUT/config3.err" &&
