@@ -140,9 +140,12 @@ edge_reasm_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
 // ---------------------------------------------------------------------------
 // WS serialize's in-region edge chunks (general_region_ser_edges) need every
 // frame's payload at 80..2,000 bytes and 16-aligned in the payload arena.
+#ifndef CFWS_SER_INREG_MAX
+#define CFWS_SER_INREG_MAX 2000
+#endif
 __device__ __forceinline__ bool ser_inreg_frame_ok(uint64_t len, uint32_t payload_off_lo)
 {
-    return len >= 80 && len <= 2000 && (payload_off_lo & 15u) == 0;
+    return len >= 80 && len <= CFWS_SER_INREG_MAX && (payload_off_lo & 15u) == 0;
 }
 
 __global__ void __launch_bounds__(kThreads)

@@ -972,7 +972,10 @@ __device__ __forceinline__ void general_region(const Pass& P, uint32_t f0, uint3
             const uint4 H = ws_header_words(v.body_len, v.hb, v.key);
             h0 = H.x;
             h1 = H.y;
-            hm = ((uint32_t)(v.out_off - base) & 0xffffu) | v.pre << 16;
+            // the header start, clamped below (a long frame's header far
+            // before the region is simply before it)
+            const int64_t ho = (int64_t)v.out_off - (int64_t)base;
+            hm = ((uint32_t)(ho < -64 ? -64 : (int)ho) & 0xffffu) | v.pre << 16;
             tk = v.key;
         }
     }
@@ -1252,13 +1255,23 @@ __device__ __forceinline__ void region_loop(const Pass& P, const uint64_t* __res
         if (f1 > f0 && offs[f0 + 1] >= end) f1 = f0;
         const FrameView va = frame_view<kMode>(P, f0);
         constexpr bool kEdges = kInreg && kMode == kModeH2Ser;   // edge chunks in-region
+        // the in-region WS send: every region holding a header goes to
+        // general_region, whose edge chunks need no frame-size bound
+        // (payloads over 2,000 bytes, CFWS_SER_INREG_MAX, make such regions
+        // one- or two-frame ones)
+        constexpr bool kSerGen = kInreg && kMode == kModeSer;
         if (f0 == f1) {
             if (base >= va.body_start && end <= va.body_start + va.body_len)
                 fast_region<kMode>(P, va, base, lane);
+            else if (kSerGen)
+                general_region<kMode>(P, f0, f0, base, lane, true);
             else
                 two_frame_region<kMode, kEdges>(P, va, va, base, lane);   // partial body, one frame
         } else if (f1 == f0 + 1 || offs[f0 + 2] >= end) {
-            two_frame_region<kMode, kEdges>(P, va, frame_view<kMode>(P, f0 + 1), base, lane);
+            if (kSerGen)
+                general_region<kMode>(P, f0, f0 + 1, base, lane, true);
+            else
+                two_frame_region<kMode, kEdges>(P, va, frame_view<kMode>(P, f0 + 1), base, lane);
         } else {
             general_region<kMode>(P, f0, f1, base, lane, kInreg);
         }

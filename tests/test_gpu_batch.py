@@ -584,6 +584,40 @@ def test_serialize_in_region_edges(n):
     check_serialize(payload, d3, plan_execute=True)
 
 
+@pytest.mark.parametrize("case", ["mixed", "region_starts", "64k"])
+def test_serialize_aligned_large_frames(case):
+    """WS serialize of payloads at 16-aligned source offsets past 2,000
+    bytes -- the in-region send's bound (CFWS_SER_INREG_MAX) -- where a
+    region holding a header is a one- or two-frame region: mixed 80 B-70 KB
+    payloads; 4,088-byte masked payloads (4,096 wire bytes: every frame
+    starts on a region boundary); 64 KiB frames (14-byte headers). Against
+    the oracle, whole and cut at a capacity, through both launch forms."""
+    rng = np.random.default_rng({"mixed": 1, "region_starts": 2, "64k": 3}[case])
+    payload = O.fill_splitmix(1 << 22, 77, 0)
+    if case == "mixed":
+        desc = _mixed_desc(rng, 3000, 1 << 22, lo=80, hi=70000)
+        desc["payload_off"] = (rng.integers(0, (1 << 22) - 70016, 3000) & ~15).astype(np.uint64)
+    elif case == "region_starts":
+        desc = _mixed_desc(rng, 2000, 1 << 22)
+        desc["payload_size"] = 4088
+        desc["mask"] = 1
+        desc["mask_key"] = rng.integers(1, 1 << 32, 2000, dtype=np.uint64).astype(np.uint32)
+        desc["payload_off"] = (rng.integers(0, (1 << 22) - 4096, 2000) & ~15).astype(np.uint64)
+    else:
+        desc = _mixed_desc(rng, 200, 1 << 22)
+        desc["payload_size"] = 65536
+        desc["payload_off"] = (rng.integers(0, (1 << 22) - 65536, 200) & ~15).astype(np.uint64)
+    wire, total = check_serialize(payload, desc)
+    if case == "region_starts":
+        assert total == 4096 * 2000
+    exp = wire[:total].copy()
+    for pe in (False, True):
+        cap = total // 2 + 4101
+        got, _, tot, _ = gpu_serialize(payload, desc, capacity=cap, plan_execute=pe)
+        assert tot == total
+        assert np.array_equal(got[:cap], exp[:cap]) and (got[cap:] == 0xEE).all()
+
+
 @pytest.mark.parametrize("align", [16, 64, 4096])
 def test_fused_deserialize_mixed_and_errors(align):
     """The fused deserialize (cfws_deserialize_batch on > 1,024 frames of
