@@ -143,6 +143,8 @@ edge_reasm_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
 #ifndef CFWS_SER_INREG_MAX
 #define CFWS_SER_INREG_MAX 2000
 #endif
+// general_region_ser_edges carries a header as two words: 16-bit lengths
+static_assert(CFWS_SER_INREG_MAX <= 65535, "in-region headers are at most 8 bytes");
 __device__ __forceinline__ bool ser_inreg_frame_ok(uint64_t len, uint32_t payload_off_lo)
 {
     return len >= 80 && len <= CFWS_SER_INREG_MAX && (payload_off_lo & 15u) == 0;

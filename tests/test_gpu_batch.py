@@ -584,19 +584,22 @@ def test_serialize_in_region_edges(n):
     check_serialize(payload, d3, plan_execute=True)
 
 
-@pytest.mark.parametrize("case", ["mixed", "region_starts", "64k"])
+@pytest.mark.parametrize("case", ["mixed", "mixed16k", "mixed64k", "region_starts", "64k"])
 def test_serialize_aligned_large_frames(case):
     """WS serialize of payloads at 16-aligned source offsets past 2,000
     bytes -- the in-region send's bound (CFWS_SER_INREG_MAX) -- where a
     region holding a header is a one- or two-frame region: mixed 80 B-70 KB
-    payloads; 4,088-byte masked payloads (4,096 wire bytes: every frame
-    starts on a region boundary); 64 KiB frames (14-byte headers). Against
+    payloads, and up to 16,000 / 65,535 bytes (16-bit lengths: in-region
+    under a raised bound); 4,088-byte masked payloads (4,096 wire bytes:
+    every frame starts on a region boundary); 64 KiB frames (14-byte
+    headers: always the edge workgroups). Against
     the oracle, whole and cut at a capacity, through both launch forms."""
-    rng = np.random.default_rng({"mixed": 1, "region_starts": 2, "64k": 3}[case])
+    rng = np.random.default_rng({"mixed": 1, "mixed16k": 4, "mixed64k": 5, "region_starts": 2, "64k": 3}[case])
     payload = O.fill_splitmix(1 << 22, 77, 0)
-    if case == "mixed":
-        desc = _mixed_desc(rng, 3000, 1 << 22, lo=80, hi=70000)
-        desc["payload_off"] = (rng.integers(0, (1 << 22) - 70016, 3000) & ~15).astype(np.uint64)
+    if case.startswith("mixed"):
+        hi = {"mixed": 70000, "mixed16k": 16000, "mixed64k": 65535}[case]
+        desc = _mixed_desc(rng, 3000, 1 << 22, lo=80, hi=hi)
+        desc["payload_off"] = (rng.integers(0, (1 << 22) - hi - 16, 3000) & ~15).astype(np.uint64)
     elif case == "region_starts":
         desc = _mixed_desc(rng, 2000, 1 << 22)
         desc["payload_size"] = 4088
