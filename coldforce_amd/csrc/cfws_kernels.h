@@ -807,12 +807,12 @@ __device__ __forceinline__ void general_region_search(const Pass& P, uint32_t f0
 #endif
 
 // WS serialize, in-region edge chunks (`inreg`: the plan found every frame
-// with an 80..2,000-byte payload at a 16-aligned source offset; see
+// with an 80..2,048-byte payload at a 16-aligned source offset; see
 // ser_inreg_frame_ok). Such frames are longer than a chunk, so a chunk that
-// is not inside one body holds exactly one frame's header bytes, with frame
-// j's body tail before them and the header frame's body head after them;
-// and no region holding a boundary is fast_region or two_frame_region (two
-// frames of <= 2,014 wire bytes cannot cover 4 KiB). Each part comes from
+// is not inside one body holds exactly one frame's header bytes (at most 8:
+// 16-bit lengths), with frame j's body tail before them and the header
+// frame's body head after them; and every region holding a header comes
+// here (region_loop sends the one- and two-frame ones too). Each part comes from
 // registers the region already holds: the header words from the frames'
 // views, the body tail from the lane's own source blocks, the body head from
 // the next chunk's first block (that chunk lies inside the same body, whose
