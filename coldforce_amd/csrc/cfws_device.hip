@@ -141,7 +141,7 @@ edge_reasm_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
 // WS serialize's in-region edge chunks (general_region_ser_edges) need every
 // frame's payload at 80..2,000 bytes and 16-aligned in the payload arena.
 #ifndef CFWS_SER_INREG_MAX
-#define CFWS_SER_INREG_MAX 2048
+#define CFWS_SER_INREG_MAX 3584
 #endif
 // general_region_ser_edges carries a header as two words: 16-bit lengths
 static_assert(CFWS_SER_INREG_MAX <= 65535, "in-region headers are at most 8 bytes");

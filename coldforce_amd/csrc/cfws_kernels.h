@@ -807,7 +807,7 @@ __device__ __forceinline__ void general_region_search(const Pass& P, uint32_t f0
 #endif
 
 // WS serialize, in-region edge chunks (`inreg`: the plan found every frame
-// with an 80..2,048-byte payload at a 16-aligned source offset; see
+// with an 80..3,584-byte payload at a 16-aligned source offset; see
 // ser_inreg_frame_ok). Such frames are longer than a chunk, so a chunk that
 // is not inside one body holds exactly one frame's header bytes (at most 8:
 // 16-bit lengths), with frame j's body tail before them and the header
