@@ -139,7 +139,9 @@ edge_reasm_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
 // WS plan kernels
 // ---------------------------------------------------------------------------
 // WS serialize's in-region edge chunks (general_region_ser_edges) need every
-// frame's payload at 80..2,000 bytes and 16-aligned in the payload arena.
+// frame's payload at 80..CFWS_SER_INREG_MAX bytes and 16-aligned in the payload
+// arena (3,584: 2 to 3.5 KiB frames 1.5-8 % faster in-region, 4 KiB 5 % slower;
+// profiles/r04/inreg_bound_ab/).
 #ifndef CFWS_SER_INREG_MAX
 #define CFWS_SER_INREG_MAX 3584
 #endif

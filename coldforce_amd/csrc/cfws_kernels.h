@@ -1257,7 +1257,7 @@ __device__ __forceinline__ void region_loop(const Pass& P, const uint64_t* __res
         constexpr bool kEdges = kInreg && kMode == kModeH2Ser;   // edge chunks in-region
         // the in-region WS send: every region holding a header goes to
         // general_region, whose edge chunks need no frame-size bound
-        // (payloads over 2,000 bytes, CFWS_SER_INREG_MAX, make such regions
+        // (payloads over 2,000 bytes, up to CFWS_SER_INREG_MAX, make such regions
         // one- or two-frame ones)
         constexpr bool kSerGen = kInreg && kMode == kModeSer;
         if (f0 == f1) {
@@ -1353,7 +1353,7 @@ xform_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
     P.sid = sid;
     P.parent = parent;
     // In-region edge chunks (the plan's flag word clear): WS serialize of
-    // 80..2,000-byte frames (the general regions write them) and the fused
+    // 80..3,584-byte frames (the general regions write them) and the fused
     // HTTP/2 send of DATA frames >= kRegion + 32 bytes (the two-frame
     // regions write them): every edge chunk below the tail region.
     const bool inreg = (kMode == kModeSer || kMode == kModeH2Ser) && inreg_flag && *inreg_flag == 0;

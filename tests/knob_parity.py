@@ -95,7 +95,7 @@ def main():
     roundtrip(np.full(20000, 1024), rng, 2, 16, opcodes=np.full(20000, 1), fins=np.ones(20000))
     # 600 K tiny frames: plans of > 2,048 blocks (single-pass unless CFWS_PLAN_SINGLE=0)
     roundtrip(rng.integers(0, 31, 600000), rng, 4, 1)
-    # 80..2,000-byte payloads at 16-aligned offsets: in-region send edge chunks
+    # 80..2,000-byte payloads at 16-aligned offsets (bound 3,584): in-region send edge chunks
     # unless CFWS_SER_INREG=0 or CFWS_EDGE_SPLIT=1 (reduce + apply plan, then
     # the single-pass plan)
     roundtrip(rng.integers(80, 2001, 20000), rng, 5, 16, aligned=True)

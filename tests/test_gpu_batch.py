@@ -546,7 +546,8 @@ def _mixed_desc(rng, n, payload_len, lo=80, hi=2000):
 
 @pytest.mark.parametrize("n", [30_000, 600_000])
 def test_serialize_in_region_edges(n):
-    """WS serialize with in-region edge chunks (every payload 80..2,000 bytes
+    """WS serialize with in-region edge chunks (every payload 80..2,000 bytes,
+    inside the 3,584-byte bound
     at a 16-aligned source offset: general_region_ser_edges writes each edge
     chunk with its segment): both plan forms (30 K frames: reduce + apply;
     600 K: the single-pass plan), masked and unmasked frames, 7- and 16-bit
@@ -584,22 +585,33 @@ def test_serialize_in_region_edges(n):
     check_serialize(payload, d3, plan_execute=True)
 
 
-@pytest.mark.parametrize("case", ["mixed", "mixed16k", "mixed64k", "region_starts", "64k"])
+@pytest.mark.parametrize("case", ["mixed", "mixed3k", "half_regions", "mixed16k", "mixed64k", "region_starts",
+                                  "64k"])
 def test_serialize_aligned_large_frames(case):
     """WS serialize of payloads at 16-aligned source offsets past 2,000
     bytes -- the in-region send's bound (CFWS_SER_INREG_MAX) -- where a
     region holding a header is a one- or two-frame region: mixed 80 B-70 KB
-    payloads, and up to 16,000 / 65,535 bytes (16-bit lengths: in-region
-    under a raised bound); 4,088-byte masked payloads (4,096 wire bytes:
+    payloads, 1,800-3,584 bytes (in-region: one- and two-frame regions
+    through general_region), 2,040-byte masked payloads (2,048 wire bytes:
+    two frames per region, one starting on its boundary), and up to
+    16,000 / 65,535 bytes (16-bit lengths: in-region under a raised
+    CFWS_SER_INREG_MAX); 4,088-byte masked payloads (4,096 wire bytes:
     every frame starts on a region boundary); 64 KiB frames (14-byte
     headers: always the edge workgroups). Against
     the oracle, whole and cut at a capacity, through both launch forms."""
-    rng = np.random.default_rng({"mixed": 1, "mixed16k": 4, "mixed64k": 5, "region_starts": 2, "64k": 3}[case])
+    rng = np.random.default_rng({"mixed": 1, "mixed3k": 6, "half_regions": 7, "mixed16k": 4, "mixed64k": 5,
+                                 "region_starts": 2, "64k": 3}[case])
     payload = O.fill_splitmix(1 << 22, 77, 0)
     if case.startswith("mixed"):
-        hi = {"mixed": 70000, "mixed16k": 16000, "mixed64k": 65535}[case]
-        desc = _mixed_desc(rng, 3000, 1 << 22, lo=80, hi=hi)
+        lo, hi = {"mixed": (80, 70000), "mixed3k": (1800, 3584), "mixed16k": (80, 16000),
+                  "mixed64k": (80, 65535)}[case]
+        desc = _mixed_desc(rng, 3000, 1 << 22, lo=lo, hi=hi)
         desc["payload_off"] = (rng.integers(0, (1 << 22) - hi - 16, 3000) & ~15).astype(np.uint64)
+    elif case == "half_regions":
+        desc = _mixed_desc(rng, 4000, 1 << 22)
+        desc["payload_size"] = 2040                       # 2,048 wire bytes masked: two per region
+        desc["mask"] = 1
+        desc["mask_key"] = rng.integers(1, 1 << 32, 4000, dtype=np.uint64).astype(np.uint32)
     elif case == "region_starts":
         desc = _mixed_desc(rng, 2000, 1 << 22)
         desc["payload_size"] = 4088
@@ -613,6 +625,8 @@ def test_serialize_aligned_large_frames(case):
     wire, total = check_serialize(payload, desc)
     if case == "region_starts":
         assert total == 4096 * 2000
+    if case == "half_regions":
+        assert total == 2048 * 4000
     exp = wire[:total].copy()
     for pe in (False, True):
         cap = total // 2 + 4101
