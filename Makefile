@@ -13,7 +13,14 @@ HDR      := include/cfws.h include/cfws_co_ws_frame.h coldforce_amd/csrc/cfws_in
 LIB      := coldforce_amd/libcfws.so
 OBJDIR   := build
 
-all: $(LIB) oracle examples
+all: $(LIB) oracle examples guard
+
+# test infrastructure: device buffers between unmapped guard ranges
+# (tests/test_gpu_guard.py); host code only, no kernels
+guard: tests/native/libguardmem.so
+
+tests/native/libguardmem.so: tests/native/guardmem.cpp
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $<
 
 # C users of the ABI (no Python): built against include/, linked to libcfws.so
 examples: build/examples/batch_roundtrip
@@ -48,10 +55,10 @@ asm: $(HDR) coldforce_amd/csrc/cfws_kernels.h
 	    -save-temps=obj -Rpass-analysis=kernel-resource-usage 2>> $(OBJDIR)/asm/resource-usage.txt || exit 1; done
 
 clean:
-	rm -rf $(OBJDIR) $(LIB)
+	rm -rf $(OBJDIR) $(LIB) tests/native/libguardmem.so
 	$(MAKE) -s -C oracle clean
 
-.PHONY: all oracle ref asm clean examples
+.PHONY: all oracle ref asm clean examples guard
 
 # A/B build variants of the numeric tunables (kept out of git under build/): make variant V=ser4 F="-DCFWS_SER_LDS=40000"
 variant: $(HDR)

@@ -176,6 +176,55 @@ def cpu_baseline(frame_size: int, seconds: float):
     }
 
 
+def cpu_baseline_h2(frame_size: int, max_frame: int, seconds: float):
+    """Config 5 on this host through the reference compiled in place
+    (oracle/_ref: co_ws_frame.c + co_http2_frame.c + the send split of
+    co_http2_stream.c:933-1013 and the pooling of :550-608, per WS frame; see
+    oracle/cpu_bench.c ref_h2_cpu_bench), swept like cpu_baseline over thread
+    counts up to the cgroup's grant; the main sample on the fastest. None
+    when oracle/_ref was not built."""
+    import oracle
+    if oracle.ref_lib("O2") is None:
+        return None
+    cpus, eff = host_cpus(), effective_cpus()
+
+    def rate(threads, target_s):
+        n = max(256, 64 * threads)
+        oracle.cpu_h2_bench(n, frame_size, max_frame, threads, 1)
+        s1, r1 = oracle.cpu_h2_bench(n, frame_size, max_frame, threads, 2)
+        it = max(1, int(math.ceil(2 * target_s / max(s1 + r1, 1e-3))))
+        if it > 1:
+            s1, r1 = oracle.cpu_h2_bench(n, frame_size, max_frame, threads, it)
+        return n * frame_size * it, s1, r1, it, n
+
+    sweep = []
+    for t in sorted({1, 8, 16, 32, 64, eff, cpus}):
+        if t > cpus or (t > eff and t != cpus):
+            continue
+        p, s1, r1, _, _ = rate(t, 1.5)
+        sweep.append({"threads": t, "gibs": round(2 * p / (s1 + r1) / GIB, 3)})
+    best = max(sweep, key=lambda r: r["gibs"])["threads"]
+    p, s1, r1, iters, n = rate(best, seconds)
+    return {
+        "value": round(2 * p / (s1 + r1) / GIB, 3),
+        "unit": "GiB/s",
+        "cores": best,
+        "kind": "reference",
+        "sample": (f"{n} x {size_label(frame_size)} binary frames x {iters} iters, per WS frame "
+                   f"co_ws_frame_serialize(mask) + DATA frames of <= {max_frame} B through "
+                   f"co_http2_frame.c (send), co_http2_frame_deserialize + pooling + "
+                   f"co_ws_frame_deserialize (receive); reference -O2 (oracle/_ref), {best} threads "
+                   f"(the fastest of the sweep; cgroup grants {eff} of nproc = {cpus}); send and "
+                   f"receive timed as one combined rate"),
+        "send_GiBps": round(p / s1 / GIB, 3),
+        "receive_GiBps": round(p / r1 / GIB, 3),
+        "seconds": round(s1 + r1, 2),
+        "nproc": cpus,
+        "effective_cpus": eff,
+        "scaling_O2": sweep,
+    }
+
+
 def size_label(n: int) -> str:
     """64 KiB, 1 KiB, 256 B, 16376 B: the frame size as the workload names it."""
     return f"{n // 1024} KiB" if n >= 1024 and n % 1024 == 0 else f"{n} B"
@@ -233,35 +282,68 @@ def bench_h2(args, rank, world, dev):
                                                                       back.numel()),
                        dtype=torch.uint8, device=dev)
 
-    def step():
+    def step(ev=None):
+        # ev: the streaming pass of each call timed by events on its stream
+        # (cfws_time_next_pass: recorded right around the xform_kernel launch)
+        if ev:
+            cfws.time_next_pass(ev[0], ev[1])
         cfws.h2_serialize(payload, d_t, wire, h2, 1, S, ws_s, tot)
+        if ev:
+            cfws.time_next_pass(ev[2], ev[3])
         return cfws.h2_deserialize(h2, h2_total, idx_t, pool, back, S, align=1, ws_t=ws_d)
 
     for _ in range(args.warmup):
         step()
+    events = [[cfws.TimingEvent() for _ in range(4)] for _ in range(args.steps)]
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        st, md, ms, ptot, m = step()
+    for k in range(args.steps):
+        st, md, ms, ptot, m = step(events[k])
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
     local = time.perf_counter() - t0
     elapsed = shard.max_over_ranks(local, dev)
+    send_ms = sum(e[0].elapsed_time(e[1]) for e in events) / args.steps
+    recv_ms = sum(e[2].elapsed_time(e[3]) for e in events) / args.steps
+    del events
+    # algorithmic bytes per pass: read the payload n, write n plus every
+    # header (WS + DATA) on the send; the receive reads what the send wrote
+    # past the headers and writes n -- 2n + headers either way
+    alg = F * fs + h2_total
+    kern = {"h2_serialize_pass": {"kernel": "xform_kernel<3>", "ms": round(send_ms, 4),
+                                  "GBps": round(alg / (send_ms * 1e-3) / 1e9, 1)},
+            "h2_deserialize_pass": {"kernel": "xform_kernel<1>", "ms": round(recv_ms, 4),
+                                    "GBps": round(alg / (recv_ms * 1e-3) / 1e9, 1)}}
+    dom = "h2_serialize_pass" if send_ms >= recv_ms else "h2_deserialize_pass"
+    dom_ms = max(send_ms, recv_ms)
+    achieved = alg / (dom_ms * 1e-3) / 1e9
     rows = shard.gather_floats([local, F * fs], dev)
     ok = (m == F and int(ptot.item()) == F * fs and bool((st == 0).all()) and bool((ms == 0).all())
           and torch.equal(back[:F * fs], payload[:F * fs]))
+    ok = shard.sum_over_ranks(1.0 if ok else 0.0, dev) == world
     line = {"metric": "WS-over-HTTP/2 payload GiB/s device-resident (config 5)",
             "value": round(2.0 * F * fs * world * args.steps / elapsed / GIB, 2), "unit": "GiB/s",
-            "n_gpus": world, "steps": args.steps, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
+            "scaling": "weak", "dtype": "u8",
             "config": {"workload": f"config5: {F} binary frames x {fs} B per GPU, client-mask + "
                                    f"HTTP/2 DATA wrap (max frame {S}), then DATA unwrap + pool + "
                                    f"server-unmask", "h2_bytes_per_gpu": h2_total,
                        "data_frames_per_gpu": len(starts)},
+            "roofline": {"bound": "hbm", "kernel": kern[dom]["kernel"], "achieved": round(achieved, 1),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": load_traffic(kern[dom]["kernel"], f"config5:{F}x{fs}"),
+                         "algorithmic_bytes_per_launch": alg, "avg_launch_ms": round(dom_ms, 4)},
+            "kernels": kern,
             "note": "one fused streaming pass per direction: WS frames straight into DATA frames (send), WS payload slices straight out of DATA frames (receive)",
             "per_gpu": per_gpu_rows(rows, args.steps), "verified": ok}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline_h2(fs, S, args.cpu_seconds)
+    else:
+        line["cpu_baseline"] = None
     if rank == 0:
         print(json.dumps(line), flush=True)
     return 0 if ok else 1

@@ -43,7 +43,7 @@ assert DESC_DTYPE.itemsize == 32
 # Every function include/*.h declares (tests check the exports against the
 # headers themselves).
 BATCH_SYMBOLS = (
-    "cfws_init", "cfws_init_device", "cfws_device_copy", "cfws_bind_thread_device", "cfws_thread_device", "cfws_last_error", "cfws_version", "cfws_workspace_size",
+    "cfws_init", "cfws_init_device", "cfws_device_copy", "cfws_time_next_pass", "cfws_bind_thread_device", "cfws_thread_device", "cfws_last_error", "cfws_version", "cfws_workspace_size",
     "cfws_serialize_plan", "cfws_serialize_execute", "cfws_serialize_batch",
     "cfws_deserialize_plan", "cfws_deserialize_execute", "cfws_deserialize_batch",
     "cfws_xor_mask", "cfws_draw_mask_keys", "cfws_draw_mask_keys_seeded",
@@ -135,6 +135,7 @@ def lib(path: str = LIB_PATH) -> C.CDLL:
         "cfws_release_thread_resources": ([], None),
         "cfws_init_device": ([C.c_int], C.c_int),
         "cfws_device_copy": ([_vp, _vp, _u64, _vp], C.c_int),
+        "cfws_time_next_pass": ([_vp, _vp], C.c_int),
         "cfws_bind_thread_device": ([C.c_int], C.c_int),
         "cfws_thread_device": ([], C.c_int),
         "cfws_set_dropin_gpu_min": ([_sz], None),
@@ -481,6 +482,13 @@ def unmask_batch(wire_t, desc_t, status_t, payload_t, max_payload_size: int,
 def xor_mask(src_t, dst_t, n: int, key: int, phase: int = 0, stream=None) -> None:
     _check(lib().cfws_xor_mask(_p(src_t), _p(dst_t), n, key, phase, _stream(stream)),
            "cfws_xor_mask")
+
+
+def time_next_pass(start: "TimingEvent | None", stop: "TimingEvent | None") -> None:
+    """cfws_time_next_pass: the calling thread's next streaming pass records
+    start before and stop after its launch (None, None clears)."""
+    _check(lib().cfws_time_next_pass(start.ev if start else None, stop.ev if stop else None),
+           "cfws_time_next_pass")
 
 
 def device_copy(src_t, dst_t, n: int | None = None, stream=None) -> None:

@@ -5,12 +5,15 @@
 // (co_ws_send, the receive loops, the ws_http2 extension) link against this
 // library unchanged. The payload XOR of a masked frame -- the reference's
 // scalar byte loops at co_ws_frame.c:93-97 and :234-242 -- runs on the
-// MI355X through cfws_xor_mask(); the 2-14 header bytes and the byte-array
-// bookkeeping stay on the calling thread. Unmasked frames are plain copies
-// in the reference too and stay plain copies here. There is no CPU XOR
-// path: without a gfx950 device a masked frame fails (serialize returns
-// false, deserialize CO_WS_ERROR_OUT_OF_MEMORY) and the reason goes to
-// stderr and cfws_last_error().
+// MI355X through cfws_xor_mask() at or above the size policy's threshold
+// (CFWS_DROPIN_GPU_MIN), and on the calling thread below it (the library's
+// own vector loop, host_xor: the reference's per-frame loop, done faster).
+// The 2-14 header bytes and the byte-array bookkeeping stay on the calling
+// thread. Unmasked frames are plain copies in the reference too and stay
+// plain copies here. A frame the policy sends to the device fails without a
+// gfx950 device (serialize returns false, deserialize
+// CO_WS_ERROR_OUT_OF_MEMORY) and the reason goes to stderr and
+// cfws_last_error(); a frame below the threshold never touches HIP.
 #include <hip/hip_runtime.h>
 
 #include <stdio.h>
@@ -39,6 +42,7 @@ size_t g_max_receive_payload_size = 32u * 1024u * 1024u;
 struct ThreadDevice {
     int device = -1;               // the device the stream and buffers belong to
     hipStream_t stream = nullptr;
+    hipEvent_t done_ev = nullptr;  // CFWS_DROPIN_WAIT=block: the frame's completion
     void* buf = nullptr;           // device memory (DMA path)
     size_t cap = 0;
     uint8_t* host = nullptr;       // pinned host memory (zero-copy path)
@@ -271,6 +275,15 @@ double service_life_s()
     return v;
 }
 
+// How long a thread waits for the service's answer before it retires its
+// slot and takes the launch path (CFWS_DROPIN_SERVICE_TIMEOUT_US, default
+// 5 s; tests shorten it to make retirements happen).
+double service_timeout_s()
+{
+    static const double v = env_us("CFWS_DROPIN_SERVICE_TIMEOUT_US", 5e6, 1.0);
+    return v;
+}
+
 double now_s()
 {
     return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
@@ -288,7 +301,11 @@ struct ServiceDevice {
     uint64_t idle_ticks = 0, life_ticks = 0;
     std::atomic<uint64_t> launched{0};     // generation of the last launch
     uint64_t free_slots = ~0ull;           // under mu
-    uint64_t lost_slots = 0;               // given up after a timeout: never reused
+    // given up after a timeout, under mu: a slot comes back once its done
+    // word reaches the seq it was given up at (a later kernel did finish
+    // that request, and nothing is posted on the slot after it)
+    uint64_t lost_slots = 0;
+    uint32_t lost_seq[kCfwsServiceSlots] = {};
     bool failed = false;                   // set-up failed: launch path only
 };
 
@@ -369,9 +386,26 @@ bool service_ensure_running(ServiceDevice& sd, int dev)
     return true;
 }
 
+// Lost slots whose request has since completed go back to the free list
+// (under sd.mu). A kernel stalled behind other work on a shared hardware
+// queue can answer after the 5 s wait: each such stall would otherwise cost
+// a slot for the rest of the process.
+void service_reclaim(ServiceDevice& sd)
+{
+    for (uint64_t m = sd.lost_slots; m; m &= m - 1) {
+        const int s = __builtin_ctzll(m);
+        const uint32_t done = (uint32_t)(__atomic_load_n(&sd.ctl[kCfwsServiceDoneWord + s], __ATOMIC_ACQUIRE) >> 48);
+        if (done == sd.lost_seq[s]) {
+            sd.lost_slots &= ~(1ull << s);
+            sd.free_slots |= 1ull << s;
+        }
+    }
+}
+
 int service_take_slot(ServiceDevice& sd)
 {
     std::lock_guard<std::mutex> lock(sd.mu);
+    if (!sd.free_slots && sd.lost_slots) service_reclaim(sd);
     if (!sd.free_slots) return -1;
     const int s = __builtin_ctzll(sd.free_slots);
     sd.free_slots &= sd.free_slots - 1;
@@ -418,13 +452,16 @@ int service_xor(ThreadDevice& t_dev, int dev, const uint8_t* src, uint8_t* dst, 
             // the kernel may have ended (idle or lifetime) without taking
             // the request: launch the next one
             if (!service_ensure_running(*sd, dev)) return -1;
-            if (now_s() - t0 > 5.0) {
-                // give the slot up for good: the request stays posted, and a
-                // later kernel may still XOR that buffer
-                fprintf(stderr, "cfws: frame service: no answer in 5 s (slot %d given up)\n", s);
+            if (now_s() - t0 > service_timeout_s()) {
+                // give the slot up until its request completes: the request
+                // stays posted, and a later kernel may still XOR that buffer
+                // (service_reclaim returns the slot after that)
+                fprintf(stderr, "cfws: frame service: no answer in %.0f us (slot %d retired)\n",
+                        service_timeout_s() * 1e6, s);
                 {
                     std::lock_guard<std::mutex> lock(sd->mu);
                     sd->lost_slots |= 1ull << s;
+                    sd->lost_seq[s] = seq;
                 }
                 t_dev.svc_slot = -1;
                 return -1;
@@ -440,19 +477,17 @@ std::atomic<bool> g_runtime_up{false};   // the HIP runtime has been initialised
 
 // ---- the size policy --------------------------------------------------------
 // Below CFWS_DROPIN_GPU_MIN bytes (cfws_set_dropin_gpu_min at run time) a
-// masked payload is XORed on the calling thread: a frame that small costs
-// less there than one PCIe round trip to the device (SURVEY.md section 7:
-// the socket-driven per-frame API is latency-bound; profiles/r04_dropin_lat
-// has both sides measured). At or above it, the device paths below run. The
-// policy still needs the device: the first masked frame of the process
-// initialises it, and without a gfx950 agent every masked frame fails, on
-// both sides of the threshold, as before. The batch ABI (include/cfws.h) has
-// no host path at any size.
+// masked payload is XORed on the calling thread: a per-frame call is
+// latency-bound, and the payload would cross PCIe twice (SURVEY.md section 7;
+// DESIGN.md section 6 has wall and CPU time per frame for every path). That
+// path is the library's own loop and needs no device: a frame below the
+// threshold makes no HIP call. At or above it, the device paths below run,
+// and without a gfx950 agent such a frame fails. The batch ABI
+// (include/cfws.h) has no host path at any size.
 std::atomic<size_t> g_gpu_min{[] {
     const char* s = getenv("CFWS_DROPIN_GPU_MIN");
     return s && *s ? (size_t)strtoull(s, nullptr, 10) : (size_t)CFWS_DROPIN_GPU_MIN_DEFAULT;
 }()};
-std::atomic<bool> g_device_ok{false};     // a gfx950 device answered cfws_init
 
 // dst[i] = src[i] ^ key[i % 4] (key byte j = bits 8j..8j+7), 16 bytes per
 // step on two 64-bit words (the compiler keeps them in one SSE register).
@@ -477,19 +512,20 @@ bool device_xor(const uint8_t* src, uint8_t* dst, size_t n, uint32_t key);
 bool payload_xor(const uint8_t* src, uint8_t* dst, size_t n, uint32_t key)
 {
     if (n >= g_gpu_min.load(std::memory_order_relaxed)) return device_xor(src, dst, n, key);
-    if (!g_device_ok.load(std::memory_order_acquire)) {
-        RandomStateGuard keep_random_stream;
-        if (!g_runtime_up.load(std::memory_order_acquire)) keep_random_stream.engage();
-        const int dev = target_device();
-        if ((dev < 0 ? cfws_init() : cfws_init_device(dev)) != CFWS_OK || dev < 0) {
-            fprintf(stderr, "cfws: drop-in has no usable device (%s)\n", cfws_last_error());
-            return false;
-        }
-        g_runtime_up.store(true, std::memory_order_release);
-        g_device_ok.store(true, std::memory_order_release);
-    }
     host_xor(src, dst, n, key);
     return true;
+}
+
+// How the launch path waits for its frame: spinning in hipStreamSynchronize
+// (default), or blocked on an event created with hipEventBlockingSync
+// (CFWS_DROPIN_WAIT=block), which gives the core back while the device works.
+bool wait_blocking()
+{
+    static const bool v = [] {
+        const char* s = getenv("CFWS_DROPIN_WAIT");
+        return s && strcmp(s, "block") == 0;
+    }();
+    return v;
 }
 
 bool device_xor(const uint8_t* src, uint8_t* dst, size_t n, uint32_t key)
@@ -529,7 +565,17 @@ bool device_xor(const uint8_t* src, uint8_t* dst, size_t n, uint32_t key)
         if (cfws_xor_mask(t_dev.buf, t_dev.buf, n, key, 0, st) != CFWS_OK) return false;
         if (hipMemcpyAsync(dst, t_dev.buf, n, hipMemcpyDeviceToHost, st) != hipSuccess) return false;
     }
-    hipError_t e = hipStreamSynchronize(st);
+    hipError_t e;
+    if (wait_blocking()) {
+        if (!t_dev.done_ev && hipEventCreateWithFlags(&t_dev.done_ev, hipEventBlockingSync | hipEventDisableTiming) != hipSuccess) {
+            t_dev.done_ev = nullptr;
+            return false;
+        }
+        e = hipEventRecord(t_dev.done_ev, st);
+        if (e == hipSuccess) e = hipEventSynchronize(t_dev.done_ev);
+    } else {
+        e = hipStreamSynchronize(st);
+    }
     if (e != hipSuccess) {
         fprintf(stderr, "cfws: device XOR failed: %s\n", hipGetErrorString(e));
         return false;
@@ -733,6 +779,7 @@ void cfws_release_thread_resources(void)
     if (t_dev.svc_slot >= 0) service_give_slot(t_dev.device, t_dev.svc_slot);
     if (t_dev.buf) (void)hipFree(t_dev.buf);
     if (t_dev.host) (void)hipHostFree(t_dev.host);
+    if (t_dev.done_ev) (void)hipEventDestroy(t_dev.done_ev);
     if (t_dev.stream) (void)hipStreamDestroy(t_dev.stream);
     t_slot.forget();
 }

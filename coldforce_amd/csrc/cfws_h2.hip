@@ -580,6 +580,10 @@ h2_units_kernel(const cfws_frame_desc_t* __restrict__ pdesc, const int32_t* __re
 }
 
 
+// Messages of at most this many DATA frames in a wave are walked by their own
+// thread; a wave holding a longer one deals its frames out over its lanes.
+constexpr uint64_t kUnitsPerThread = 8;
+
 // deserialize_plan_apply_kernel (one message per thread, no reassembly) and
 // h2_units_kernel in one launch (CFWS_H2_UNITS_MERGED, default): the
 // thread of message m lays it out (payload offset, the capacity rule, the
@@ -641,22 +645,82 @@ h2_msg_apply_units_kernel(cfws_frame_desc_t* __restrict__ mdesc, int32_t* __rest
         }
     }
     if (m == 0) *pass_total = *pooled_p <= pool_cap ? t : 0;
-    // the units of message m's DATA frames
+    // the units of message m's DATA frames [d0, d1)
+    uint64_t d0 = 0, d1 = 0, s_m = 0, next = 0;
     if (m < n_msg) {
-        const uint64_t d0 = first[m], d1 = m + 1 < n_msg ? first[m + 1] : (n_msg < n ? first[n_msg] : n);
-        const uint64_t s_m = starts[m];
-        const uint64_t next = m + 1 < n_msg ? run + v : g;    // where the next unit starts
-        cfws_frame_desc_t u, u1;
-        uint64_t lo = d0 < d1 ? h2_unit_of(pdesc, h2_status, poff, d0, true, s_m, M, ms, g, u) : 0;
-        for (uint64_t d = d0; d < d1; ++d) {
-            const uint64_t hi = d + 1 < d1 ? h2_unit_of(pdesc, h2_status, poff, d + 1, true, s_m, M, ms, g, u1)
-                                           : next;
+        d0 = first[m];
+        d1 = m + 1 < n_msg ? first[m + 1] : (n_msg < n ? first[n_msg] : n);
+        s_m = starts[m];
+        next = m + 1 < n_msg ? run + v : g;                   // where the next unit starts
+    }
+    const uint64_t cnt = d1 - d0;
+    uint64_t wmax = cnt;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        const uint64_t y = __shfl_xor(wmax, o, 64);
+        wmax = y > wmax ? y : wmax;
+    }
+    if (wmax <= kUnitsPerThread) {
+        // short messages (config 5: one or two DATA frames each): each
+        // thread walks its own, one unit computed per frame
+        if (cnt) {
+            cfws_frame_desc_t u, u1;
+            uint64_t lo = h2_unit_of(pdesc, h2_status, poff, d0, true, s_m, M, ms, g, u);
+            for (uint64_t d = d0; d < d1; ++d) {
+                const uint64_t hi = d + 1 < d1 ? h2_unit_of(pdesc, h2_status, poff, d + 1, true, s_m, M, ms, g, u1)
+                                               : next;
+                udesc[d] = u;
+                ustatus[d] = CFWS_PARSE_COMPLETE;
+                uoffs[d] = lo;
+                map_range(lo, hi, d, t, umap);
+                lo = hi;
+                u = u1;
+            }
+        }
+    } else {
+        // a long message in the wave (a multi-MiB message is hundreds to
+        // thousands of DATA frames): the wave's frames are dealt out 64 at a
+        // time over all its lanes, each lane finding its frame's message by a
+        // binary search over the lanes' inclusive counts, that message's
+        // fields over shuffles (one lane walking thousands of
+        // frames serialized the kernel on it)
+        const uint32_t lane = threadIdx.x & 63u;
+        uint64_t inc = cnt;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint64_t y = __shfl_up(inc, o, 64);
+            if (lane >= (uint32_t)o) inc += y;
+        }
+        const uint64_t total = __shfl(inc, 63, 64);
+        const uint64_t exc = inc - cnt;
+        for (uint64_t base = 0; base < total; base += 64) {
+            const uint64_t i = base + lane;
+            int o = 0;
+#pragma unroll
+            for (int step = 32; step >= 1; step >>= 1) {
+                const uint64_t x = __shfl(inc, o + step - 1, 64);
+                if (x <= i) o += step;
+            }
+            // the owner's message, every lane taking part in the shuffles
+            cfws_frame_desc_t Mo = {};
+            Mo.payload_off = __shfl(M.payload_off, o, 64);
+            Mo.payload_size = __shfl(M.payload_size, o, 64);
+            Mo.header_size = (uint8_t)__shfl((int)M.header_size, o, 64);
+            Mo.mask = (uint8_t)__shfl((int)M.mask, o, 64);
+            Mo.mask_key = (uint32_t)__shfl((int)M.mask_key, o, 64);
+            const int32_t mso = __shfl(ms, o, 64);
+            const uint64_t s_o = __shfl(s_m, o, 64), d0o = __shfl(d0, o, 64), d1o = __shfl(d1, o, 64);
+            const uint64_t exo = __shfl(exc, o, 64), nexto = __shfl(next, o, 64);
+            if (i >= total) continue;
+            const uint64_t d = d0o + (i - exo);
+            cfws_frame_desc_t u, u1;
+            const uint64_t lo = h2_unit_of(pdesc, h2_status, poff, d, true, s_o, Mo, mso, g, u);
+            const uint64_t hi = d + 1 < d1o ? h2_unit_of(pdesc, h2_status, poff, d + 1, true, s_o, Mo, mso, g, u1)
+                                            : nexto;
             udesc[d] = u;
             ustatus[d] = CFWS_PARSE_COMPLETE;
             uoffs[d] = lo;
             map_range(lo, hi, d, t, umap);
-            lo = hi;
-            u = u1;
         }
     }
     // frames in no message: empty units at the layout's end

@@ -17,6 +17,14 @@ uint64_t cfws_internal_h2_grand_total_offset(uint64_t n_h2, uint64_t pool_cap, u
 // address dev_dst (cfws_mapped_device_pointer); no mapping check.
 int cfws_internal_copy_out(const void* d_src, void* dev_dst, uint64_t n, void* stream);
 
+// cfws_time_next_pass: the calling thread's pending event pair (hipEvent_t),
+// taken (and cleared) by the next launch_streaming on this thread.
+struct CfwsPassEvents {
+    void* start;
+    void* stop;
+};
+CfwsPassEvents& cfws_internal_pass_events();
+
 // The drop-in's frame service (cfws_ops.hip, used by cfws_frame.cpp): one
 // resident workgroup per device that serves every calling thread of the
 // process. Each thread owns a slot: a request word and a done word in the

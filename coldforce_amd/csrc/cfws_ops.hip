@@ -948,6 +948,12 @@ int launch_payload_xor(const void* src, void* dst, const cfws_frame_desc_t* d_de
 
 }  // namespace
 
+CfwsPassEvents& cfws_internal_pass_events()
+{
+    thread_local CfwsPassEvents e = {nullptr, nullptr};
+    return e;
+}
+
 extern "C" {
 
 int cfws_mask_batch(const void* d_payload, const cfws_frame_desc_t* d_desc, size_t n,
@@ -990,6 +996,14 @@ int cfws_internal_service_launch(uint64_t* dev_ctl, uint8_t* dev_bufs, uint64_t 
     dropin_service_kernel<<<1, kServiceThreads, 0, static_cast<hipStream_t>(stream)>>>(dev_ctl, dev_bufs, gen,
                                                                                      idle_ticks, life_ticks);
     return launch_check("dropin_service");
+}
+
+int cfws_time_next_pass(void* start, void* stop)
+{
+    if ((start == nullptr) != (stop == nullptr))
+        return set_err(CFWS_ERROR_INVALID_ARGUMENT, "start and stop events go together", hipSuccess);
+    cfws_internal_pass_events() = {start, stop};
+    return CFWS_OK;
 }
 
 int cfws_device_copy(const void* d_src, void* d_dst, uint64_t n, void* stream)

@@ -450,6 +450,16 @@ size_t cfws_dropin_gpu_min(void);
  * multiples of 16. */
 int cfws_device_copy(const void* d_src, void* d_dst, uint64_t n, void* stream);
 
+/* ---- profiling ------------------------------------------------------------
+ * The next streaming pass the CALLING THREAD launches (the execute half of
+ * a batch call: xform_kernel with its edge workgroups; the one fused pass of
+ * cfws_h2_serialize_batch / cfws_h2_deserialize_batch) records `start`
+ * (a hipEvent_t) on its stream right before the launch and `stop` right
+ * after it. One pass only, then the pair is cleared; NULL, NULL clears it.
+ * Lets a caller time that one kernel of a multi-kernel call with events
+ * (bench.py's config-5 roofline). */
+int cfws_time_next_pass(void* start, void* stop);
+
 /* ---- synthetic input (bench / tests) -------------------------------------
  * d_dst[i] = byte ((byte_base + i) % 8) of splitmix64 output number
  * (byte_base + i) / 8 for `seed`; byte_base must be a multiple of 8. */

@@ -248,6 +248,27 @@ def cpu_bench(n_frames: int, frame_size: int, threads: int, iters: int, kind: st
     return ms.value, us.value
 
 
+def cpu_h2_bench(n_frames: int, frame_size: int, max_frame: int, threads: int, iters: int,
+                 opt: str = "O2"):
+    """Config 5 on the host through the reference compiled in place
+    (oracle/_ref, ref_h2_cpu_bench): per WS frame co_ws_frame_serialize(mask)
+    + the DATA split of co_http2_stream_send_data through co_http2_frame.c
+    (send), then co_http2_frame_deserialize + the stream's pooling +
+    co_ws_frame_deserialize (receive). Returns (send_s, recv_s)."""
+    L = ref_lib(opt)
+    if L is None:
+        raise FileNotFoundError("oracle/_ref not built")
+    f = L.ref_h2_cpu_bench
+    f.argtypes = [_u64, _u64, C.c_uint32, C.c_int, C.c_int, C.POINTER(C.c_double),
+                  C.POINTER(C.c_double)]
+    f.restype = C.c_int
+    ss, rs = C.c_double(0), C.c_double(0)
+    rc = f(n_frames, frame_size, max_frame, threads, iters, C.byref(ss), C.byref(rs))
+    if rc != 0:
+        raise RuntimeError(f"h2 cpu bench failed rc={rc}")
+    return ss.value, rs.value
+
+
 # ---- the reference itself (oracle/_ref), when built -------------------------
 
 

@@ -206,6 +206,169 @@ int ACCEPT_BENCH_FN(const char* keys, const uint64_t* off, uint64_t n, int threa
     return 0;
 }
 
+#ifdef CFWS_BENCH_REF
+/* ---- WebSocket over HTTP/2 (config 5), reference only -------------------
+ * Per WS frame, the send side of co_http2_stream_send_ws_frame
+ * (co_ws_http2_extension.c:166-199): co_ws_frame_serialize(mask) into a
+ * fresh byte array, then co_http2_stream_send_data's split
+ * (co_http2_stream.c:933-1013: DATA frames of at most max_frame bytes,
+ * END_STREAM on the last) with each DATA frame made by
+ * co_http2_create_data_frame and serialized by co_http2_frame_serialize
+ * (co_http2_frame.c:33-72) into the connection's send bytes (one byte
+ * array per WS frame here; the stream's window assumed open). The receive
+ * side: co_http2_frame_deserialize (co_http2_frame.c:211-300) of each DATA
+ * frame, the stream's data pooling (co_http2_stream.c:550-608: the payload
+ * taken as is when END_STREAM comes with an empty pool, else appended and
+ * NUL-terminated), then co_http2_stream_receive_ws_frame's
+ * co_ws_frame_deserialize (co_ws_http2_extension.c:134-164) and destroy.
+ * All of it the reference's own code, compiled in place. */
+#include <coldforce/http2/co_http2_frame.h>
+
+typedef struct {
+    const uint8_t* payload;
+    uint64_t first, count, frame_size;
+    uint32_t max_frame;
+    co_byte_array_t** wire;
+    volatile uint64_t sink;
+    int fail;
+} h2_job_t;
+
+static void h2_data_frame(const uint8_t* data, uint32_t len, bool end_stream, co_byte_array_t* out)
+{
+    co_http2_frame_t* f = co_http2_create_data_frame(false, end_stream, data, len, NULL, 0);
+    f->header.stream_id = 1;
+    co_http2_frame_serialize(f, out);
+    co_http2_frame_destroy(f);
+}
+
+static double h2_phase(void* (*fn)(void*), h2_job_t* jobs, int threads)
+{
+    pthread_t tid[256];
+    double t0 = bench_now();
+    for (int t = 0; t < threads; ++t) pthread_create(&tid[t], NULL, fn, &jobs[t]);
+    for (int t = 0; t < threads; ++t) pthread_join(tid[t], NULL);
+    return bench_now() - t0;
+}
+
+static void* h2_send_run(void* arg)
+{
+    h2_job_t* j = (h2_job_t*)arg;
+    for (uint64_t i = 0; i < j->count; ++i) {
+        co_byte_array_t* ws = co_byte_array_create();
+        if (!co_ws_frame_serialize(true, 0x2, true, j->payload + (j->first + i) * j->frame_size,
+                                   j->frame_size, ws))
+            j->fail = 1;
+        const uint8_t* p = co_byte_array_get_ptr(ws, 0);
+        const uint32_t total = (uint32_t)co_byte_array_get_count(ws);
+        co_byte_array_t* out = co_byte_array_create();
+        if (total > j->max_frame) {
+            uint32_t index = 0;
+            do {
+                const uint32_t sz = total - index > j->max_frame ? j->max_frame : total - index;
+                h2_data_frame(p + index, sz, index + sz == total, out);
+                index += sz;
+            } while (index < total);
+        } else {
+            h2_data_frame(p, total, true, out);
+        }
+        co_byte_array_destroy(ws);
+        j->wire[i] = out;
+    }
+    return NULL;
+}
+
+static void* h2_recv_run(void* arg)
+{
+    h2_job_t* j = (h2_job_t*)arg;
+    uint64_t s = 0;
+    for (uint64_t i = 0; i < j->count; ++i) {
+        const co_byte_array_t* in = j->wire[i];
+        const size_t n = co_byte_array_get_count(in);
+        size_t idx = 0;
+        co_byte_array_t* pool = NULL;
+        while (idx < n) {
+            co_http2_frame_t* f = co_http2_frame_create();
+            if (co_http2_frame_deserialize(in, &idx, j->max_frame, f) != 0) {
+                j->fail = 1;
+                free(f);
+                break;
+            }
+            if (f->header.flags & CO_HTTP2_FRAME_FLAG_END_STREAM) {
+                uint8_t* ptr;
+                size_t size;
+                if (pool == NULL || co_byte_array_get_count(pool) == 0) {
+                    ptr = f->payload.data.data;
+                    size = f->payload.data.data_length;
+                    f->payload.data.data = NULL;
+                    f->payload.data.data_length = 0;
+                } else {
+                    if (f->payload.data.data_length > 0)
+                        co_byte_array_add(pool, f->payload.data.data, f->payload.data.data_length);
+                    co_byte_array_add(pool, "\0", 1);
+                    size = co_byte_array_get_count(pool) - 1;
+                    ptr = co_byte_array_detach(pool);
+                }
+                co_ws_frame_t* w = co_ws_frame_create();
+                size_t unused = 0;
+                if (co_ws_frame_deserialize(w, ptr, size, &unused) != 0) j->fail = 1;
+                else s += w->payload_data[0];
+                co_ws_frame_destroy(w);
+                free(ptr);
+            } else {
+                if (pool == NULL) pool = co_byte_array_create();
+                if (f->payload.data.data_length > 0)
+                    co_byte_array_add(pool, f->payload.data.data, f->payload.data.data_length);
+            }
+            co_http2_frame_destroy(f);
+        }
+        if (pool) co_byte_array_destroy(pool);
+    }
+    j->sink = s;
+    return NULL;
+}
+
+int ref_h2_cpu_bench(uint64_t n_frames, uint64_t frame_size, uint32_t max_frame, int threads, int iters,
+                     double* send_seconds, double* recv_seconds)
+{
+    if (threads < 1) threads = 1;
+    if (threads > 256) threads = 256;
+    uint8_t* payload = (uint8_t*)malloc(n_frames * frame_size);
+    co_byte_array_t** wire = (co_byte_array_t**)calloc(n_frames, sizeof(*wire));
+    h2_job_t* jobs = (h2_job_t*)calloc((size_t)threads, sizeof(*jobs));
+    if (!payload || !wire || !jobs) return -1;
+    for (uint64_t i = 0; i < n_frames * frame_size; ++i)
+        payload[i] = (uint8_t)(i * 2654435761u >> 13);
+    uint64_t per = n_frames / (uint64_t)threads, rem = n_frames % (uint64_t)threads, at = 0;
+    for (int t = 0; t < threads; ++t) {
+        uint64_t c = per + ((uint64_t)t < rem ? 1 : 0);
+        jobs[t].payload = payload;
+        jobs[t].first = at;
+        jobs[t].count = c;
+        jobs[t].frame_size = frame_size;
+        jobs[t].max_frame = max_frame;
+        jobs[t].wire = wire + at;
+        at += c;
+    }
+    double ss = 0, rs = 0;
+    int fail = 0;
+    for (int it = 0; it < iters; ++it) {
+        ss += h2_phase(h2_send_run, jobs, threads);
+        rs += h2_phase(h2_recv_run, jobs, threads);
+        for (uint64_t i = 0; i < n_frames; ++i) {
+            if (wire[i]) co_byte_array_destroy(wire[i]);
+            wire[i] = NULL;
+        }
+    }
+    for (int t = 0; t < threads; ++t) fail |= jobs[t].fail;
+    free(jobs);
+    free(wire);
+    free(payload);
+    *send_seconds = ss;
+    *recv_seconds = rs;
+    return fail ? -2 : 0;
+}
+#endif
+
 #ifndef CFWS_BENCH_REF
 /* ---- receive-buffer indexing, port only --------------
  * The receive loop's walk over each connection's bytes [begin[c], end[c])

@@ -41,12 +41,14 @@ static void fill(uint8_t* d, size_t n)
 
 #include <time.h>
 
-static double now(void)
+static double clk(clockid_t c)
 {
     struct timespec t;
-    clock_gettime(CLOCK_MONOTONIC, &t);
+    clock_gettime(c, &t);
     return t.tv_sec + 1e-9 * t.tv_nsec;
 }
+
+static double now(void) { return clk(CLOCK_MONOTONIC); }
 
 /* `dropin_link bench SIZE N`: per-frame latency of the drop-in, as a
  * receive/send loop sees it -- N x (co_ws_frame_serialize(mask) into a
@@ -61,24 +63,32 @@ static int bench(size_t size, long n)
         co_byte_array_clear(b);
         if (!co_ws_frame_serialize(true, CO_WS_OPCODE_BINARY, true, data, size, b)) return 2;
     }
-    double ts = 0, td = 0;
+    double ts = 0, td = 0, cs = 0, cd = 0;
+    const double p0 = clk(CLOCK_PROCESS_CPUTIME_ID), w0 = now();
     for (long i = 0; i < n; ++i) {
         co_byte_array_clear(b);
-        const double t0 = now();
+        const double c0 = clk(CLOCK_THREAD_CPUTIME_ID), t0 = now();
         if (!co_ws_frame_serialize(true, CO_WS_OPCODE_BINARY, true, data, size, b)) return 2;
-        const double t1 = now();
+        const double c1 = clk(CLOCK_THREAD_CPUTIME_ID), t1 = now();
         co_ws_frame_t* f = co_ws_frame_create();
         size_t index = 0;
         const int r = co_ws_frame_deserialize(f, co_byte_array_get_ptr(b, 0), co_byte_array_get_count(b),
                                               &index);
-        const double t2 = now();
+        const double c2 = clk(CLOCK_THREAD_CPUTIME_ID), t2 = now();
+        cs += c1 - c0;
+        cd += c2 - c1;
         if (r != CO_WS_PARSE_COMPLETE || memcmp(co_ws_frame_get_payload_data(f), data, size) != 0) return 3;
         co_ws_frame_destroy(f);
         ts += t1 - t0;
         td += t2 - t1;
     }
-    printf("{\"frame_bytes\": %zu, \"frames\": %ld, \"serialize_us\": %.2f, \"deserialize_us\": %.2f}\n",
-           size, n, 1e6 * ts / n, 1e6 * td / n);
+    /* wall time, the calling thread's CPU time, and the whole process's CPU
+     * time per frame (the HIP runtime's own threads included) */
+    const double pc = clk(CLOCK_PROCESS_CPUTIME_ID) - p0, wall = now() - w0;
+    printf("{\"frame_bytes\": %zu, \"frames\": %ld, \"serialize_us\": %.2f, \"deserialize_us\": %.2f, "
+           "\"serialize_cpu_us\": %.2f, \"deserialize_cpu_us\": %.2f, \"process_cpu_us_per_pair\": %.2f, "
+           "\"wall_us_per_pair\": %.2f}\n",
+           size, n, 1e6 * ts / n, 1e6 * td / n, 1e6 * cs / n, 1e6 * cd / n, 1e6 * pc / n, 1e6 * wall / n);
     co_byte_array_destroy(b);
     free(data);
     return 0;

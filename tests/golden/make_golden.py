@@ -414,9 +414,15 @@ def handshake_cases(R):
 
 def small_batches(R):
     # the bench's payload / key seeds (bench.py PAYLOAD_SEED, KEY_SEED);
-    # 1 KiB as TEXT (config 1's frames), 256 B as BINARY
+    # 1 KiB as TEXT (config 1's frames), 256 B as BINARY; the in-region
+    # send's range (payloads up to 3,584 B, round 4): 2 KiB and 3 KiB batches
+    # of 4 GiB as the bench runs them (bench.py --frame-size: 4 GiB // size
+    # frames), and payloads of exactly the bound
     return [small_batch_digest(R, 4 << 20, 1024, 0x5EED0002, 2, 1),
-            small_batch_digest(R, 16 << 20, 256, 0x5EED0002, 2, 2)]
+            small_batch_digest(R, 16 << 20, 256, 0x5EED0002, 2, 2),
+            small_batch_digest(R, (4 << 30) // 2048, 2048, 0x5EED0002, 2, 2),
+            small_batch_digest(R, (4 << 30) // 3072, 3072, 0x5EED0002, 2, 2),
+            small_batch_digest(R, (4 << 30) // 3584, 3584, 0x5EED0002, 2, 1)]
 
 
 def main():

@@ -126,6 +126,7 @@ def main():
         T2.test_gpu_h2_roundtrip_random(16384)
         T2.test_gpu_h2_deserialize_headers_across_data_frames(13)
         T2.test_gpu_h2_rows_past_message_count_are_empty(2)
+        T2.test_gpu_h2_long_messages(1000)
     # a small batch (single-launch path unless CFWS_SMALL=0)
     roundtrip(np.full(256, 1000), rng, 3, 16)
     # fragments + pings, reassembled (two passes, pass-1 capped grid)

@@ -124,14 +124,36 @@ def test_dropin_host_paths_without_device():
 
 @pytest.mark.skipif(gpu_present(), reason="checks the no-device behaviour")
 def test_no_cpu_fallback():
+    """No gfx950 device: the batch API fails, and so does every masked frame
+    the drop-in's size policy sends to the device. A frame below the
+    policy's threshold is the library's own calling-thread loop (host_xor,
+    not the oracle) and needs no device (VERDICT r4 #7): it runs, bit-exact."""
     from coldforce_amd import cfws
-    assert cfws.lib().cfws_init() == -4          # CFWS_ERROR_NO_DEVICE
+    L = cfws.lib()
+    assert L.cfws_init() == -4          # CFWS_ERROR_NO_DEVICE
     with pytest.raises(cfws.CodecError):
         cfws.init()
-    ok, _ = cfws.frame_serialize(True, 2, True, b"x" * 100)   # masked: needs the device
-    assert not ok
-    w = O.serialize_keyed(True, 2, True, 0x11223344, b"x" * 100)
-    assert cfws.frame_deserialize(w)["rc"] == -7006
+    saved = L.cfws_dropin_gpu_min()
+    data = bytes(range(256)) * 4 + b"xyz"
+    try:
+        L.cfws_set_dropin_gpu_min(0)                               # every frame: device
+        ok, _ = cfws.frame_serialize(True, 2, True, b"x" * 100)
+        assert not ok
+        w = O.serialize_keyed(True, 2, True, 0x11223344, b"x" * 100)
+        assert cfws.frame_deserialize(w)["rc"] == -7006
+        L.cfws_set_dropin_gpu_min(len(data) + 1)                   # below: calling thread
+        ok, wire = cfws.frame_serialize(True, 2, True, data)
+        assert ok
+        key = int.from_bytes(wire[4:8], "little")                  # 126..65535: 2 + 2 B, key
+        assert wire == O.serialize_keyed(True, 2, True, key, data)
+        r = cfws.frame_deserialize(wire)
+        assert r["rc"] == 0 and r["payload"] == data + b"\0"
+        L.cfws_set_dropin_gpu_min(len(data))                       # at the threshold: device
+        ok, _ = cfws.frame_serialize(True, 2, True, data)
+        assert not ok
+        assert cfws.frame_deserialize(wire)["rc"] == -7006
+    finally:
+        L.cfws_set_dropin_gpu_min(saved)
 
 
 def test_link_level_dropin_fails_loudly_without_device():
@@ -143,7 +165,14 @@ def test_link_level_dropin_fails_loudly_without_device():
     exe = os.path.join(O.HERE, "_ref", "dropin_link")
     if not os.path.exists(exe):
         pytest.skip("oracle/_ref/dropin_link not built (needs /root/reference)")
-    r = subprocess.run([exe, "77"], capture_output=True, text=True, timeout=60)
+    env = dict(os.environ, CFWS_DROPIN_GPU_MIN="0")
+    r = subprocess.run([exe, "77"], capture_output=True, text=True, timeout=60, env=env)
     assert r.returncode == 2
     assert "serialize failed size=1 mask=1" in r.stdout
     assert "no HIP device" in r.stderr or "gfx950" in r.stderr
+    # the default size policy: frames below the threshold run on the calling
+    # thread without a device; the first masked frame at or above it fails
+    env["CFWS_DROPIN_GPU_MIN"] = "65536"
+    r = subprocess.run([exe, "77"], capture_output=True, text=True, timeout=60, env=env)
+    assert r.returncode == 2
+    assert "serialize failed size=65536 mask=1" in r.stdout

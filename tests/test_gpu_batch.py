@@ -319,10 +319,14 @@ def _sha_device(t: "torch.Tensor", n: int) -> str:
     return h.hexdigest()
 
 
-@pytest.mark.parametrize("which", [0, 1], ids=["4M_x_1KiB_text", "16M_x_256B_binary"])
+@pytest.mark.parametrize("which", [0, 1, 2, 3, 4],
+                         ids=["4M_x_1KiB_text", "16M_x_256B_binary", "2M_x_2KiB_binary",
+                              "1398101_x_3KiB_binary", "1198372_x_3584B_text"])
 def test_small_frame_reference_digests(which):
-    """The small-frame batches the bench quotes (4,194,304 x 1 KiB TEXT and
-    16,777,216 x 256 B BINARY, the bench's seeds) through the bench's own
+    """The small-frame batches the bench quotes (4,194,304 x 1 KiB TEXT,
+    16,777,216 x 256 B BINARY, and the in-region send's range: 2,097,152 x
+    2 KiB, 1,398,101 x 3 KiB and 1,198,372 x 3,584 B -- the bound itself --
+    every one 4 GiB of payload at the bench's seeds) through the bench's own
     calls: serialize plan + execute (single-pass look-back plan, in-region
     send edges) and deserialize plan + execute at 16-byte slots. The wire's
     SHA-256 equals the reference's co_ws_frame_serialize output

@@ -408,3 +408,43 @@ def test_service_idle_gap_keeps_random_stream():
         time.sleep(0.02)                                 # > CFWS_DROPIN_SERVICE_IDLE_US (2 ms)
     O.srandom(Lo, 4321)
     assert got == [O.ref_serialize(Lo, True, 2, True, d) for d in datas]
+
+
+def test_service_retired_slots_come_back():
+    """A thread whose service answer does not come within the timeout retires
+    its slot (the request stays posted; a later kernel may still XOR that
+    buffer) and sends the frame through the launch path. Once the request
+    completes the slot returns to the pool (before, each such
+    stall lost a slot for good, and after 64 every frame took the launch
+    path). With a 1 us timeout nearly every service frame retires its slot:
+    more than 64 retirements in one process can only happen if slots come
+    back, and every frame still equals the reference's."""
+    import os
+    import subprocess
+    import sys
+    script = r"""
+import ctypes, sys
+sys.path.insert(0, sys.argv[1])
+import oracle as O
+from coldforce_amd import cfws
+cfws.init()
+L = cfws.lib(); L.cfws_set_dropin_gpu_min(0)
+libc = ctypes.CDLL(None); Lo = O.lib()
+data = bytes(range(256)) * 4
+for k in range(400):
+    libc.srandom(k)
+    ok, w = cfws.frame_serialize(True, 2, True, data)
+    O.srandom(Lo, k)
+    assert ok and w == O.ref_serialize(Lo, True, 2, True, data), k
+    r = cfws.frame_deserialize(w)
+    assert r["rc"] == 0 and r["payload"] == data + b"\0", k
+print("ok")
+"""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, CFWS_DROPIN_SERVICE_TIMEOUT_US="1")
+    r = subprocess.run([sys.executable, "-c", script, root], capture_output=True, text=True,
+                       timeout=120, env=env)
+    assert r.returncode == 0 and "ok" in r.stdout, (r.stdout[-2000:], r.stderr[-2000:])
+    retired = r.stderr.count("retired")
+    print("retirements", retired)
+    assert retired > 64, r.stderr[-2000:]

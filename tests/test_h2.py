@@ -268,6 +268,33 @@ def test_gpu_h2_roundtrip_random(S):
 
 @pytest.mark.gpu
 @pytest.mark.skipif(not gpu_present(), reason="needs the MI355X")
+@pytest.mark.parametrize("S", [16384, 1000])
+def test_gpu_h2_long_messages(S):
+    """Messages of 1-4 MiB (64-256 DATA frames each at 16,384, 1,000-4,000 at
+    1,000) between runs of short ones: the receive's merged layout + units
+    kernel deals a long message's DATA frames out over the wave's lanes
+    (ADVICE r4), and the short runs keep the per-thread walk; against the
+    oracle, with a capacity cut through a long message, and the two-launch
+    form (CFWS_H2_UNITS_MERGED=0) in tests/knob_parity.py."""
+    rng = random.Random(S + 77)
+    payload = O.fill_splitmix(5 << 20, 77, 0)
+    d = []
+    for i in range(90):
+        if i % 9 == 4:
+            sz = rng.choice([1 << 20, 3 << 20, (4 << 20) - 14, rng.randrange(1 << 20, 4 << 20)])
+        else:
+            sz = rng.choice([0, 5, 126, 999, 16376, 20000])
+        d.append((rng.randrange(0, (5 << 20) - sz), 0, sz, rng.getrandbits(32), 1,
+                  rng.choice([1, 2]), rng.random() < .8, 0))
+    d = np.array(d, dtype=O.DESC_DTYPE)
+    h2, _ = O.h2_serialize_batch(payload, d, 1, S)
+    index = O.h2_index(h2)
+    check_h2_deserialize(h2, index, S=S)
+    check_h2_deserialize(h2, index, S=S, align=1, payload_cap=len(h2) // 2)
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not gpu_present(), reason="needs the MI355X")
 @pytest.mark.parametrize("S", [5, 13, 64])
 def test_gpu_h2_deserialize_headers_across_data_frames(S):
     """DATA frames smaller than the WS header (max_frame_size 5 / 13) put a

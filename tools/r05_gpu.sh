@@ -1,0 +1,76 @@
+#!/bin/bash
+# Round-5 GPU session: parity suite, benches, kernel stats, PMC passes.
+# Each GPU step has its own time limit; a fault, abort, segfault or time
+# limit (rc 124/134/137/139 or > 128) ends the script; a plain test failure
+# (rc 1) does not.
+# usage: tools/r05_gpu.sh TAG STEP...   (steps: pytest bench split c5 fs1k config1 kstats pmc list)
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp
+R=$GRAFT_REPO_ROOT
+TAG=$1; shift
+OUT=$R/gpurun_out/$TAG
+mkdir -p "$OUT"
+step() {  # name limit cmd...
+  local name=$1 lim=$2; shift 2
+  echo "== $name $(date +%T)"
+  timeout -k 10 "$lim" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc $(date +%T)"
+  tail -3 "$OUT/$name.log"
+  if [ $rc -ge 124 ] || [ $rc -gt 128 ]; then echo "STOP after $name (rc=$rc)"; exit $rc; fi
+  # a device fault reported as a Python exception (rc 1): stop too
+  if grep -q -E "illegal memory access|Memory access fault|hipErrorIllegalAddress|HSA_STATUS_ERROR" "$OUT/$name.log"; then
+    echo "STOP after $name (device fault)"; exit 3
+  fi
+  return 0
+}
+pmc() {  # name workload-args... ; counters in $C
+  step "pmc_$1" 120 rocprofv3 --pmc $C --output-format csv -d "$OUT/pmc_$1" -o pmc -- python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline "${@:2}"
+}
+for s in "$@"; do
+  case $s in
+    pytest) step pytest 900 python3 -u -m pytest $R/tests -m gpu -x -v --timeout 300 --timeout-method thread ;;
+    guard) step guard 600 python3 -u -m pytest $R/tests/test_gpu_guard.py -m gpu -x -v --timeout 300 --timeout-method thread ;;
+    digests) step digests 600 python3 -u -m pytest $R/tests/test_gpu_batch.py -m gpu -x -v -k small_frame_reference_digests --timeout 300 --timeout-method thread ;;
+    pyk) step pyk_$(echo "$K" | tr -c 'a-zA-Z0-9' _) 900 python3 -u -m pytest $(for f in $TESTS; do echo $R/tests/$f; done) -m gpu -x -v -k "$K" --timeout 300 --timeout-method thread ;;
+    pytest_sub) step pytest_sub 900 python3 -u -m pytest $(for f in $TESTS; do echo $R/tests/$f; done) -m gpu -x -v --timeout 300 --timeout-method thread ;;
+    bench) step bench 400 python3 $R/bench.py ;;
+    split) step split 200 python3 $R/bench.py --workload split --no-cpu-baseline ;;
+    c5) step c5 200 python3 $R/bench.py --workload config5 --no-cpu-baseline ;;
+    c3) step c3 200 python3 $R/bench.py --workload config3 --no-cpu-baseline ;;
+    fs256) step fs256 200 python3 $R/bench.py --frames 16777216 --frame-size 256 --no-cpu-baseline ;;
+    kstats_fs256) step kstats_fs256 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kstats_fs256" -o ks -- python3 $R/bench.py --frames 16777216 --frame-size 256 --steps 10 --warmup 3 --no-cpu-baseline ;;
+    fs1k) step fs1k 200 python3 $R/bench.py --frames 4194304 --frame-size 1024 --no-cpu-baseline ;;
+    config1) step config1 400 python3 $R/tools/config1_bench.py --out "$OUT/config1.jsonl" --reps 2 ;;
+    dropin) step dropin 400 env TAG=$TAG bash $R/tools/dropin_lat.sh ;;
+    kstats) step kstats 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kstats" -o ks -- python3 $R/bench.py --steps 10 --warmup 3 --no-cpu-baseline ;;
+    kstats_c5) step kstats_c5 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kstats_c5" -o ks -- python3 $R/bench.py --workload config5 --steps 10 --warmup 3 --no-cpu-baseline ;;
+    kstats_fs1k) step kstats_fs1k 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kstats_fs1k" -o ks -- python3 $R/bench.py --frames 4194304 --frame-size 1024 --steps 10 --warmup 3 --no-cpu-baseline ;;
+    kstats_split) step kstats_split 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kstats_split" -o ks -- python3 $R/bench.py --workload split --steps 10 --warmup 3 --no-cpu-baseline ;;
+    knobs_fused) step knobs_fused 600 python3 -u -m pytest $R/tests/test_knobs.py -m gpu -x -v -k FUSED --timeout 300 --timeout-method thread ;;
+    envab_fs1k) step envab_fs1k 600 env TAG=$TAG/envab_fs1k ARGS="--frames 4194304 --frame-size 1024" bash $R/tools/envab.sh ;;
+    envab_fs256) step envab_fs256 600 env TAG=$TAG/envab_fs256 ARGS="--frames 16777216 --frame-size 256" bash $R/tools/envab.sh ;;
+    kstats_staged) step kstats_staged 200 env CFWS_FUSED_DESER=2 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kstats_staged" -o ks -- python3 $R/bench.py --frames 4194304 --frame-size 1024 --steps 10 --warmup 3 --no-cpu-baseline ;;
+    list) step list 60 rocprofv3 -L ;;
+    prof_c2) step prof_c2 400 env TAG=$TAG/prof_c2 bash $R/tools/profile.sh ;;
+    prof_fs1k) step prof_fs1k 400 env TAG=$TAG/prof_fs1k ARGS="--frames 4194304 --frame-size 1024" bash $R/tools/profile.sh ;;
+    prof_fs256) step prof_fs256 400 env TAG=$TAG/prof_fs256 ARGS="--frames 16777216 --frame-size 256" bash $R/tools/profile.sh ;;
+    ab) step ab 600 env TAG=$TAG/ab bash $R/tools/ab.sh ;;
+    ab_fs1k) step ab_fs1k 600 env TAG=$TAG/ab_fs1k ARGS="--frames 4194304 --frame-size 1024" bash $R/tools/ab.sh ;;
+    ab_fs256) step ab_fs256 600 env TAG=$TAG/ab_fs256 ARGS="--frames 16777216 --frame-size 256" bash $R/tools/ab.sh ;;
+    envab) step envab 600 env TAG=$TAG/envab bash $R/tools/envab.sh ;;
+    pmc_c5ab)
+      for v in 1 0; do
+        step pmc_c5ab_wr$v 120 env CFWS_H2_INREG=$v rocprofv3 --pmc TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum --output-format csv -d "$OUT/pmc_c5ab_wr$v" -o pmc -- python3 $R/bench.py --workload config5 --steps 2 --warmup 1 --no-cpu-baseline
+        step pmc_c5ab_sq$v 120 env CFWS_H2_INREG=$v rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_BUSY_CYCLES --output-format csv -d "$OUT/pmc_c5ab_sq$v" -o pmc -- python3 $R/bench.py --workload config5 --steps 2 --warmup 1 --no-cpu-baseline
+      done ;;
+    pmc)
+      C="SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_BUSY_CYCLES"
+      pmc sq_c2 && pmc sq_c5 --workload config5
+      C="TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum"
+      pmc tcc_c2 && pmc tcc_c5 --workload config5
+      C="TCP_TCC_WRITE_REQ_sum TCP_TCC_READ_REQ_sum GRBM_GUI_ACTIVE GRBM_COUNT"
+      pmc tcp_c2 && pmc tcp_c5 --workload config5 ;;
+  esac
+done
+echo "== done $(date +%T)"
