@@ -42,7 +42,6 @@ size_t g_max_receive_payload_size = 32u * 1024u * 1024u;
 struct ThreadDevice {
     int device = -1;               // the device the stream and buffers belong to
     hipStream_t stream = nullptr;
-    hipEvent_t done_ev = nullptr;  // CFWS_DROPIN_WAIT=block: the frame's completion
     void* buf = nullptr;           // device memory (DMA path)
     size_t cap = 0;
     uint8_t* host = nullptr;       // pinned host memory (zero-copy path)
@@ -478,12 +477,14 @@ std::atomic<bool> g_runtime_up{false};   // the HIP runtime has been initialised
 // ---- the size policy --------------------------------------------------------
 // Below CFWS_DROPIN_GPU_MIN bytes (cfws_set_dropin_gpu_min at run time) a
 // masked payload is XORed on the calling thread: a per-frame call is
-// latency-bound, and the payload would cross PCIe twice (SURVEY.md section 7;
-// DESIGN.md section 6 has wall and CPU time per frame for every path). That
-// path is the library's own loop and needs no device: a frame below the
-// threshold makes no HIP call. At or above it, the device paths below run,
-// and without a gfx950 agent such a frame fails. The batch ABI
-// (include/cfws.h) has no host path at any size.
+// latency-bound, and the payload would cross PCIe twice.
+// DESIGN.md section 6 has wall and CPU time per frame for every path: the
+// calling thread wins both at every size measured (125 B - 4 MiB), so the
+// default threshold is SIZE_MAX and the device paths below are opt-in. The
+// host path is the library's own loop and needs no device: a frame below the
+// threshold makes no HIP call. At or above it the device paths run, and
+// without a gfx950 agent such a frame fails. The batch ABI (include/cfws.h)
+// has no host path at any size.
 std::atomic<size_t> g_gpu_min{[] {
     const char* s = getenv("CFWS_DROPIN_GPU_MIN");
     return s && *s ? (size_t)strtoull(s, nullptr, 10) : (size_t)CFWS_DROPIN_GPU_MIN_DEFAULT;
@@ -516,17 +517,7 @@ bool payload_xor(const uint8_t* src, uint8_t* dst, size_t n, uint32_t key)
     return true;
 }
 
-// How the launch path waits for its frame: spinning in hipStreamSynchronize
-// (default), or blocked on an event created with hipEventBlockingSync
-// (CFWS_DROPIN_WAIT=block), which gives the core back while the device works.
-bool wait_blocking()
-{
-    static const bool v = [] {
-        const char* s = getenv("CFWS_DROPIN_WAIT");
-        return s && strcmp(s, "block") == 0;
-    }();
-    return v;
-}
+
 
 bool device_xor(const uint8_t* src, uint8_t* dst, size_t n, uint32_t key)
 {
@@ -565,17 +556,9 @@ bool device_xor(const uint8_t* src, uint8_t* dst, size_t n, uint32_t key)
         if (cfws_xor_mask(t_dev.buf, t_dev.buf, n, key, 0, st) != CFWS_OK) return false;
         if (hipMemcpyAsync(dst, t_dev.buf, n, hipMemcpyDeviceToHost, st) != hipSuccess) return false;
     }
-    hipError_t e;
-    if (wait_blocking()) {
-        if (!t_dev.done_ev && hipEventCreateWithFlags(&t_dev.done_ev, hipEventBlockingSync | hipEventDisableTiming) != hipSuccess) {
-            t_dev.done_ev = nullptr;
-            return false;
-        }
-        e = hipEventRecord(t_dev.done_ev, st);
-        if (e == hipSuccess) e = hipEventSynchronize(t_dev.done_ev);
-    } else {
-        e = hipStreamSynchronize(st);
-    }
+    // (a wait blocked on a hipEventBlockingSync event instead measured the
+    // same calling-thread CPU time as this spin)
+    hipError_t e = hipStreamSynchronize(st);
     if (e != hipSuccess) {
         fprintf(stderr, "cfws: device XOR failed: %s\n", hipGetErrorString(e));
         return false;
@@ -779,7 +762,6 @@ void cfws_release_thread_resources(void)
     if (t_dev.svc_slot >= 0) service_give_slot(t_dev.device, t_dev.svc_slot);
     if (t_dev.buf) (void)hipFree(t_dev.buf);
     if (t_dev.host) (void)hipHostFree(t_dev.host);
-    if (t_dev.done_ev) (void)hipEventDestroy(t_dev.done_ev);
     if (t_dev.stream) (void)hipStreamDestroy(t_dev.stream);
     t_slot.forget();
 }

@@ -431,16 +431,21 @@ int cfws_bind_thread_device(int device);
 int cfws_thread_device(void);
 
 /* Size policy of the drop-in co_ws_frame_* calls (cfws_frame.cpp). A masked
- * payload of fewer than `bytes` bytes is XORed on the calling thread, where
- * one small frame costs less than a round trip to the device (SURVEY.md §7:
- * the per-frame path is latency-bound; DESIGN.md §6.2 has the measured
- * crossover); larger payloads run on the device. The policy never runs
- * without the device: the first masked frame initialises it, and with no
- * gfx950 agent every masked frame fails at any size. Default
- * CFWS_DROPIN_GPU_MIN_DEFAULT, or the CFWS_DROPIN_GPU_MIN environment
- * variable read at load; 0 sends every masked frame to the device.
+ * payload of fewer than `bytes` bytes is XORed on the calling thread by the
+ * library's own vector loop; payloads of `bytes` or more go to the device
+ * (the frame service up to 32 KiB, a launch per frame above). Measured per
+ * frame on the MI355X box, the calling thread is faster
+ * at every size from 125 B to 4 MiB and spends less CPU time: a per-frame
+ * device call copies the payload into and out of pinned staging on the
+ * calling thread and waits on PCIe, and its wait spins (or, blocked on an
+ * event, cost as much thread CPU time). So the default keeps every frame on
+ * the calling thread and the device is opt-in: CFWS_DROPIN_GPU_MIN_DEFAULT
+ * is SIZE_MAX; the CFWS_DROPIN_GPU_MIN environment variable (read at load)
+ * or this call sets another threshold, 0 sends every masked frame to the
+ * device. A frame below the threshold makes no HIP call and needs no
+ * device; a frame at or above it fails without a gfx950 agent.
  * Process-wide. The batch ABI above has no host path at any size. */
-#define CFWS_DROPIN_GPU_MIN_DEFAULT 65536
+#define CFWS_DROPIN_GPU_MIN_DEFAULT ((size_t)-1)
 void cfws_set_dropin_gpu_min(size_t bytes);
 size_t cfws_dropin_gpu_min(void);
 

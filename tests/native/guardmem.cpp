@@ -122,7 +122,14 @@ int guard_free(uint64_t ptr)
     if (e != hipSuccess) return fail("hipDeviceSynchronize", e);
     if ((e = hipMemUnmap(g.mapped, g.mapped_n)) != hipSuccess) return fail("hipMemUnmap", e);
     if ((e = hipMemRelease(g.h)) != hipSuccess) return fail("hipMemRelease", e);
-    if ((e = hipMemAddressFree(g.base, g.reserved)) != hipSuccess) return fail("hipMemAddressFree", e);
+    // The address range stays reserved for the rest of the process: on this
+    // stack (ROCm 7.2, gfx950) a range freed with hipMemAddressFree and handed
+    // out again by the next hipMemAddressReserve, with new memory mapped
+    // under it, was read by kernels through the old translation -- a
+    // serialize read a stale payload (the wire came out as key bytes over a
+    // constant) while hipMemcpy of the same range read the new bytes
+    // (tools/guard_debug.py --free, profiles/r05/guard_debug.txt). Never
+    // reusing a range keeps every buffer's first kernel on fresh addresses.
     return 0;
 }
 

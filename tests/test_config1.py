@@ -113,14 +113,24 @@ def test_stock_wire_is_deterministic(tmp_path):
 
 
 @pytest.mark.skipif(__import__("conftest").gpu_present(), reason="checks the no-device behaviour")
-def test_dropin_build_fails_loudly_without_device():
-    """No GPU: the drop-in build's first masked frame fails (co_ws_send
-    ignores the false return, co_ws_client.c:445-449, so nothing is sent) and
-    the client never completes; libcfws says why on stderr."""
+@pytest.mark.parametrize("gpu_min", ["0", None], ids=["device_policy", "default_policy"])
+def test_dropin_build_without_device(gpu_min):
+    """No GPU. With every masked frame sent to the device
+    (CFWS_DROPIN_GPU_MIN=0) the drop-in build's first masked frame fails
+    (co_ws_send ignores the false return, co_ws_client.c:445-449, so nothing
+    is sent), the client never completes, and libcfws says why on stderr.
+    Under the default size policy config 1's 1 KiB frames are below the
+    threshold: the library's own calling-thread loop masks them with no
+    device, and the echo completes."""
     _need("cfws")
-    # run the client against a stock server so only the client needs the device
+    # run the client against a stock server so only the client uses the drop-in
+    import os
     import subprocess
     from echo_util import BUILDS, _read_line
+    env = dict(os.environ)
+    env.pop("CFWS_DROPIN_GPU_MIN", None)
+    if gpu_min is not None:
+        env["CFWS_DROPIN_GPU_MIN"] = gpu_min
     port = free_port()
     srv = subprocess.Popen([BUILDS["stock"], "ws-server", str(port)], stdout=subprocess.PIPE,
                            stderr=subprocess.PIPE)
@@ -128,13 +138,16 @@ def test_dropin_build_fails_loudly_without_device():
         assert '"listening"' in _read_line(srv, 30)
         try:
             cli = subprocess.run([BUILDS["cfws"], "ws-client", f"ws://127.0.0.1:{port}/", "4", "1024", "1", "1"],
-                                 capture_output=True, text=True, timeout=5)
+                                 capture_output=True, text=True, timeout=5 if gpu_min else 30, env=env)
             out, err = cli.stdout, cli.stderr
         except subprocess.TimeoutExpired as e:
             out = (e.stdout or b"").decode() if isinstance(e.stdout, bytes) else (e.stdout or "")
             err = (e.stderr or b"").decode() if isinstance(e.stderr, bytes) else (e.stderr or "")
-        assert '"received": 4' not in out
-        assert "no HIP device" in err or "gfx950" in err or "usable device" in err
+        if gpu_min is not None:
+            assert '"received": 4' not in out
+            assert "no HIP device" in err or "gfx950" in err or "usable device" in err
+        else:
+            assert '"received": 4' in out, (out, err)
     finally:
         srv.kill()
         srv.wait(timeout=10)

@@ -314,16 +314,18 @@ def test_size_policy_both_sides():
     """The drop-in's size policy (cfws_set_dropin_gpu_min): payloads below the
     threshold are XORed on the calling thread, at or above it on the device;
     the wire and the decoded payloads equal the reference's on both sides,
-    at the default threshold and at moved ones (0: all device; huge: all
-    host), for sizes around the 16-byte step and the threshold itself."""
+    at the default threshold (SIZE_MAX: the calling thread at every size,
+    the measured winner on wall and CPU time) and at
+    moved ones (0: all device; 1000 and 65,536: both sides), for sizes
+    around the 16-byte step and the thresholds themselves."""
     import ctypes
     libc = ctypes.CDLL(None)
     L = cfws.lib()
     Lo = O.lib()
     default = L.cfws_dropin_gpu_min()
-    assert default == 65536
+    assert default == (1 << 64) - 1          # SIZE_MAX: every frame on the calling thread
     rng = random.Random(12)
-    for gmin in (default, 0, 1000, 1 << 40):
+    for gmin in (default, 0, 1000, 65536):
         L.cfws_set_dropin_gpu_min(gmin)
         for n in (1, 3, 15, 16, 17, 999, 1000, 1001, 4096, 65535, 65536, 65537, 300000):
             data = rng.randbytes(n)

@@ -332,7 +332,8 @@ def test_guard_h2_roundtrip(guards):
 
 def test_guard_index_frames(guards):
     payload, desc = _seed21_batch(26)
-    wire, total = O.serialize_batch(payload, desc.view(O.DESC_DTYPE))
+    wire, _ = O.serialize_batch(payload, desc.view(O.DESC_DTYPE))
+    total = len(wire)
     buf = guards(total).upload(wire)
     cuts = [0, 1000, 50_000, 120_000, total]
     begin = torch.tensor(cuts[:-1], dtype=torch.int64, device="cuda")

@@ -7,17 +7,15 @@
 #   launch   launch + synchronise per frame (CFWS_DROPIN_SERVICE=0: zero-copy
 #            up to 1 MiB)
 #   dma      H2D + kernel + D2H (CFWS_DROPIN_ZC_MAX=0)
-#   launch_block / dma_block: the same, the thread blocked on an event
-#            (CFWS_DROPIN_WAIT=block) instead of spinning
 # Each line has wall and CPU time per frame (the calling thread's, and the
 # process's per serialize + deserialize pair).
-# The crossover of `host` with the best device path is the size policy's
-# threshold (CFWS_DROPIN_GPU_MIN_DEFAULT).
+# The size policy's default (CFWS_DROPIN_GPU_MIN_DEFAULT) follows from these:
+# `host` wins on wall and on CPU time at every size.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 OUT=gpurun_out/${TAG:-dropin}
 mkdir -p "$OUT"
-for mode in ${MODES:-host service launch dma launch_block dma_block}; do
+for mode in ${MODES:-host service launch dma}; do
   for size in ${SIZES:-125 1024 4096 16384 32768 65536 262144 1048576 4194304}; do
     n=4000; [ $size -ge 262144 ] && n=300; [ $size -ge 4194304 ] && n=60
     case $mode in
@@ -25,8 +23,6 @@ for mode in ${MODES:-host service launch dma launch_block dma_block}; do
       service) env="CFWS_DROPIN_GPU_MIN=0 CFWS_DROPIN_SERVICE_MAX=65536" ;;
       launch) env="CFWS_DROPIN_GPU_MIN=0 CFWS_DROPIN_SERVICE=0" ;;
       dma) env="CFWS_DROPIN_GPU_MIN=0 CFWS_DROPIN_SERVICE=0 CFWS_DROPIN_ZC_MAX=0" ;;
-      launch_block) env="CFWS_DROPIN_GPU_MIN=0 CFWS_DROPIN_SERVICE=0 CFWS_DROPIN_WAIT=block" ;;
-      dma_block) env="CFWS_DROPIN_GPU_MIN=0 CFWS_DROPIN_SERVICE=0 CFWS_DROPIN_ZC_MAX=0 CFWS_DROPIN_WAIT=block" ;;
     esac
     [ $mode = service ] && [ $size -gt 65536 ] && continue
     line=$(env $env timeout -k 10 120 oracle/_ref/dropin_link bench $size $n) || exit 1
