@@ -37,6 +37,8 @@ for s in "$@"; do
     bench) step bench 400 python3 $R/bench.py ;;
     split) step split 200 python3 $R/bench.py --workload split --no-cpu-baseline ;;
     c5) step c5 200 python3 $R/bench.py --workload config5 --no-cpu-baseline ;;
+    c5cpu) step c5cpu 300 python3 $R/bench.py --workload config5 ;;
+    prof_c5) step prof_c5 600 env TAG=$TAG/prof_c5 ARGS="--workload config5" bash $R/tools/profile.sh ;;
     c3) step c3 200 python3 $R/bench.py --workload config3 --no-cpu-baseline ;;
     fs256) step fs256 200 python3 $R/bench.py --frames 16777216 --frame-size 256 --no-cpu-baseline ;;
     kstats_fs256) step kstats_fs256 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kstats_fs256" -o ks -- python3 $R/bench.py --frames 16777216 --frame-size 256 --steps 10 --warmup 3 --no-cpu-baseline ;;
