@@ -713,27 +713,30 @@ def main():
     tot_ser = torch.zeros(1, dtype=torch.int64, device=dev)
     tot_de = torch.zeros(1, dtype=torch.int64, device=dev)
 
-    # batches of small frames (<= 512 B of wire per frame on average, no
-    # reassembly) deserialize in one call: cfws_deserialize_batch runs the
-    # fused plan + copy kernel there (deserialize_plan_single_kernel<true>),
-    # so the timed kernel is that launch; other batches plan, then execute
+    # Each direction is one batch call (cfws_serialize_batch,
+    # cfws_deserialize_batch), and the timed kernel is the call's streaming
+    # pass, bracketed by events the library records right around its launch
+    # (cfws_time_next_pass): the execute kernel after the plan, or for
+    # batches of small frames (<= 512 B of wire per frame, no reassembly) the
+    # fused plan + copy kernel of the receive,
+    # deserialize_plan_single_kernel<true>
     fused_de = (flags == 0 and F > 1024 and os.environ.get("CFWS_FUSED_DESER", "1") != "0"
                 and wire_total // F <= int(os.environ.get("CFWS_FUSED_AVG_MAX", "512")))  # fused_avg_max()
 
     def step(ev=None):
-        cfws.serialize_plan(desc_ser, wire.numel(), tot_ser, ws_ser)
-        if ev: ev[0].record()
-        cfws.serialize_execute(payload, desc_ser, wire, ws_ser)
-        if ev: ev[1].record()
-        if fused_de:
-            if ev: ev[2].record()
-            cfws.deserialize(wire, wire_total, index, back, desc_de, status, ws_de, tot_de, align=16)
-        else:
+        if ev: cfws.time_next_pass(ev[0], ev[1])
+        cfws.serialize(payload, desc_ser, wire, ws_ser, tot_ser)
+        if flags:
+            # reassembly: two streaming passes (data frames, then control
+            # frames), timed together after the plan
             cfws.deserialize_plan(wire, wire_total, index, desc_de, status, back.numel(), tot_de,
                                   ws_de, align=16, flags=flags)
             if ev: ev[2].record()
             cfws.deserialize_execute(wire, desc_de, status, back, ws_de, flags=flags)
-        if ev: ev[3].record()
+            if ev: ev[3].record()
+        else:
+            if ev: cfws.time_next_pass(ev[2], ev[3])
+            cfws.deserialize(wire, wire_total, index, back, desc_de, status, ws_de, tot_de, align=16)
 
     for _ in range(args.warmup):
         step()

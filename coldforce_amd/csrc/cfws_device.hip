@@ -1240,10 +1240,15 @@ int cfws_deserialize_batch(const void* d_wire, uint64_t wire_size, const uint64_
         const uint32_t sb = grid_for(n, uint64_t(kThreads) * kFusedItems);
         if (hipMemsetAsync(look, 0, look_bytes(sb), st) != hipSuccess)
             return launch_check("deserialize_batch(fused)");
+        CfwsPassEvents& pe = cfws_internal_pass_events();
+        const CfwsPassEvents timed = pe;
+        pe = {nullptr, nullptr};
+        if (timed.start) (void)hipEventRecord(static_cast<hipEvent_t>(timed.start), st);
         deserialize_plan_single_kernel<true><<<sb, kThreads, 0, st>>>(
             static_cast<const uint8_t*>(d_wire), wire_size, d_index, nullptr, n, max_payload, align, d_desc,
             d_status, nullptr, look, ws_ptr<uint64_t>(ws, L.hdr), cap, nullptr, d_total,
             static_cast<uint8_t*>(d_payload));
+        if (timed.stop) (void)hipEventRecord(static_cast<hipEvent_t>(timed.stop), st);
         return launch_check("deserialize_batch(fused)");
     }
     if (int rc = cfws_deserialize_plan(d_wire, wire_size, d_index, n, max_payload, align, flags,

@@ -457,8 +457,10 @@ int cfws_device_copy(const void* d_src, void* d_dst, uint64_t n, void* stream);
 
 /* ---- profiling ------------------------------------------------------------
  * The next streaming pass the CALLING THREAD launches (the execute half of
- * a batch call: xform_kernel with its edge workgroups; the one fused pass of
- * cfws_h2_serialize_batch / cfws_h2_deserialize_batch) records `start`
+ * a batch call: xform_kernel with its edge workgroups; the fused plan +
+ * copy kernel of cfws_deserialize_batch for batches of small frames; the
+ * one fused pass of cfws_h2_serialize_batch /
+ * cfws_h2_deserialize_batch) records `start`
  * (a hipEvent_t) on its stream right before the launch and `stop` right
  * after it. One pass only, then the pair is cleared; NULL, NULL clears it.
  * Lets a caller time that one kernel of a multi-kernel call with events

@@ -32,7 +32,7 @@ for s in "$@"; do
     pytest) step pytest 900 python3 -u -m pytest $R/tests -m gpu -x -v --timeout 300 --timeout-method thread ;;
     guard) step guard 600 python3 -u -m pytest $R/tests/test_gpu_guard.py -m gpu -x -v --timeout 300 --timeout-method thread ;;
     digests) step digests 600 python3 -u -m pytest $R/tests/test_gpu_batch.py -m gpu -x -v -k small_frame_reference_digests --timeout 300 --timeout-method thread ;;
-    pyk) step pyk_$(echo "$K" | tr -c 'a-zA-Z0-9' _) 900 python3 -u -m pytest $(for f in $TESTS; do echo $R/tests/$f; done) -m gpu -x -v -k "$K" --timeout 300 --timeout-method thread ;;
+    pyk) step pyk_$(echo "$K" | tr -c 'a-zA-Z0-9' _ | cut -c1-60) 900 python3 -u -m pytest $(for f in $TESTS; do echo $R/tests/$f; done) -m gpu -x -v -k "$K" --timeout 300 --timeout-method thread ;;
     pytest_sub) step pytest_sub 900 python3 -u -m pytest $(for f in $TESTS; do echo $R/tests/$f; done) -m gpu -x -v --timeout 300 --timeout-method thread ;;
     bench) step bench 400 python3 $R/bench.py ;;
     split) step split 200 python3 $R/bench.py --workload split --no-cpu-baseline ;;
@@ -42,6 +42,8 @@ for s in "$@"; do
     c3) step c3 200 python3 $R/bench.py --workload config3 --no-cpu-baseline ;;
     fs256) step fs256 200 python3 $R/bench.py --frames 16777216 --frame-size 256 --no-cpu-baseline ;;
     kstats_fs256) step kstats_fs256 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kstats_fs256" -o ks -- python3 $R/bench.py --frames 16777216 --frame-size 256 --steps 10 --warmup 3 --no-cpu-baseline ;;
+    fs2k) step fs2k 200 python3 $R/bench.py --frames 2097152 --frame-size 2048 --no-cpu-baseline ;;
+    fs3k) step fs3k 200 python3 $R/bench.py --frames 1398101 --frame-size 3072 --no-cpu-baseline ;;
     fs1k) step fs1k 200 python3 $R/bench.py --frames 4194304 --frame-size 1024 --no-cpu-baseline ;;
     config1) step config1 400 python3 $R/tools/config1_bench.py --out "$OUT/config1.jsonl" --reps 2 ;;
     dropin) step dropin 400 env TAG=$TAG bash $R/tools/dropin_lat.sh ;;
