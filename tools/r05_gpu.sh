@@ -37,6 +37,8 @@ for s in "$@"; do
     bench) step bench 400 python3 $R/bench.py ;;
     split) step split 200 python3 $R/bench.py --workload split --no-cpu-baseline ;;
     c5) step c5 200 python3 $R/bench.py --workload config5 --no-cpu-baseline ;;
+    e2e) for w in config2 config3 config5; do step e2e_$w 400 python3 $R/bench_e2e.py --workload $w; done
+         step e2e_config5_64k 400 python3 $R/bench_e2e.py --workload config5 --frame-size 65536 ;;
     c5cpu) step c5cpu 300 python3 $R/bench.py --workload config5 ;;
     prof_c5) step prof_c5 600 env TAG=$TAG/prof_c5 ARGS="--workload config5" bash $R/tools/profile.sh ;;
     c3) step c3 200 python3 $R/bench.py --workload config3 --no-cpu-baseline ;;
