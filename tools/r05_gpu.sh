@@ -55,6 +55,12 @@ for s in "$@"; do
     kstats_split) step kstats_split 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kstats_split" -o ks -- python3 $R/bench.py --workload split --steps 10 --warmup 3 --no-cpu-baseline ;;
     knobs_fused) step knobs_fused 600 python3 -u -m pytest $R/tests/test_knobs.py -m gpu -x -v -k FUSED --timeout 300 --timeout-method thread ;;
     envab_fs1k) step envab_fs1k 600 env TAG=$TAG/envab_fs1k ARGS="--frames 4194304 --frame-size 1024" bash $R/tools/envab.sh ;;
+    envab_fs3k) step envab_fs3k 900 env TAG=$TAG/envab_fs3k ARGS="--frames 1398101 --frame-size 3072" bash $R/tools/envab.sh ;;
+    envab_fs1k2) step envab_fs1k2 900 env TAG=$TAG/envab_fs1k ARGS="--frames 4194304 --frame-size 1024" bash $R/tools/envab.sh ;;
+    envab_fs2k) step envab_fs2k 900 env TAG=$TAG/envab_fs2k ARGS="--frames 2097152 --frame-size 2048" bash $R/tools/envab.sh ;;
+    envab_fs4k) step envab_fs4k 900 env TAG=$TAG/envab_fs4k ARGS="--frames 1048576 --frame-size 4096" bash $R/tools/envab.sh ;;
+    envab_fs8k) step envab_fs8k 900 env TAG=$TAG/envab_fs8k ARGS="--frames 524288 --frame-size 8192" bash $R/tools/envab.sh ;;
+    envab_c3) step envab_c3 900 env TAG=$TAG/envab_c3 WL=config3 bash $R/tools/envab.sh ;;
     envab_fs256) step envab_fs256 600 env TAG=$TAG/envab_fs256 ARGS="--frames 16777216 --frame-size 256" bash $R/tools/envab.sh ;;
     kstats_staged) step kstats_staged 200 env CFWS_FUSED_DESER=2 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kstats_staged" -o ks -- python3 $R/bench.py --frames 4194304 --frame-size 1024 --steps 10 --warmup 3 --no-cpu-baseline ;;
     list) step list 60 rocprofv3 -L ;;
