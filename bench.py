@@ -52,6 +52,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="target CPU time of the cpu_baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--recv-slots", action="store_true",
+                    help="config2: receive into fixed payload slots of frame-size bytes "
+                         "(cfws_deserialize_slots) instead of the packed layout")
     ap.add_argument("--keys", type=int, default=1 << 20, help="accept workload: client keys per GPU")
     ap.add_argument("--connections", type=int, default=16384, help="index workload: connections")
     ap.add_argument("--index-mib", type=int, default=1024, help="index workload: receive-buffer MiB")
@@ -720,7 +723,10 @@ def main():
     # batches of small frames (<= 512 B of wire per frame, no reassembly) the
     # fused plan + copy kernel of the receive,
     # deserialize_plan_single_kernel<true>
-    fused_de = (flags == 0 and F > 1024 and os.environ.get("CFWS_FUSED_DESER", "1") != "0"
+    slot = W.round16(max(fs, 16)) if args.recv_slots else 0
+    if slot and (flags or slot != fs):
+        sys.exit("bench.py: --recv-slots needs config2 with a frame size that is a multiple of 16")
+    fused_de = (not slot and flags == 0 and F > 1024 and os.environ.get("CFWS_FUSED_DESER", "1") != "0"
                 and wire_total // F <= int(os.environ.get("CFWS_FUSED_AVG_MAX", "512")))  # fused_avg_max()
 
     def step(ev=None):
@@ -736,7 +742,10 @@ def main():
             if ev: ev[3].record()
         else:
             if ev: cfws.time_next_pass(ev[2], ev[3])
-            cfws.deserialize(wire, wire_total, index, back, desc_de, status, ws_de, tot_de, align=16)
+            if slot:
+                cfws.deserialize_slots(wire, wire_total, index, back, slot, desc_de, status, tot_de)
+            else:
+                cfws.deserialize(wire, wire_total, index, back, desc_de, status, ws_de, tot_de, align=16)
 
     for _ in range(args.warmup):
         step()
@@ -794,9 +803,11 @@ def main():
     achieved = alg_bytes / (dom_ms * 1e-3) / 1e9
     kernel_symbol = ("xform_kernel<0>" if dom_name == "serialize_execute"   # kModeSer
                      else "deserialize_plan_single_kernel<true>" if fused_de  # fused plan + copy
+                     else "deserialize_slots_window_kernel" if 0 < slot <= 992  # fixed slots
+                     else "deserialize_slots_kernel" if slot
                      else "xform_kernel<1>")                                 # kModeDeser
     # the PMC summary a traffic figure may come from: the same workload only
-    traffic_key = (f"config2:{F}x{fs}" if args.workload == "config2" else
+    traffic_key = (f"config2:{F}x{fs}" + (":slots" if slot else "") if args.workload == "config2" else
                    "config3" if args.workload == "config3" else f"config4:{F}x{fs}")
     rows = shard.gather_floats([local, arena_bytes, ser_ms, de_ms, alg_bytes], dev)
     total_payload = 2.0 * sum(r[1] for r in rows) * args.steps
@@ -816,6 +827,8 @@ def main():
         "config": {
             "workload": (f"config2: {F} binary frames x {size_label(fs)} per GPU, client-mask "
                          f"(serialize) then server-unmask (deserialize), device resident"
+                         + (f"; the receive into fixed {slot} B payload slots (cfws_deserialize_slots)"
+                            if slot else "")
                          if args.workload == "config2" else
                          f"config4: shard {rank} of 8 of the 8 M x 64 KiB batch ({F} frames, "
                          f"64 GiB per GPU), client-mask then server-unmask, device resident"

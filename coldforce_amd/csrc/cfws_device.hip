@@ -468,6 +468,7 @@ struct FusedChunk {
     uint32_t need, nbytes, key;
 };
 
+template <int kUnroll = kFusedUnroll>
 __device__ __forceinline__ void fused_item(const uint8_t* __restrict__ wire, uint8_t* __restrict__ out,
                                            uint64_t total, uint64_t run, uint64_t src, uint32_t len,
                                            uint32_t nb, uint32_t key, uint32_t lane)
@@ -486,12 +487,12 @@ __device__ __forceinline__ void fused_item(const uint8_t* __restrict__ wire, uin
         uint32_t G = 1;
         while (G * 16 < m) G <<= 1;
         const uint32_t P = 64 / G, g = lane / G, c = lane % G;
-        for (uint32_t r0 = 0; r0 < G; r0 += kFusedUnroll) {
-            uint4 A[kFusedUnroll], E[kFusedUnroll];
-            FusedChunk q[kFusedUnroll];
-            bool nl[kFusedUnroll];
+        for (uint32_t r0 = 0; r0 < G; r0 += kUnroll) {
+            uint4 A[kUnroll], E[kUnroll];
+            FusedChunk q[kUnroll];
+            bool nl[kUnroll];
 #pragma unroll
-            for (int u = 0; u < kFusedUnroll; ++u) {
+            for (int u = 0; u < kUnroll; ++u) {
                 const uint32_t r = r0 + u;
                 const int fl = (int)((r < G ? r : 0) * P + g);
                 const uint64_t runj = __shfl(run, fl, 64), srcj = __shfl(src, fl, 64);
@@ -509,7 +510,7 @@ __device__ __forceinline__ void fused_item(const uint8_t* __restrict__ wire, uin
                            ? ld16(wire + (q[u].s & ~uint64_t(15)) + 16) : z;
             }
 #pragma unroll
-            for (int u = 0; u < kFusedUnroll; ++u) {
+            for (int u = 0; u < kUnroll; ++u) {
                 const uint4 nb4 = from_next_lane(A[u], E[u]);      // every lane: DPP needs the full wave
                 if (!q[u].nbytes) continue;
                 const uint32_t ph = (uint32_t)(q[u].s & 15u);
@@ -532,12 +533,12 @@ __device__ __forceinline__ void fused_item(const uint8_t* __restrict__ wire, uin
         const uint64_t lenj = (uint32_t)__builtin_amdgcn_readlane((int)len, j);
         const uint32_t kj = (uint32_t)__shfl((int)key, j, 64);
         const uint32_t ph = (uint32_t)(srcj & 15u);
-        for (uint64_t c0 = 0; c0 < nbj; c0 += 64 * 16 * kFusedUnroll) {
-            uint4 A[kFusedUnroll], E[kFusedUnroll];
-            uint32_t need[kFusedUnroll];
-            bool nl[kFusedUnroll];
+        for (uint64_t c0 = 0; c0 < nbj; c0 += 64 * 16 * kUnroll) {
+            uint4 A[kUnroll], E[kUnroll];
+            uint32_t need[kUnroll];
+            bool nl[kUnroll];
 #pragma unroll
-            for (int u = 0; u < kFusedUnroll; ++u) {
+            for (int u = 0; u < kUnroll; ++u) {
                 const uint64_t k0 = c0 + (uint64_t)u * 1024 + 16 * lane;
                 need[u] = k0 < lenj ? (uint32_t)(lenj - k0 < 16 ? lenj - k0 : 16) : 0u;
                 nl[u] = lane != 63 && k0 + 16 < lenj;
@@ -546,7 +547,7 @@ __device__ __forceinline__ void fused_item(const uint8_t* __restrict__ wire, uin
                 E[u] = need[u] && ph && !nl[u] && ph + need[u] > 16 ? ld16(wire + (s & ~uint64_t(15)) + 16) : z;
             }
 #pragma unroll
-            for (int u = 0; u < kFusedUnroll; ++u) {
+            for (int u = 0; u < kUnroll; ++u) {
                 const uint4 nb4 = from_next_lane(A[u], E[u]);
                 const uint64_t k0 = c0 + (uint64_t)u * 1024 + 16 * lane;
                 if (k0 >= nbj) continue;
@@ -730,6 +731,191 @@ bool fused_deser()
 uint64_t fused_avg_max()
 {
     static const uint64_t v = (uint64_t)env_knob("CFWS_FUSED_AVG_MAX", 512);
+    return v;
+}
+
+// ---------------------------------------------------------------------------
+// fixed payload slots (cfws_deserialize_slots)
+// ---------------------------------------------------------------------------
+// Frame i's payload goes to slot i (payload_off = i * slot): no prefix, so
+// no look-back, and the pass reads each wire line once. The packed receive
+// cannot: a frame's destination needs every earlier header, so its header
+// line is fetched by the parse and again by the copy (§9: 6.86 GB per
+// 16 M x 256 B launch against 4.43 GB of wire).
+//
+// Slots of at most kSlotWindowMax bytes (deserialize_slots_window_kernel):
+// G = slot / 16 + 2 lanes per frame load the frame's window -- the 16-byte
+// block holding its first byte and the G - 1 after it (block phase <= 15
+// plus header <= 14 plus payload <= slot bytes) -- one block each, P = 64 / G
+// frames per wave-round. A wave takes R rounds (R P <= 64 frames) per
+// iteration: lane l loads frame l's index, every round's window block is
+// issued at once together with each frame's 16 header bytes (one unaligned
+// load, lane = frame: the same lines as the windows, in flight together, so
+// HBM sees them once), each lane parses its frame and writes its descriptor
+// and status (consecutive lanes, consecutive entries), and each round then
+// takes its frames' (length, header end, key) from the parsing lanes. A
+// lane's 16 payload bytes start (phase + header) bytes into its own block:
+// blocks c and c + 1 of the group, or c + 1 and c + 2 past 16 (DPP shifts by
+// one lane, no LDS), funnelled and unmasked (each chunk starts at a payload
+// index that is a multiple of 16: no key rotation). Blocks at or past the
+// wire's end are not loaded. The first form parsed in every lane of every
+// round (480 instructions per 3 frames at 256 B) and ran at 5.2 TB/s.
+constexpr uint64_t kSlotWindowMax = 64 * 16 - 32;   // 992: G <= 64
+// Rounds per iteration (their loads in flight together): 8 for one frame per
+// round (slots over 480 B), 4 for more (16 M x 256 B receive 1.686 -> 1.620
+// ms; 12 or 16 rounds: 3.3 ms; 8 M x 512 B at 4 rounds 1.59 -> 1.76 ms).
+#ifndef CFWS_SLOT_ROUNDS
+#define CFWS_SLOT_ROUNDS 8
+#endif
+#ifndef CFWS_SLOT_ROUNDS_MULTI
+#define CFWS_SLOT_ROUNDS_MULTI 4
+#endif
+
+__device__ __forceinline__ uint64_t shfl64(uint64_t v, int src)
+{
+    return (uint64_t)__shfl((long long)v, src, 64);
+}
+
+// The slot rule: a COMPLETE frame whose non-empty payload is longer than the
+// slot, or ends past the capacity, gets CFWS_ERROR_OUT_OF_MEMORY (the
+// reference's failed allocation, co_ws_frame.c:216-223); its slot is not
+// written.
+__device__ __forceinline__ int32_t slot_rule(int32_t st, uint64_t run, uint64_t ps, uint64_t slot, uint64_t cap)
+{
+    return st == CFWS_PARSE_COMPLETE && ps > 0 && (ps > slot || run + ps > cap) ? CFWS_ERROR_OUT_OF_MEMORY : st;
+}
+
+__device__ __forceinline__ void slot_desc(cfws_frame_desc_t* desc, int32_t* status, uint64_t f, uint64_t run,
+                                          const cfws_frame_desc_t& d, int32_t st)
+{
+    uint4* q = reinterpret_cast<uint4*>(desc + f);
+    const uint64_t w3 = (uint64_t)d.mask_key | (uint64_t)d.fin << 32 | (uint64_t)d.opcode << 40 |
+                        (uint64_t)d.mask << 48 | (uint64_t)d.header_size << 56;
+    q[0] = make_uint4((uint32_t)run, (uint32_t)(run >> 32), (uint32_t)d.wire_off, (uint32_t)(d.wire_off >> 32));
+    q[1] = make_uint4((uint32_t)d.payload_size, (uint32_t)(d.payload_size >> 32), (uint32_t)w3,
+                      (uint32_t)(w3 >> 32));
+    status[f] = st;
+}
+
+template <int kSlotRounds>
+__global__ void __launch_bounds__(kThreads)
+deserialize_slots_window_kernel(const uint8_t* __restrict__ wire, uint64_t wire_size,
+                                const uint64_t* __restrict__ index, uint64_t n, uint64_t max_payload,
+                                uint64_t slot, uint32_t G, cfws_frame_desc_t* __restrict__ desc,
+                                int32_t* __restrict__ status, uint8_t* __restrict__ out, uint64_t capacity,
+                                uint64_t* __restrict__ user_total)
+{
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t P = 64u / G, g = lane / G, c = lane - g * G;
+    const uint32_t R = P * kSlotRounds <= 64 ? (uint32_t)kSlotRounds : 64u / P;
+    const uint64_t FI = uint64_t(R) * P;                 // frames per wave-iteration
+    const uint64_t stride = uint64_t(gridDim.x) * kWaves * FI;
+    const uint4 z = make_uint4(0, 0, 0, 0);
+    const bool b16 = wire_size >= 16;
+    const uint64_t lastu = wire_size - 16;
+    for (uint64_t f0 = (uint64_t(blockIdx.x) * kWaves + (threadIdx.x >> 6)) * FI; f0 < n; f0 += stride) {
+        const uint64_t fl = f0 + lane;
+        const bool mine = lane < FI && fl < n;
+        const uint64_t wl = mine ? index[fl] : ~uint64_t(0);
+        // every round's window block, then each frame's header bytes
+        uint4 A[kSlotRounds];
+#pragma unroll
+        for (int u = 0; u < kSlotRounds; ++u) {
+            const uint32_t src = (uint32_t)u * P + g;
+            const uint64_t wo = shfl64(wl, (int)(src < 64 ? src : 63));
+            const uint64_t blk = (wo & ~uint64_t(15)) + 16ull * c;
+            A[u] = (uint32_t)u < R && g < P && wo < wire_size && blk < wire_size ? ld16(wire + blk) : z;
+        }
+        const uint4 hw = mine && b16 && wl <= lastu ? ld16u(wire + wl) : z;
+        // lane l parses frame f0 + l; its round info: payload length (<= slot
+        // < 2^16) | (phase + header size) << 16, zero when not copied
+        uint32_t info = 0, key = 0;
+        if (mine) {
+            cfws_frame_desc_t d;
+            int32_t st;
+            if (b16 && wl <= lastu) {
+                const uint32_t w[4] = {hw.x, hw.y, hw.z, hw.w};
+                st = parse_ws_header_regs(w, wire_size - wl, max_payload, d);
+                d.wire_off = wl;
+            } else {
+                st = parse_ws_header(wire, wire_size, wl, max_payload, d);
+            }
+            const uint64_t run = fl * slot;
+            st = slot_rule(st, run, d.payload_size, slot, capacity);
+            slot_desc(desc, status, fl, run, d, st);
+            if (fl == n - 1 && user_total) {
+                const uint64_t t = n * slot;
+                *user_total = t < capacity ? t : capacity;
+            }
+            if (st == CFWS_PARSE_COMPLETE && d.payload_size > 0)
+                info = (uint32_t)d.payload_size | ((uint32_t)(wl & 15u) + d.header_size) << 16;
+            key = d.mask ? d.mask_key : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < kSlotRounds; ++u) {
+            if ((uint32_t)u >= R) break;   // wave-uniform
+            const uint32_t src = (uint32_t)u * P + g;
+            const int s = (int)(src < 64 ? src : 63);
+            const uint32_t inf = (uint32_t)__shfl((int)info, s, 64);
+            const uint32_t k = (uint32_t)__shfl((int)key, s, 64);
+            const uint32_t len = inf & 0xffffu, off = inf >> 16;
+            // blocks c + 1 and c + 2 of the window, by DPP (every lane)
+            const uint4 n1 = from_next_lane(A[u], z);
+            const uint4 n2 = from_next_lane(n1, z);
+            if (g < P && 16u * c < len) {
+                const bool k1 = off >= 16;
+                const uint4 B0 = k1 ? n1 : A[u], B1 = k1 ? n2 : n1;
+                const uint32_t sh = off & 15u;
+                uint4 o = sh ? funnel16(B0, B1, sh) : B0;
+                xor4(o, k);
+                if (len - 16u * c < 16u) o = and4(o, byte_range(0, len - 16u * c));
+                fused_store(out, (f0 + src) * slot + 16ull * c, capacity, o);
+            }
+        }
+    }
+}
+
+#ifndef CFWS_SLOT_UNROLL
+#define CFWS_SLOT_UNROLL 16      // 4 M x 1 KiB: 4 -> 1.84-1.89 ms, 8 -> 1.69, 16 -> 1.63
+#endif
+constexpr int kSlotUnroll = CFWS_SLOT_UNROLL;   // deserialize_slots_kernel: rounds of loads in flight
+
+// Slots over kSlotWindowMax: one frame per thread parsed (its header line
+// fetched twice, a small share of a frame this long), the payloads copied
+// by fused_item.
+__global__ void __launch_bounds__(kThreads)
+deserialize_slots_kernel(const uint8_t* __restrict__ wire, uint64_t wire_size, const uint64_t* __restrict__ index,
+                         uint64_t n, uint64_t max_payload, uint64_t slot, cfws_frame_desc_t* __restrict__ desc,
+                         int32_t* __restrict__ status, uint8_t* __restrict__ out, uint64_t capacity,
+                         uint64_t* __restrict__ user_total)
+{
+    const uint64_t f = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
+    uint64_t run = 0, src = 0;
+    uint32_t len = 0, nb = 0, key = 0;
+    if (f < n) {
+        cfws_frame_desc_t d;
+        const uint64_t s0 = index[f];
+        run = f * slot;
+        const int32_t st = slot_rule(parse_ws_header(wire, wire_size, s0, max_payload, d), run, d.payload_size,
+                                     slot, capacity);
+        slot_desc(desc, status, f, run, d, st);
+        if (st == CFWS_PARSE_COMPLETE) {
+            len = (uint32_t)d.payload_size;   // <= slot < 2^31
+            nb = (len + 15u) & ~15u;
+            src = s0 + d.header_size;
+            key = d.mask ? d.mask_key : 0u;
+        }
+        if (f == n - 1 && user_total) {
+            const uint64_t t = n * slot;
+            *user_total = t < capacity ? t : capacity;
+        }
+    }
+    fused_item<kSlotUnroll>(wire, out, capacity, run, src, len, nb, key, threadIdx.x & 63u);
+}
+
+bool slots_window()
+{
+    static const bool v = env_knob("CFWS_SLOTS_WINDOW", 1) != 0;
     return v;
 }
 
@@ -1255,6 +1441,58 @@ int cfws_deserialize_batch(const void* d_wire, uint64_t wire_size, const uint64_
                                        d_desc, d_status, cap, d_total, ws, ws_size, stream))
         return rc;
     return cfws_deserialize_execute(d_wire, d_desc, d_status, n, flags, d_payload, cap, ws, stream);
+}
+
+int cfws_deserialize_slots(const void* d_wire, uint64_t wire_size, const uint64_t* d_index, size_t n,
+                           uint64_t max_payload, uint64_t slot, cfws_frame_desc_t* d_desc, int32_t* d_status,
+                           void* d_payload, uint64_t cap, uint64_t* d_total, void* stream)
+{
+    if (int rc = check_init()) return rc;
+    if (slot < 16 || (slot & 15) || slot > (1ull << 31))
+        return set_err(CFWS_ERROR_INVALID_ARGUMENT, "slot_bytes must be a multiple of 16 in [16, 2^31]",
+                       hipSuccess);
+    if (n > 0xffffffffull) return set_err(CFWS_ERROR_INVALID_ARGUMENT, "too many frames", hipSuccess);
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    if (n == 0) {
+        if (d_total && hipMemsetAsync(d_total, 0, sizeof(uint64_t), st) != hipSuccess)
+            return launch_check("deserialize_slots");
+        return CFWS_OK;
+    }
+    if (!d_wire || !d_index || !d_desc || !d_status || (cap && !d_payload))
+        return set_err(CFWS_ERROR_INVALID_ARGUMENT, "null pointer", hipSuccess);
+    if (misaligned(d_payload, d_wire))
+        return set_err(CFWS_ERROR_INVALID_ARGUMENT, "arenas must be 16-byte aligned", hipSuccess);
+    CfwsPassEvents& pe = cfws_internal_pass_events();
+    const CfwsPassEvents timed = pe;
+    pe = {nullptr, nullptr};
+    if (timed.start) (void)hipEventRecord(static_cast<hipEvent_t>(timed.start), st);
+    const uint8_t* w = static_cast<const uint8_t*>(d_wire);
+    uint8_t* out = static_cast<uint8_t*>(d_payload);
+    if (slot <= kSlotWindowMax && slots_window()) {
+        // one wave-iteration of R P frames per wave (CFWS_SLOT_GRID caps the
+        // workgroups: a grid-stride loop; A/B knob)
+        const uint32_t G = (uint32_t)(slot / 16 + 2), P = 64 / G;
+        const uint64_t RK = P > 1 ? CFWS_SLOT_ROUNDS_MULTI : CFWS_SLOT_ROUNDS;
+        const uint64_t R = P * RK <= 64 ? RK : 64 / P;
+        const uint64_t per_block = uint64_t(kWaves) * R * P;
+        static const uint64_t cap_blocks = [] {
+            const int64_t v = env_knob("CFWS_SLOT_GRID", 0);   // 0: one iteration per wave
+            return v > 0 ? (uint64_t)v : 0x7fffffffull;
+        }();
+        const uint64_t want = (n + per_block - 1) / per_block;
+        const uint32_t grid = (uint32_t)(want < cap_blocks ? want : cap_blocks);
+        if (P > 1)
+            deserialize_slots_window_kernel<CFWS_SLOT_ROUNDS_MULTI><<<grid, kThreads, 0, st>>>(
+                w, wire_size, d_index, n, max_payload, slot, G, d_desc, d_status, out, cap, d_total);
+        else
+            deserialize_slots_window_kernel<CFWS_SLOT_ROUNDS><<<grid, kThreads, 0, st>>>(
+                w, wire_size, d_index, n, max_payload, slot, G, d_desc, d_status, out, cap, d_total);
+    } else {
+        deserialize_slots_kernel<<<grid_for(n, kThreads), kThreads, 0, st>>>(
+            w, wire_size, d_index, n, max_payload, slot, d_desc, d_status, out, cap, d_total);
+    }
+    if (timed.stop) (void)hipEventRecord(static_cast<hipEvent_t>(timed.stop), st);
+    return launch_check("deserialize_slots");
 }
 
 }  // extern "C"

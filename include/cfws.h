@@ -138,6 +138,28 @@ int cfws_deserialize_batch(const void* d_wire, uint64_t wire_size,
                            uint64_t* d_payload_total, void* d_workspace,
                            size_t workspace_size, void* stream);
 
+/* ---- deserialize into fixed payload slots --------------------------------
+ * The batch receive with frame i's payload at payload_off = i * slot_bytes
+ * (slot_bytes a multiple of 16 in [16, 2^31]): the slab form of the
+ * reference's one allocation per frame (co_ws_frame_deserialize,
+ * src/ws/co_ws_frame.c:216-223). One launch, no workspace: no payload offset
+ * depends on another frame, so each wire line is read once.
+ *   d_desc[i], d_status[i]: as cfws_deserialize_plan (flags = 0), with the
+ *     slot rule in place of the packing: a COMPLETE frame whose non-empty
+ *     payload is longer than slot_bytes, or ends past payload_capacity, gets
+ *     CFWS_ERROR_OUT_OF_MEMORY.
+ *   slot i of a COMPLETE frame: the unmasked payload, then zeros up to the
+ *     next 16-byte boundary (cut at the capacity); the rest of every slot,
+ *     and the slots of all other frames, are not written.
+ *   *d_payload_total (may be NULL) = min(n_frames * slot_bytes, capacity).
+ * Frames of the same wire may be indexed in any order, overlapping or not. */
+int cfws_deserialize_slots(const void* d_wire, uint64_t wire_size,
+                           const uint64_t* d_frame_index, size_t n_frames,
+                           uint64_t max_payload, uint64_t slot_bytes,
+                           cfws_frame_desc_t* d_desc, int32_t* d_status,
+                           void* d_payload, uint64_t payload_capacity,
+                           uint64_t* d_payload_total, void* stream);
+
 /* ---- split ops: headers and payload XOR as separate passes ---------------
  * The two halves of the codec over frames the caller lays out itself (a send
  * path that gathers headers and payloads into iovecs, a receive path that

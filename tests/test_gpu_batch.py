@@ -370,6 +370,15 @@ def test_small_frame_reference_digests(which):
     torch.cuda.synchronize()
     assert ptot2.item() == n * fs and bool((st2 == 0).all())
     assert _sha_device(back, n * fs) == g["payload_sha256"]
+    # cfws_deserialize_slots at slots of fs bytes: the same arena (every fs
+    # here is a multiple of 16); 256 B takes the window kernel, the rest the
+    # per-frame one
+    back.fill_(0xEE)
+    status.fill_(99)
+    _, st3, ptot3 = cfws.deserialize_slots(wire, total, idx, back, fs, desc_de, status)
+    torch.cuda.synchronize()
+    assert ptot3.item() == n * fs and bool((st3 == 0).all())
+    assert _sha_device(back, n * fs) == g["payload_sha256"]
 
 
 def _roundtrip_digest(g, full=False):

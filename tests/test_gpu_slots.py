@@ -1,0 +1,202 @@
+"""cfws_deserialize_slots (include/cfws.h): frame i's payload at i * slot.
+
+The expectation is the oracle's own parse and unmask (oracle
+deserialize_batch, following co_ws_frame.c:121-247) relocated into slot i:
+the slot layout is this library's (the slab form of the reference's one
+allocation per frame, co_ws_frame.c:216-223), so the relocation and the slot
+rule are restated here, in the test. Every arena is guarded
+(tests/native/guardmem.cpp): the wire ends at its round16(wire_size), the
+payload arena at round16(capacity), and bytes past the capacity, past each
+payload's 16-byte round-up and in the slots of non-COMPLETE frames are
+checked to keep their sentinel. Slots up to 992 bytes take the window
+kernel, larger ones the per-frame kernel."""
+import random
+
+import numpy as np
+import pytest
+
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+from coldforce_amd import cfws  # noqa: E402
+from coldforce_amd import workloads as W  # noqa: E402
+from test_gpu_guard import GuardBuf, _glib, _seed21_batch  # noqa: E402
+
+SENT = 0xEE
+
+
+@pytest.fixture(scope="module", autouse=True)
+def device():
+    cfws.init()
+    torch.cuda.synchronize()
+    if not _glib().guard_supported():
+        pytest.skip("no HIP virtual memory management on this device")
+    return torch.device("cuda", 0)
+
+
+@pytest.fixture
+def guards():
+    bufs = []
+
+    def make(n, flush_end=True):
+        b = GuardBuf(n, flush_end, SENT)
+        bufs.append(b)
+        return b
+    yield make
+    torch.cuda.synchronize()
+    for b in bufs:
+        b.free()
+
+
+def expect_slots(wire, wire_size, starts, slot, cap, max_payload=O.DEFAULT_MAX_PAYLOAD):
+    """(arena of round16(cap) bytes, desc, status, total) as
+    cfws_deserialize_slots defines them, from the oracle's packed receive."""
+    n = len(starts)
+    # packed with room for every COMPLETE payload (indices may repeat)
+    p_d, p_st = O.parse_headers(wire[:wire_size], starts, max_payload)
+    room = int(p_d["payload_size"][p_st == O.PARSE_COMPLETE].sum()) + 16
+    e_out, e_d, e_st, _ = O.deserialize_batch(wire[:wire_size], starts, align=1, max_payload=max_payload,
+                                              capacity=room)
+    ps = e_d["payload_size"].astype(np.uint64)
+    run = np.arange(n, dtype=np.uint64) * np.uint64(slot)
+    st = e_st.copy()
+    oom = (st == O.PARSE_COMPLETE) & (ps > 0) & ((ps > slot) | (run + ps > cap))
+    st[oom] = O.ERROR_OUT_OF_MEMORY
+    arena = np.full(W.round16(max(cap, 1)), SENT, np.uint8)
+    for i in np.nonzero((st == O.PARSE_COMPLETE) & (ps > 0))[0]:
+        r, L, o = int(run[i]), int(ps[i]), int(e_d["payload_off"][i])
+        arena[r:r + L] = e_out[o:o + L]
+        arena[r + L:min(r + W.round16(L), cap)] = 0
+    d = e_d.copy()
+    d["payload_off"] = run
+    return arena, d, st, min(n * slot, cap)
+
+
+def run_slots(guards, wire, starts, slot, cap=None, wire_size=None, max_payload=O.DEFAULT_MAX_PAYLOAD,
+              flush_end=True):
+    ws_n = len(wire) if wire_size is None else wire_size
+    n = len(starts)
+    cap = n * slot if cap is None else cap
+    w = guards(max(ws_n, 1), flush_end).upload(wire[:ws_n])
+    out = guards(max(cap, 1), flush_end)
+    idx = torch.from_numpy(np.asarray(starts, dtype=np.uint64).view(np.int64)).cuda()
+    d_t, st_t, tot = cfws.deserialize_slots(w, ws_n, idx, out, slot, max_payload=max_payload,
+                                            payload_capacity=cap)
+    torch.cuda.synchronize()
+    e_arena, e_d, e_st, e_tot = expect_slots(wire, ws_n, starts, slot, cap, max_payload)
+    assert int(tot.item()) == e_tot
+    st = st_t.cpu().numpy()
+    bad = np.nonzero(st != e_st)[0]
+    assert bad.size == 0, f"{bad.size} statuses differ, first {[(int(i), int(st[i]), int(e_st[i])) for i in bad[:6]]}"
+    d = cfws.desc_from_device(d_t)
+    for f in ("payload_off", "wire_off", "payload_size", "mask_key", "opcode", "header_size"):
+        assert np.array_equal(d[f], e_d[f]), f
+    ok = e_st == O.PARSE_COMPLETE
+    for f in ("fin", "mask"):
+        assert np.array_equal(d[f][ok], e_d[f][ok]), f
+    got = out.download()
+    bad = np.nonzero(got != e_arena)[0]
+    assert bad.size == 0, f"{bad.size} arena bytes differ, first at {bad[:8]} (cap {cap})"
+    return e_st
+
+
+def _wire_of(payload, desc):
+    wire, _ = O.serialize_batch(payload, desc.view(O.DESC_DTYPE))
+    starts, consumed = O.index_frames(wire, len(desc) + 1)
+    assert consumed == len(wire)
+    return wire, starts
+
+
+@pytest.mark.parametrize("slot", [16, 48, 80, 256, 512, 992, 1008, 4096, 8192])
+@pytest.mark.parametrize("seed", [21, 22])
+def test_slots_mixed(guards, seed, slot):
+    """6,000 frames of 30-80 B (masked and not, data and control) with a
+    5,000-byte frame every 97th: at slots under 80 B some frames are OOM,
+    under 5,000 B the long ones are."""
+    payload, desc = _seed21_batch(seed)
+    wire, starts = _wire_of(payload, desc)
+    st = run_slots(guards, wire, starts, slot)
+    if slot >= 80:
+        assert (st == O.PARSE_COMPLETE).any()
+    if slot < 5000:
+        assert (st == O.ERROR_OUT_OF_MEMORY).any()
+
+
+@pytest.mark.parametrize("flush_end", [True, False], ids=["end", "start"])
+@pytest.mark.parametrize("slot", [256, 4096])
+def test_slots_guard_start(guards, slot, flush_end):
+    payload, desc = _seed21_batch(25)
+    wire, starts = _wire_of(payload, desc)
+    run_slots(guards, wire, starts, slot, flush_end=flush_end)
+
+
+@pytest.mark.parametrize("fs", [0, 1, 125, 126, 240, 256, 977, 992, 1000, 1024, 65536])
+def test_slots_uniform(guards, fs):
+    """Uniform batches at slot = round16(fs) (at least 16): the bench's shape,
+    every frame COMPLETE and every slot full."""
+    n = max(64, min(150_000, (24 << 20) // max(fs, 1)))
+    desc = W.uniform_batch(n, fs, 2, opcode=cfws.OPCODE_BINARY)
+    payload = O.fill_splitmix(max(n * fs, 16), 0x5EED0003, 0)[:n * fs]
+    wire, starts = _wire_of(payload, desc)
+    st = run_slots(guards, wire, starts, max(16, W.round16(fs)))
+    assert (st == O.PARSE_COMPLETE).all()
+
+
+def test_slots_capacity_cuts(guards):
+    """Capacities inside a slot and inside a payload, at odd byte counts."""
+    payload, desc = _seed21_batch(23)
+    wire, starts = _wire_of(payload, desc)
+    n = len(starts)
+    for slot in (96, 6016):
+        for cap in (n * slot // 2 + 5, n * slot - 3, 1001, 17, 0):
+            run_slots(guards, wire, starts, slot, cap=cap)
+
+
+def test_slots_truncated_wire(guards):
+    """The wire ends inside the last frame, at every offset of its header
+    and into its payload (MORE_DATA), and starts past the wire's end."""
+    payload, desc = _seed21_batch(24)
+    desc = desc[:2000]
+    wire, starts = _wire_of(payload, desc)
+    last = int(starts[-1])
+    for slot in (128, 5008):
+        for cut in (last + 1, last + 2, last + 3, last + 7, len(wire) - 1):
+            st = run_slots(guards, wire, starts, slot, wire_size=cut)
+            assert st[-1] == O.PARSE_MORE_DATA
+
+
+def test_slots_any_index(guards):
+    """Indices in any order, repeated, inside payloads (whatever header the
+    bytes there make: invalid frames, DATA_TOO_BIG, MORE_DATA) and past the
+    wire's end; a small max_payload."""
+    payload, desc = _seed21_batch(26)
+    wire, starts = _wire_of(payload, desc)
+    rng = random.Random(26)
+    idx = list(starts)
+    idx += [rng.randrange(0, len(wire)) for _ in range(3000)]
+    idx += [len(wire), len(wire) + 5, (1 << 40), (1 << 64) - 1]
+    idx += list(starts[:500])
+    rng.shuffle(idx)
+    idx = np.array(idx, dtype=np.uint64)
+    for slot in (64, 256, 992, 2048):
+        st = run_slots(guards, wire, idx, slot)
+        assert (st == O.ERROR_INVALID_FRAME).any() and (st == O.PARSE_MORE_DATA).any()
+        run_slots(guards, wire, idx, slot, max_payload=60)
+
+
+def test_slots_arguments(guards):
+    wire = np.zeros(64, np.uint8)
+    w = guards(64).upload(wire)
+    out = guards(64)
+    idx = torch.zeros(1, dtype=torch.int64, device="cuda")
+    for slot in (0, 8, 24, (1 << 31) + 16):
+        with pytest.raises(cfws.CodecError):
+            cfws.deserialize_slots(w, 64, idx, out, slot)
+    e = torch.empty(0, dtype=torch.int64, device="cuda")
+    _, _, tot = cfws.deserialize_slots(w, 64, e, out, 16, total_t=torch.full((1,), 7, dtype=torch.int64,
+                                                                                device="cuda"))
+    torch.cuda.synchronize()
+    assert tot.item() == 0

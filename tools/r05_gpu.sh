@@ -42,6 +42,20 @@ for s in "$@"; do
     c5cpu) step c5cpu 300 python3 $R/bench.py --workload config5 ;;
     prof_c5) step prof_c5 600 env TAG=$TAG/prof_c5 ARGS="--workload config5" bash $R/tools/profile.sh ;;
     c3) step c3 200 python3 $R/bench.py --workload config3 --no-cpu-baseline ;;
+    slots) step slots 600 python3 -u -m pytest $R/tests/test_gpu_slots.py -m gpu -x -v --timeout 300 --timeout-method thread ;;
+    fs256s) step fs256s 200 python3 $R/bench.py --frames 16777216 --frame-size 256 --no-cpu-baseline --recv-slots ;;
+    fs1ks) step fs1ks 200 python3 $R/bench.py --frames 4194304 --frame-size 1024 --no-cpu-baseline --recv-slots ;;
+    fs512s) step fs512s 200 python3 $R/bench.py --frames 8388608 --frame-size 512 --no-cpu-baseline --recv-slots ;;
+    fs512) step fs512 200 python3 $R/bench.py --frames 8388608 --frame-size 512 --no-cpu-baseline ;;
+    kstats_fs256s) step kstats_fs256s 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kstats_fs256s" -o ks -- python3 $R/bench.py --frames 16777216 --frame-size 256 --steps 10 --warmup 3 --no-cpu-baseline --recv-slots ;;
+    prof_fs256s) step prof_fs256s 400 env TAG=$TAG/prof_fs256s ARGS="--frames 16777216 --frame-size 256 --recv-slots" bash $R/tools/profile.sh ;;
+    prof_fs256s_gen) step prof_fs256s_gen 400 env CFWS_SLOTS_WINDOW=0 TAG=$TAG/prof_fs256s_gen ARGS="--frames 16777216 --frame-size 256 --recv-slots" bash $R/tools/profile.sh ;;
+    fs256s_gen) step fs256s_gen 200 env CFWS_SLOTS_WINDOW=0 python3 $R/bench.py --frames 16777216 --frame-size 256 --no-cpu-baseline --recv-slots ;;
+    fs512s_gen) step fs512s_gen 200 env CFWS_SLOTS_WINDOW=0 python3 $R/bench.py --frames 8388608 --frame-size 512 --no-cpu-baseline --recv-slots ;;
+    slotab) step slotab 600 env TAG=$TAG/slotab ENVS="X=0;CFWS_SLOT_GRID=2048;CFWS_SLOT_GRID=4096" ARGS="--frames 16777216 --frame-size 256 --recv-slots" bash $R/tools/envab.sh ;;
+    ab_slots256) step ab_slots256 900 env TAG=$TAG/ab_slots256 VARIANTS="${V256:-base}" ARGS="--frames 16777216 --frame-size 256 --recv-slots" bash $R/tools/ab.sh ;;
+    ab_slots512) step ab_slots512 900 env TAG=$TAG/ab_slots512 VARIANTS="${V512:-base}" ARGS="--frames 8388608 --frame-size 512 --recv-slots" bash $R/tools/ab.sh ;;
+    ab_slots1k) step ab_slots1k 900 env TAG=$TAG/ab_slots1k VARIANTS="${V1K:-base}" ARGS="--frames 4194304 --frame-size 1024 --recv-slots" bash $R/tools/ab.sh ;;
     fs256) step fs256 200 python3 $R/bench.py --frames 16777216 --frame-size 256 --no-cpu-baseline ;;
     kstats_fs256) step kstats_fs256 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kstats_fs256" -o ks -- python3 $R/bench.py --frames 16777216 --frame-size 256 --steps 10 --warmup 3 --no-cpu-baseline ;;
     fs2k) step fs2k 200 python3 $R/bench.py --frames 2097152 --frame-size 2048 --no-cpu-baseline ;;
