@@ -761,6 +761,8 @@ uint64_t fused_avg_max()
 // wire's end are not loaded. The first form parsed in every lane of every
 // round (480 instructions per 3 frames at 256 B) and ran at 5.2 TB/s.
 constexpr uint64_t kSlotWindowMax = 64 * 16 - 32;   // 992: G <= 64
+constexpr uint64_t kSlotWindow2Max = 128 * 16 - 32; // 2,016: G <= 128, two blocks per lane
+constexpr uint64_t kSlotWindow4Max = 256 * 16 - 32; // 4,064: G <= 256, four blocks per lane
 // Rounds per iteration (their loads in flight together): 8 for one frame per
 // round (slots over 480 B), 4 for more (16 M x 256 B receive 1.686 -> 1.620
 // ms; 12 or 16 rounds: 3.3 ms; 8 M x 512 B at 4 rounds 1.59 -> 1.76 ms).
@@ -770,6 +772,18 @@ constexpr uint64_t kSlotWindowMax = 64 * 16 - 32;   // 992: G <= 64
 #ifndef CFWS_SLOT_ROUNDS_MULTI
 #define CFWS_SLOT_ROUNDS_MULTI 4
 #endif
+#ifndef CFWS_SLOT_ROUNDS2
+#define CFWS_SLOT_ROUNDS2 4      // two blocks per lane (1,008-2,016 B): 2,016 B 2 / 4 / 6 -> 1.61-1.62 / 1.61 / 1.63 ms
+#endif
+#ifndef CFWS_SLOT_ROUNDS4
+#define CFWS_SLOT_ROUNDS4 1      // four blocks per lane (2,032-4,064 B): 3 KiB 1 / 2 / 4 -> 1.48 / 1.55 / 1.59 ms
+#endif
+
+__device__ __forceinline__ uint4 shfl16(uint4 v, int src)
+{
+    return make_uint4((uint32_t)__shfl((int)v.x, src, 64), (uint32_t)__shfl((int)v.y, src, 64),
+                      (uint32_t)__shfl((int)v.z, src, 64), (uint32_t)__shfl((int)v.w, src, 64));
+}
 
 __device__ __forceinline__ uint64_t shfl64(uint64_t v, int src)
 {
@@ -797,7 +811,7 @@ __device__ __forceinline__ void slot_desc(cfws_frame_desc_t* desc, int32_t* stat
     status[f] = st;
 }
 
-template <int kSlotRounds>
+template <int kSlotRounds, int kSub>
 __global__ void __launch_bounds__(kThreads)
 deserialize_slots_window_kernel(const uint8_t* __restrict__ wire, uint64_t wire_size,
                                 const uint64_t* __restrict__ index, uint64_t n, uint64_t max_payload,
@@ -806,7 +820,9 @@ deserialize_slots_window_kernel(const uint8_t* __restrict__ wire, uint64_t wire_
                                 uint64_t* __restrict__ user_total)
 {
     const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t P = 64u / G, g = lane / G, c = lane - g * G;
+    // kSub = 2 / 4: one frame per round over 64 < G <= 64 kSub blocks, lane c
+    // holding blocks c, 64 + c, ...
+    const uint32_t P = kSub > 1 ? 1u : 64u / G, g = kSub > 1 ? 0u : lane / G, c = lane - g * G;
     const uint32_t R = P * kSlotRounds <= 64 ? (uint32_t)kSlotRounds : 64u / P;
     const uint64_t FI = uint64_t(R) * P;                 // frames per wave-iteration
     const uint64_t stride = uint64_t(gridDim.x) * kWaves * FI;
@@ -818,13 +834,18 @@ deserialize_slots_window_kernel(const uint8_t* __restrict__ wire, uint64_t wire_
         const bool mine = lane < FI && fl < n;
         const uint64_t wl = mine ? index[fl] : ~uint64_t(0);
         // every round's window block, then each frame's header bytes
-        uint4 A[kSlotRounds];
+        uint4 A[kSlotRounds][kSub];
 #pragma unroll
         for (int u = 0; u < kSlotRounds; ++u) {
             const uint32_t src = (uint32_t)u * P + g;
             const uint64_t wo = shfl64(wl, (int)(src < 64 ? src : 63));
-            const uint64_t blk = (wo & ~uint64_t(15)) + 16ull * c;
-            A[u] = (uint32_t)u < R && g < P && wo < wire_size && blk < wire_size ? ld16(wire + blk) : z;
+#pragma unroll
+            for (int sw = 0; sw < kSub; ++sw) {
+                const uint32_t cb = 64u * sw + c;   // block of the window
+                const uint64_t blk = (wo & ~uint64_t(15)) + 16ull * cb;
+                A[u][sw] = (uint32_t)u < R && g < P && cb < G && wo < wire_size && blk < wire_size
+                               ? ld16(wire + blk) : z;
+            }
         }
         const uint4 hw = mine && b16 && wl <= lastu ? ld16u(wire + wl) : z;
         // lane l parses frame f0 + l; its round info: payload length (<= slot
@@ -859,24 +880,32 @@ deserialize_slots_window_kernel(const uint8_t* __restrict__ wire, uint64_t wire_
             const uint32_t inf = (uint32_t)__shfl((int)info, s, 64);
             const uint32_t k = (uint32_t)__shfl((int)key, s, 64);
             const uint32_t len = inf & 0xffffu, off = inf >> 16;
-            // blocks c + 1 and c + 2 of the window, by DPP (every lane)
-            const uint4 n1 = from_next_lane(A[u], z);
-            const uint4 n2 = from_next_lane(n1, z);
-            if (g < P && 16u * c < len) {
-                const bool k1 = off >= 16;
-                const uint4 B0 = k1 ? n1 : A[u], B1 = k1 ? n2 : n1;
-                const uint32_t sh = off & 15u;
-                uint4 o = sh ? funnel16(B0, B1, sh) : B0;
-                xor4(o, k);
-                if (len - 16u * c < 16u) o = and4(o, byte_range(0, len - 16u * c));
-                fused_store(out, (f0 + src) * slot + 16ull * c, capacity, o);
+#pragma unroll
+            for (int sw = 0; sw < kSub; ++sw) {
+                // blocks c + 1 and c + 2 of this sub-window, by DPP (every
+                // lane); lanes 62 and 63 of a sub-window take the next one's
+                // first two blocks
+                const uint4 l0 = sw + 1 < kSub ? shfl16(A[u][sw + 1 < kSub ? sw + 1 : sw], 0) : z;
+                const uint4 l1 = sw + 1 < kSub ? shfl16(A[u][sw + 1 < kSub ? sw + 1 : sw], 1) : z;
+                const uint4 n1 = from_next_lane(A[u][sw], l0);
+                const uint4 n2 = from_next_lane(n1, l1);
+                const uint32_t q = 64u * sw + c;   // payload chunk
+                if (g < P && 16u * q < len) {
+                    const bool k1 = off >= 16;
+                    const uint4 B0 = k1 ? n1 : A[u][sw], B1 = k1 ? n2 : n1;
+                    const uint32_t sh = off & 15u;
+                    uint4 o = sh ? funnel16(B0, B1, sh) : B0;
+                    xor4(o, k);
+                    if (len - 16u * q < 16u) o = and4(o, byte_range(0, len - 16u * q));
+                    fused_store(out, (f0 + src) * slot + 16ull * q, capacity, o);
+                }
             }
         }
     }
 }
 
 #ifndef CFWS_SLOT_UNROLL
-#define CFWS_SLOT_UNROLL 16      // 4 M x 1 KiB: 4 -> 1.84-1.89 ms, 8 -> 1.69, 16 -> 1.63
+#define CFWS_SLOT_UNROLL 4       // slots over 4,064 B: 16 rounds (246 VGPRs) took 2 M x 2 KiB to 2.87 ms
 #endif
 constexpr int kSlotUnroll = CFWS_SLOT_UNROLL;   // deserialize_slots_kernel: rounds of loads in flight
 
@@ -1468,11 +1497,12 @@ int cfws_deserialize_slots(const void* d_wire, uint64_t wire_size, const uint64_
     if (timed.start) (void)hipEventRecord(static_cast<hipEvent_t>(timed.start), st);
     const uint8_t* w = static_cast<const uint8_t*>(d_wire);
     uint8_t* out = static_cast<uint8_t*>(d_payload);
-    if (slot <= kSlotWindowMax && slots_window()) {
+    if (slot <= kSlotWindow4Max && slots_window()) {
         // one wave-iteration of R P frames per wave (CFWS_SLOT_GRID caps the
         // workgroups: a grid-stride loop; A/B knob)
-        const uint32_t G = (uint32_t)(slot / 16 + 2), P = 64 / G;
-        const uint64_t RK = P > 1 ? CFWS_SLOT_ROUNDS_MULTI : CFWS_SLOT_ROUNDS;
+        const uint32_t G = (uint32_t)(slot / 16 + 2), P = G > 64 ? 1 : 64 / G;
+        const uint64_t RK = G > 128 ? CFWS_SLOT_ROUNDS4 : G > 64 ? CFWS_SLOT_ROUNDS2
+                            : P > 1 ? CFWS_SLOT_ROUNDS_MULTI : CFWS_SLOT_ROUNDS;
         const uint64_t R = P * RK <= 64 ? RK : 64 / P;
         const uint64_t per_block = uint64_t(kWaves) * R * P;
         static const uint64_t cap_blocks = [] {
@@ -1481,11 +1511,17 @@ int cfws_deserialize_slots(const void* d_wire, uint64_t wire_size, const uint64_
         }();
         const uint64_t want = (n + per_block - 1) / per_block;
         const uint32_t grid = (uint32_t)(want < cap_blocks ? want : cap_blocks);
-        if (P > 1)
-            deserialize_slots_window_kernel<CFWS_SLOT_ROUNDS_MULTI><<<grid, kThreads, 0, st>>>(
+        if (G > 128)
+            deserialize_slots_window_kernel<CFWS_SLOT_ROUNDS4, 4><<<grid, kThreads, 0, st>>>(
+                w, wire_size, d_index, n, max_payload, slot, G, d_desc, d_status, out, cap, d_total);
+        else if (G > 64)
+            deserialize_slots_window_kernel<CFWS_SLOT_ROUNDS2, 2><<<grid, kThreads, 0, st>>>(
+                w, wire_size, d_index, n, max_payload, slot, G, d_desc, d_status, out, cap, d_total);
+        else if (P > 1)
+            deserialize_slots_window_kernel<CFWS_SLOT_ROUNDS_MULTI, 1><<<grid, kThreads, 0, st>>>(
                 w, wire_size, d_index, n, max_payload, slot, G, d_desc, d_status, out, cap, d_total);
         else
-            deserialize_slots_window_kernel<CFWS_SLOT_ROUNDS><<<grid, kThreads, 0, st>>>(
+            deserialize_slots_window_kernel<CFWS_SLOT_ROUNDS, 1><<<grid, kThreads, 0, st>>>(
                 w, wire_size, d_index, n, max_payload, slot, G, d_desc, d_status, out, cap, d_total);
     } else {
         deserialize_slots_kernel<<<grid_for(n, kThreads), kThreads, 0, st>>>(

@@ -56,6 +56,15 @@ for s in "$@"; do
     ab_slots256) step ab_slots256 900 env TAG=$TAG/ab_slots256 VARIANTS="${V256:-base}" ARGS="--frames 16777216 --frame-size 256 --recv-slots" bash $R/tools/ab.sh ;;
     ab_slots512) step ab_slots512 900 env TAG=$TAG/ab_slots512 VARIANTS="${V512:-base}" ARGS="--frames 8388608 --frame-size 512 --recv-slots" bash $R/tools/ab.sh ;;
     ab_slots1k) step ab_slots1k 900 env TAG=$TAG/ab_slots1k VARIANTS="${V1K:-base}" ARGS="--frames 4194304 --frame-size 1024 --recv-slots" bash $R/tools/ab.sh ;;
+    fs2ks) step fs2ks 200 python3 $R/bench.py --frames 2097152 --frame-size 2048 --no-cpu-baseline --recv-slots ;;
+    fs1500s) step fs1500s 200 python3 $R/bench.py --frames 2796202 --frame-size 1536 --no-cpu-baseline --recv-slots ;;
+    fs3ks) step fs3ks 200 python3 $R/bench.py --frames 1398101 --frame-size 3072 --no-cpu-baseline --recv-slots ;;
+    fs4ks) step fs4ks 200 python3 $R/bench.py --frames 1048576 --frame-size 4096 --no-cpu-baseline --recv-slots ;;
+    fs8ks) step fs8ks 200 python3 $R/bench.py --frames 524288 --frame-size 8192 --no-cpu-baseline --recv-slots ;;
+    fs4k) step fs4k 200 python3 $R/bench.py --frames 1048576 --frame-size 4096 --no-cpu-baseline ;;
+    fs8k) step fs8k 200 python3 $R/bench.py --frames 524288 --frame-size 8192 --no-cpu-baseline ;;
+    ab_slots2k) step ab_slots2k 900 env TAG=$TAG/ab_slots2k VARIANTS="${V2K:-base}" ARGS="--frames 2097152 --frame-size 2016 --recv-slots" bash $R/tools/ab.sh ;;
+    ab_slots3k) step ab_slots3k 900 env TAG=$TAG/ab_slots3k VARIANTS="${V3K:-base}" ARGS="--frames 1398101 --frame-size 3072 --recv-slots" bash $R/tools/ab.sh ;;
     fs256) step fs256 200 python3 $R/bench.py --frames 16777216 --frame-size 256 --no-cpu-baseline ;;
     kstats_fs256) step kstats_fs256 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kstats_fs256" -o ks -- python3 $R/bench.py --frames 16777216 --frame-size 256 --steps 10 --warmup 3 --no-cpu-baseline ;;
     fs2k) step fs2k 200 python3 $R/bench.py --frames 2097152 --frame-size 2048 --no-cpu-baseline ;;
