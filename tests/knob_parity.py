@@ -16,6 +16,10 @@ tests/test_knobs.py runs this script once per setting):
                         default: the fused plan + copy)
   CFWS_H2_UNITS_MERGED=0  the HTTP/2 receive's message layout and payload
                         units as two launches (1, the default: one)
+  CFWS_SLOTS_WINDOW=0   the fixed-slot receive on its per-frame kernel for
+                        every slot size
+  CFWS_SLOT_GRID=N      the fixed-slot window kernel as a grid-stride loop
+                        over N workgroups
 
 Each case is checked byte for byte against the oracle. Prints "KNOB OK".
 """
@@ -127,6 +131,30 @@ def main():
         T2.test_gpu_h2_deserialize_headers_across_data_frames(13)
         T2.test_gpu_h2_rows_past_message_count_are_empty(2)
         T2.test_gpu_h2_long_messages(1000)
+    if "CFWS_SLOTS_WINDOW" in os.environ or "CFWS_SLOT_GRID" in os.environ:
+        # the fixed-slot receive: every slot size on the per-frame kernel
+        # (CFWS_SLOTS_WINDOW=0), or the window kernel as a grid-stride loop
+        # over a capped grid (CFWS_SLOT_GRID), over guarded arenas
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import test_gpu_slots as TS
+        if TS._glib().guard_supported():
+            bufs = []
+
+            def make(n, flush_end=True):
+                b = TS.GuardBuf(n, flush_end, TS.SENT)
+                bufs.append(b)
+                return b
+            for slot in (16, 256, 992, 1504, 4064):
+                for seed in (21, 22):
+                    TS.test_slots_mixed(make, seed, slot)
+            TS.test_slots_capacity_cuts(make)
+            TS.test_slots_truncated_wire(make)
+            TS.test_slots_any_index(make)
+            for fs in (256, 1000, 3072):
+                TS.test_slots_uniform(make, fs)
+            torch.cuda.synchronize()
+            for b in bufs:
+                b.free()
     # a small batch (single-launch path unless CFWS_SMALL=0)
     roundtrip(np.full(256, 1000), rng, 3, 16)
     # fragments + pings, reassembled (two passes, pass-1 capped grid)

@@ -20,6 +20,8 @@ KNOBS = [
     {"CFWS_H2_INREG": "1"},
     {"CFWS_FUSED_DESER": "0"},
     {"CFWS_H2_UNITS_MERGED": "0"},
+    {"CFWS_SLOTS_WINDOW": "0"},
+    {"CFWS_SLOT_GRID": "37"},
 ]
 
 
