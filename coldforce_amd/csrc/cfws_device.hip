@@ -760,9 +760,9 @@ uint64_t fused_avg_max()
 // index that is a multiple of 16: no key rotation). Blocks at or past the
 // wire's end are not loaded. The first form parsed in every lane of every
 // round (480 instructions per 3 frames at 256 B) and ran at 5.2 TB/s.
-constexpr uint64_t kSlotWindowMax = 64 * 16 - 32;   // 992: G <= 64
-constexpr uint64_t kSlotWindow2Max = 128 * 16 - 32; // 2,016: G <= 128, two blocks per lane
-constexpr uint64_t kSlotWindow4Max = 256 * 16 - 32; // 4,064: G <= 256, four blocks per lane
+// one block per lane up to 992 B (G <= 64), two up to 2,016 (G <= 128),
+// four up to 4,064 (G <= 256)
+constexpr uint64_t kSlotWindow4Max = 256 * 16 - 32;
 // Rounds per iteration (their loads in flight together): 8 for one frame per
 // round (slots over 480 B), 4 for more (16 M x 256 B receive 1.686 -> 1.620
 // ms; 12 or 16 rounds: 3.3 ms; 8 M x 512 B at 4 rounds 1.59 -> 1.76 ms).

@@ -125,6 +125,64 @@ def test_gpu_h2_serialize_random(S):
     assert bad.size == 0, bad[:10]
 
 
+@pytest.mark.gpu
+@pytest.mark.skipif(not gpu_present(), reason="needs the MI355X")
+@pytest.mark.parametrize("n", [1, 255, 256, 257, 65536, 65537, 524288, 524289])
+def test_gpu_h2_serialize_plan_grid_sizes(n):
+    """The send plan around its block bounds (256 frames per block; past
+    2,048 blocks a scan launch between reduce and apply), called twice on
+    the same arenas."""
+    rng = np.random.default_rng(n)
+    payload = O.fill_splitmix(1 << 20, 77, 0)
+    d = np.zeros(n, dtype=O.DESC_DTYPE)
+    d["payload_size"] = rng.choice([0, 1, 125, 126, 3000, 16376, 20000] if n < 65536 else [0, 1, 125, 126, 300], n)
+    d["payload_off"] = rng.integers(0, (1 << 20) - 20000, n).astype(np.uint64)
+    d["mask"] = (rng.random(n) < .7).astype(np.uint8)
+    d["mask_key"] = rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32) * d["mask"]
+    d["fin"], d["opcode"] = 1, 2
+    exp, _ = O.h2_serialize_batch(payload, d, 3, 16384)
+    for _ in range(2):
+        got, t = gpu_h2_serialize(payload, d, 3, 16384)
+        assert t == len(exp)
+        assert np.array_equal(got, exp)
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not gpu_present(), reason="needs the MI355X")
+def test_gpu_h2_serialize_streams():
+    """Sends queued on two streams without a synchronize between them, each
+    checked against the oracle."""
+    torch, cfws = _gpu()
+    from coldforce_amd import workloads as W
+    rng = np.random.default_rng(5)
+    payload = O.fill_splitmix(1 << 20, 78, 0)
+    pay = torch.from_numpy(payload).cuda()
+    jobs = []
+    for j in range(2):
+        n = 20000 + 7 * j
+        d = np.zeros(n, dtype=O.DESC_DTYPE)
+        d["payload_size"] = rng.choice([0, 125, 126, 5000, 16376, 17000], n)
+        d["payload_off"] = rng.integers(0, (1 << 20) - 17000, n).astype(np.uint64)
+        d["mask"] = (rng.random(n) < .5).astype(np.uint8)
+        d["mask_key"] = rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32) * d["mask"]
+        d["fin"], d["opcode"] = 1, 2
+        exp, _ = O.h2_serialize_batch(payload, d, 1 + j, 16384)
+        _, wtotal = W.wire_layout(d)
+        wire = torch.empty(W.round16(wtotal) + 16, dtype=torch.uint8, device="cuda")
+        h2 = torch.empty(cfws.h2_wrapped_bound(wire.numel(), n, 16384), dtype=torch.uint8, device="cuda")
+        jobs.append((torch.cuda.Stream(), cfws.desc_to_device(d), wire, h2, exp, 1 + j))
+    torch.cuda.synchronize()
+    tots = [[], []]
+    for _ in range(6):
+        for j, (st, d_t, wire, h2, exp, sid) in enumerate(jobs):
+            with torch.cuda.stream(st):
+                tots[j].append(cfws.h2_serialize(pay, d_t, wire, h2, sid, 16384, stream=st))
+    torch.cuda.synchronize()
+    for j, (st, d_t, wire, h2, exp, sid) in enumerate(jobs):
+        assert all(int(t.item()) == len(exp) for t in tots[j])
+        assert np.array_equal(h2[:len(exp)].cpu().numpy(), exp)
+
+
 def _units(d, S):
     """Output lengths of the DATA frames the send makes (9 + slice)."""
     out = []
