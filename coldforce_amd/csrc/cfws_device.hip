@@ -295,6 +295,28 @@ deserialize_plan_reduce_kernel(const uint8_t* __restrict__ wire, uint64_t wire_s
 #endif
 constexpr int kSingleItemsSer = CFWS_SINGLE_ITEMS_SER;
 constexpr int kSingleItemsDeser = CFWS_SINGLE_ITEMS_DESER;
+// Threads per block of the single-pass plans (serialize, deserialize) and
+// of the fused deserialize. A block's look-back waits on the inclusive
+// frontier, which advances 64 blocks per poll round trip (about 2.3 us
+// under load: tools/plan_trace.py timed the serialize plan's blocks at
+// 5.2 us of loads, 6.6 us of look-back, 4.0 us of stores, 465 resident),
+// so a block of more frames moves the frontier further per round trip. On
+// 16 M x 256 B: serialize plan 305 -> 274 us at 512 threads (1,024: 128
+// VGPRs, spills); fused receive 1.95 -> 1.79 ms at 1,024 threads (512:
+// 1.87); step 3.84-3.87 -> 3.65-3.66 ms. 1 KiB and 3 KiB unchanged, and the
+// receive plan at 512 / 1,024 threads too (profiles/r05/plan_blocks_ab/).
+#ifndef CFWS_SER_PLAN_THREADS
+#define CFWS_SER_PLAN_THREADS 512
+#endif
+#ifndef CFWS_DE_PLAN_THREADS
+#define CFWS_DE_PLAN_THREADS 256
+#endif
+#ifndef CFWS_FUSED_THREADS
+#define CFWS_FUSED_THREADS 1024
+#endif
+constexpr int kSerPlanThreads = CFWS_SER_PLAN_THREADS;
+constexpr int kDePlanThreads = CFWS_DE_PLAN_THREADS;
+constexpr int kFusedThreads = CFWS_FUSED_THREADS;
 
 // The flag word the serialize plan leaves for the execute: 0 = in-region
 // edges (the single-pass plan found every frame qualifying), else not. It
@@ -302,7 +324,7 @@ constexpr int kSingleItemsDeser = CFWS_SINGLE_ITEMS_DESER;
 // look area (>= 64 words, and >= n / 256 + 1).
 uint32_t* ser_inreg_flag(const WsLayout& L, const void* ws, uint64_t n)
 {
-    return ws_ptr<uint32_t>(ws, L.look) + grid_for(n, uint64_t(kThreads) * kSingleItemsSer) + 1;
+    return ws_ptr<uint32_t>(ws, L.look) + grid_for(n, uint64_t(kSerPlanThreads) * kSingleItemsSer) + 1;
 }
 
 // CFWS_SER_INREG=0: the edge workgroups write every serialize edge chunk
@@ -336,6 +358,7 @@ __device__ __forceinline__ uint64_t wave_scan_items(const uint64_t (&v)[kSingleI
 
 // This block's exclusive prefix from the look-back, plus each wave's offset
 // within the block (s_wave: the waves' totals).
+template <int kNW = kWaves>
 __device__ __forceinline__ uint64_t single_block_prefix(uint32_t b, uint64_t wave_total, uint64_t* s_wave,
                                                         uint64_t* s_prefix, uint32_t* look)
 {
@@ -344,7 +367,7 @@ __device__ __forceinline__ uint64_t single_block_prefix(uint32_t b, uint64_t wav
     __syncthreads();
     uint64_t before = 0, all = 0;
 #pragma unroll
-    for (uint32_t w = 0; w < kWaves; ++w) {
+    for (uint32_t w = 0; w < (uint32_t)kNW; ++w) {
         if (w < wid) before += s_wave[w];
         all += s_wave[w];
     }
@@ -356,18 +379,37 @@ __device__ __forceinline__ uint64_t single_block_prefix(uint32_t b, uint64_t wav
     return *s_prefix + before;
 }
 
-__global__ void __launch_bounds__(kThreads)
+// CFWS_PLAN_TRACE builds (tools/plan_trace.py; never the shipped library):
+// per block ticket, wall-clock stamps at the ticket, after the loads and
+// the block scan, after the look-back, at the end.
+#ifndef CFWS_PLAN_TRACE
+#define CFWS_PLAN_TRACE 0
+#endif
+#if CFWS_PLAN_TRACE
+constexpr uint32_t kTraceBlocks = 1u << 16;
+__device__ uint64_t g_plan_trace[kTraceBlocks][4];
+#define PLAN_STAMP(b, i)                                                                       \
+    do {                                                                                       \
+        if (threadIdx.x == 0 && (b) < kTraceBlocks) g_plan_trace[(b)][(i)] = wall_clock64();   \
+    } while (0)
+#else
+#define PLAN_STAMP(b, i) do {} while (0)
+#endif
+
+template <int kBT>
+__global__ void __launch_bounds__(kBT)
 serialize_plan_single_kernel(cfws_frame_desc_t* __restrict__ desc, uint64_t* __restrict__ offs, uint64_t n,
                              uint32_t* __restrict__ look, uint64_t* __restrict__ hdr, uint64_t capacity,
                              uint32_t* __restrict__ map, uint64_t* __restrict__ user_total)
 {
-    __shared__ uint64_t s_wave[kWaves];
+    __shared__ uint64_t s_wave[kBT / 64];
     __shared__ uint64_t s_prefix;
     __shared__ uint32_t s_bid;
     constexpr int kSingleItems = kSingleItemsSer;
     static_assert(kSingleItems <= 16, "4-bit header sizes in one word");
-    constexpr uint64_t kSingleFrames = uint64_t(kThreads) * kSingleItems;
+    constexpr uint64_t kSingleFrames = uint64_t(kBT) * kSingleItems;
     const uint32_t b = plan_ticket(look, &s_bid);
+    PLAN_STAMP(b, 0);
     const uint64_t f0 = uint64_t(b) * kSingleFrames + uint64_t(threadIdx.x >> 6) * (64 * kSingleItems) +
                         (threadIdx.x & 63u);
     uint64_t v[kSingleItems], ex[kSingleItems];
@@ -397,7 +439,10 @@ serialize_plan_single_kernel(cfws_frame_desc_t* __restrict__ desc, uint64_t* __r
         hsp |= uint64_t(hs) << (4 * k);
         v[k] = f < n ? hs + len[k] : 0;
     }
-    const uint64_t pre = single_block_prefix(b, wave_scan_items(v, ex), s_wave, &s_prefix, look);
+    const uint64_t wt = wave_scan_items(v, ex);
+    PLAN_STAMP(b, 1);
+    const uint64_t pre = single_block_prefix<kBT / 64>(b, wt, s_wave, &s_prefix, look);
+    PLAN_STAMP(b, 2);
 #pragma unroll
     for (int k = 0; k < kSingleItems; ++k) {
         const uint64_t f = f0 + uint64_t(k) * 64;
@@ -423,6 +468,7 @@ serialize_plan_single_kernel(cfws_frame_desc_t* __restrict__ desc, uint64_t* __r
     // in-region edges only when every frame qualifies (look[gridDim.x + 1],
     // zeroed with the tickets)
     if (__syncthreads_or(bad) && threadIdx.x == 0) atomicOr(look + gridDim.x + 1, 1u);
+    PLAN_STAMP(b, 3);
 }
 
 // ---- the fused deserialize: plan and copy in one pass ------------------------
@@ -584,8 +630,8 @@ __device__ __forceinline__ uint4 ld16u(const uint8_t* p)
 #endif
 constexpr int kFusedItems = CFWS_FUSED_ITEMS;   // frames per thread in the fused form (registers)
 
-template <bool kCopy>
-__global__ void __launch_bounds__(kThreads, kCopy ? CFWS_FUSED_MIN_BLOCKS : 1)
+template <bool kCopy, int kBT>
+__global__ void __launch_bounds__(kBT, kCopy ? CFWS_FUSED_MIN_BLOCKS * 256 / kBT : 1)
 deserialize_plan_single_kernel(const uint8_t* __restrict__ wire, uint64_t wire_size_all,
                                const uint64_t* __restrict__ index, const uint64_t* __restrict__ ends,
                                uint64_t n, uint64_t max_payload, uint64_t align,
@@ -594,12 +640,13 @@ deserialize_plan_single_kernel(const uint8_t* __restrict__ wire, uint64_t wire_s
                                uint64_t* __restrict__ hdr, uint64_t capacity, uint32_t* __restrict__ map,
                                uint64_t* __restrict__ user_total, uint8_t* __restrict__ out = nullptr)
 {
-    __shared__ uint64_t s_wave[kWaves];
+    __shared__ uint64_t s_wave[kBT / 64];
     __shared__ uint64_t s_prefix;
     __shared__ uint32_t s_bid;
     constexpr int kSingleItems = kCopy ? kFusedItems : kSingleItemsDeser;
-    constexpr uint64_t kSingleFrames = uint64_t(kThreads) * kSingleItems;
+    constexpr uint64_t kSingleFrames = uint64_t(kBT) * kSingleItems;
     const uint32_t b = plan_ticket(look, &s_bid);
+    if (kCopy) PLAN_STAMP(b, 0);
     const uint64_t f0 = uint64_t(b) * kSingleFrames + uint64_t(threadIdx.x >> 6) * (64 * kSingleItems) +
                         (threadIdx.x & 63u);
     // each descriptor is written once, whole, with its offset: the parsed
@@ -662,7 +709,10 @@ deserialize_plan_single_kernel(const uint8_t* __restrict__ wire, uint64_t wire_s
             v[k] = (len + align - 1) & ~(align - 1);
         }
     }
-    const uint64_t pre = single_block_prefix(b, wave_scan_items(v, ex), s_wave, &s_prefix, look);
+    const uint64_t wt = wave_scan_items(v, ex);
+    if (kCopy) PLAN_STAMP(b, 1);
+    const uint64_t pre = single_block_prefix<kBT / 64>(b, wt, s_wave, &s_prefix, look);
+    if (kCopy) PLAN_STAMP(b, 2);
     // kCopy: what the copy needs per item, compact (the parse's arrays die here)
     uint64_t c_run[kSingleItems], c_src[kSingleItems];
     uint32_t c_len[kSingleItems], c_nb[kSingleItems], c_key[kSingleItems];
@@ -714,6 +764,10 @@ deserialize_plan_single_kernel(const uint8_t* __restrict__ wire, uint64_t wire_s
 #pragma unroll
     for (int k = 0; k < kSingleItems; ++k)
         fused_item(wire, out, capacity, c_run[k], c_src[k], c_len[k], c_nb[k], c_key[k], lane);
+#if CFWS_PLAN_TRACE
+    __syncthreads();
+    PLAN_STAMP(b, 3);
+#endif
 }
 
 // The fused deserialize (deserialize_plan_single_kernel<true>) for batches
@@ -1282,10 +1336,10 @@ int deserialize_plan_impl(const void* d_wire, uint64_t wire_size, const uint64_t
     const uint32_t nb = grid_for(n, kPlanBlock);
     if (!reasm && nb > kSelfScanBlocks && plan_single()) {
         uint32_t* look = ws_ptr<uint32_t>(ws, L.look);
-        const uint32_t sb = grid_for(n, uint64_t(kThreads) * kSingleItemsDeser);
+        const uint32_t sb = grid_for(n, uint64_t(kDePlanThreads) * kSingleItemsDeser);
         if (hipMemsetAsync(look, 0, look_bytes(sb), st) != hipSuccess)
             return launch_check("deserialize_plan");
-        deserialize_plan_single_kernel<false><<<sb, kThreads, 0, st>>>(
+        deserialize_plan_single_kernel<false, kDePlanThreads><<<sb, kDePlanThreads, 0, st>>>(
             static_cast<const uint8_t*>(d_wire), wire_size, d_index, d_ends, n, max_payload, align, d_desc,
             d_status, offs0, look, hdr, cap, ws_ptr<uint32_t>(ws, L.map[0]), d_total);
         return launch_check("deserialize_plan");
@@ -1338,10 +1392,10 @@ int cfws_serialize_plan(cfws_frame_desc_t* d_desc, size_t n, uint64_t cap, uint6
     const uint32_t self_scan = nb <= kSelfScanBlocks ? 1u : 0u;
     if (!self_scan && plan_single()) {
         uint32_t* look = ws_ptr<uint32_t>(ws, L.look);
-        const uint32_t sb = grid_for(n, uint64_t(kThreads) * kSingleItemsSer);
+        const uint32_t sb = grid_for(n, uint64_t(kSerPlanThreads) * kSingleItemsSer);
         if (hipMemsetAsync(look, 0, look_bytes(sb), st) != hipSuccess)
             return launch_check("serialize_plan");
-        serialize_plan_single_kernel<<<sb, kThreads, 0, st>>>(d_desc, offs, n, look, hdr, cap,
+        serialize_plan_single_kernel<kSerPlanThreads><<<sb, kSerPlanThreads, 0, st>>>(d_desc, offs, n, look, hdr, cap,
                                                               ws_ptr<uint32_t>(ws, L.map[0]), d_total);
         return launch_check("serialize_plan");
     }
@@ -1452,14 +1506,14 @@ int cfws_deserialize_batch(const void* d_wire, uint64_t wire_size, const uint64_
         const WsLayout L = ws_layout(n, cap);
         hipStream_t st = static_cast<hipStream_t>(stream);
         uint32_t* look = ws_ptr<uint32_t>(ws, L.look);
-        const uint32_t sb = grid_for(n, uint64_t(kThreads) * kFusedItems);
+        const uint32_t sb = grid_for(n, uint64_t(kFusedThreads) * kFusedItems);
         if (hipMemsetAsync(look, 0, look_bytes(sb), st) != hipSuccess)
             return launch_check("deserialize_batch(fused)");
         CfwsPassEvents& pe = cfws_internal_pass_events();
         const CfwsPassEvents timed = pe;
         pe = {nullptr, nullptr};
         if (timed.start) (void)hipEventRecord(static_cast<hipEvent_t>(timed.start), st);
-        deserialize_plan_single_kernel<true><<<sb, kThreads, 0, st>>>(
+        deserialize_plan_single_kernel<true, kFusedThreads><<<sb, kFusedThreads, 0, st>>>(
             static_cast<const uint8_t*>(d_wire), wire_size, d_index, nullptr, n, max_payload, align, d_desc,
             d_status, nullptr, look, ws_ptr<uint64_t>(ws, L.hdr), cap, nullptr, d_total,
             static_cast<uint8_t*>(d_payload));
@@ -1530,5 +1584,14 @@ int cfws_deserialize_slots(const void* d_wire, uint64_t wire_size, const uint64_
     if (timed.stop) (void)hipEventRecord(static_cast<hipEvent_t>(timed.stop), st);
     return launch_check("deserialize_slots");
 }
+
+#if CFWS_PLAN_TRACE
+// tools/plan_trace.py: the last traced launch's stamps, blocks [0, n)
+int cfws_debug_plan_trace(void* out, size_t n)
+{
+    if (n > kTraceBlocks) n = kTraceBlocks;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_plan_trace), n * 4 * sizeof(uint64_t)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 }  // extern "C"
