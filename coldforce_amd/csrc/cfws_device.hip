@@ -646,7 +646,7 @@ deserialize_plan_single_kernel(const uint8_t* __restrict__ wire, uint64_t wire_s
     constexpr int kSingleItems = kCopy ? kFusedItems : kSingleItemsDeser;
     constexpr uint64_t kSingleFrames = uint64_t(kBT) * kSingleItems;
     const uint32_t b = plan_ticket(look, &s_bid);
-    if (kCopy) PLAN_STAMP(b, 0);
+    PLAN_STAMP(b, 0);
     const uint64_t f0 = uint64_t(b) * kSingleFrames + uint64_t(threadIdx.x >> 6) * (64 * kSingleItems) +
                         (threadIdx.x & 63u);
     // each descriptor is written once, whole, with its offset: the parsed
@@ -710,9 +710,9 @@ deserialize_plan_single_kernel(const uint8_t* __restrict__ wire, uint64_t wire_s
         }
     }
     const uint64_t wt = wave_scan_items(v, ex);
-    if (kCopy) PLAN_STAMP(b, 1);
+    PLAN_STAMP(b, 1);
     const uint64_t pre = single_block_prefix<kBT / 64>(b, wt, s_wave, &s_prefix, look);
-    if (kCopy) PLAN_STAMP(b, 2);
+    PLAN_STAMP(b, 2);
     // kCopy: what the copy needs per item, compact (the parse's arrays die here)
     uint64_t c_run[kSingleItems], c_src[kSingleItems];
     uint32_t c_len[kSingleItems], c_nb[kSingleItems], c_key[kSingleItems];
@@ -757,7 +757,13 @@ deserialize_plan_single_kernel(const uint8_t* __restrict__ wire, uint64_t wire_s
             if (user_total) *user_total = t;
         }
     }
-    if (!kCopy) return;
+    if (!kCopy) {
+#if CFWS_PLAN_TRACE
+        __syncthreads();
+        PLAN_STAMP(b, 3);
+#endif
+        return;
+    }
     // the copy: every slot byte below the pass total min(grand total,
     // capacity), cut at the capacity itself (above)
     const uint32_t lane = threadIdx.x & 63u;

@@ -62,8 +62,8 @@ for rep in range(3):
     cfws.serialize_plan(d_t, wire.numel(), tot, ws)
     torch.cuda.synchronize()
 ITEMS = int(os.environ.get("TRACE_ITEMS", "8"))
-SER_T = int(os.environ.get("TRACE_SER_THREADS", "256"))
-FUSED_T = int(os.environ.get("TRACE_FUSED_THREADS", "256"))
+SER_T = int(os.environ.get("TRACE_SER_THREADS", "512"))
+FUSED_T = int(os.environ.get("TRACE_FUSED_THREADS", "1024"))
 sb = (F + SER_T * ITEMS - 1) // (SER_T * ITEMS)
 out["serialize_plan"] = trace(sb)
 cfws.serialize_execute(payload, d_t, wire, ws)
@@ -71,5 +71,11 @@ torch.cuda.synchronize()
 for rep in range(3):
     cfws.deserialize(wire, total, idx, back, ws_t=ws_de, align=16)
     torch.cuda.synchronize()
-out["fused_receive"] = trace((F + 2 * FUSED_T - 1) // (2 * FUSED_T))
+# the fused receive (frames averaging <= 512 B of wire), else the receive
+# plan (deserialize_plan_single_kernel<false>, traced the same way)
+DE_T = int(os.environ.get("TRACE_DE_THREADS", "256"))
+if total // F <= 512:
+    out["fused_receive"] = trace((F + 2 * FUSED_T - 1) // (2 * FUSED_T))
+else:
+    out["receive_plan"] = trace((F + 8 * DE_T - 1) // (8 * DE_T))
 print(json.dumps(out))
