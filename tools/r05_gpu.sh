@@ -70,6 +70,8 @@ for s in "$@"; do
     ab_wide) for w in "16777216 256" "4194304 1024" "1398101 3072"; do set -- $w; step ab_wide_$2 900 env TAG=$TAG/ab_wide_$2 VARIANTS="base wide" ARGS="--frames $1 --frame-size $2" bash $R/tools/ab.sh; done ;;
     ab_plan) for w in "16777216 256" "4194304 1024" "1398101 3072"; do set -- $w; step ab_plan_$2 900 env TAG=$TAG/ab_plan_$2 VARIANTS="${VPLAN:-base}" ARGS="--frames $1 --frame-size $2" bash $R/tools/ab.sh; done ;;
     ab_fused256) step ab_fused256 900 env TAG=$TAG/ab_fused256 VARIANTS="${VF:-base}" ARGS="--frames 16777216 --frame-size 256" bash $R/tools/ab.sh ;;
+    envab_fused512) step envab_fused512 600 env TAG=$TAG/envab_fused512 ENVS="X=0;CFWS_FUSED_AVG_MAX=600" ARGS="--frames 8388608 --frame-size 512" bash $R/tools/envab.sh ;;
+    envab_fused1k) step envab_fused1k 600 env TAG=$TAG/envab_fused1k ENVS="X=0;CFWS_FUSED_AVG_MAX=1100" ARGS="--frames 4194304 --frame-size 1024" bash $R/tools/envab.sh ;;
     fs256) step fs256 200 python3 $R/bench.py --frames 16777216 --frame-size 256 --no-cpu-baseline ;;
     kstats_fs256) step kstats_fs256 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kstats_fs256" -o ks -- python3 $R/bench.py --frames 16777216 --frame-size 256 --steps 10 --warmup 3 --no-cpu-baseline ;;
     fs2k) step fs2k 200 python3 $R/bench.py --frames 2097152 --frame-size 2048 --no-cpu-baseline ;;
