@@ -880,9 +880,17 @@ deserialize_slots_window_kernel(const uint8_t* __restrict__ wire, uint64_t wire_
                                 uint64_t* __restrict__ user_total)
 {
     const uint32_t lane = threadIdx.x & 63u;
-    // kSub = 2 / 4: one frame per round over 64 < G <= 64 kSub blocks, lane c
-    // holding blocks c, 64 + c, ...
-    const uint32_t P = kSub > 1 ? 1u : 64u / G, g = kSub > 1 ? 0u : lane / G, c = lane - g * G;
+    // kSub sub-windows of 64 lanes make 64 kSub virtual lanes, v = 64 sw +
+    // lane; frame g of a round takes virtual lanes [g G, g G + G), P = 64 kSub
+    // / G frames, so lane `lane` of sub-window sw holds block c[sw] of the
+    // round's frame g[sw]
+    const uint32_t P = 64u * kSub / G;
+    uint32_t g[kSub], c[kSub];
+#pragma unroll
+    for (int sw = 0; sw < kSub; ++sw) {
+        g[sw] = (64u * sw + lane) / G;
+        c[sw] = 64u * sw + lane - g[sw] * G;
+    }
     const uint32_t R = P * kSlotRounds <= 64 ? (uint32_t)kSlotRounds : 64u / P;
     const uint64_t FI = uint64_t(R) * P;                 // frames per wave-iteration
     const uint64_t stride = uint64_t(gridDim.x) * kWaves * FI;
@@ -897,13 +905,12 @@ deserialize_slots_window_kernel(const uint8_t* __restrict__ wire, uint64_t wire_
         uint4 A[kSlotRounds][kSub];
 #pragma unroll
         for (int u = 0; u < kSlotRounds; ++u) {
-            const uint32_t src = (uint32_t)u * P + g;
-            const uint64_t wo = shfl64(wl, (int)(src < 64 ? src : 63));
 #pragma unroll
             for (int sw = 0; sw < kSub; ++sw) {
-                const uint32_t cb = 64u * sw + c;   // block of the window
-                const uint64_t blk = (wo & ~uint64_t(15)) + 16ull * cb;
-                A[u][sw] = (uint32_t)u < R && g < P && cb < G && wo < wire_size && blk < wire_size
+                const uint32_t src = (uint32_t)u * P + g[sw];
+                const uint64_t wo = shfl64(wl, (int)(src < 64 ? src : 63));
+                const uint64_t blk = (wo & ~uint64_t(15)) + 16ull * c[sw];   // block c of the window
+                A[u][sw] = (uint32_t)u < R && g[sw] < P && wo < wire_size && blk < wire_size
                                ? ld16(wire + blk) : z;
             }
         }
@@ -935,13 +942,13 @@ deserialize_slots_window_kernel(const uint8_t* __restrict__ wire, uint64_t wire_
 #pragma unroll
         for (int u = 0; u < kSlotRounds; ++u) {
             if ((uint32_t)u >= R) break;   // wave-uniform
-            const uint32_t src = (uint32_t)u * P + g;
-            const int s = (int)(src < 64 ? src : 63);
-            const uint32_t inf = (uint32_t)__shfl((int)info, s, 64);
-            const uint32_t k = (uint32_t)__shfl((int)key, s, 64);
-            const uint32_t len = inf & 0xffffu, off = inf >> 16;
 #pragma unroll
             for (int sw = 0; sw < kSub; ++sw) {
+                const uint32_t src = (uint32_t)u * P + g[sw];
+                const int s = (int)(src < 64 ? src : 63);
+                const uint32_t inf = (uint32_t)__shfl((int)info, s, 64);
+                const uint32_t k = (uint32_t)__shfl((int)key, s, 64);
+                const uint32_t len = inf & 0xffffu, off = inf >> 16;
                 // blocks c + 1 and c + 2 of this sub-window, by DPP (every
                 // lane); lanes 62 and 63 of a sub-window take the next one's
                 // first two blocks
@@ -949,8 +956,8 @@ deserialize_slots_window_kernel(const uint8_t* __restrict__ wire, uint64_t wire_
                 const uint4 l1 = sw + 1 < kSub ? shfl16(A[u][sw + 1 < kSub ? sw + 1 : sw], 1) : z;
                 const uint4 n1 = from_next_lane(A[u][sw], l0);
                 const uint4 n2 = from_next_lane(n1, l1);
-                const uint32_t q = 64u * sw + c;   // payload chunk
-                if (g < P && 16u * q < len) {
+                const uint32_t q = c[sw];          // payload chunk
+                if (g[sw] < P && 16u * q < len) {
                     const bool k1 = off >= 16;
                     const uint4 B0 = k1 ? n1 : A[u][sw], B1 = k1 ? n2 : n1;
                     const uint32_t sh = off & 15u;
@@ -1000,6 +1007,19 @@ deserialize_slots_kernel(const uint8_t* __restrict__ wire, uint64_t wire_size, c
         }
     }
     fused_item<kSlotUnroll>(wire, out, capacity, run, src, len, nb, key, threadIdx.x & 63u);
+}
+
+// Frames of at least CFWS_SLOT_SUB2_G lanes (default 33: slots of 496
+// bytes and more) that fit three to a 128-lane pair of sub-windows (up to
+// 42 lanes: slots up to 640 bytes) pack two sub-windows per round instead of
+// one frame per round. Receive, two sub-windows against one: 512 B 1.535 ->
+// 1.498 ms; 768 B (two frames per pair) 1.447 -> 1.490; 256 B and 384 B
+// (already 2-3 frames per sub-window) 1.508 -> 1.552, 1.473 -> 1.506
+// (profiles/r05/slots/sub2_ab/). A/B knob; 65 turns the packing off.
+uint32_t slot_sub2_g()
+{
+    static const uint32_t v = (uint32_t)env_knob("CFWS_SLOT_SUB2_G", 33);
+    return v;
 }
 
 bool slots_window()
@@ -1560,8 +1580,10 @@ int cfws_deserialize_slots(const void* d_wire, uint64_t wire_size, const uint64_
     if (slot <= kSlotWindow4Max && slots_window()) {
         // one wave-iteration of R P frames per wave (CFWS_SLOT_GRID caps the
         // workgroups: a grid-stride loop; A/B knob)
-        const uint32_t G = (uint32_t)(slot / 16 + 2), P = G > 64 ? 1 : 64 / G;
-        const uint64_t RK = G > 128 ? CFWS_SLOT_ROUNDS4 : G > 64 ? CFWS_SLOT_ROUNDS2
+        const uint32_t G = (uint32_t)(slot / 16 + 2);
+        const uint32_t S = G > 128 ? 4 : G > 64 || (G >= slot_sub2_g() && 128 / G >= 3) ? 2 : 1;   // sub-windows
+        const uint32_t P = 64 * S / G;
+        const uint64_t RK = S == 4 ? CFWS_SLOT_ROUNDS4 : S == 2 ? CFWS_SLOT_ROUNDS2
                             : P > 1 ? CFWS_SLOT_ROUNDS_MULTI : CFWS_SLOT_ROUNDS;
         const uint64_t R = P * RK <= 64 ? RK : 64 / P;
         const uint64_t per_block = uint64_t(kWaves) * R * P;
@@ -1571,10 +1593,10 @@ int cfws_deserialize_slots(const void* d_wire, uint64_t wire_size, const uint64_
         }();
         const uint64_t want = (n + per_block - 1) / per_block;
         const uint32_t grid = (uint32_t)(want < cap_blocks ? want : cap_blocks);
-        if (G > 128)
+        if (S == 4)
             deserialize_slots_window_kernel<CFWS_SLOT_ROUNDS4, 4><<<grid, kThreads, 0, st>>>(
                 w, wire_size, d_index, n, max_payload, slot, G, d_desc, d_status, out, cap, d_total);
-        else if (G > 64)
+        else if (S == 2)
             deserialize_slots_window_kernel<CFWS_SLOT_ROUNDS2, 2><<<grid, kThreads, 0, st>>>(
                 w, wire_size, d_index, n, max_payload, slot, G, d_desc, d_status, out, cap, d_total);
         else if (P > 1)
