@@ -1022,6 +1022,14 @@ uint32_t slot_sub2_g()
     return v;
 }
 
+// The same for four sub-windows: frames of CFWS_SLOT_SUB4_G (default 129:
+// off) to 85 lanes, three to 256 virtual lanes (A/B knob)
+uint32_t slot_sub4_g()
+{
+    static const uint32_t v = (uint32_t)env_knob("CFWS_SLOT_SUB4_G", 129);
+    return v;
+}
+
 bool slots_window()
 {
     static const bool v = env_knob("CFWS_SLOTS_WINDOW", 1) != 0;
@@ -1581,7 +1589,8 @@ int cfws_deserialize_slots(const void* d_wire, uint64_t wire_size, const uint64_
         // one wave-iteration of R P frames per wave (CFWS_SLOT_GRID caps the
         // workgroups: a grid-stride loop; A/B knob)
         const uint32_t G = (uint32_t)(slot / 16 + 2);
-        const uint32_t S = G > 128 ? 4 : G > 64 || (G >= slot_sub2_g() && 128 / G >= 3) ? 2 : 1;   // sub-windows
+        const uint32_t S = G > 128 || (G >= slot_sub4_g() && 256 / G >= 3) ? 4
+                           : G > 64 || (G >= slot_sub2_g() && 128 / G >= 3) ? 2 : 1;   // sub-windows
         const uint32_t P = 64 * S / G;
         const uint64_t RK = S == 4 ? CFWS_SLOT_ROUNDS4 : S == 2 ? CFWS_SLOT_ROUNDS2
                             : P > 1 ? CFWS_SLOT_ROUNDS_MULTI : CFWS_SLOT_ROUNDS;
