@@ -5,7 +5,9 @@
  *   client side:  payloads (pinned host) -> H2D -> cfws_serialize_batch
  *                 (mask keys drawn like co_ws_frame_serialize draws them)
  *   server side:  cfws_index_frames_batch over the wire as one connection's
- *                 receive buffer -> cfws_deserialize_batch -> D2H payloads
+ *                 receive buffer -> cfws_deserialize_batch -> D2H payloads,
+ *                 and the same frames through cfws_deserialize_slots (frame
+ *                 i's payload at i * slot)
  *
  * Checks that every payload comes back and that the wire equals what
  * sequential co_ws_frame_serialize calls (the drop-in, same library) append
@@ -141,9 +143,26 @@ int main(int argc, char** argv)
     int ok = same && n_found == n && consumed == wire_total && stop == CFWS_PARSE_COMPLETE &&
              back_total == arena && memcmp(back, payload, arena) == 0;
     for (size_t i = 0; ok && i < n; ++i) ok = status[i] == CFWS_PARSE_COMPLETE;
+
+    /* the same frames into fixed slots of the largest payload, 16-aligned */
+    const uint64_t slot = max_len < 16 ? 16 : (max_len + 15) / 16 * 16;
+    void* d_slots;
+    CHECK(hipMalloc(&d_slots, n * slot));
+    CHECK(cfws_deserialize_slots(d_wire, wire_total, d_starts, n_found, CFWS_DEFAULT_MAX_RECEIVE_PAYLOAD_SIZE,
+                                 slot, d_desc2, d_status, d_slots, n * slot, d_total, st));
+    uint64_t slots_total = 0;
+    CHECK(hipMemcpyAsync(&slots_total, d_total, 8, hipMemcpyDeviceToHost, st));
+    CHECK(hipStreamSynchronize(st));
+    uint8_t* slots = malloc(n * slot);
+    CHECK(hipMemcpy(slots, d_slots, n * slot, hipMemcpyDeviceToHost));
+    CHECK(hipMemcpy(status, d_status, n * sizeof *status, hipMemcpyDeviceToHost));
+    int slots_ok = n_found == n && slots_total == n * slot;
+    for (size_t i = 0; slots_ok && i < n; ++i)
+        slots_ok = status[i] == CFWS_PARSE_COMPLETE &&
+                   memcmp(slots + i * slot, payload + desc[i].payload_off, desc[i].payload_size) == 0;
     printf("{\"frames\": %zu, \"payload_bytes\": %llu, \"wire_bytes\": %llu, "
-           "\"wire_equals_dropin\": %s, \"indexed\": %llu, \"roundtrip\": %s}\n",
+           "\"wire_equals_dropin\": %s, \"indexed\": %llu, \"roundtrip\": %s, \"slots\": %s}\n",
            n, (unsigned long long)arena, (unsigned long long)wire_total, same ? "true" : "false",
-           (unsigned long long)n_found, ok ? "true" : "false");
-    return ok ? 0 : 2;
+           (unsigned long long)n_found, ok ? "true" : "false", slots_ok ? "true" : "false");
+    return ok && slots_ok ? 0 : 2;
 }
