@@ -803,7 +803,7 @@ def main():
     achieved = alg_bytes / (dom_ms * 1e-3) / 1e9
     kernel_symbol = ("xform_kernel<0>" if dom_name == "serialize_execute"   # kModeSer
                      else "deserialize_plan_single_kernel<true>" if fused_de  # fused plan + copy
-                     else "deserialize_slots_window_kernel" if 0 < slot <= 4064  # fixed slots
+                     else "deserialize_slots_window_kernel" if 0 < slot <= 8160  # fixed slots
                      else "deserialize_slots_kernel" if slot
                      else "xform_kernel<1>")                                 # kModeDeser
     # the PMC summary a traffic figure may come from: the same workload only

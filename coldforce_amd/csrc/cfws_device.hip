@@ -821,8 +821,8 @@ uint64_t fused_avg_max()
 // wire's end are not loaded. The first form parsed in every lane of every
 // round (480 instructions per 3 frames at 256 B) and ran at 5.2 TB/s.
 // one block per lane up to 992 B (G <= 64), two up to 2,016 (G <= 128),
-// four up to 4,064 (G <= 256)
-constexpr uint64_t kSlotWindow4Max = 256 * 16 - 32;
+// four up to 4,064 (G <= 256), eight up to 8,160 (G <= 512)
+constexpr uint64_t kSlotWindow8Max = 512 * 16 - 32;   // eight blocks per lane up to 8,160 B
 // Rounds per iteration (their loads in flight together): 8 for one frame per
 // round (slots over 480 B), 4 for more (16 M x 256 B receive 1.686 -> 1.620
 // ms; 12 or 16 rounds: 3.3 ms; 8 M x 512 B at 4 rounds 1.59 -> 1.76 ms).
@@ -834,6 +834,9 @@ constexpr uint64_t kSlotWindow4Max = 256 * 16 - 32;
 #endif
 #ifndef CFWS_SLOT_ROUNDS2
 #define CFWS_SLOT_ROUNDS2 4      // two blocks per lane (1,008-2,016 B): 2,016 B 2 / 4 / 6 -> 1.61-1.62 / 1.61 / 1.63 ms
+#endif
+#ifndef CFWS_SLOT_ROUNDS8
+#define CFWS_SLOT_ROUNDS8 1      // eight blocks per lane (4,080-8,160 B)
 #endif
 #ifndef CFWS_SLOT_ROUNDS4
 #define CFWS_SLOT_ROUNDS4 1      // four blocks per lane (2,032-4,064 B): 3 KiB 1 / 2 / 4 -> 1.48 / 1.55 / 1.59 ms
@@ -976,7 +979,7 @@ deserialize_slots_window_kernel(const uint8_t* __restrict__ wire, uint64_t wire_
 #endif
 constexpr int kSlotUnroll = CFWS_SLOT_UNROLL;   // deserialize_slots_kernel: rounds of loads in flight
 
-// Slots over kSlotWindowMax: one frame per thread parsed (its header line
+// Slots over kSlotWindow8Max: one frame per thread parsed (its header line
 // fetched twice, a small share of a frame this long), the payloads copied
 // by fused_item.
 __global__ void __launch_bounds__(kThreads)
@@ -1585,14 +1588,15 @@ int cfws_deserialize_slots(const void* d_wire, uint64_t wire_size, const uint64_
     if (timed.start) (void)hipEventRecord(static_cast<hipEvent_t>(timed.start), st);
     const uint8_t* w = static_cast<const uint8_t*>(d_wire);
     uint8_t* out = static_cast<uint8_t*>(d_payload);
-    if (slot <= kSlotWindow4Max && slots_window()) {
+    if (slot <= kSlotWindow8Max && slots_window()) {
         // one wave-iteration of R P frames per wave (CFWS_SLOT_GRID caps the
         // workgroups: a grid-stride loop; A/B knob)
         const uint32_t G = (uint32_t)(slot / 16 + 2);
-        const uint32_t S = G > 128 || (G >= slot_sub4_g() && 256 / G >= 3) ? 4
+        const uint32_t S = G > 256 ? 8
+                           : G > 128 || (G >= slot_sub4_g() && 256 / G >= 3) ? 4
                            : G > 64 || (G >= slot_sub2_g() && 128 / G >= 3) ? 2 : 1;   // sub-windows
         const uint32_t P = 64 * S / G;
-        const uint64_t RK = S == 4 ? CFWS_SLOT_ROUNDS4 : S == 2 ? CFWS_SLOT_ROUNDS2
+        const uint64_t RK = S == 8 ? CFWS_SLOT_ROUNDS8 : S == 4 ? CFWS_SLOT_ROUNDS4 : S == 2 ? CFWS_SLOT_ROUNDS2
                             : P > 1 ? CFWS_SLOT_ROUNDS_MULTI : CFWS_SLOT_ROUNDS;
         const uint64_t R = P * RK <= 64 ? RK : 64 / P;
         const uint64_t per_block = uint64_t(kWaves) * R * P;
@@ -1602,7 +1606,10 @@ int cfws_deserialize_slots(const void* d_wire, uint64_t wire_size, const uint64_
         }();
         const uint64_t want = (n + per_block - 1) / per_block;
         const uint32_t grid = (uint32_t)(want < cap_blocks ? want : cap_blocks);
-        if (S == 4)
+        if (S == 8)
+            deserialize_slots_window_kernel<CFWS_SLOT_ROUNDS8, 8><<<grid, kThreads, 0, st>>>(
+                w, wire_size, d_index, n, max_payload, slot, G, d_desc, d_status, out, cap, d_total);
+        else if (S == 4)
             deserialize_slots_window_kernel<CFWS_SLOT_ROUNDS4, 4><<<grid, kThreads, 0, st>>>(
                 w, wire_size, d_index, n, max_payload, slot, G, d_desc, d_status, out, cap, d_total);
         else if (S == 2)

@@ -144,7 +144,7 @@ def main():
                 b = TS.GuardBuf(n, flush_end, TS.SENT)
                 bufs.append(b)
                 return b
-            for slot in (16, 256, 992, 1504, 4064):
+            for slot in (16, 256, 992, 1504, 4064, 8160):
                 for seed in (21, 22):
                     TS.test_slots_mixed(make, seed, slot)
             TS.test_slots_capacity_cuts(make)

@@ -10,7 +10,7 @@ payload arena at round16(capacity), and bytes past the capacity, past each
 payload's 16-byte round-up and in the slots of non-COMPLETE frames are
 checked to keep their sentinel. Slots up to 992 bytes take the window
 kernel with one block per lane, up to 2,016 with two, up to 4,064 with
-four, larger ones the per-frame kernel."""
+four, up to 8,160 with eight, larger ones the per-frame kernel."""
 import random
 
 import numpy as np
@@ -111,7 +111,7 @@ def _wire_of(payload, desc):
     return wire, starts
 
 
-@pytest.mark.parametrize("slot", [16, 48, 80, 256, 512, 992, 1008, 1504, 2016, 2032, 3008, 4064, 4080, 8192])
+@pytest.mark.parametrize("slot", [16, 48, 80, 256, 512, 992, 1008, 1504, 2016, 2032, 3008, 4064, 4080, 6000, 8160, 8176])
 @pytest.mark.parametrize("seed", [21, 22])
 def test_slots_mixed(guards, seed, slot):
     """6,000 frames of 30-80 B (masked and not, data and control) with a
@@ -127,14 +127,14 @@ def test_slots_mixed(guards, seed, slot):
 
 
 @pytest.mark.parametrize("flush_end", [True, False], ids=["end", "start"])
-@pytest.mark.parametrize("slot", [256, 1504, 3008, 4096])
+@pytest.mark.parametrize("slot", [256, 1504, 3008, 4096, 8208])
 def test_slots_guard_start(guards, slot, flush_end):
     payload, desc = _seed21_batch(25)
     wire, starts = _wire_of(payload, desc)
     run_slots(guards, wire, starts, slot, flush_end=flush_end)
 
 
-@pytest.mark.parametrize("fs", [0, 1, 125, 126, 240, 256, 977, 992, 1000, 1024, 2000, 2016, 2017, 3072, 4064, 4065, 65536])
+@pytest.mark.parametrize("fs", [0, 1, 125, 126, 240, 256, 977, 992, 1000, 1024, 2000, 2016, 2017, 3072, 4064, 4065, 8160, 8161, 65536])
 def test_slots_uniform(guards, fs):
     """Uniform batches at slot = round16(fs) (at least 16): the bench's shape,
     every frame COMPLETE and every slot full."""
@@ -182,7 +182,7 @@ def test_slots_any_index(guards):
     idx += list(starts[:500])
     rng.shuffle(idx)
     idx = np.array(idx, dtype=np.uint64)
-    for slot in (64, 256, 992, 1504, 2048, 4080):
+    for slot in (64, 256, 992, 1504, 2048, 4080, 8192):
         st = run_slots(guards, wire, idx, slot)
         assert (st == O.ERROR_INVALID_FRAME).any() and (st == O.PARSE_MORE_DATA).any()
         run_slots(guards, wire, idx, slot, max_payload=60)
