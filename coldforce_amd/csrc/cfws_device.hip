@@ -803,25 +803,27 @@ uint64_t fused_avg_max()
 // line is fetched by the parse and again by the copy (§9: 6.86 GB per
 // 16 M x 256 B launch against 4.43 GB of wire).
 //
-// Slots of at most kSlotWindowMax bytes (deserialize_slots_window_kernel):
-// G = slot / 16 + 2 lanes per frame load the frame's window -- the 16-byte
-// block holding its first byte and the G - 1 after it (block phase <= 15
-// plus header <= 14 plus payload <= slot bytes) -- one block each, P = 64 / G
-// frames per wave-round. A wave takes R rounds (R P <= 64 frames) per
-// iteration: lane l loads frame l's index, every round's window block is
-// issued at once together with each frame's 16 header bytes (one unaligned
-// load, lane = frame: the same lines as the windows, in flight together, so
-// HBM sees them once), each lane parses its frame and writes its descriptor
-// and status (consecutive lanes, consecutive entries), and each round then
-// takes its frames' (length, header end, key) from the parsing lanes. A
-// lane's 16 payload bytes start (phase + header) bytes into its own block:
-// blocks c and c + 1 of the group, or c + 1 and c + 2 past 16 (DPP shifts by
-// one lane, no LDS), funnelled and unmasked (each chunk starts at a payload
-// index that is a multiple of 16: no key rotation). Blocks at or past the
-// wire's end are not loaded. The first form parsed in every lane of every
-// round (480 instructions per 3 frames at 256 B) and ran at 5.2 TB/s.
-// one block per lane up to 992 B (G <= 64), two up to 2,016 (G <= 128),
-// four up to 4,064 (G <= 256), eight up to 8,160 (G <= 512)
+// Slots of at most kSlotWindow8Max bytes (deserialize_slots_window_kernel):
+// a frame's window is the 16-byte block holding its first byte and the
+// G - 1 after it, G = slot / 16 + 2 (block phase <= 15 plus header <= 14 plus
+// payload <= slot bytes), one block per virtual lane. S sub-windows of 64
+// lanes give 64 S virtual lanes (S = 1 up to 992 B -- 2 for 496-640 B, three
+// frames to a pair --, 2 up to 2,016 B, 4 up to 4,064 B, 8 up to 8,160 B),
+// so P = 64 S / G frames share a wave-round. A wave takes R rounds (R P <=
+// 64 frames) per iteration: lane l loads frame l's index, every round's
+// window blocks are issued at once together with each frame's 16 header
+// bytes (one unaligned load, lane = frame: the same lines as the windows, in
+// flight together, so HBM sees them once), each lane parses its frame and
+// writes its descriptor and status (consecutive lanes, consecutive
+// entries), and each round then takes its frames' (length, phase + header,
+// key) from the parsing lanes. A virtual lane's 16 payload bytes start
+// (phase + header) bytes into its own block: blocks c and c + 1, or c + 1
+// and c + 2 past 16 (DPP shifts by one lane, no LDS; a sub-window's last two
+// lanes take the next sub-window's first two blocks), funnelled and
+// unmasked (each chunk starts at a payload index that is a multiple of 16:
+// no key rotation). Blocks at or past the wire's end are not loaded. The
+// first form parsed in every lane of every round (480 instructions per 3
+// frames at 256 B) and ran at 5.2 TB/s.
 constexpr uint64_t kSlotWindow8Max = 512 * 16 - 32;   // eight blocks per lane up to 8,160 B
 // Rounds per iteration (their loads in flight together): 8 for one frame per
 // round (slots over 480 B), 4 for more (16 M x 256 B receive 1.686 -> 1.620
