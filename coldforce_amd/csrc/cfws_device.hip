@@ -977,7 +977,7 @@ deserialize_slots_window_kernel(const uint8_t* __restrict__ wire, uint64_t wire_
 }
 
 #ifndef CFWS_SLOT_UNROLL
-#define CFWS_SLOT_UNROLL 4       // slots over 4,064 B: 16 rounds (246 VGPRs) took 2 M x 2 KiB to 2.87 ms
+#define CFWS_SLOT_UNROLL 16      // slots over 8,160 B: 64 K x 64 KiB receive 2.04 / 1.76 / 1.71 ms at 4 / 8 / 16 rounds, 8 KiB 1.72 at each
 #endif
 constexpr int kSlotUnroll = CFWS_SLOT_UNROLL;   // deserialize_slots_kernel: rounds of loads in flight
 
