@@ -201,3 +201,22 @@ def test_slots_arguments(guards):
                                                                                 device="cuda"))
     torch.cuda.synchronize()
     assert tot.item() == 0
+
+
+@pytest.mark.parametrize("slot", [16, 256, 2048, 16384])
+def test_slots_tiny_wires(guards, slot):
+    """Wires of 0 to 40 bytes (the header parsed from single bytes below 16,
+    window blocks cut at the wire's end), one to three frames."""
+    frames = [(bytes(range(3)), 0x0A0B0C0D), (b"", None), (bytes(range(9)), None)]
+    sizes = np.array([len(p) for p, _ in frames], dtype=np.uint64)
+    desc = np.zeros(3, dtype=O.DESC_DTYPE)
+    desc["payload_size"] = sizes
+    desc["payload_off"] = np.concatenate([[0], np.cumsum(sizes[:-1])]).astype(np.uint64)
+    desc["fin"], desc["opcode"] = 1, 1
+    desc["mask"] = [1, 0, 0]
+    desc["mask_key"] = [0x0A0B0C0D, 0, 0]
+    arena = np.frombuffer(b"".join(p for p, _ in frames), np.uint8).copy()
+    wire, _ = O.serialize_batch(arena, desc)
+    starts, _ = O.index_frames(wire, 4)
+    for cut in range(0, len(wire) + 1, 3):
+        run_slots(guards, wire, starts, slot, wire_size=cut)
