@@ -3,7 +3,10 @@
 # Each GPU step has its own time limit; a fault, abort, segfault or time
 # limit (rc 124/134/137/139 or > 128) ends the script; a plain test failure
 # (rc 1) does not.
-# usage: tools/r05_gpu.sh TAG STEP...   (steps: pytest bench split c5 fs1k config1 kstats pmc list)
+# usage: tools/r05_gpu.sh TAG STEP...   (steps: the case labels below, e.g.
+#   pytest smoke bench digests guard slots fs256 fs256s fs1k fs1ks kstats
+#   kstats_fs256s c5cpu e2e ab_plan ab_slots256 envab_sub2 pmc_sq_send ...;
+#   VARIANTS / V256 / VPLAN / VF / VBIG pick build/variants for the ab_ steps)
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
