@@ -46,7 +46,7 @@ BATCH_SYMBOLS = (
     "cfws_init", "cfws_init_device", "cfws_device_copy", "cfws_time_next_pass", "cfws_bind_thread_device", "cfws_thread_device", "cfws_last_error", "cfws_version", "cfws_workspace_size",
     "cfws_serialize_plan", "cfws_serialize_execute", "cfws_serialize_batch",
     "cfws_deserialize_plan", "cfws_deserialize_execute", "cfws_deserialize_batch",
-    "cfws_deserialize_slots", "cfws_xor_mask", "cfws_draw_mask_keys", "cfws_draw_mask_keys_seeded",
+    "cfws_deserialize_slots", "cfws_deserialize_scatter", "cfws_xor_mask", "cfws_draw_mask_keys", "cfws_draw_mask_keys_seeded",
     "cfws_release_thread_resources", "cfws_set_dropin_gpu_min", "cfws_dropin_gpu_min",
     "cfws_fill_splitmix", "cfws_pipeline_create", "cfws_pipeline_destroy",
     "cfws_pipeline_serialize", "cfws_pipeline_deserialize", "cfws_pipeline_receive",
@@ -115,6 +115,8 @@ def lib(path: str = LIB_PATH) -> C.CDLL:
                                     _vp, _vp, _sz, _vp], C.c_int),
         "cfws_deserialize_slots": ([_vp, _u64, _vp, _sz, _u64, _u64, _vp, _vp, _vp, _u64, _vp, _vp],
                                    C.c_int),
+        "cfws_deserialize_scatter": ([_vp, _u64, _vp, _vp, _sz, _u64, _u64, _vp, _vp, _vp, _u64, _vp],
+                                     C.c_int),
         "cfws_encode_headers": ([_vp, _sz, _vp, _u64, _vp], C.c_int),
         "cfws_parse_headers": ([_vp, _u64, _vp, _sz, _u64, _vp, _vp, _vp], C.c_int),
         "cfws_mask_batch": ([_vp, _vp, _sz, _u64, _vp, _u64, _vp], C.c_int),
@@ -339,6 +341,26 @@ def deserialize_slots(wire_t, wire_size: int, index_t, payload_t, slot_bytes: in
                                         _stream(stream)),
            "cfws_deserialize_slots")
     return desc_t, status_t, total_t
+
+
+def deserialize_scatter(wire_t, wire_size: int, index_t, payload_off_t, payload_t, max_slot: int,
+                        desc_t=None, status_t=None, max_payload: int = DEFAULT_MAX_PAYLOAD,
+                        payload_capacity: int | None = None, stream=None):
+    """cfws_deserialize_scatter: frame i's payload at payload_off_t[i] of
+    payload_t. Returns (desc_t, status_t)."""
+    import torch
+    n = index_t.numel()
+    dev = wire_t.device
+    if desc_t is None:
+        desc_t = torch.empty((n, 32), dtype=torch.uint8, device=dev)
+    if status_t is None:
+        status_t = torch.empty(n, dtype=torch.int32, device=dev)
+    cap = payload_t.numel() if payload_capacity is None else payload_capacity
+    _check(lib().cfws_deserialize_scatter(_p(wire_t), wire_size, _p(index_t), _p(payload_off_t), n, max_payload,
+                                          max_slot, _p(desc_t), _p(status_t), _p(payload_t), cap,
+                                          _stream(stream)),
+           "cfws_deserialize_scatter")
+    return desc_t, status_t
 
 
 # ---- HIP graphs of a batch (cfws_graph_*) -----------------------------------

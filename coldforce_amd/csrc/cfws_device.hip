@@ -31,6 +31,7 @@
 #include "cfws_kernels.h"
 
 #include <mutex>
+#include <type_traits>
 
 namespace cfws_rt {
 
@@ -861,7 +862,18 @@ __device__ __forceinline__ uint64_t shfl64(uint64_t v, int src)
 // written.
 __device__ __forceinline__ int32_t slot_rule(int32_t st, uint64_t run, uint64_t ps, uint64_t slot, uint64_t cap)
 {
-    return st == CFWS_PARSE_COMPLETE && ps > 0 && (ps > slot || run + ps > cap) ? CFWS_ERROR_OUT_OF_MEMORY : st;
+    return st == CFWS_PARSE_COMPLETE && ps > 0 && (ps > slot || run > cap || ps > cap - run)
+               ? CFWS_ERROR_OUT_OF_MEMORY : st;
+}
+
+// The scatter form (cfws_deserialize_scatter): frame i's payload at the
+// caller's dst[i] instead of i * slot, which must be a multiple of 16 (the
+// copy stores whole aligned blocks); a frame whose offset is not does not
+// fit either.
+__device__ __forceinline__ int32_t scatter_rule(int32_t st, uint64_t run, uint64_t ps, uint64_t slot, uint64_t cap)
+{
+    st = slot_rule(st, run, ps, slot, cap);
+    return st == CFWS_PARSE_COMPLETE && ps > 0 && (run & 15u) ? CFWS_ERROR_OUT_OF_MEMORY : st;
 }
 
 __device__ __forceinline__ void slot_desc(cfws_frame_desc_t* desc, int32_t* status, uint64_t f, uint64_t run,
@@ -876,13 +888,13 @@ __device__ __forceinline__ void slot_desc(cfws_frame_desc_t* desc, int32_t* stat
     status[f] = st;
 }
 
-template <int kSlotRounds, int kSub>
+template <int kSlotRounds, int kSub, bool kScatter>
 __global__ void __launch_bounds__(kThreads)
 deserialize_slots_window_kernel(const uint8_t* __restrict__ wire, uint64_t wire_size,
                                 const uint64_t* __restrict__ index, uint64_t n, uint64_t max_payload,
                                 uint64_t slot, uint32_t G, cfws_frame_desc_t* __restrict__ desc,
                                 int32_t* __restrict__ status, uint8_t* __restrict__ out, uint64_t capacity,
-                                uint64_t* __restrict__ user_total)
+                                uint64_t* __restrict__ user_total, const uint64_t* __restrict__ dst)
 {
     const uint32_t lane = threadIdx.x & 63u;
     // kSub sub-windows of 64 lanes make 64 kSub virtual lanes, v = 64 sw +
@@ -906,6 +918,8 @@ deserialize_slots_window_kernel(const uint8_t* __restrict__ wire, uint64_t wire_
         const uint64_t fl = f0 + lane;
         const bool mine = lane < FI && fl < n;
         const uint64_t wl = mine ? index[fl] : ~uint64_t(0);
+        // the frame's payload offset: its slot, or the caller's (scatter)
+        const uint64_t runl = !mine ? 0 : kScatter ? dst[fl] : fl * slot;
         // every round's window block, then each frame's header bytes
         uint4 A[kSlotRounds][kSub];
 #pragma unroll
@@ -933,8 +947,9 @@ deserialize_slots_window_kernel(const uint8_t* __restrict__ wire, uint64_t wire_
             } else {
                 st = parse_ws_header(wire, wire_size, wl, max_payload, d);
             }
-            const uint64_t run = fl * slot;
-            st = slot_rule(st, run, d.payload_size, slot, capacity);
+            const uint64_t run = runl;
+            st = kScatter ? scatter_rule(st, run, d.payload_size, slot, capacity)
+                          : slot_rule(st, run, d.payload_size, slot, capacity);
             slot_desc(desc, status, fl, run, d, st);
             if (fl == n - 1 && user_total) {
                 const uint64_t t = n * slot;
@@ -954,6 +969,7 @@ deserialize_slots_window_kernel(const uint8_t* __restrict__ wire, uint64_t wire_
                 const uint32_t inf = (uint32_t)__shfl((int)info, s, 64);
                 const uint32_t k = (uint32_t)__shfl((int)key, s, 64);
                 const uint32_t len = inf & 0xffffu, off = inf >> 16;
+                const uint64_t runf = kScatter ? shfl64(runl, s) : (f0 + src) * slot;
                 // blocks c + 1 and c + 2 of this sub-window, by DPP (every
                 // lane); lanes 62 and 63 of a sub-window take the next one's
                 // first two blocks
@@ -969,7 +985,7 @@ deserialize_slots_window_kernel(const uint8_t* __restrict__ wire, uint64_t wire_
                     uint4 o = sh ? funnel16(B0, B1, sh) : B0;
                     xor4(o, k);
                     if (len - 16u * q < 16u) o = and4(o, byte_range(0, len - 16u * q));
-                    fused_store(out, (f0 + src) * slot + 16ull * q, capacity, o);
+                    fused_store(out, runf + 16ull * q, capacity, o);
                 }
             }
         }
@@ -984,11 +1000,12 @@ constexpr int kSlotUnroll = CFWS_SLOT_UNROLL;   // deserialize_slots_kernel: rou
 // Slots over kSlotWindow8Max: one frame per thread parsed (its header line
 // fetched twice, a small share of a frame this long), the payloads copied
 // by fused_item.
+template <bool kScatter>
 __global__ void __launch_bounds__(kThreads)
 deserialize_slots_kernel(const uint8_t* __restrict__ wire, uint64_t wire_size, const uint64_t* __restrict__ index,
                          uint64_t n, uint64_t max_payload, uint64_t slot, cfws_frame_desc_t* __restrict__ desc,
                          int32_t* __restrict__ status, uint8_t* __restrict__ out, uint64_t capacity,
-                         uint64_t* __restrict__ user_total)
+                         uint64_t* __restrict__ user_total, const uint64_t* __restrict__ dst)
 {
     const uint64_t f = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
     uint64_t run = 0, src = 0;
@@ -996,9 +1013,10 @@ deserialize_slots_kernel(const uint8_t* __restrict__ wire, uint64_t wire_size, c
     if (f < n) {
         cfws_frame_desc_t d;
         const uint64_t s0 = index[f];
-        run = f * slot;
-        const int32_t st = slot_rule(parse_ws_header(wire, wire_size, s0, max_payload, d), run, d.payload_size,
-                                     slot, capacity);
+        run = kScatter ? dst[f] : f * slot;
+        const int32_t p = parse_ws_header(wire, wire_size, s0, max_payload, d);
+        const int32_t st = kScatter ? scatter_rule(p, run, d.payload_size, slot, capacity)
+                                    : slot_rule(p, run, d.payload_size, slot, capacity);
         slot_desc(desc, status, f, run, d, st);
         if (st == CFWS_PARSE_COMPLETE) {
             len = (uint32_t)d.payload_size;   // <= slot < 2^31
@@ -1565,22 +1583,29 @@ int cfws_deserialize_batch(const void* d_wire, uint64_t wire_size, const uint64_
     return cfws_deserialize_execute(d_wire, d_desc, d_status, n, flags, d_payload, cap, ws, stream);
 }
 
-int cfws_deserialize_slots(const void* d_wire, uint64_t wire_size, const uint64_t* d_index, size_t n,
-                           uint64_t max_payload, uint64_t slot, cfws_frame_desc_t* d_desc, int32_t* d_status,
-                           void* d_payload, uint64_t cap, uint64_t* d_total, void* stream)
+}  // extern "C"
+
+namespace {
+
+// cfws_deserialize_slots (dst null: frame i at i * slot) and
+// cfws_deserialize_scatter (frame i at dst[i], slot = the largest payload
+// a frame may have)
+int slots_impl(const void* d_wire, uint64_t wire_size, const uint64_t* d_index, const uint64_t* dst, size_t n,
+               uint64_t max_payload, uint64_t slot, cfws_frame_desc_t* d_desc, int32_t* d_status,
+               void* d_payload, uint64_t cap, uint64_t* d_total, void* stream, bool scatter, const char* what)
 {
     if (int rc = check_init()) return rc;
     if (slot < 16 || (slot & 15) || slot > (1ull << 31))
-        return set_err(CFWS_ERROR_INVALID_ARGUMENT, "slot_bytes must be a multiple of 16 in [16, 2^31]",
+        return set_err(CFWS_ERROR_INVALID_ARGUMENT, "slot bytes must be a multiple of 16 in [16, 2^31]",
                        hipSuccess);
     if (n > 0xffffffffull) return set_err(CFWS_ERROR_INVALID_ARGUMENT, "too many frames", hipSuccess);
     hipStream_t st = static_cast<hipStream_t>(stream);
     if (n == 0) {
         if (d_total && hipMemsetAsync(d_total, 0, sizeof(uint64_t), st) != hipSuccess)
-            return launch_check("deserialize_slots");
+            return launch_check(what);
         return CFWS_OK;
     }
-    if (!d_wire || !d_index || !d_desc || !d_status || (cap && !d_payload))
+    if (!d_wire || !d_index || !d_desc || !d_status || (cap && !d_payload) || (scatter && !dst))
         return set_err(CFWS_ERROR_INVALID_ARGUMENT, "null pointer", hipSuccess);
     if (misaligned(d_payload, d_wire))
         return set_err(CFWS_ERROR_INVALID_ARGUMENT, "arenas must be 16-byte aligned", hipSuccess);
@@ -1608,27 +1633,61 @@ int cfws_deserialize_slots(const void* d_wire, uint64_t wire_size, const uint64_
         }();
         const uint64_t want = (n + per_block - 1) / per_block;
         const uint32_t grid = (uint32_t)(want < cap_blocks ? want : cap_blocks);
-        if (S == 8)
-            deserialize_slots_window_kernel<CFWS_SLOT_ROUNDS8, 8><<<grid, kThreads, 0, st>>>(
-                w, wire_size, d_index, n, max_payload, slot, G, d_desc, d_status, out, cap, d_total);
-        else if (S == 4)
-            deserialize_slots_window_kernel<CFWS_SLOT_ROUNDS4, 4><<<grid, kThreads, 0, st>>>(
-                w, wire_size, d_index, n, max_payload, slot, G, d_desc, d_status, out, cap, d_total);
-        else if (S == 2)
-            deserialize_slots_window_kernel<CFWS_SLOT_ROUNDS2, 2><<<grid, kThreads, 0, st>>>(
-                w, wire_size, d_index, n, max_payload, slot, G, d_desc, d_status, out, cap, d_total);
-        else if (P > 1)
-            deserialize_slots_window_kernel<CFWS_SLOT_ROUNDS_MULTI, 1><<<grid, kThreads, 0, st>>>(
-                w, wire_size, d_index, n, max_payload, slot, G, d_desc, d_status, out, cap, d_total);
+        auto window = [&](auto scatter) {
+            constexpr bool kSc = decltype(scatter)::value;
+            if (S == 8)
+                deserialize_slots_window_kernel<CFWS_SLOT_ROUNDS8, 8, kSc><<<grid, kThreads, 0, st>>>(
+                    w, wire_size, d_index, n, max_payload, slot, G, d_desc, d_status, out, cap, d_total, dst);
+            else if (S == 4)
+                deserialize_slots_window_kernel<CFWS_SLOT_ROUNDS4, 4, kSc><<<grid, kThreads, 0, st>>>(
+                    w, wire_size, d_index, n, max_payload, slot, G, d_desc, d_status, out, cap, d_total, dst);
+            else if (S == 2)
+                deserialize_slots_window_kernel<CFWS_SLOT_ROUNDS2, 2, kSc><<<grid, kThreads, 0, st>>>(
+                    w, wire_size, d_index, n, max_payload, slot, G, d_desc, d_status, out, cap, d_total, dst);
+            else if (P > 1)
+                deserialize_slots_window_kernel<CFWS_SLOT_ROUNDS_MULTI, 1, kSc><<<grid, kThreads, 0, st>>>(
+                    w, wire_size, d_index, n, max_payload, slot, G, d_desc, d_status, out, cap, d_total, dst);
+            else
+                deserialize_slots_window_kernel<CFWS_SLOT_ROUNDS, 1, kSc><<<grid, kThreads, 0, st>>>(
+                    w, wire_size, d_index, n, max_payload, slot, G, d_desc, d_status, out, cap, d_total, dst);
+        };
+        // the scatter form as its own instantiation: its per-round offset
+        // shuffle, as a run-time branch in one kernel, cost the 1 KiB slot
+        // receive 11 % (1.525 -> 1.70 ms)
+        if (scatter)
+            window(std::true_type{});
         else
-            deserialize_slots_window_kernel<CFWS_SLOT_ROUNDS, 1><<<grid, kThreads, 0, st>>>(
-                w, wire_size, d_index, n, max_payload, slot, G, d_desc, d_status, out, cap, d_total);
+            window(std::false_type{});
+    } else if (scatter) {
+        deserialize_slots_kernel<true><<<grid_for(n, kThreads), kThreads, 0, st>>>(
+            w, wire_size, d_index, n, max_payload, slot, d_desc, d_status, out, cap, d_total, dst);
     } else {
-        deserialize_slots_kernel<<<grid_for(n, kThreads), kThreads, 0, st>>>(
-            w, wire_size, d_index, n, max_payload, slot, d_desc, d_status, out, cap, d_total);
+        deserialize_slots_kernel<false><<<grid_for(n, kThreads), kThreads, 0, st>>>(
+            w, wire_size, d_index, n, max_payload, slot, d_desc, d_status, out, cap, d_total, dst);
     }
     if (timed.stop) (void)hipEventRecord(static_cast<hipEvent_t>(timed.stop), st);
-    return launch_check("deserialize_slots");
+    return launch_check(what);
+}
+
+}  // namespace
+
+extern "C" {
+
+int cfws_deserialize_slots(const void* d_wire, uint64_t wire_size, const uint64_t* d_index, size_t n,
+                           uint64_t max_payload, uint64_t slot, cfws_frame_desc_t* d_desc, int32_t* d_status,
+                           void* d_payload, uint64_t cap, uint64_t* d_total, void* stream)
+{
+    return slots_impl(d_wire, wire_size, d_index, nullptr, n, max_payload, slot, d_desc, d_status, d_payload, cap,
+                      d_total, stream, false, "deserialize_slots");
+}
+
+int cfws_deserialize_scatter(const void* d_wire, uint64_t wire_size, const uint64_t* d_index,
+                             const uint64_t* d_payload_off, size_t n, uint64_t max_payload, uint64_t max_slot,
+                             cfws_frame_desc_t* d_desc, int32_t* d_status, void* d_payload, uint64_t cap,
+                             void* stream)
+{
+    return slots_impl(d_wire, wire_size, d_index, d_payload_off, n, max_payload, max_slot, d_desc, d_status,
+                      d_payload, cap, nullptr, stream, true, "deserialize_scatter");
 }
 
 #if CFWS_PLAN_TRACE

@@ -160,6 +160,24 @@ int cfws_deserialize_slots(const void* d_wire, uint64_t wire_size,
                            void* d_payload, uint64_t payload_capacity,
                            uint64_t* d_payload_total, void* stream);
 
+/* ---- deserialize, each payload to the caller's offset ---------------------
+ * cfws_deserialize_slots with payload_off = d_payload_off[i] (the caller's
+ * own buffer for each frame, as the reference allocates one per frame,
+ * co_ws_frame.c:216-223): one launch, each wire line read once. Every
+ * offset must be a multiple of 16; max_slot (a multiple of 16 in [16, 2^31])
+ * bounds the payloads. A COMPLETE frame with a non-empty payload gets
+ * CFWS_ERROR_OUT_OF_MEMORY when that payload is longer than max_slot, ends
+ * past payload_capacity, or has an offset that is not a multiple of 16; its
+ * destination is not written. Otherwise as cfws_deserialize_slots: the
+ * unmasked payload, then zeros to the next 16-byte boundary (cut at the
+ * capacity); nothing else is written. Destinations that overlap are the
+ * caller's to avoid. */
+int cfws_deserialize_scatter(const void* d_wire, uint64_t wire_size,
+                             const uint64_t* d_frame_index, const uint64_t* d_payload_off,
+                             size_t n_frames, uint64_t max_payload, uint64_t max_slot,
+                             cfws_frame_desc_t* d_desc, int32_t* d_status,
+                             void* d_payload, uint64_t payload_capacity, void* stream);
+
 /* ---- split ops: headers and payload XOR as separate passes ---------------
  * The two halves of the codec over frames the caller lays out itself (a send
  * path that gathers headers and payloads into iovecs, a receive path that

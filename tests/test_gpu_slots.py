@@ -52,9 +52,11 @@ def guards():
         b.free()
 
 
-def expect_slots(wire, wire_size, starts, slot, cap, max_payload=O.DEFAULT_MAX_PAYLOAD):
+def expect_slots(wire, wire_size, starts, slot, cap, max_payload=O.DEFAULT_MAX_PAYLOAD, offs=None):
     """(arena of round16(cap) bytes, desc, status, total) as
-    cfws_deserialize_slots defines them, from the oracle's packed receive."""
+    cfws_deserialize_slots defines them, from the oracle's packed receive;
+    with offs, as cfws_deserialize_scatter does (frame i at offs[i], which
+    must be a multiple of 16; slot is then max_slot; total is None)."""
     n = len(starts)
     # packed with room for every COMPLETE payload (indices may repeat)
     p_d, p_st = O.parse_headers(wire[:wire_size], starts, max_payload)
@@ -62,9 +64,12 @@ def expect_slots(wire, wire_size, starts, slot, cap, max_payload=O.DEFAULT_MAX_P
     e_out, e_d, e_st, _ = O.deserialize_batch(wire[:wire_size], starts, align=1, max_payload=max_payload,
                                               capacity=room)
     ps = e_d["payload_size"].astype(np.uint64)
-    run = np.arange(n, dtype=np.uint64) * np.uint64(slot)
+    run = np.arange(n, dtype=np.uint64) * np.uint64(slot) if offs is None else np.asarray(offs, np.uint64)
     st = e_st.copy()
-    oom = (st == O.PARSE_COMPLETE) & (ps > 0) & ((ps > slot) | (run + ps > cap))
+    fits = (ps <= slot) & (run <= np.uint64(cap)) & (ps <= np.uint64(cap) - np.minimum(run, np.uint64(cap)))
+    if offs is not None:
+        fits &= (run % np.uint64(16)) == 0
+    oom = (st == O.PARSE_COMPLETE) & (ps > 0) & ~fits
     st[oom] = O.ERROR_OUT_OF_MEMORY
     arena = np.full(W.round16(max(cap, 1)), SENT, np.uint8)
     for i in np.nonzero((st == O.PARSE_COMPLETE) & (ps > 0))[0]:
@@ -73,22 +78,31 @@ def expect_slots(wire, wire_size, starts, slot, cap, max_payload=O.DEFAULT_MAX_P
         arena[r + L:min(r + W.round16(L), cap)] = 0
     d = e_d.copy()
     d["payload_off"] = run
-    return arena, d, st, min(n * slot, cap)
+    return arena, d, st, (min(n * slot, cap) if offs is None else None)
 
 
 def run_slots(guards, wire, starts, slot, cap=None, wire_size=None, max_payload=O.DEFAULT_MAX_PAYLOAD,
-              flush_end=True):
+              flush_end=True, offs=None):
+    """cfws_deserialize_slots, or with offs cfws_deserialize_scatter (slot
+    is then max_slot), against expect_slots."""
     ws_n = len(wire) if wire_size is None else wire_size
     n = len(starts)
     cap = n * slot if cap is None else cap
     w = guards(max(ws_n, 1), flush_end).upload(wire[:ws_n])
     out = guards(max(cap, 1), flush_end)
     idx = torch.from_numpy(np.asarray(starts, dtype=np.uint64).view(np.int64)).cuda()
-    d_t, st_t, tot = cfws.deserialize_slots(w, ws_n, idx, out, slot, max_payload=max_payload,
-                                            payload_capacity=cap)
+    if offs is None:
+        d_t, st_t, tot = cfws.deserialize_slots(w, ws_n, idx, out, slot, max_payload=max_payload,
+                                                payload_capacity=cap)
+    else:
+        off_t = torch.from_numpy(np.asarray(offs, dtype=np.uint64).view(np.int64)).cuda()
+        d_t, st_t = cfws.deserialize_scatter(w, ws_n, idx, off_t, out, slot, max_payload=max_payload,
+                                             payload_capacity=cap)
+        tot = None
     torch.cuda.synchronize()
-    e_arena, e_d, e_st, e_tot = expect_slots(wire, ws_n, starts, slot, cap, max_payload)
-    assert int(tot.item()) == e_tot
+    e_arena, e_d, e_st, e_tot = expect_slots(wire, ws_n, starts, slot, cap, max_payload, offs)
+    if tot is not None:
+        assert int(tot.item()) == e_tot
     st = st_t.cpu().numpy()
     bad = np.nonzero(st != e_st)[0]
     assert bad.size == 0, f"{bad.size} statuses differ, first {[(int(i), int(st[i]), int(e_st[i])) for i in bad[:6]]}"
@@ -220,3 +234,40 @@ def test_slots_tiny_wires(guards, slot):
     starts, _ = O.index_frames(wire, 4)
     for cut in range(0, len(wire) + 1, 3):
         run_slots(guards, wire, starts, slot, wire_size=cut)
+
+
+def _scatter_offsets(n, max_slot, rng, cap_slack=0):
+    """Non-overlapping 16-aligned destinations in a shuffled order with gaps
+    of 0-48 bytes: frame i's region is [offs[i], offs[i] + max_slot)."""
+    stride = max_slot + 64
+    perm = rng.permutation(n).astype(np.uint64)
+    return perm * np.uint64(stride) + rng.integers(0, 4, n).astype(np.uint64) * np.uint64(16), n * stride + cap_slack
+
+
+@pytest.mark.parametrize("max_slot", [16, 96, 256, 1504, 4064, 8160, 16384])
+def test_scatter_permuted(guards, max_slot):
+    """cfws_deserialize_scatter over every kernel (window with one to eight
+    blocks per lane, per-frame): destinations shuffled, with gaps left
+    untouched, and frames too long for max_slot OUT_OF_MEMORY."""
+    payload, desc = _seed21_batch(31)
+    wire, starts = _wire_of(payload, desc)
+    rng = np.random.default_rng(max_slot)
+    offs, cap = _scatter_offsets(len(starts), max_slot, rng)
+    run_slots(guards, wire, starts, max_slot, cap=cap, offs=offs)
+
+
+def test_scatter_bad_offsets(guards):
+    """Offsets that are not multiples of 16, that end past the capacity, or
+    that are near 2^64 (no wrap): OUT_OF_MEMORY, nothing written for them."""
+    payload, desc = _seed21_batch(32)
+    wire, starts = _wire_of(payload, desc)
+    n = len(starts)
+    rng = np.random.default_rng(32)
+    offs, cap = _scatter_offsets(n, 5008, rng)
+    offs = offs.copy()
+    offs[::7] += np.uint64(8)                       # misaligned
+    offs[3::11] = np.uint64(cap - 16)              # ends past the capacity (unless tiny)
+    offs[5::13] = np.uint64((1 << 64) - 16)         # would wrap
+    for max_slot in (256, 5008):
+        st = run_slots(guards, wire, starts, max_slot, cap=cap, offs=offs)
+        assert (st == O.ERROR_OUT_OF_MEMORY).any() and (st == O.PARSE_COMPLETE).any()
