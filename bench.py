@@ -55,6 +55,9 @@ def parse():
     ap.add_argument("--recv-slots", action="store_true",
                     help="config2: receive into fixed payload slots of frame-size bytes "
                          "(cfws_deserialize_slots) instead of the packed layout")
+    ap.add_argument("--recv-scatter", action="store_true",
+                    help="config2: receive each frame to its own offset, the slots in a "
+                         "shuffled order (cfws_deserialize_scatter)")
     ap.add_argument("--keys", type=int, default=1 << 20, help="accept workload: client keys per GPU")
     ap.add_argument("--connections", type=int, default=16384, help="index workload: connections")
     ap.add_argument("--index-mib", type=int, default=1024, help="index workload: receive-buffer MiB")
@@ -644,6 +647,7 @@ def per_gpu_rows(rows, steps: int):
 
 def main():
     args = parse()
+    import numpy as np
     import torch
     import torch.distributed as dist
 
@@ -723,9 +727,13 @@ def main():
     # batches of small frames (<= 512 B of wire per frame, no reassembly) the
     # fused plan + copy kernel of the receive,
     # deserialize_plan_single_kernel<true>
-    slot = W.round16(max(fs, 16)) if args.recv_slots else 0
+    slot = W.round16(max(fs, 16)) if args.recv_slots or args.recv_scatter else 0
     if slot and (flags or slot != fs):
-        sys.exit("bench.py: --recv-slots needs config2 with a frame size that is a multiple of 16")
+        sys.exit("bench.py: --recv-slots / --recv-scatter need config2 with a frame size that is a multiple of 16")
+    # --recv-scatter: frame i to slot perm[i] (a seeded shuffle)
+    perm = (torch.from_numpy(np.random.default_rng(5).permutation(F).astype(np.int64)).to(dev)
+            if args.recv_scatter else None)
+    dst_off = perm * slot if perm is not None else None
     fused_de = (not slot and flags == 0 and F > 1024 and os.environ.get("CFWS_FUSED_DESER", "1") != "0"
                 and wire_total // F <= int(os.environ.get("CFWS_FUSED_AVG_MAX", "512")))  # fused_avg_max()
 
@@ -742,7 +750,9 @@ def main():
             if ev: ev[3].record()
         else:
             if ev: cfws.time_next_pass(ev[2], ev[3])
-            if slot:
+            if dst_off is not None:
+                cfws.deserialize_scatter(wire, wire_total, index, dst_off, back, slot, desc_de, status)
+            elif slot:
                 cfws.deserialize_slots(wire, wire_total, index, back, slot, desc_de, status, tot_de)
             else:
                 cfws.deserialize(wire, wire_total, index, back, desc_de, status, ws_de, tot_de, align=16)
@@ -763,9 +773,16 @@ def main():
     elapsed = shard.max_over_ranks(local, dev)
 
     # correctness of what was timed: unmask(mask(P)) == P, every frame COMPLETE
-    verified = (int(tot_ser.item()) == wire_total and int(tot_de.item()) == arena_bytes
-                and bool((status == 0).all().item())
-                and torch.equal(back[:arena_bytes], payload[:arena_bytes]))
+    if perm is not None:
+        # frame i's payload is slot perm[i]: gather the slots back into frame order
+        got = back[:arena_bytes].view(F, slot)[perm]
+        verified = (int(tot_ser.item()) == wire_total and bool((status == 0).all().item())
+                    and torch.equal(got.reshape(-1), payload[:arena_bytes]))
+        del got
+    else:
+        verified = (int(tot_ser.item()) == wire_total and int(tot_de.item()) == arena_bytes
+                    and bool((status == 0).all().item())
+                    and torch.equal(back[:arena_bytes], payload[:arena_bytes]))
     verified = shard.sum_over_ranks(1.0 if verified else 0.0, dev) == world
 
     # practical ceiling: a bare streaming copy of the same byte count
@@ -807,7 +824,8 @@ def main():
                      else "deserialize_slots_kernel" if slot
                      else "xform_kernel<1>")                                 # kModeDeser
     # the PMC summary a traffic figure may come from: the same workload only
-    traffic_key = (f"config2:{F}x{fs}" + (":slots" if slot else "") if args.workload == "config2" else
+    traffic_key = (f"config2:{F}x{fs}" + (":scatter" if perm is not None else ":slots" if slot else "")
+                   if args.workload == "config2" else
                    "config3" if args.workload == "config3" else f"config4:{F}x{fs}")
     rows = shard.gather_floats([local, arena_bytes, ser_ms, de_ms, alg_bytes], dev)
     total_payload = 2.0 * sum(r[1] for r in rows) * args.steps
@@ -827,7 +845,9 @@ def main():
         "config": {
             "workload": (f"config2: {F} binary frames x {size_label(fs)} per GPU, client-mask "
                          f"(serialize) then server-unmask (deserialize), device resident"
-                         + (f"; the receive into fixed {slot} B payload slots (cfws_deserialize_slots)"
+                         + (f"; the receive to a shuffled order of {slot} B slots (cfws_deserialize_scatter)"
+                            if perm is not None else
+                            f"; the receive into fixed {slot} B payload slots (cfws_deserialize_slots)"
                             if slot else "")
                          if args.workload == "config2" else
                          f"config4: shard {rank} of 8 of the 8 M x 64 KiB batch ({F} frames, "

@@ -83,6 +83,8 @@ for s in "$@"; do
     fs6ks) step fs6ks 200 python3 $R/bench.py --frames 699050 --frame-size 6144 --no-cpu-baseline --recv-slots ;;
     fs6k) step fs6k 200 python3 $R/bench.py --frames 699050 --frame-size 6144 --no-cpu-baseline ;;
     ab_slots_big) for w in "524288 8192" "65536 65536"; do set -- $w; step ab_slots_big_$2 900 env TAG=$TAG/ab_slots_big_$2 VARIANTS="${VBIG:-base}" ARGS="--frames $1 --frame-size $2 --recv-slots" bash $R/tools/ab.sh; done ;;
+    fs256x) step fs256x 200 python3 $R/bench.py --frames 16777216 --frame-size 256 --no-cpu-baseline --recv-scatter ;;
+    fs1kx) step fs1kx 200 python3 $R/bench.py --frames 4194304 --frame-size 1024 --no-cpu-baseline --recv-scatter ;;
     fs256) step fs256 200 python3 $R/bench.py --frames 16777216 --frame-size 256 --no-cpu-baseline ;;
     kstats_fs256) step kstats_fs256 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kstats_fs256" -o ks -- python3 $R/bench.py --frames 16777216 --frame-size 256 --steps 10 --warmup 3 --no-cpu-baseline ;;
     fs2k) step fs2k 200 python3 $R/bench.py --frames 2097152 --frame-size 2048 --no-cpu-baseline ;;
