@@ -7,7 +7,8 @@
  *   server side:  cfws_index_frames_batch over the wire as one connection's
  *                 receive buffer -> cfws_deserialize_batch -> D2H payloads,
  *                 and the same frames through cfws_deserialize_slots (frame
- *                 i's payload at i * slot)
+ *                 i's payload at i * slot) and cfws_deserialize_scatter
+ *                 (each payload to a buffer of its own size, last frame first)
  *
  * Checks that every payload comes back and that the wire equals what
  * sequential co_ws_frame_serialize calls (the drop-in, same library) append
@@ -160,9 +161,35 @@ int main(int argc, char** argv)
     for (size_t i = 0; slots_ok && i < n; ++i)
         slots_ok = status[i] == CFWS_PARSE_COMPLETE &&
                    memcmp(slots + i * slot, payload + desc[i].payload_off, desc[i].payload_size) == 0;
+
+    /* each payload to its own 16-aligned buffer, sized to it, in reverse
+       frame order: the reference's one allocation per frame */
+    uint64_t* off = malloc(n * sizeof *off);
+    uint64_t sc_cap = 0;
+    for (size_t k = n; k-- > 0;) {
+        off[k] = sc_cap;
+        sc_cap += (desc[k].payload_size + 15) / 16 * 16;
+    }
+    void *d_sc, *d_off;
+    CHECK(hipMalloc(&d_sc, sc_cap + 16));
+    CHECK(hipMalloc(&d_off, n * sizeof *off));
+    CHECK(hipMemcpyAsync(d_off, off, n * sizeof *off, hipMemcpyHostToDevice, st));
+    CHECK(cfws_deserialize_scatter(d_wire, wire_total, d_starts, (const uint64_t*)d_off, n_found,
+                                   CFWS_DEFAULT_MAX_RECEIVE_PAYLOAD_SIZE, slot, d_desc2, d_status, d_sc,
+                                   sc_cap + 16, st));
+    CHECK(hipStreamSynchronize(st));
+    uint8_t* sc = malloc(sc_cap + 16);
+    CHECK(hipMemcpy(sc, d_sc, sc_cap + 16, hipMemcpyDeviceToHost));
+    CHECK(hipMemcpy(status, d_status, n * sizeof *status, hipMemcpyDeviceToHost));
+    int scatter_ok = n_found == n;
+    for (size_t i = 0; scatter_ok && i < n; ++i)
+        scatter_ok = status[i] == CFWS_PARSE_COMPLETE &&
+                     memcmp(sc + off[i], payload + desc[i].payload_off, desc[i].payload_size) == 0;
     printf("{\"frames\": %zu, \"payload_bytes\": %llu, \"wire_bytes\": %llu, "
-           "\"wire_equals_dropin\": %s, \"indexed\": %llu, \"roundtrip\": %s, \"slots\": %s}\n",
+           "\"wire_equals_dropin\": %s, \"indexed\": %llu, \"roundtrip\": %s, \"slots\": %s, "
+           "\"scatter\": %s}\n",
            n, (unsigned long long)arena, (unsigned long long)wire_total, same ? "true" : "false",
-           (unsigned long long)n_found, ok ? "true" : "false", slots_ok ? "true" : "false");
-    return ok && slots_ok ? 0 : 2;
+           (unsigned long long)n_found, ok ? "true" : "false", slots_ok ? "true" : "false",
+           scatter_ok ? "true" : "false");
+    return ok && slots_ok && scatter_ok ? 0 : 2;
 }

@@ -1,6 +1,6 @@
 """examples/batch_roundtrip.c: the batch C ABI driven from plain C (no
 Python in the process): serialize, index the wire as a receive buffer,
-deserialize (packed, and into fixed slots); the wire must equal the
+deserialize (packed, into fixed slots, and to per-frame offsets); the wire must equal the
 drop-in's co_ws_frame_serialize appends for the same random() stream and
 every payload must come back."""
 import json
@@ -33,4 +33,4 @@ def test_example_roundtrip(n, maxlen):
     assert r.returncode == 0, r.stdout + r.stderr
     out = json.loads(r.stdout.strip().splitlines()[-1])
     assert out["frames"] == n and out["indexed"] == n
-    assert out["wire_equals_dropin"] and out["roundtrip"] and out["slots"]
+    assert out["wire_equals_dropin"] and out["roundtrip"] and out["slots"] and out["scatter"]
