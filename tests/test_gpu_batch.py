@@ -328,8 +328,9 @@ def test_small_frame_reference_digests(which):
     2 KiB, 1,398,101 x 3 KiB and 1,198,372 x 3,584 B -- the bound itself --
     every one 4 GiB of payload at the bench's seeds) through the bench's own
     calls: serialize plan + execute (single-pass look-back plan, in-region
-    send edges) and deserialize plan + execute at 16-byte slots. The wire's
-    SHA-256 equals the reference's co_ws_frame_serialize output
+    send edges) and deserialize plan + execute at 16-byte slots, then the
+    slot and scatter receives. The wire's SHA-256 equals the reference's
+    co_ws_frame_serialize output
     (co_ws_frame.c:21-119, compiled in place, tests/golden/make_golden.py
     small_batch_digest), and the unmasked payloads' SHA-256 equals what the
     reference's co_ws_frame_deserialize walk (co_ws_frame.c:121-247) returned
@@ -371,14 +372,24 @@ def test_small_frame_reference_digests(which):
     assert ptot2.item() == n * fs and bool((st2 == 0).all())
     assert _sha_device(back, n * fs) == g["payload_sha256"]
     # cfws_deserialize_slots at slots of fs bytes: the same arena (every fs
-    # here is a multiple of 16); 256 B takes the window kernel, the rest the
-    # per-frame one
+    # here is a multiple of 16); up to 8,160 B the window kernel
     back.fill_(0xEE)
     status.fill_(99)
     _, st3, ptot3 = cfws.deserialize_slots(wire, total, idx, back, fs, desc_de, status)
     torch.cuda.synchronize()
     assert ptot3.item() == n * fs and bool((st3 == 0).all())
     assert _sha_device(back, n * fs) == g["payload_sha256"]
+    # cfws_deserialize_scatter: frame i to slot (i + h) mod n, so no frame
+    # lands where slot order puts it; rolled back, the payloads' SHA-256
+    h = n // 2 + 1
+    dst = ((torch.arange(n, dtype=torch.int64, device="cuda") + h) % n) * fs
+    back.fill_(0xEE)
+    status.fill_(99)
+    _, st4 = cfws.deserialize_scatter(wire, total, idx, dst, back, fs, desc_de, status)
+    torch.cuda.synchronize()
+    assert bool((st4 == 0).all())
+    rolled = torch.roll(back[:n * fs].view(n, fs), shifts=-h, dims=0).reshape(-1)
+    assert _sha_device(rolled, n * fs) == g["payload_sha256"]
 
 
 def _roundtrip_digest(g, full=False):
