@@ -798,9 +798,13 @@ __device__ __forceinline__ void general_region_search(const Pass& P, uint32_t f0
 // loads), reduced to four words relative to the region base: the frame's
 // output start, its body range, its source delta and its key rotated for
 // 16-aligned chunks. Each chunk then finds its frame by a binary search over
-// the lanes (shuffles) and loads only its source blocks.
+// the lanes (shuffles) and loads only its source blocks. Up to
+// CFWS_GENERAL_SCAN frames a count of the frame starts replaces the search:
+// 8 -> 12 took 384 B and 512 B steps 1.3 % and 2.3 % faster (512 B send
+// 1.523 -> 1.473 ms, receive 1.489 -> 1.461), 256 B and 768 B unchanged; 16
+// and 64 cost the 256 B send 0.4-0.6 % (profiles/r05/general_scan_ab/)
 #ifndef CFWS_GENERAL_SCAN
-#define CFWS_GENERAL_SCAN 8
+#define CFWS_GENERAL_SCAN 12
 #endif
 #ifndef CFWS_GENERAL_DIRECT
 #define CFWS_GENERAL_DIRECT 1
