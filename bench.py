@@ -20,7 +20,10 @@ created without the system-scope fence, which torch.cuda.Event records and
 which left ~6 us of idle GPU in the stream at each record).
 
 Usage: python bench.py [--gpus N --steps K --warmup W]
-       torchrun --nproc-per-node N bench.py --gpus N ...   (N > 1)
+         (N > 1: this process starts N workers itself, one per GPU, and makes
+          no GPU call; spawn_ranks)
+       torchrun --nproc-per-node N bench.py --gpus N ...   (the same run under torchrun)
+The ranks' bookkeeping collectives run over gloo (RCCL is never initialised).
 """
 from __future__ import annotations
 
@@ -52,6 +55,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="target CPU time of the cpu_baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="no GPU: only the multi-rank launch and bookkeeping (CPU test)")
     ap.add_argument("--recv-slots", action="store_true",
                     help="config2: receive into fixed payload slots of frame-size bytes "
                          "(cfws_deserialize_slots) instead of the packed layout")
@@ -645,8 +650,126 @@ def per_gpu_rows(rows, steps: int):
     return out
 
 
+def _free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(args) -> int:
+    """`bench.py --gpus N` (N > 1) started without a launcher: this process
+    makes no HIP call (torch is never imported here) and starts N fresh
+    worker processes of this same script, one per GPU, with the environment
+    torchrun would give them (RANK / LOCAL_RANK / WORLD_SIZE, rendezvous on
+    127.0.0.1). Rank 0 prints the one JSON line; the exit status is the
+    first failing rank's. If a rank fails, the others (blocked in a
+    bookkeeping barrier) are given 30 s and then killed by PID."""
+    import subprocess
+    port = _free_port()
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), GROUP_RANK="0", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), CFWS_BENCH_LAUNCHER="spawn")
+        env.setdefault("GLOO_SOCKET_IFNAME", "lo")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                                      env=env, stdout=None if r == 0 else sys.stderr.fileno()))
+    rc, failed_at = 0, None
+    while any(p.poll() is None for p in procs):
+        for p in procs:
+            if p.returncode not in (None, 0) and rc == 0:
+                rc, failed_at = p.returncode, time.monotonic()
+        if failed_at is not None and time.monotonic() - failed_at > 30:
+            for p in procs:
+                if p.poll() is None:
+                    p.kill()
+        time.sleep(0.2)
+    for p in procs:
+        if p.returncode != 0 and rc == 0:
+            rc = p.returncode
+    return 0 if rc == 0 else (rc if rc > 0 else 1)
+
+
+def init_ranks(args):
+    """(rank, world, device) of this process. One process per GPU: under
+    torchrun, under spawn_ranks, or alone (N = 1). The bookkeeping
+    collectives (the timing barriers, a max and a gather of a few CPU
+    scalars) run over gloo on every box: the data path has no collective
+    (SURVEY.md §8e), so RCCL is never initialised. CFWS_BENCH_REHEARSE=1:
+    more ranks than GPUs (ranks share devices) -- a check of the multi-rank
+    path on a smaller box, not a measurement."""
+    import torch
+    import torch.distributed as dist
+
+    from coldforce_amd import cfws, shard
+    rank, local_rank, world = shard.world()
+    if world != args.gpus and rank == 0:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: running {world} ranks",
+              file=sys.stderr)
+    if args.dry_run:
+        dev = None
+    else:
+        ngpu = torch.cuda.device_count()
+        rehearse = os.environ.get("CFWS_BENCH_REHEARSE") == "1"
+        if local_rank >= ngpu and not rehearse:
+            sys.exit(f"bench.py: rank {rank} has no GPU ({ngpu} visible)")
+        gpu = local_rank % ngpu
+        torch.cuda.set_device(gpu)
+        dev = torch.device("cuda", gpu)
+    if world > 1:
+        os.environ.setdefault("GLOO_SOCKET_IFNAME", "lo")
+        # gloo announces its connections on fd 1: keep stdout for the one
+        # JSON line by sending fd 1 to stderr while the group forms
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            dist.init_process_group("gloo")
+        finally:
+            os.dup2(saved, 1)
+            os.close(saved)
+    if dev is not None:
+        cfws.init()
+    return rank, world, dev
+
+
+def launcher_name(world: int) -> str:
+    """How this rank was started: "spawn" (spawn_ranks), "torchrun", or
+    "single" (one process, N = 1)."""
+    return os.environ.get("CFWS_BENCH_LAUNCHER", "torchrun" if "WORLD_SIZE" in os.environ else "single")
+
+
+def bench_dry(args, rank, world):
+    """--dry-run: the launch and bookkeeping of a multi-rank run with no GPU
+    (the CPU test of spawn_ranks / torchrun): each rank builds its shard's
+    descriptors on the host, times that, and the ranks meet in the same
+    barrier / max / gather the GPU workloads use. The line carries no rate
+    of the metric ("value": null)."""
+    from coldforce_amd import shard
+    t0 = time.perf_counter()
+    for _ in range(args.warmup + args.steps):
+        desc, _ = shard.uniform_shard(args.frames, args.frame_size, KEY_SEED, rank, world)
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+    local = time.perf_counter() - t0
+    elapsed = shard.max_over_ranks(local)
+    rows = shard.gather_floats([local, len(desc) * args.frame_size])
+    line = {"metric": METRIC, "value": None, "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "dry_run": True, "launcher": launcher_name(world),
+            "config": {"workload": f"dry run: {args.frames} x {size_label(args.frame_size)} descriptors per rank"},
+            "per_gpu": per_gpu_rows(rows, args.steps), "verified": True}
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    return 0
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args))
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -654,22 +777,12 @@ def main():
     from coldforce_amd import cfws, shard
     from coldforce_amd import workloads as W
 
-    rank, local_rank, world = shard.world()
-    if args.gpus != world and world == 1 and args.gpus > 1:
-        sys.exit("bench.py: --gpus > 1 needs torchrun (one process per GPU)")
-    # CFWS_BENCH_REHEARSE=1: more ranks than GPUs (ranks share devices,
-    # bookkeeping collectives over gloo) -- a check of the multi-rank path on
-    # a smaller box, not a measurement
-    rehearse = os.environ.get("CFWS_BENCH_REHEARSE") == "1"
-    gpu = local_rank % torch.cuda.device_count() if rehearse else local_rank
-    torch.cuda.set_device(gpu)
-    dev = torch.device("cuda", gpu)
-    if world > 1:
-        if rehearse:
-            dist.init_process_group("gloo")
-        else:
-            dist.init_process_group("nccl", device_id=dev)
-    cfws.init()
+    rank, world, dev = init_ranks(args)
+    if args.dry_run:
+        rc = bench_dry(args, rank, world)
+        if world > 1:
+            dist.destroy_process_group()
+        sys.exit(rc)
 
     F, fs = args.frames, args.frame_size
     if args.workload in ("config5", "split", "accept", "index"):
@@ -861,6 +974,7 @@ def main():
             "payload_bytes_per_gpu": arena_bytes,
             "wire_bytes_per_gpu": wire_total,
             "parallelism": f"shard-per-gpu x{world} (no collective)",
+            "launcher": launcher_name(world),
         },
         "roofline": {
             "bound": "hbm",

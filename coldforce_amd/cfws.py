@@ -459,6 +459,9 @@ class TimingEvent:
         ms = C.c_float()
         rc = self._h.hipEventElapsedTime(C.byref(ms), self.ev, end.ev)
         if rc != 0:
+            # the failure also sets the thread's last HIP error: clear it, or
+            # the next library call's launch check reports it as its own
+            self._h.hipGetLastError()
             raise CodecError(f"hipEventElapsedTime rc={rc}")
         return ms.value
 

@@ -491,9 +491,16 @@ serialize_plan_single_kernel(cfws_frame_desc_t* __restrict__ desc, uint64_t* __r
 #ifndef CFWS_FUSED_UNROLL
 #define CFWS_FUSED_UNROLL 4
 #endif
-#ifndef CFWS_FUSED_MIN_BLOCKS
-#define CFWS_FUSED_MIN_BLOCKS 5
+// The fused kernel's occupancy hint, stated as what it is: workgroups of
+// kFusedThreads per CU (__launch_bounds__' second argument). 1 at 1024
+// threads = 16 waves per CU, 4 per SIMD: the register budget every fused
+// measurement in DESIGN.md ran with (the hint used to be written as
+// 5 * 256 / kBT, which truncated to this same 1).
+#ifndef CFWS_FUSED_MIN_BLOCKS_PER_CU
+#define CFWS_FUSED_MIN_BLOCKS_PER_CU 1
 #endif
+constexpr int kFusedMinBlocksPerCU = CFWS_FUSED_MIN_BLOCKS_PER_CU;
+static_assert(kFusedMinBlocksPerCU >= 1, "the fused kernel's occupancy hint must be at least 1");
 constexpr int kFusedUnroll = CFWS_FUSED_UNROLL;   // rounds of loads in flight per wave
 
 __device__ __forceinline__ void fused_store(uint8_t* __restrict__ out, uint64_t D, uint64_t total, uint4 o)
@@ -632,7 +639,7 @@ __device__ __forceinline__ uint4 ld16u(const uint8_t* p)
 constexpr int kFusedItems = CFWS_FUSED_ITEMS;   // frames per thread in the fused form (registers)
 
 template <bool kCopy, int kBT>
-__global__ void __launch_bounds__(kBT, kCopy ? CFWS_FUSED_MIN_BLOCKS * 256 / kBT : 1)
+__global__ void __launch_bounds__(kBT, kCopy ? kFusedMinBlocksPerCU : 1)
 deserialize_plan_single_kernel(const uint8_t* __restrict__ wire, uint64_t wire_size_all,
                                const uint64_t* __restrict__ index, const uint64_t* __restrict__ ends,
                                uint64_t n, uint64_t max_payload, uint64_t align,
@@ -1435,6 +1442,7 @@ size_t cfws_workspace_size(size_t n_frames, uint64_t out_capacity)
 int cfws_serialize_plan(cfws_frame_desc_t* d_desc, size_t n, uint64_t cap, uint64_t* d_total,
                         void* ws, size_t ws_size, void* stream)
 {
+    const CfwsPassScope pass_scope;
     if (int rc = check_init()) return rc;
     const WsLayout L = ws_layout(n, cap);
     if (!ws || ws_size < L.bytes) return set_err(CFWS_ERROR_WORKSPACE, "workspace too small", hipSuccess);
@@ -1468,6 +1476,7 @@ int cfws_serialize_plan(cfws_frame_desc_t* d_desc, size_t n, uint64_t cap, uint6
 int cfws_serialize_execute(const void* d_payload, const cfws_frame_desc_t* d_desc, size_t n,
                            void* d_wire, uint64_t cap, const void* ws, void* stream)
 {
+    const CfwsPassScope pass_scope;
     if (int rc = check_init()) return rc;
     if (n == 0 || cap == 0) return CFWS_OK;
     if (!d_payload || !d_desc || !d_wire || !ws)
@@ -1484,10 +1493,12 @@ int cfws_serialize_execute(const void* d_payload, const cfws_frame_desc_t* d_des
 int cfws_serialize_batch(const void* d_payload, cfws_frame_desc_t* d_desc, size_t n, void* d_wire,
                          uint64_t cap, uint64_t* d_total, void* ws, size_t ws_size, void* stream)
 {
+    const CfwsPassScope pass_scope;
     // small batch, every argument valid: one launch (serialize_small_kernel)
     if (small_path() && n > 0 && n <= kSmallFrames && cap <= kSmallBytes && check_init() == CFWS_OK &&
         d_desc && ws && ws_size >= ws_layout(n, cap).bytes &&
         (cap == 0 || (d_payload && d_wire && !misaligned(d_payload, d_wire)))) {
+        const CfwsPassTimer timer(stream);
         serialize_small_kernel<<<small_grid(cap), kThreads, 0, static_cast<hipStream_t>(stream)>>>(
             static_cast<const uint8_t*>(d_payload), d_desc, (uint32_t)n, static_cast<uint8_t*>(d_wire),
             cap, ws_ptr<uint64_t>(ws, ws_layout(n, cap).hdr), d_total);
@@ -1503,6 +1514,7 @@ int cfws_deserialize_plan(const void* d_wire, uint64_t wire_size, const uint64_t
                           cfws_frame_desc_t* d_desc, int32_t* d_status, uint64_t cap,
                           uint64_t* d_total, void* ws, size_t ws_size, void* stream)
 {
+    const CfwsPassScope pass_scope;
     return deserialize_plan_impl(d_wire, wire_size, d_index, nullptr, n, max_payload, align, flags,
                                  d_desc, d_status, cap, d_total, ws, ws_size, stream);
 }
@@ -1511,6 +1523,7 @@ int cfws_deserialize_execute(const void* d_wire, const cfws_frame_desc_t* d_desc
                              const int32_t* d_status, size_t n, uint32_t flags, void* d_payload,
                              uint64_t cap, const void* ws, void* stream)
 {
+    const CfwsPassScope pass_scope;
     if (int rc = check_init()) return rc;
     if (n == 0 || cap == 0) return CFWS_OK;
     if (!d_wire || !d_desc || !d_status || !d_payload || !ws)
@@ -1523,6 +1536,7 @@ int cfws_deserialize_execute(const void* d_wire, const cfws_frame_desc_t* d_desc
         // every edge chunk of both passes is disjoint from the body chunks
         // either streaming pass writes, so pass 0's launch carries them all
         const bool split = edge_split();
+        const CfwsPassTimer timer(st);      // both passes: one timed span
         launch_pass<kModeDeser>(L, 0, d_wire, d_payload, d_desc, d_status, ws, cap, n, kClassData, st,
                                 0, !split, !split);
         launch_pass<kModeDeser>(L, 1, d_wire, d_payload, d_desc, d_status, ws, cap, n, kClassControl,
@@ -1544,11 +1558,13 @@ int cfws_deserialize_batch(const void* d_wire, uint64_t wire_size, const uint64_
                            uint64_t cap, uint64_t* d_total, void* ws, size_t ws_size,
                            void* stream)
 {
+    const CfwsPassScope pass_scope;
     // small batch without reassembly, every argument valid: one launch
     if (small_path() && n > 0 && n <= kSmallFrames && cap <= kSmallBytes && flags == 0 && align != 0 &&
         (align & (align - 1)) == 0 && align <= 4096 && check_init() == CFWS_OK && d_wire && d_index &&
         d_desc && d_status && ws && ws_size >= ws_layout(n, cap).bytes &&
         (cap == 0 || (d_payload && !misaligned(d_payload, d_wire)))) {
+        const CfwsPassTimer timer(stream);
         deserialize_small_kernel<<<small_grid(cap), kThreads, 0, static_cast<hipStream_t>(stream)>>>(
             static_cast<const uint8_t*>(d_wire), wire_size, d_index, (uint32_t)n, max_payload, align,
             d_desc, d_status, static_cast<uint8_t*>(d_payload), cap,
@@ -1566,15 +1582,11 @@ int cfws_deserialize_batch(const void* d_wire, uint64_t wire_size, const uint64_
         const uint32_t sb = grid_for(n, uint64_t(kFusedThreads) * kFusedItems);
         if (hipMemsetAsync(look, 0, look_bytes(sb), st) != hipSuccess)
             return launch_check("deserialize_batch(fused)");
-        CfwsPassEvents& pe = cfws_internal_pass_events();
-        const CfwsPassEvents timed = pe;
-        pe = {nullptr, nullptr};
-        if (timed.start) (void)hipEventRecord(static_cast<hipEvent_t>(timed.start), st);
+        const CfwsPassTimer timer(st);
         deserialize_plan_single_kernel<true, kFusedThreads><<<sb, kFusedThreads, 0, st>>>(
             static_cast<const uint8_t*>(d_wire), wire_size, d_index, nullptr, n, max_payload, align, d_desc,
             d_status, nullptr, look, ws_ptr<uint64_t>(ws, L.hdr), cap, nullptr, d_total,
             static_cast<uint8_t*>(d_payload));
-        if (timed.stop) (void)hipEventRecord(static_cast<hipEvent_t>(timed.stop), st);
         return launch_check("deserialize_batch(fused)");
     }
     if (int rc = cfws_deserialize_plan(d_wire, wire_size, d_index, n, max_payload, align, flags,
@@ -1609,12 +1621,9 @@ int slots_impl(const void* d_wire, uint64_t wire_size, const uint64_t* d_index, 
         return set_err(CFWS_ERROR_INVALID_ARGUMENT, "null pointer", hipSuccess);
     if (misaligned(d_payload, d_wire))
         return set_err(CFWS_ERROR_INVALID_ARGUMENT, "arenas must be 16-byte aligned", hipSuccess);
-    CfwsPassEvents& pe = cfws_internal_pass_events();
-    const CfwsPassEvents timed = pe;
-    pe = {nullptr, nullptr};
-    if (timed.start) (void)hipEventRecord(static_cast<hipEvent_t>(timed.start), st);
     const uint8_t* w = static_cast<const uint8_t*>(d_wire);
     uint8_t* out = static_cast<uint8_t*>(d_payload);
+    const CfwsPassTimer timer(st);
     if (slot <= kSlotWindow8Max && slots_window()) {
         // one wave-iteration of R P frames per wave (CFWS_SLOT_GRID caps the
         // workgroups: a grid-stride loop; A/B knob)
@@ -1665,7 +1674,6 @@ int slots_impl(const void* d_wire, uint64_t wire_size, const uint64_t* d_index, 
         deserialize_slots_kernel<false><<<grid_for(n, kThreads), kThreads, 0, st>>>(
             w, wire_size, d_index, n, max_payload, slot, d_desc, d_status, out, cap, d_total, dst);
     }
-    if (timed.stop) (void)hipEventRecord(static_cast<hipEvent_t>(timed.stop), st);
     return launch_check(what);
 }
 
@@ -1677,6 +1685,7 @@ int cfws_deserialize_slots(const void* d_wire, uint64_t wire_size, const uint64_
                            uint64_t max_payload, uint64_t slot, cfws_frame_desc_t* d_desc, int32_t* d_status,
                            void* d_payload, uint64_t cap, uint64_t* d_total, void* stream)
 {
+    const CfwsPassScope pass_scope;
     return slots_impl(d_wire, wire_size, d_index, nullptr, n, max_payload, slot, d_desc, d_status, d_payload, cap,
                       d_total, stream, false, "deserialize_slots");
 }
@@ -1686,6 +1695,7 @@ int cfws_deserialize_scatter(const void* d_wire, uint64_t wire_size, const uint6
                              cfws_frame_desc_t* d_desc, int32_t* d_status, void* d_payload, uint64_t cap,
                              void* stream)
 {
+    const CfwsPassScope pass_scope;
     return slots_impl(d_wire, wire_size, d_index, d_payload_off, n, max_payload, max_slot, d_desc, d_status,
                       d_payload, cap, nullptr, stream, true, "deserialize_scatter");
 }

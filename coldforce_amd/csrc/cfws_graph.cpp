@@ -20,6 +20,7 @@
 #include <stdio.h>
 
 #include "cfws.h"
+#include "cfws_internal.h"
 
 struct cfws_graph {
     hipGraph_t graph = nullptr;
@@ -77,6 +78,8 @@ int cfws_graph_serialize(const void* d_payload, cfws_frame_desc_t* d_desc, size_
                          uint64_t wire_capacity, uint64_t* d_wire_total, void* d_workspace,
                          size_t workspace_size, cfws_graph_t** out)
 {
+    const CfwsPassScope pass_scope;
+    (void)cfws_internal_take_pass();   // not timed (cfws_time_next_pass): the pair is dropped
     return capture([&](hipStream_t s) {
         return cfws_serialize_batch(d_payload, d_desc, n, d_wire, wire_capacity, d_wire_total,
                                     d_workspace, workspace_size, s);
@@ -89,6 +92,8 @@ int cfws_graph_deserialize(const void* d_wire, uint64_t wire_size, const uint64_
                            uint64_t payload_capacity, uint64_t* d_payload_total, void* d_workspace,
                            size_t workspace_size, cfws_graph_t** out)
 {
+    const CfwsPassScope pass_scope;
+    (void)cfws_internal_take_pass();   // not timed (cfws_time_next_pass): the pair is dropped
     return capture([&](hipStream_t s) {
         return cfws_deserialize_batch(d_wire, wire_size, d_index, n, max_payload, align, flags, d_desc,
                                       d_status, d_payload, payload_capacity, d_payload_total,
@@ -98,6 +103,8 @@ int cfws_graph_deserialize(const void* d_wire, uint64_t wire_size, const uint64_
 
 int cfws_graph_launch(cfws_graph_t* g, void* stream)
 {
+    const CfwsPassScope pass_scope;
+    (void)cfws_internal_take_pass();   // not timed (cfws_time_next_pass): the pair is dropped
     if (!g || !g->exec) return CFWS_ERROR_INVALID_ARGUMENT;
     const hipError_t e = hipGraphLaunch(g->exec, static_cast<hipStream_t>(stream));
     return e == hipSuccess ? CFWS_OK : graph_fail("launch", e);

@@ -949,6 +949,7 @@ int cfws_h2_serialize_batch(const void* d_payload, cfws_frame_desc_t* d_desc, si
                             void* d_h2, uint64_t h2_cap, uint64_t* d_h2_total, void* ws,
                             size_t ws_size, void* stream)
 {
+    const CfwsPassScope pass_scope;
     if (int rc = check_init()) return rc;
     if (S == 0) S = CFWS_H2_DEFAULT_MAX_FRAME_SIZE;
     if (S > 0xffffff) return set_err(CFWS_ERROR_INVALID_ARGUMENT, "max_frame_size > 2^24-1", hipSuccess);
@@ -1017,6 +1018,7 @@ int cfws_h2_deserialize_batch(const void* d_h2, uint64_t h2_size, const uint64_t
                               void* d_payload, uint64_t payload_cap, uint64_t* d_payload_total,
                               size_t* n_messages, void* ws, size_t ws_size, void* stream)
 {
+    const CfwsPassScope pass_scope;
     if (int rc = check_init()) return rc;
     if (S == 0) S = CFWS_H2_DEFAULT_MAX_FRAME_SIZE;
     const H2DeLayout L = h2_de_layout(n, pool_cap, payload_cap);
@@ -1111,9 +1113,15 @@ int cfws_h2_deserialize_batch(const void* d_h2, uint64_t h2_size, const uint64_t
             pdesc, d_h2_status, poffs, es, n, n_msg_d, starts, d_msg_desc, d_msg_status, hdr, udesc,
             ustatus, uoffs, umap, phdr + 3, pool_cap, pass_total);
     }
+    // the call's timed pass (cfws_time_next_pass): this fused pass, or, when
+    // the pool overflows and it stores nothing, the general form's passes
+    // below (the pair is recorded again around them)
+    const CfwsPassEvents timed = cfws_internal_take_pass();
+    if (timed.start) (void)hipEventRecord(static_cast<hipEvent_t>(timed.start), st);
     if (payload_cap)
         launch_streaming<kModeDeser>(d_h2, d_payload, udesc, ustatus, uoffs, umap, pass_total, nullptr,
                                      WL.regions, payload_cap, n, kClassAll, 0, st);
+    if (timed.stop) (void)hipEventRecord(static_cast<hipEvent_t>(timed.stop), st);
     if (int rc = launch_check("h2_deserialize")) return fail(rc);
     auto read_counts = [&]() -> int {
         hipError_t e = hipMemcpyAsync(&counts[0], n_msg_d, 8, hipMemcpyDeviceToHost, st);
@@ -1163,6 +1171,12 @@ int cfws_h2_deserialize_batch(const void* d_h2, uint64_t h2_size, const uint64_t
     // 3'. each pooled message through co_ws_frame_deserialize against its
     //     own size (co_ws_http2_extension.c:134-164), from the materialised
     //     pool (layout-first OOM rule)
+    if (timed.start) (void)hipEventRecord(static_cast<hipEvent_t>(timed.start), st);
+    struct StopAtExit {
+        const CfwsPassEvents& e;
+        hipStream_t st;
+        ~StopAtExit() { if (e.stop) (void)hipEventRecord(static_cast<hipEvent_t>(e.stop), st); }
+    } stop_at_exit{timed, st};
     if (pool_cap)
         launch_pass<kModeDeser>(PL, 0, d_h2, d_pool, pdesc, d_h2_status, pws, pool_cap, n, kClassAll, st);
     if (int rc = deserialize_plan_impl(d_pool, pool_cap, starts, ends, counts[0], max_payload, align, 0,

@@ -17,13 +17,39 @@ uint64_t cfws_internal_h2_grand_total_offset(uint64_t n_h2, uint64_t pool_cap, u
 // address dev_dst (cfws_mapped_device_pointer); no mapping check.
 int cfws_internal_copy_out(const void* d_src, void* dev_dst, uint64_t n, void* stream);
 
-// cfws_time_next_pass: the calling thread's pending event pair (hipEvent_t),
-// taken (and cleared) by the next launch_streaming on this thread.
+// cfws_time_next_pass: an event pair (hipEvent_t) for the calling thread's
+// NEXT public batch call. Every public call that launches work opens a
+// CfwsPassScope on entry: the outermost scope moves the pending pair into
+// the call (the pending slot is empty from then on) and drops whatever is
+// left of it on exit, so a pair never outlives the call that took it (an
+// error return, an empty batch, a path with no timed pass included). Inside
+// the call, the launch site of its timed pass takes the pair once
+// (cfws_internal_take_pass) and records start before / stop after its
+// kernel; nested public calls (a batch call's plan and execute) share the
+// outer call's pair.
 struct CfwsPassEvents {
     void* start;
     void* stop;
 };
-CfwsPassEvents& cfws_internal_pass_events();
+CfwsPassEvents& cfws_internal_pass_events();     // the pending pair
+CfwsPassEvents cfws_internal_take_pass();        // the current call's pair, once; then empty
+struct CfwsPassScope {
+    CfwsPassScope();
+    ~CfwsPassScope();
+    CfwsPassScope(const CfwsPassScope&) = delete;
+    CfwsPassScope& operator=(const CfwsPassScope&) = delete;
+};
+// The timed pass's launch site: takes the call's pair (if it still holds
+// one) and records start on `stream` now, stop when the timer goes out of
+// scope (after the pass's kernels were queued).
+struct CfwsPassTimer {
+    explicit CfwsPassTimer(void* stream);
+    ~CfwsPassTimer();
+    CfwsPassTimer(const CfwsPassTimer&) = delete;
+    CfwsPassTimer& operator=(const CfwsPassTimer&) = delete;
+    CfwsPassEvents e;
+    void* stream;
+};
 
 // The drop-in's frame service (cfws_ops.hip, used by cfws_frame.cpp): one
 // resident workgroup per device that serves every calling thread of the

@@ -1971,10 +1971,7 @@ void launch_streaming(const void* src, void* dst, const cfws_frame_desc_t* desc,
     // is far above their output (an oversized arena; the HTTP/2 receive passes
     // len(h2) + 16 n) may get the large-frame residency for small frames --
     // a speed effect only, the bytes written are the same.
-    CfwsPassEvents& pe = cfws_internal_pass_events();
-    const CfwsPassEvents timed = pe;
-    pe = {nullptr, nullptr};
-    if (timed.start) (void)hipEventRecord(static_cast<hipEvent_t>(timed.start), st);
+    const CfwsPassTimer timer(st);
     xform_kernel<kMode><<<eb + sg, kThreads, xform_lds_bytes(kMode, n ? cap / n : cap), st>>>(
         static_cast<const uint8_t*>(src), static_cast<uint8_t*>(dst), desc, status, offs, map,
         total_p, base_p, cap, (uint32_t)n, klass, sid, parent, eb, eb ? reasm_offs1 : nullptr,
@@ -1985,7 +1982,6 @@ void launch_streaming(const void* src, void* dst, const cfws_frame_desc_t* desc,
     if (split) edge_kernel<kMode><<<grid_for(edge_threads(n), kEdgeThreads), kEdgeThreads, 0, st>>>(
         static_cast<const uint8_t*>(src), static_cast<uint8_t*>(dst), desc, status, offs,
         total_p, base_p, cap, (uint32_t)n, klass, sid, parent);
-    if (timed.stop) (void)hipEventRecord(static_cast<hipEvent_t>(timed.stop), st);
 }
 
 template <int kMode>

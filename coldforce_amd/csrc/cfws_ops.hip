@@ -782,6 +782,7 @@ int cfws_index_frames_batch(const void* d_buf, const uint64_t* d_begin, const ui
                             uint64_t* d_first, uint64_t* d_consumed, int32_t* d_stop,
                             uint64_t* d_total, void* ws, size_t ws_size, void* stream)
 {
+    const CfwsPassScope pass_scope;
     if (int rc = check_init()) return rc;
     if (ws_size < cfws_index_workspace_size(n))
         return set_err(CFWS_ERROR_WORKSPACE, "index workspace too small", hipSuccess);
@@ -813,6 +814,7 @@ int cfws_index_frames_batch(const void* d_buf, const uint64_t* d_begin, const ui
 int cfws_ws_accept_keys_batch(const void* d_keys, const uint64_t* d_key_off, size_t n,
                               char* d_accept, void* stream)
 {
+    const CfwsPassScope pass_scope;
     if (int rc = check_init()) return rc;
     if (n == 0) return CFWS_OK;
     if (!d_keys || !d_key_off || !d_accept)
@@ -837,6 +839,7 @@ void* cfws_mapped_device_pointer(const void* h_ptr)
 
 int cfws_copy_to_host(const void* d_src, void* h_dst, uint64_t n, void* stream)
 {
+    const CfwsPassScope pass_scope;
     if (int rc = check_init()) return rc;
     if (n == 0) return CFWS_OK;
     if (!d_src || !h_dst) return set_err(CFWS_ERROR_INVALID_ARGUMENT, "null pointer", hipSuccess);
@@ -849,6 +852,7 @@ int cfws_copy_to_host(const void* d_src, void* h_dst, uint64_t n, void* stream)
 int cfws_encode_headers(cfws_frame_desc_t* d_desc, size_t n, void* d_wire, uint64_t wire_capacity,
                         void* stream)
 {
+    const CfwsPassScope pass_scope;
     if (int rc = check_init()) return rc;
     if (n == 0) return CFWS_OK;
     if (!d_desc || !d_wire) return set_err(CFWS_ERROR_INVALID_ARGUMENT, "null pointer", hipSuccess);
@@ -862,6 +866,7 @@ int cfws_parse_headers(const void* d_wire, uint64_t wire_size, const uint64_t* d
                        uint64_t max_payload, cfws_frame_desc_t* d_desc, int32_t* d_status,
                        void* stream)
 {
+    const CfwsPassScope pass_scope;
     if (int rc = check_init()) return rc;
     if (n == 0) return CFWS_OK;
     if (!d_wire || !d_frame_index || !d_desc || !d_status)
@@ -954,11 +959,48 @@ CfwsPassEvents& cfws_internal_pass_events()
     return e;
 }
 
+namespace {
+thread_local CfwsPassEvents t_call_pass = {nullptr, nullptr};   // the open call's pair
+thread_local int t_pass_depth = 0;                               // open public calls
+}  // namespace
+
+CfwsPassScope::CfwsPassScope()
+{
+    if (t_pass_depth++ == 0) {
+        CfwsPassEvents& pe = cfws_internal_pass_events();
+        t_call_pass = pe;
+        pe = {nullptr, nullptr};
+    }
+}
+
+CfwsPassScope::~CfwsPassScope()
+{
+    if (--t_pass_depth == 0) t_call_pass = {nullptr, nullptr};
+}
+
+CfwsPassEvents cfws_internal_take_pass()
+{
+    const CfwsPassEvents e = t_call_pass;
+    t_call_pass = {nullptr, nullptr};
+    return e;
+}
+
+CfwsPassTimer::CfwsPassTimer(void* s) : e(cfws_internal_take_pass()), stream(s)
+{
+    if (e.start) (void)hipEventRecord(static_cast<hipEvent_t>(e.start), static_cast<hipStream_t>(stream));
+}
+
+CfwsPassTimer::~CfwsPassTimer()
+{
+    if (e.stop) (void)hipEventRecord(static_cast<hipEvent_t>(e.stop), static_cast<hipStream_t>(stream));
+}
+
 extern "C" {
 
 int cfws_mask_batch(const void* d_payload, const cfws_frame_desc_t* d_desc, size_t n,
                     uint64_t max_payload_size, void* d_wire, uint64_t wire_capacity, void* stream)
 {
+    const CfwsPassScope pass_scope;
     return launch_payload_xor<false>(d_payload, d_wire, d_desc, nullptr, n, max_payload_size,
                                      wire_capacity, stream, "mask_batch");
 }
@@ -966,6 +1008,7 @@ int cfws_mask_batch(const void* d_payload, const cfws_frame_desc_t* d_desc, size
 int cfws_mask_batch_packed(const void* d_payload, const cfws_frame_desc_t* d_desc, size_t n,
                            uint64_t max_payload_size, void* d_wire, uint64_t wire_capacity, void* stream)
 {
+    const CfwsPassScope pass_scope;
     return launch_payload_xor<false>(d_payload, d_wire, d_desc, nullptr, n, max_payload_size,
                                      wire_capacity, stream, "mask_batch_packed", 1u);
 }
@@ -974,6 +1017,7 @@ int cfws_unmask_batch(const void* d_wire, const cfws_frame_desc_t* d_desc, const
                       size_t n, uint64_t max_payload_size, void* d_payload,
                       uint64_t payload_capacity, void* stream)
 {
+    const CfwsPassScope pass_scope;
     return launch_payload_xor<true>(d_wire, d_payload, d_desc, d_status, n, max_payload_size,
                                     payload_capacity, stream, "unmask_batch");
 }
@@ -981,6 +1025,7 @@ int cfws_unmask_batch(const void* d_wire, const cfws_frame_desc_t* d_desc, const
 int cfws_xor_mask(const void* d_src, void* d_dst, uint64_t n, uint32_t key, uint32_t phase,
                   void* stream)
 {
+    const CfwsPassScope pass_scope;
     if (int rc = check_init()) return rc;
     if (n == 0) return CFWS_OK;
     const uint64_t blocks = (n / 16 + kThreads - 1) / kThreads;
@@ -1008,6 +1053,7 @@ int cfws_time_next_pass(void* start, void* stop)
 
 int cfws_device_copy(const void* d_src, void* d_dst, uint64_t n, void* stream)
 {
+    const CfwsPassScope pass_scope;
     if (int rc = check_init()) return rc;
     if (n == 0) return CFWS_OK;
     if (misaligned(d_src, d_dst) || (n & 15u))
@@ -1024,6 +1070,7 @@ int cfws_device_copy(const void* d_src, void* d_dst, uint64_t n, void* stream)
 
 int cfws_fill_splitmix(void* d_dst, uint64_t n, uint64_t seed, uint64_t byte_base, void* stream)
 {
+    const CfwsPassScope pass_scope;
     if (int rc = check_init()) return rc;
     if (byte_base & 7u) return set_err(CFWS_ERROR_INVALID_ARGUMENT, "byte_base % 8 != 0", hipSuccess);
     if (reinterpret_cast<uintptr_t>(d_dst) & 15u)

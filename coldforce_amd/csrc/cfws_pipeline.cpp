@@ -195,6 +195,8 @@ int cfws_pipeline_set_d2h(cfws_pipeline_t* p, int mode)
 int cfws_pipeline_serialize(cfws_pipeline_t* p, const void* h_payload, cfws_frame_desc_t* h_desc,
                             size_t n, void* h_wire, uint64_t wire_capacity, uint64_t* wire_total)
 {
+    const CfwsPassScope pass_scope;
+    (void)cfws_internal_take_pass();   // not timed (cfws_time_next_pass): the pair is dropped
     if (!p || (n && (!h_payload || !h_desc || !h_wire))) return fail("null argument");
     // Layout on the host copy of the descriptors (same rule as the device
     // plan) so that chunks can be cut by wire bytes.
@@ -461,6 +463,8 @@ int cfws_pipeline_deserialize(cfws_pipeline_t* p, const void* h_wire, uint64_t w
                               int32_t* h_status, void* h_payload, uint64_t payload_capacity,
                               uint64_t* payload_total)
 {
+    const CfwsPassScope pass_scope;
+    (void)cfws_internal_take_pass();   // not timed (cfws_time_next_pass): the pair is dropped
     if (!p || (n && (!h_wire || !h_index || !h_desc || !h_status || !h_payload)))
         return fail("null argument");
     if (flags != 0) return fail("the pipeline supports flags = 0 only");
@@ -479,6 +483,8 @@ int cfws_pipeline_receive(cfws_pipeline_t* p, const void* h_wire, uint64_t begin
                           int32_t* h_status, size_t* n_frames, uint64_t* consumed, int32_t* stop,
                           void* h_payload, uint64_t payload_capacity, uint64_t* payload_total)
 {
+    const CfwsPassScope pass_scope;
+    (void)cfws_internal_take_pass();   // not timed (cfws_time_next_pass): the pair is dropped
     if (!p || !n_frames || (end > begin && !h_wire)) return fail("null argument");
     if (*n_frames && (!h_desc || !h_status || !h_payload)) return fail("null argument");
     if (align == 0 || (align & (align - 1)) || align > 4096) return fail("bad align");
@@ -571,6 +577,8 @@ int cfws_pipeline_h2_serialize(cfws_pipeline_t* p, const void* h_payload, cfws_f
                                size_t n, uint32_t stream_id, uint32_t max_frame_size, void* h_h2,
                                uint64_t h2_capacity, uint64_t* h2_total)
 {
+    const CfwsPassScope pass_scope;
+    (void)cfws_internal_take_pass();   // not timed (cfws_time_next_pass): the pair is dropped
     if (!p || (n && (!h_payload || !h_desc || !h_h2))) return fail("null argument");
     const uint64_t mfs = max_frame_size ? max_frame_size : CFWS_H2_DEFAULT_MAX_FRAME_SIZE;
     // the WS layout (as cfws_serialize_plan) and each frame's DATA-stream bytes
@@ -664,6 +672,8 @@ int cfws_pipeline_h2_deserialize(cfws_pipeline_t* p, const void* h_h2, uint64_t 
                                  size_t* n_messages, void* h_payload, uint64_t payload_capacity,
                                  uint64_t* payload_total)
 {
+    const CfwsPassScope pass_scope;
+    (void)cfws_internal_take_pass();   // not timed (cfws_time_next_pass): the pair is dropped
     if (!p || !n_messages ||
         (n && (!h_h2 || !h_index || !h_h2_status || !h_msg_desc || !h_msg_status || !h_payload)))
         return fail("null argument");

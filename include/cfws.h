@@ -496,15 +496,24 @@ size_t cfws_dropin_gpu_min(void);
 int cfws_device_copy(const void* d_src, void* d_dst, uint64_t n, void* stream);
 
 /* ---- profiling ------------------------------------------------------------
- * The next streaming pass the CALLING THREAD launches (the execute half of
- * a batch call: xform_kernel with its edge workgroups; the fused plan +
- * copy kernel of cfws_deserialize_batch for batches of small frames; the
- * one fused pass of cfws_h2_serialize_batch /
- * cfws_h2_deserialize_batch) records `start`
- * (a hipEvent_t) on its stream right before the launch and `stop` right
- * after it. One pass only, then the pair is cleared; NULL, NULL clears it.
- * Lets a caller time that one kernel of a multi-kernel call with events
- * (bench.py's config-5 roofline). */
+ * `start` / `stop` (hipEvent_t) for the CALLING THREAD's next batch call
+ * (any function above that takes a stream). That call takes the pair on
+ * entry -- from then on no pair is pending -- and records `start` on its
+ * stream right before its timed pass and `stop` right after it:
+ *   cfws_serialize_batch / _execute, cfws_deserialize_batch / _execute:
+ *     the streaming pass (xform_kernel with its edge workgroups; both
+ *     passes of a reassembling execute are one timed span); for batches of
+ *     small frames the one kernel the call launches instead (the small-batch
+ *     kernel, or the fused plan + copy kernel of cfws_deserialize_batch);
+ *   cfws_deserialize_slots / _scatter: their one kernel;
+ *   cfws_h2_serialize_batch: its DATA-frame pass; cfws_h2_deserialize_batch:
+ *     its fused payload pass, or, when the pooled bytes exceed pool_capacity
+ *     (that pass then stores nothing), the pool + plan + payload passes of
+ *     the general form that does the work.
+ * Any other call, an error return, an empty batch, a graph capture / launch
+ * or a pipeline call records nothing and drops the pair. NULL, NULL clears
+ * a pending pair. Lets a caller time the one kernel of a multi-kernel call
+ * that moves the bytes (bench.py's roofline figures). */
 int cfws_time_next_pass(void* start, void* stop);
 
 /* ---- synthetic input (bench / tests) -------------------------------------
