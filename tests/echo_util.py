@@ -120,6 +120,20 @@ def h2_frames(stream: bytes, preface: bool):
     return out
 
 
+def h2_data_frames(stream: bytes, preface: bool) -> list[tuple[int, bytes]]:
+    """(flags, raw frame bytes: 9-byte header + payload) of every DATA frame
+    (type 0) in a captured HTTP/2 byte stream, in order."""
+    p = 24 if preface else 0
+    out = []
+    while p + 9 <= len(stream):
+        n = int.from_bytes(stream[p:p + 3], "big")
+        if stream[p + 3] == 0:
+            out.append((stream[p + 4], stream[p:p + 9 + n]))
+        p += 9 + n
+    assert p == len(stream), "trailing partial HTTP/2 frame"
+    return out
+
+
 def frame_text(k: int, payload: int) -> bytes:
     """Frame k's payload: byte j is 'a' + (j + k) % 26 (oracle/ws_echo.c)."""
     base = bytes(97 + i % 26 for i in range(payload + 26))

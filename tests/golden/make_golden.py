@@ -18,6 +18,9 @@ Fixtures (inputs + expected outputs):
                         deserialize output for the small-frame batches the
                         bench quotes (4 M x 1 KiB TEXT, 16 M x 256 B BINARY)
   handshake_cases.json  Sec-WebSocket-Accept keys (co_sha1.c + co_base64.c)
+  h2_echo_digests.json  DATA frames the stock HTTP/2 echo pair (the reference's
+                        co_http2_stream.c send split and pooling) put on the wire
+                        for WS frames of 16,376-65,536 B (--only h2echo)
   index_cases.json      receive-loop frame indexing (co_ws_server.c:107-169 around
                         the reference's co_ws_frame_deserialize): frame starts,
                         consumed index, stop code per connection stream
@@ -344,6 +347,44 @@ def h2_digest(R, n_frames, frame_size, payload_seed, key_seed, S=16384, sid=1):
                 key_seed=key_seed, max_frame=S, sid=sid, h2_len=total, h2_sha256=h.hexdigest())
 
 
+H2_ECHO_SIZES = (16376, 16377, 40000, 65536)
+
+
+def h2_echo_cases():
+    """The reference's own HTTP/2 stream code on WS frames that span several
+    DATA frames: the stock echo pair (oracle/_ref/ws_echo_stock, h2 mode:
+    co_http2_stream_send_ws_frame -> co_http2_stream_send_data's split,
+    co_http2_stream.c:933-1013, and the receiver's pooling, :550-608) sends
+    `frames` TEXT frames of each size, client-masked with the srandom(seed)
+    stream, and echoes them unmasked. The capture of each side gives the
+    DATA frames (9-byte header + payload) that carried the WS frames: their
+    count, the DATA payload sizes of one WS frame, and the SHA-256 of all of
+    them back to back."""
+    import tempfile
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from echo_util import available, h2_data_frames, run_echo
+    assert available("stock"), "oracle/_ref/ws_echo_stock not built"
+    out = []
+    for i, payload in enumerate(H2_ECHO_SIZES):
+        frames, window, seed = 64, 8, 21 + i
+        with tempfile.TemporaryDirectory() as tmp:
+            r = run_echo("stock", "h2", frames, payload, window=window, seed=seed, capture_dir=tmp)
+            assert r["client_rc"] == 0 and r["client"]["received"] == frames and r["client"]["bad_echo"] == 0
+            case = dict(payload=payload, frames=frames, window=window, seed=seed, opcode=1, sid=1,
+                        max_frame=16384)
+            for side in ("client", "server"):
+                with open(r["capture"][side], "rb") as f:
+                    data = h2_data_frames(f.read(), preface=side == "client")
+                raw = b"".join(d for _, d in data)
+                per = len(data) // frames
+                case[side] = dict(mask=side == "client", data_frames=len(data),
+                                  end_stream=sum(1 for fl, _ in data if fl & 1),
+                                  split=[len(d) - 9 for _, d in data[:per]], data_len=len(raw),
+                                  data_sha256=sha(raw))
+        out.append(case)
+    return out
+
+
 def index_cases(R):
     """Streams of reference-serialized frames, cut and corrupted the ways a
     receive buffer can be; the reference's loop gives starts/consumed/stop.
@@ -412,17 +453,20 @@ def handshake_cases(R):
     return [dict(key_hex=k.hex(), accept=O.ref_ws_accept_key(R, k)) for k in keys]
 
 
-def small_batches(R):
+SMALL_BATCHES = [(4 << 20, 1024, 1), (16 << 20, 256, 2), ((4 << 30) // 2048, 2048, 2),
+                 ((4 << 30) // 3072, 3072, 2), ((4 << 30) // 3584, 3584, 1), (8 << 20, 512, 2)]
+
+
+def small_batches(R, have=()):
     # the bench's payload / key seeds (bench.py PAYLOAD_SEED, KEY_SEED);
-    # 1 KiB as TEXT (config 1's frames), 256 B as BINARY; the in-region
-    # send's range (payloads up to 3,584 B, round 4): 2 KiB and 3 KiB batches
-    # of 4 GiB as the bench runs them (bench.py --frame-size: 4 GiB // size
-    # frames), and payloads of exactly the bound
-    return [small_batch_digest(R, 4 << 20, 1024, 0x5EED0002, 2, 1),
-            small_batch_digest(R, 16 << 20, 256, 0x5EED0002, 2, 2),
-            small_batch_digest(R, (4 << 30) // 2048, 2048, 0x5EED0002, 2, 2),
-            small_batch_digest(R, (4 << 30) // 3072, 3072, 0x5EED0002, 2, 2),
-            small_batch_digest(R, (4 << 30) // 3584, 3584, 0x5EED0002, 2, 1)]
+    # 1 KiB as TEXT (config 1's frames), 256 B and 512 B as BINARY; the
+    # in-region send's range (payloads up to 3,584 B, round 4): 2 KiB and
+    # 3 KiB batches of 4 GiB as the bench runs them (bench.py --frame-size:
+    # 4 GiB // size frames), and payloads of exactly the bound. Entries
+    # already in `have` (same frames, size, opcode) are kept, not recomputed.
+    old = {(d["n_frames"], d["frame_size"], d["opcode"]): d for d in have}
+    return [old.get((n, fs, op)) or small_batch_digest(R, n, fs, 0x5EED0002, 2, op)
+            for n, fs, op in SMALL_BATCHES]
 
 
 def main():
@@ -437,10 +481,15 @@ def main():
         dump("index_cases.json", index_cases(R))
         return
     if a.only == "small":
-        dump("small_batch_digests.json", small_batches(R))
+        path = os.path.join(OUT, "small_batch_digests.json")
+        have = json.load(open(path)) if os.path.exists(path) else []
+        dump("small_batch_digests.json", small_batches(R, have))
         return
     if a.only == "handshake":
         dump("handshake_cases.json", handshake_cases(R))
+        return
+    if a.only == "h2echo":
+        dump("h2_echo_digests.json", h2_echo_cases())
         return
     dump("rfc6455_kat.json", rfc6455(R))
     dump("serialize_cases.json", serialize_cases(R))
@@ -462,6 +511,7 @@ def main():
     dump("h2_digests.json", h2d)
     dump("index_cases.json", index_cases(R))
     dump("handshake_cases.json", handshake_cases(R))
+    dump("h2_echo_digests.json", h2_echo_cases())
     if not a.skip_full:
         dump("small_batch_digests.json", small_batches(R))
 

@@ -195,9 +195,10 @@ def test_dropin_echo_wire_identical_to_stock(mode, policy, tmp_path):
 def test_dropin_echo_small_frames_and_binary_sizes(tmp_path):
     """Frame sizes around the header-length boundaries through the real
     callers (125/126 B, 65,535/65,536 B) are checked by every echo; the wire
-    equals the stock build's. 65,535 B is the last size the default size
-    policy XORs on the calling thread, 65,536 B the first it sends to the
-    device."""
+    equals the stock build's. Under the default size policy
+    (CFWS_DROPIN_GPU_MIN_DEFAULT = SIZE_MAX, include/cfws.h) every one of
+    these frames is XORed on the calling thread; the device paths at these
+    sizes are test_dropin_device_paths_wire_identical_to_stock's."""
     _need("stock")
     _need("cfws")
     for payload, frames in ((125, 2000), (126, 2000), (65535, 200), (65536, 200)):
@@ -247,3 +248,46 @@ def test_device_accept_key_matches_reference_server(tmp_path):
     pairs = _accept_pairs(tmp_path, (1, 2, 3, 99, 12345))
     got = cfws.ws_accept_keys([k for k, _ in pairs])
     assert got == [a for _, a in pairs]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode,payload,frames", [("ws", 65536, 200), ("ws", 2 << 20, 24),
+                                                 ("h2", 16376, 64), ("h2", 16377, 64),
+                                                 ("h2", 40000, 64), ("h2", 65536, 64)])
+def test_dropin_device_paths_wire_identical_to_stock(mode, payload, frames, tmp_path):
+    """The drop-in's device paths through the reference's callers, every
+    masked frame sent to the device (CFWS_DROPIN_GPU_MIN=0): 65,536 B takes
+    the per-frame launch on mapped staging, 2 MiB the DMA path (under the
+    32 MiB receive limit), 16,376-40,000 B the frame service. The callers
+    are co_ws_send (co_ws_client.c:427-460) and the receive loops
+    (co_ws_server.c:85-173, co_ws_client.c:178-274); in h2 mode
+    co_http2_stream_send_ws_frame / co_http2_stream_receive_ws_frame over
+    the reference's co_http2_stream_send_data split into several DATA frames
+    (co_http2_stream.c:933-1013) and the receiver's pooling (:550-608). The
+    wire equals the stock build's byte for byte in both directions, and the
+    h2 runs equal tests/golden/h2_echo_digests.json (the stock capture)."""
+    _need("stock")
+    _need("cfws")
+    import hashlib
+    from conftest import golden
+    from echo_util import h2_data_frames
+    window = 4 if payload >= (1 << 20) else 8
+    seed = payload % 1000 + 1
+    g = None
+    if mode == "h2":
+        g = next(c for c in golden("h2_echo_digests.json") if c["payload"] == payload)
+        frames, window, seed = g["frames"], g["window"], g["seed"]
+    port = free_port()
+    caps = {}
+    for build in ("stock", "cfws"):
+        r = run_echo(build, mode, frames, payload, window=window, seed=seed, port=port,
+                     capture_dir=str(tmp_path / build), timeout=240,
+                     env={"CFWS_DROPIN_GPU_MIN": "0"} if build == "cfws" else None)
+        _ok(r, frames)
+        caps[build] = {side: _read(r["capture"][side]) for side in ("client", "server")}
+    for side in ("client", "server"):
+        assert caps["stock"][side] == caps["cfws"][side], (mode, payload, side)
+        if g is not None:
+            data = h2_data_frames(caps["cfws"][side], preface=side == "client")
+            raw = b"".join(x for _, x in data)
+            assert hashlib.sha256(raw).hexdigest() == g[side]["data_sha256"], side

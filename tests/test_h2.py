@@ -633,3 +633,97 @@ def test_gpu_h2_deserialize_stream_on_other_device():
         s.synchronize()
         assert m == exp["n_msg"] and int(tot.item()) == exp["total"]
         assert np.array_equal(pay[:exp["total"]].cpu().numpy(), exp["payload"][:exp["total"]])
+
+
+# ---- the reference's own stream code on multi-DATA-frame WS frames ---------------
+# tests/golden/h2_echo_digests.json: the DATA frames the stock echo pair
+# (oracle/_ref/ws_echo_stock: co_http2_stream_send_ws_frame ->
+# co_http2_stream_send_data, co_http2_stream.c:933-1013, and the peer's
+# pooling, :550-608) put on the wire for TEXT frames of 16,376 B (one DATA
+# frame), 16,377 B (16,384 + 1), 40,000 B (2 x 16,384 + 7,240) and 65,536 B
+# (4 x 16,384 + 14), client-masked after srandom(seed), echoed unmasked.
+
+def _echo_batch(case, side):
+    """The WS frames one side of the echo sent: frame k is TEXT, fin, with
+    payload 'a' + (j + k) % 26 (oracle/ws_echo.c fill_frame), masked with
+    the k-th key of srandom(seed) on the client side."""
+    from echo_util import frame_text
+    n, fs = case["frames"], case["payload"]
+    arena = np.frombuffer(b"".join(frame_text(k, fs) for k in range(n)), np.uint8).copy()
+    d = np.zeros(n, dtype=O.DESC_DTYPE)
+    d["payload_off"] = np.arange(n, dtype=np.uint64) * fs
+    d["payload_size"], d["fin"], d["opcode"] = fs, 1, case["opcode"]
+    if case[side]["mask"]:
+        d["mask"] = 1
+        d["mask_key"] = O.keys(case["seed"], n)
+    return arena, d
+
+
+def _echo_cases():
+    return golden("h2_echo_digests.json")
+
+
+@pytest.mark.parametrize("i", range(4))
+def test_oracle_matches_stock_h2_echo_golden(i):
+    """The restatement's DATA split (cfws_oracle.c) gives the bytes the
+    reference's stream code put on the wire, both directions, and its
+    receive pools them back into the payloads."""
+    case = _echo_cases()[i]
+    for side in ("client", "server"):
+        g = case[side]
+        arena, d = _echo_batch(case, side)
+        h2, _ = O.h2_serialize_batch(arena, d, case["sid"], case["max_frame"])
+        assert len(h2) == g["data_len"] and sha(h2) == g["data_sha256"], side
+        idx = O.h2_index(h2)
+        assert len(idx) == g["data_frames"]
+        assert [int(h2[p]) << 16 | int(h2[p + 1]) << 8 | int(h2[p + 2]) for p in idx[:len(g["split"])]] \
+            == g["split"]
+        r = O.h2_deserialize_batch(h2, idx, case["max_frame"], align=1, payload_capacity=len(arena))
+        assert r["n_msg"] == case["frames"] and (r["msg_status"][:r["n_msg"]] == 0).all()
+        assert np.array_equal(r["payload"][:len(arena)], arena)
+
+
+@pytest.mark.parametrize("i", range(4))
+def test_stock_h2_echo_reproduces_golden(i, tmp_path):
+    """Re-runs the stock echo pair (the reference's http2 + ws_http2 code
+    compiled in place) and checks its capture against the fixture."""
+    from echo_util import available, h2_data_frames, run_echo
+    if not available("stock"):
+        pytest.skip("oracle/_ref/ws_echo_stock not built")
+    case = _echo_cases()[i]
+    r = run_echo("stock", "h2", case["frames"], case["payload"], window=case["window"], seed=case["seed"],
+                 capture_dir=str(tmp_path))
+    assert r["client_rc"] == 0 and r["client"]["received"] == case["frames"] and r["client"]["bad_echo"] == 0
+    for side in ("client", "server"):
+        with open(r["capture"][side], "rb") as f:
+            data = h2_data_frames(f.read(), preface=side == "client")
+        raw = b"".join(x for _, x in data)
+        assert sha(raw) == case[side]["data_sha256"], side
+        assert sum(1 for fl, _ in data if fl & 1) == case[side]["end_stream"] == case["frames"]
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not gpu_present(), reason="needs the MI355X")
+@pytest.mark.parametrize("i", range(4))
+def test_gpu_h2_matches_stock_h2_echo(i):
+    """cfws_h2_serialize_batch on the echo's frames gives the DATA frames
+    the reference's stream code sent (split, END_STREAM on the last frame of
+    each WS frame, stream 1), both directions; cfws_h2_deserialize_batch
+    pools them back into the payloads."""
+    torch, cfws = _gpu()
+    case = _echo_cases()[i]
+    for side in ("client", "server"):
+        g = case[side]
+        arena, d = _echo_batch(case, side)
+        got, t = gpu_h2_serialize(arena, d, case["sid"], case["max_frame"])
+        assert t == g["data_len"] and sha(got) == g["data_sha256"], side
+        idx = O.h2_index(got)
+        h = torch.from_numpy(np.concatenate([got, np.zeros(16, np.uint8)])).cuda()
+        idx_t = torch.from_numpy(idx.astype(np.int64)).cuda()
+        pool = torch.empty(t + 16, dtype=torch.uint8, device="cuda")
+        pay = torch.empty(len(arena) + 16 * len(idx) + 16, dtype=torch.uint8, device="cuda")
+        st, md, ms, tot, m = cfws.h2_deserialize(h, t, idx_t, pool, pay, case["max_frame"], align=1)
+        torch.cuda.synchronize()
+        assert m == case["frames"] and bool((st == 0).all()) and bool((ms == 0).all())
+        assert int(tot.item()) == len(arena)
+        assert np.array_equal(pay[:len(arena)].cpu().numpy(), arena)
