@@ -7,7 +7,7 @@
 HIPCC    ?= /opt/rocm/bin/hipcc
 ARCH     ?= gfx950
 HIPFLAGS ?= -O3 -std=c++17 -fPIC -Wall -Wno-unused-result
-DEVSRC   := cfws_device cfws_h2 cfws_ops
+DEVSRC   := cfws_device cfws_h2 cfws_ops cfws_uniform
 HOSTSRC  := cfws_frame cfws_pipeline cfws_index cfws_graph
 HDR      := include/cfws.h include/cfws_co_ws_frame.h coldforce_amd/csrc/cfws_internal.h coldforce_amd/csrc/cfws_devpolicy.h
 LIB      := coldforce_amd/libcfws.so

@@ -63,6 +63,13 @@ def parse():
     ap.add_argument("--recv-scatter", action="store_true",
                     help="config2: receive each frame to its own offset, the slots in a "
                          "shuffled order (cfws_deserialize_scatter)")
+    ap.add_argument("--send", choices=["batch", "uniform"], default="batch",
+                    help="config2: the send through cfws_serialize_batch (descriptor table + "
+                         "plan + execute) or cfws_serialize_uniform (payload + one key per "
+                         "frame, no plan: the compact form of a uniform batch)")
+    ap.add_argument("--recv-info", action="store_true",
+                    help="with --recv-slots / --recv-scatter: the compact 8-byte per-frame output "
+                         "(cfws_deserialize_slots_info / _scatter_info) instead of descriptors + statuses")
     ap.add_argument("--keys", type=int, default=1 << 20, help="accept workload: client keys per GPU")
     ap.add_argument("--connections", type=int, default=16384, help="index workload: connections")
     ap.add_argument("--index-mib", type=int, default=1024, help="index workload: receive-buffer MiB")
@@ -847,12 +854,23 @@ def main():
     perm = (torch.from_numpy(np.random.default_rng(5).permutation(F).astype(np.int64)).to(dev)
             if args.recv_scatter else None)
     dst_off = perm * slot if perm is not None else None
-    fused_de = (not slot and flags == 0 and F > 1024 and os.environ.get("CFWS_FUSED_DESER", "1") != "0"
-                and wire_total // F <= int(os.environ.get("CFWS_FUSED_AVG_MAX", "512")))  # fused_avg_max()
+    if args.recv_info and not slot:
+        sys.exit("bench.py: --recv-info needs --recv-slots or --recv-scatter")
+    uniform = args.send == "uniform"
+    if uniform and args.workload != "config2":
+        sys.exit("bench.py: --send uniform needs config2 (a uniform batch)")
+    keys_t = torch.from_numpy(desc_np["mask_key"].view(np.int32).copy()).to(dev) if uniform else None
+    info_t = torch.empty((F, 8), dtype=torch.uint8, device=dev) if args.recv_info else None
+    # the receive kernel the timed pass is, as the library routes the call
+    recv_kernel = cfws.lib().cfws_deserialize_pass_kernel(F, wire_total, 16, flags, back.numel()).decode()
 
     def step(ev=None):
         if ev: cfws.time_next_pass(ev[0], ev[1])
-        cfws.serialize(payload, desc_ser, wire, ws_ser, tot_ser)
+        if uniform:
+            cfws.serialize_uniform(payload, keys_t, F, fs, wire, opcode=cfws.OPCODE_BINARY, mask=True,
+                                   total_t=tot_ser)
+        else:
+            cfws.serialize(payload, desc_ser, wire, ws_ser, tot_ser)
         if flags:
             # reassembly: two streaming passes (data frames, then control
             # frames), timed together after the plan
@@ -863,8 +881,12 @@ def main():
             if ev: ev[3].record()
         else:
             if ev: cfws.time_next_pass(ev[2], ev[3])
-            if dst_off is not None:
+            if dst_off is not None and info_t is not None:
+                cfws.deserialize_scatter_info(wire, wire_total, index, dst_off, back, slot, info_t)
+            elif dst_off is not None:
                 cfws.deserialize_scatter(wire, wire_total, index, dst_off, back, slot, desc_de, status)
+            elif slot and info_t is not None:
+                cfws.deserialize_slots_info(wire, wire_total, index, back, slot, info_t, tot_de)
             elif slot:
                 cfws.deserialize_slots(wire, wire_total, index, back, slot, desc_de, status, tot_de)
             else:
@@ -886,6 +908,13 @@ def main():
     elapsed = shard.max_over_ranks(local, dev)
 
     # correctness of what was timed: unmask(mask(P)) == P, every frame COMPLETE
+    if info_t is not None:
+        # the compact entries: payload_size, fin 1, opcode BINARY, status COMPLETE
+        exp = fs | 1 << 32 | cfws.OPCODE_BINARY << 40
+        ok_info = bool((info_t.view(torch.int64).view(-1) == exp).all().item())
+        status.fill_(0 if ok_info else 1)
+        if perm is None:
+            tot_de.fill_(arena_bytes)
     if perm is not None:
         # frame i's payload is slot perm[i]: gather the slots back into frame order
         got = back[:arena_bytes].view(F, slot)[perm]
@@ -931,13 +960,15 @@ def main():
     dom_name = "serialize_execute" if ser_ms >= de_ms else "deserialize_execute"
     dom_ms = max(ser_ms, de_ms)
     achieved = alg_bytes / (dom_ms * 1e-3) / 1e9
-    kernel_symbol = ("xform_kernel<0>" if dom_name == "serialize_execute"   # kModeSer
-                     else "deserialize_plan_single_kernel<true>" if fused_de  # fused plan + copy
+    kernel_symbol = (("serialize_uniform_kernel" if uniform else "xform_kernel<0>")
+                     if dom_name == "serialize_execute"
                      else "deserialize_slots_window_kernel" if 0 < slot <= 8160  # fixed slots
                      else "deserialize_slots_kernel" if slot
-                     else "xform_kernel<1>")                                 # kModeDeser
+                     else recv_kernel if not flags else "xform_kernel<1>")
     # the PMC summary a traffic figure may come from: the same workload only
-    traffic_key = (f"config2:{F}x{fs}" + (":scatter" if perm is not None else ":slots" if slot else "")
+    traffic_key = (f"config2:{F}x{fs}" + (":uniform" if uniform else "")
+                   + (":scatter" if perm is not None else ":slots" if slot else "")
+                   + (":info" if info_t is not None else "")
                    if args.workload == "config2" else
                    "config3" if args.workload == "config3" else f"config4:{F}x{fs}")
     rows = shard.gather_floats([local, arena_bytes, ser_ms, de_ms, alg_bytes], dev)
@@ -958,9 +989,13 @@ def main():
         "config": {
             "workload": (f"config2: {F} binary frames x {size_label(fs)} per GPU, client-mask "
                          f"(serialize) then server-unmask (deserialize), device resident"
-                         + (f"; the receive to a shuffled order of {slot} B slots (cfws_deserialize_scatter)"
+                         + ("; the send through cfws_serialize_uniform (payload + one key per frame, "
+                            "no plan)" if uniform else "")
+                         + (f"; the receive to a shuffled order of {slot} B slots (cfws_deserialize_scatter"
+                            f"{'_info' if info_t is not None else ''})"
                             if perm is not None else
-                            f"; the receive into fixed {slot} B payload slots (cfws_deserialize_slots)"
+                            f"; the receive into fixed {slot} B payload slots (cfws_deserialize_slots"
+                            f"{'_info' if info_t is not None else ''})"
                             if slot else "")
                          if args.workload == "config2" else
                          f"config4: shard {rank} of 8 of the 8 M x 64 KiB batch ({F} frames, "

@@ -40,13 +40,18 @@ DESC_DTYPE = np.dtype([("payload_off", "<u8"), ("wire_off", "<u8"),
                        ("header_size", "u1")])
 assert DESC_DTYPE.itemsize == 32
 
+# cfws_frame_info_t, 8 bytes (the compact output of the slot / scatter receives).
+INFO_DTYPE = np.dtype([("payload_size", "<u4"), ("fin", "u1"), ("opcode", "u1"), ("status", "<i2")])
+assert INFO_DTYPE.itemsize == 8
+
 # Every function include/*.h declares (tests check the exports against the
 # headers themselves).
 BATCH_SYMBOLS = (
-    "cfws_init", "cfws_init_device", "cfws_device_copy", "cfws_time_next_pass", "cfws_bind_thread_device", "cfws_thread_device", "cfws_last_error", "cfws_version", "cfws_workspace_size",
-    "cfws_serialize_plan", "cfws_serialize_execute", "cfws_serialize_batch",
+    "cfws_init", "cfws_init_device", "cfws_device_copy", "cfws_time_next_pass", "cfws_deserialize_pass_kernel", "cfws_bind_thread_device", "cfws_thread_device", "cfws_last_error", "cfws_version", "cfws_workspace_size",
+    "cfws_serialize_plan", "cfws_serialize_execute", "cfws_serialize_batch", "cfws_serialize_uniform",
     "cfws_deserialize_plan", "cfws_deserialize_execute", "cfws_deserialize_batch",
-    "cfws_deserialize_slots", "cfws_deserialize_scatter", "cfws_xor_mask", "cfws_draw_mask_keys", "cfws_draw_mask_keys_seeded",
+    "cfws_deserialize_slots", "cfws_deserialize_scatter", "cfws_deserialize_slots_info",
+    "cfws_deserialize_scatter_info", "cfws_xor_mask", "cfws_draw_mask_keys", "cfws_draw_mask_keys_seeded",
     "cfws_release_thread_resources", "cfws_set_dropin_gpu_min", "cfws_dropin_gpu_min",
     "cfws_fill_splitmix", "cfws_pipeline_create", "cfws_pipeline_destroy",
     "cfws_pipeline_serialize", "cfws_pipeline_deserialize", "cfws_pipeline_receive",
@@ -108,6 +113,8 @@ def lib(path: str = LIB_PATH) -> C.CDLL:
         "cfws_serialize_plan": ([_vp, _sz, _u64, _vp, _vp, _sz, _vp], C.c_int),
         "cfws_serialize_execute": ([_vp, _vp, _sz, _vp, _u64, _vp, _vp], C.c_int),
         "cfws_serialize_batch": ([_vp, _vp, _sz, _vp, _u64, _vp, _vp, _sz, _vp], C.c_int),
+        "cfws_serialize_uniform": ([_vp, _vp, _sz, _u64, C.c_uint8, C.c_uint8, C.c_uint8, _vp, _u64, _vp,
+                                    _vp], C.c_int),
         "cfws_deserialize_plan": ([_vp, _u64, _vp, _sz, _u64, _u32, _u32, _vp, _vp, _u64, _vp,
                                    _vp, _sz, _vp], C.c_int),
         "cfws_deserialize_execute": ([_vp, _vp, _vp, _sz, _u32, _vp, _u64, _vp, _vp], C.c_int),
@@ -117,6 +124,9 @@ def lib(path: str = LIB_PATH) -> C.CDLL:
                                    C.c_int),
         "cfws_deserialize_scatter": ([_vp, _u64, _vp, _vp, _sz, _u64, _u64, _vp, _vp, _vp, _u64, _vp],
                                      C.c_int),
+        "cfws_deserialize_slots_info": ([_vp, _u64, _vp, _sz, _u64, _u64, _vp, _vp, _u64, _vp, _vp], C.c_int),
+        "cfws_deserialize_scatter_info": ([_vp, _u64, _vp, _vp, _sz, _u64, _u64, _vp, _vp, _u64, _vp],
+                                          C.c_int),
         "cfws_encode_headers": ([_vp, _sz, _vp, _u64, _vp], C.c_int),
         "cfws_parse_headers": ([_vp, _u64, _vp, _sz, _u64, _vp, _vp, _vp], C.c_int),
         "cfws_mask_batch": ([_vp, _vp, _sz, _u64, _vp, _u64, _vp], C.c_int),
@@ -140,6 +150,7 @@ def lib(path: str = LIB_PATH) -> C.CDLL:
         "cfws_init_device": ([C.c_int], C.c_int),
         "cfws_device_copy": ([_vp, _vp, _u64, _vp], C.c_int),
         "cfws_time_next_pass": ([_vp, _vp], C.c_int),
+        "cfws_deserialize_pass_kernel": ([_sz, _u64, _u32, _u32, _u64], C.c_char_p),
         "cfws_bind_thread_device": ([C.c_int], C.c_int),
         "cfws_thread_device": ([], C.c_int),
         "cfws_set_dropin_gpu_min": ([_sz], None),
@@ -278,6 +289,24 @@ def serialize(payload_t, desc_t, wire_t, ws_t=None, total_t=None, stream=None):
     return total_t
 
 
+def uniform_frame_bytes(payload_size: int, mask: bool) -> int:
+    """W: wire bytes of one frame of a uniform batch (header + payload)."""
+    return int(header_sizes(np.array([payload_size]), np.array([mask]))[0]) + payload_size
+
+
+def serialize_uniform(payload_t, keys_t, n: int, payload_size: int, wire_t, fin: bool = True,
+                      opcode: int = OPCODE_BINARY, mask: bool = True, total_t=None,
+                      wire_capacity: int | None = None, stream=None):
+    """cfws_serialize_uniform: n frames of payload_size bytes each, frame i's
+    payload at payload_t[i * payload_size:], its key keys_t[i] (uint32 /
+    int32 tensor; None when unmasked). Returns total_t (n * W) or None."""
+    cap = wire_t.numel() if wire_capacity is None else wire_capacity
+    _check(lib().cfws_serialize_uniform(_p(payload_t), _p(keys_t), n, payload_size, int(bool(fin)), opcode,
+                                        int(bool(mask)), _p(wire_t), cap, _p(total_t), _stream(stream)),
+           "cfws_serialize_uniform")
+    return total_t
+
+
 def deserialize_plan(wire_t, wire_size: int, index_t, desc_t, status_t, payload_capacity: int,
                      total_t, ws_t, max_payload: int = DEFAULT_MAX_PAYLOAD, align: int = 16,
                      flags: int = 0, stream=None) -> None:
@@ -361,6 +390,45 @@ def deserialize_scatter(wire_t, wire_size: int, index_t, payload_off_t, payload_
                                           _stream(stream)),
            "cfws_deserialize_scatter")
     return desc_t, status_t
+
+
+def deserialize_slots_info(wire_t, wire_size: int, index_t, payload_t, slot_bytes: int, info_t=None,
+                           total_t=None, max_payload: int = DEFAULT_MAX_PAYLOAD,
+                           payload_capacity: int | None = None, stream=None):
+    """cfws_deserialize_slots_info: the slot receive writing one 8-byte
+    cfws_frame_info_t per frame (info_t: (n, 8) uint8). Returns (info_t, total_t)."""
+    import torch
+    n = index_t.numel()
+    dev = wire_t.device
+    if info_t is None:
+        info_t = torch.empty((n, 8), dtype=torch.uint8, device=dev)
+    if total_t is None:
+        total_t = torch.zeros(1, dtype=torch.int64, device=dev)
+    cap = payload_t.numel() if payload_capacity is None else payload_capacity
+    _check(lib().cfws_deserialize_slots_info(_p(wire_t), wire_size, _p(index_t), n, max_payload, slot_bytes,
+                                             _p(info_t), _p(payload_t), cap, _p(total_t), _stream(stream)),
+           "cfws_deserialize_slots_info")
+    return info_t, total_t
+
+
+def deserialize_scatter_info(wire_t, wire_size: int, index_t, payload_off_t, payload_t, max_slot: int,
+                             info_t=None, max_payload: int = DEFAULT_MAX_PAYLOAD,
+                             payload_capacity: int | None = None, stream=None):
+    """cfws_deserialize_scatter_info. Returns info_t ((n, 8) uint8)."""
+    import torch
+    n = index_t.numel()
+    if info_t is None:
+        info_t = torch.empty((n, 8), dtype=torch.uint8, device=wire_t.device)
+    cap = payload_t.numel() if payload_capacity is None else payload_capacity
+    _check(lib().cfws_deserialize_scatter_info(_p(wire_t), wire_size, _p(index_t), _p(payload_off_t), n,
+                                               max_payload, max_slot, _p(info_t), _p(payload_t), cap,
+                                               _stream(stream)),
+           "cfws_deserialize_scatter_info")
+    return info_t
+
+
+def info_from_device(t) -> np.ndarray:
+    return t.cpu().numpy().reshape(-1).view(INFO_DTYPE).copy()
 
 
 # ---- HIP graphs of a batch (cfws_graph_*) -----------------------------------

@@ -895,13 +895,26 @@ __device__ __forceinline__ void slot_desc(cfws_frame_desc_t* desc, int32_t* stat
     status[f] = st;
 }
 
-template <int kSlotRounds, int kSub, bool kScatter>
+// The compact per-frame output (cfws_deserialize_slots_info /
+// _scatter_info): the reference frame's header fields and the status in 8
+// bytes, one u64 store per frame (consecutive lanes, consecutive entries).
+__device__ __forceinline__ void slot_info(cfws_frame_info_t* info, uint64_t f, const cfws_frame_desc_t& d, int32_t st)
+{
+    const uint32_t ps = d.payload_size > 0xffffffffull ? 0xffffffffu : (uint32_t)d.payload_size;
+    const uint32_t w1 = (uint32_t)d.fin | (uint32_t)d.opcode << 8 | ((uint32_t)st & 0xffffu) << 16;
+    reinterpret_cast<uint2*>(info)[f] = make_uint2(ps, w1);
+}
+
+// kInfo: write cfws_frame_info_t entries to `info` instead of descriptors
+// and statuses
+template <int kSlotRounds, int kSub, bool kScatter, bool kInfo>
 __global__ void __launch_bounds__(kThreads)
 deserialize_slots_window_kernel(const uint8_t* __restrict__ wire, uint64_t wire_size,
                                 const uint64_t* __restrict__ index, uint64_t n, uint64_t max_payload,
                                 uint64_t slot, uint32_t G, cfws_frame_desc_t* __restrict__ desc,
                                 int32_t* __restrict__ status, uint8_t* __restrict__ out, uint64_t capacity,
-                                uint64_t* __restrict__ user_total, const uint64_t* __restrict__ dst)
+                                uint64_t* __restrict__ user_total, const uint64_t* __restrict__ dst,
+                                cfws_frame_info_t* __restrict__ infos)
 {
     const uint32_t lane = threadIdx.x & 63u;
     // kSub sub-windows of 64 lanes make 64 kSub virtual lanes, v = 64 sw +
@@ -957,7 +970,10 @@ deserialize_slots_window_kernel(const uint8_t* __restrict__ wire, uint64_t wire_
             const uint64_t run = runl;
             st = kScatter ? scatter_rule(st, run, d.payload_size, slot, capacity)
                           : slot_rule(st, run, d.payload_size, slot, capacity);
-            slot_desc(desc, status, fl, run, d, st);
+            if constexpr (kInfo)
+                slot_info(infos, fl, d, st);
+            else
+                slot_desc(desc, status, fl, run, d, st);
             if (fl == n - 1 && user_total) {
                 const uint64_t t = n * slot;
                 *user_total = t < capacity ? t : capacity;
@@ -1007,12 +1023,13 @@ constexpr int kSlotUnroll = CFWS_SLOT_UNROLL;   // deserialize_slots_kernel: rou
 // Slots over kSlotWindow8Max: one frame per thread parsed (its header line
 // fetched twice, a small share of a frame this long), the payloads copied
 // by fused_item.
-template <bool kScatter>
+template <bool kScatter, bool kInfo>
 __global__ void __launch_bounds__(kThreads)
 deserialize_slots_kernel(const uint8_t* __restrict__ wire, uint64_t wire_size, const uint64_t* __restrict__ index,
                          uint64_t n, uint64_t max_payload, uint64_t slot, cfws_frame_desc_t* __restrict__ desc,
                          int32_t* __restrict__ status, uint8_t* __restrict__ out, uint64_t capacity,
-                         uint64_t* __restrict__ user_total, const uint64_t* __restrict__ dst)
+                         uint64_t* __restrict__ user_total, const uint64_t* __restrict__ dst,
+                         cfws_frame_info_t* __restrict__ info)
 {
     const uint64_t f = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
     uint64_t run = 0, src = 0;
@@ -1024,7 +1041,10 @@ deserialize_slots_kernel(const uint8_t* __restrict__ wire, uint64_t wire_size, c
         const int32_t p = parse_ws_header(wire, wire_size, s0, max_payload, d);
         const int32_t st = kScatter ? scatter_rule(p, run, d.payload_size, slot, capacity)
                                     : slot_rule(p, run, d.payload_size, slot, capacity);
-        slot_desc(desc, status, f, run, d, st);
+        if constexpr (kInfo)
+            slot_info(info, f, d, st);
+        else
+            slot_desc(desc, status, f, run, d, st);
         if (st == CFWS_PARSE_COMPLETE) {
             len = (uint32_t)d.payload_size;   // <= slot < 2^31
             nb = (len + 15u) & ~15u;
@@ -1552,6 +1572,41 @@ int cfws_deserialize_execute(const void* d_wire, const cfws_frame_desc_t* d_desc
     return launch_check("deserialize_execute");
 }
 
+}  // extern "C"
+
+namespace {
+
+// Which form of cfws_deserialize_batch a call with these sizes takes, its
+// other arguments valid (cfws_deserialize_pass_kernel reports the same
+// choice): the one-launch small batch, the fused plan + copy of batches of
+// small frames, or plan + execute.
+enum DeserRoute { kDeserSmall, kDeserFused, kDeserPlanExecute };
+
+DeserRoute deser_route(size_t n, uint64_t wire_size, uint32_t align, uint32_t flags, uint64_t cap)
+{
+    const bool align_ok = align != 0 && (align & (align - 1)) == 0 && align <= 4096;
+    if (small_path() && n > 0 && n <= kSmallFrames && cap <= kSmallBytes && flags == 0 && align_ok)
+        return kDeserSmall;
+    if (fused_deser() && flags == 0 && align >= 16 && align_ok && n > kSmallFrames && n <= 0xffffffffull &&
+        wire_size / n <= fused_avg_max())
+        return kDeserFused;
+    return kDeserPlanExecute;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* cfws_deserialize_pass_kernel(size_t n, uint64_t wire_size, uint32_t align, uint32_t flags,
+                                         uint64_t payload_capacity)
+{
+    switch (deser_route(n, wire_size, align, flags, payload_capacity)) {
+    case kDeserSmall: return "deserialize_small_kernel";
+    case kDeserFused: return "deserialize_plan_single_kernel<true>";
+    default: return "xform_kernel<1>";
+    }
+}
+
 int cfws_deserialize_batch(const void* d_wire, uint64_t wire_size, const uint64_t* d_index,
                            size_t n, uint64_t max_payload, uint32_t align, uint32_t flags,
                            cfws_frame_desc_t* d_desc, int32_t* d_status, void* d_payload,
@@ -1559,9 +1614,9 @@ int cfws_deserialize_batch(const void* d_wire, uint64_t wire_size, const uint64_
                            void* stream)
 {
     const CfwsPassScope pass_scope;
+    const DeserRoute route = deser_route(n, wire_size, align, flags, cap);
     // small batch without reassembly, every argument valid: one launch
-    if (small_path() && n > 0 && n <= kSmallFrames && cap <= kSmallBytes && flags == 0 && align != 0 &&
-        (align & (align - 1)) == 0 && align <= 4096 && check_init() == CFWS_OK && d_wire && d_index &&
+    if (route == kDeserSmall && check_init() == CFWS_OK && d_wire && d_index &&
         d_desc && d_status && ws && ws_size >= ws_layout(n, cap).bytes &&
         (cap == 0 || (d_payload && !misaligned(d_payload, d_wire)))) {
         const CfwsPassTimer timer(stream);
@@ -1572,8 +1627,7 @@ int cfws_deserialize_batch(const void* d_wire, uint64_t wire_size, const uint64_
         return launch_check("deserialize_batch(small)");
     }
     // small frames at 16-byte (or wider) slots: the fused plan + copy
-    if (fused_deser() && flags == 0 && align >= 16 && align <= 4096 && (align & (align - 1)) == 0 &&
-        n > kSmallFrames && n <= 0xffffffffull && wire_size / n <= fused_avg_max() && check_init() == CFWS_OK &&
+    if (route == kDeserFused && check_init() == CFWS_OK &&
         d_wire && d_index && d_desc && d_status && ws && ws_size >= ws_layout(n, cap).bytes &&
         (cap == 0 || (d_payload && !misaligned(d_payload, d_wire)))) {
         const WsLayout L = ws_layout(n, cap);
@@ -1604,7 +1658,8 @@ namespace {
 // a frame may have)
 int slots_impl(const void* d_wire, uint64_t wire_size, const uint64_t* d_index, const uint64_t* dst, size_t n,
                uint64_t max_payload, uint64_t slot, cfws_frame_desc_t* d_desc, int32_t* d_status,
-               void* d_payload, uint64_t cap, uint64_t* d_total, void* stream, bool scatter, const char* what)
+               void* d_payload, uint64_t cap, uint64_t* d_total, void* stream, bool scatter, const char* what,
+               cfws_frame_info_t* d_info = nullptr)
 {
     if (int rc = check_init()) return rc;
     if (slot < 16 || (slot & 15) || slot > (1ull << 31))
@@ -1617,7 +1672,8 @@ int slots_impl(const void* d_wire, uint64_t wire_size, const uint64_t* d_index, 
             return launch_check(what);
         return CFWS_OK;
     }
-    if (!d_wire || !d_index || !d_desc || !d_status || (cap && !d_payload) || (scatter && !dst))
+    const bool info = d_info != nullptr;
+    if (!d_wire || !d_index || (!info && (!d_desc || !d_status)) || (cap && !d_payload) || (scatter && !dst))
         return set_err(CFWS_ERROR_INVALID_ARGUMENT, "null pointer", hipSuccess);
     if (misaligned(d_payload, d_wire))
         return set_err(CFWS_ERROR_INVALID_ARGUMENT, "arenas must be 16-byte aligned", hipSuccess);
@@ -1642,37 +1698,50 @@ int slots_impl(const void* d_wire, uint64_t wire_size, const uint64_t* d_index, 
         }();
         const uint64_t want = (n + per_block - 1) / per_block;
         const uint32_t grid = (uint32_t)(want < cap_blocks ? want : cap_blocks);
-        auto window = [&](auto scatter) {
+        auto window = [&](auto scatter, auto compact) {
             constexpr bool kSc = decltype(scatter)::value;
+            constexpr bool kIn = decltype(compact)::value;
             if (S == 8)
-                deserialize_slots_window_kernel<CFWS_SLOT_ROUNDS8, 8, kSc><<<grid, kThreads, 0, st>>>(
-                    w, wire_size, d_index, n, max_payload, slot, G, d_desc, d_status, out, cap, d_total, dst);
+                deserialize_slots_window_kernel<CFWS_SLOT_ROUNDS8, 8, kSc, kIn><<<grid, kThreads, 0, st>>>(
+                    w, wire_size, d_index, n, max_payload, slot, G, d_desc, d_status, out, cap, d_total, dst, d_info);
             else if (S == 4)
-                deserialize_slots_window_kernel<CFWS_SLOT_ROUNDS4, 4, kSc><<<grid, kThreads, 0, st>>>(
-                    w, wire_size, d_index, n, max_payload, slot, G, d_desc, d_status, out, cap, d_total, dst);
+                deserialize_slots_window_kernel<CFWS_SLOT_ROUNDS4, 4, kSc, kIn><<<grid, kThreads, 0, st>>>(
+                    w, wire_size, d_index, n, max_payload, slot, G, d_desc, d_status, out, cap, d_total, dst, d_info);
             else if (S == 2)
-                deserialize_slots_window_kernel<CFWS_SLOT_ROUNDS2, 2, kSc><<<grid, kThreads, 0, st>>>(
-                    w, wire_size, d_index, n, max_payload, slot, G, d_desc, d_status, out, cap, d_total, dst);
+                deserialize_slots_window_kernel<CFWS_SLOT_ROUNDS2, 2, kSc, kIn><<<grid, kThreads, 0, st>>>(
+                    w, wire_size, d_index, n, max_payload, slot, G, d_desc, d_status, out, cap, d_total, dst, d_info);
             else if (P > 1)
-                deserialize_slots_window_kernel<CFWS_SLOT_ROUNDS_MULTI, 1, kSc><<<grid, kThreads, 0, st>>>(
-                    w, wire_size, d_index, n, max_payload, slot, G, d_desc, d_status, out, cap, d_total, dst);
+                deserialize_slots_window_kernel<CFWS_SLOT_ROUNDS_MULTI, 1, kSc, kIn><<<grid, kThreads, 0, st>>>(
+                    w, wire_size, d_index, n, max_payload, slot, G, d_desc, d_status, out, cap, d_total, dst, d_info);
             else
-                deserialize_slots_window_kernel<CFWS_SLOT_ROUNDS, 1, kSc><<<grid, kThreads, 0, st>>>(
-                    w, wire_size, d_index, n, max_payload, slot, G, d_desc, d_status, out, cap, d_total, dst);
+                deserialize_slots_window_kernel<CFWS_SLOT_ROUNDS, 1, kSc, kIn><<<grid, kThreads, 0, st>>>(
+                    w, wire_size, d_index, n, max_payload, slot, G, d_desc, d_status, out, cap, d_total, dst, d_info);
         };
         // the scatter form as its own instantiation: its per-round offset
         // shuffle, as a run-time branch in one kernel, cost the 1 KiB slot
         // receive 11 % (1.525 -> 1.70 ms)
-        if (scatter)
-            window(std::true_type{});
+        if (scatter && info)
+            window(std::true_type{}, std::true_type{});
+        else if (scatter)
+            window(std::true_type{}, std::false_type{});
+        else if (info)
+            window(std::false_type{}, std::true_type{});
         else
-            window(std::false_type{});
-    } else if (scatter) {
-        deserialize_slots_kernel<true><<<grid_for(n, kThreads), kThreads, 0, st>>>(
-            w, wire_size, d_index, n, max_payload, slot, d_desc, d_status, out, cap, d_total, dst);
+            window(std::false_type{}, std::false_type{});
     } else {
-        deserialize_slots_kernel<false><<<grid_for(n, kThreads), kThreads, 0, st>>>(
-            w, wire_size, d_index, n, max_payload, slot, d_desc, d_status, out, cap, d_total, dst);
+        auto one = [&](auto scatter, auto compact) {
+            deserialize_slots_kernel<decltype(scatter)::value, decltype(compact)::value>
+                <<<grid_for(n, kThreads), kThreads, 0, st>>>(w, wire_size, d_index, n, max_payload, slot, d_desc,
+                                                             d_status, out, cap, d_total, dst, d_info);
+        };
+        if (scatter && info)
+            one(std::true_type{}, std::true_type{});
+        else if (scatter)
+            one(std::true_type{}, std::false_type{});
+        else if (info)
+            one(std::false_type{}, std::true_type{});
+        else
+            one(std::false_type{}, std::false_type{});
     }
     return launch_check(what);
 }
@@ -1698,6 +1767,26 @@ int cfws_deserialize_scatter(const void* d_wire, uint64_t wire_size, const uint6
     const CfwsPassScope pass_scope;
     return slots_impl(d_wire, wire_size, d_index, d_payload_off, n, max_payload, max_slot, d_desc, d_status,
                       d_payload, cap, nullptr, stream, true, "deserialize_scatter");
+}
+
+int cfws_deserialize_slots_info(const void* d_wire, uint64_t wire_size, const uint64_t* d_index, size_t n,
+                                uint64_t max_payload, uint64_t slot, cfws_frame_info_t* d_info, void* d_payload,
+                                uint64_t cap, uint64_t* d_total, void* stream)
+{
+    const CfwsPassScope pass_scope;
+    if (!d_info && n) return set_err(CFWS_ERROR_INVALID_ARGUMENT, "null pointer", hipSuccess);
+    return slots_impl(d_wire, wire_size, d_index, nullptr, n, max_payload, slot, nullptr, nullptr, d_payload, cap,
+                      d_total, stream, false, "deserialize_slots_info", d_info);
+}
+
+int cfws_deserialize_scatter_info(const void* d_wire, uint64_t wire_size, const uint64_t* d_index,
+                                  const uint64_t* d_payload_off, size_t n, uint64_t max_payload, uint64_t max_slot,
+                                  cfws_frame_info_t* d_info, void* d_payload, uint64_t cap, void* stream)
+{
+    const CfwsPassScope pass_scope;
+    if (!d_info && n) return set_err(CFWS_ERROR_INVALID_ARGUMENT, "null pointer", hipSuccess);
+    return slots_impl(d_wire, wire_size, d_index, d_payload_off, n, max_payload, max_slot, nullptr, nullptr,
+                      d_payload, cap, nullptr, stream, true, "deserialize_scatter_info", d_info);
 }
 
 #if CFWS_PLAN_TRACE

@@ -1,0 +1,474 @@
+// cfws_uniform.hip -- the compact send of a uniform batch
+// (cfws_serialize_uniform, include/cfws.h).
+//
+// Every frame of the batch has the same payload size, fin, opcode and mask:
+// n sequential co_ws_frame_serialize calls (src/ws/co_ws_frame.c:21-119)
+// appending fixed-size messages to one co_byte_array. Frame i's wire bytes
+// are then [i W, (i + 1) W), W = header size + payload size, its payload
+// source [i fs, (i + 1) fs): no layout depends on another frame, so there is
+// no plan and no descriptor table. Per frame the pass reads the payload and a
+// 4-byte key and writes the frame -- the descriptor form reads a 32-byte
+// descriptor per frame in its plan and again in its execute (14 % more read
+// traffic at 256 B) and writes wire_off back into it.
+//
+// Each wave owns kUniformSpan bytes of wire (aligned 16-byte chunks, every
+// wire byte written once) in two phases:
+//  * body: lane l takes chunks l, l + 64, ... of the span; a chunk inside
+//    one payload is one or two aligned source loads, a funnel shift and the
+//    key XOR. Its frame comes from a multiply by a 32-bit reciprocal of W
+//    (host-computed) and one correction, relative to the wave's first frame.
+//  * headers: the chunks the body phase skipped are exactly the chunks that
+//    hold header bytes (frames of W >= 32 bytes: a chunk meets at most one
+//    header), one or two per frame; they are handed out one per lane --
+//    frame fr of the span to lanes 2 fr and 2 fr + 1 -- so a span of 16
+//    frames assembles its ~31 header chunks in one pass of that code rather
+//    than in every round of the body phase. Each holds the end of one
+//    payload, a header, and the start of the next payload: one source
+//    window (the two payload pieces are contiguous in the source), two keys.
+// All loads of both phases are issued before either computes.
+// Frames of W < 32 bytes (payloads up to 17-29 bytes) take a byte-wise
+// kernel.
+#include "cfws_kernels.h"
+
+namespace {
+
+#ifndef CFWS_UNIFORM_UNROLL
+#define CFWS_UNIFORM_UNROLL 4
+#endif
+constexpr int kUniformUnroll = CFWS_UNIFORM_UNROLL;               // body chunks per lane
+constexpr uint32_t kUniformSpan = 64u * 16u * kUniformUnroll;    // wire bytes per wave
+#ifndef CFWS_UNIFORM_STORE_AUX
+#define CFWS_UNIFORM_STORE_AUX 19                                 // write-through, as the WS send (st16_region)
+#endif
+
+// Uniform frame parameters (all wave-uniform).
+struct UniformFrames {
+    const uint8_t* src;
+    const uint32_t* keys;      // null: unmasked
+    uint64_t n;                // frames
+    uint64_t fs;               // payload bytes per frame (< 2^30)
+    uint32_t hs;               // header bytes (2..14)
+    uint32_t W;                // wire bytes per frame: hs + fs
+    uint32_t M;                // ceil(2^32 / W): r / W = mulhi(r, M) or one less, r < 2^31
+    uint32_t hb;               // header byte 0 | mask << 8 (ws_header_words)
+    uint64_t total;            // n W
+    double invW;               // 1 / W, for the wave's first frame
+};
+
+__device__ __forceinline__ uint32_t div_w(const UniformFrames& U, uint32_t r)
+{
+    uint32_t q = __umulhi(r, U.M);
+    if (q * U.W > r) --q;
+    return q;
+}
+
+// A chunk of the wave's span: D0 the span's start (wave-uniform, the base of
+// the buffer resource `rs`), D the chunk's. Past the capacity byte by byte.
+template <typename Rsrc>
+__device__ __forceinline__ void uniform_store(uint8_t* __restrict__ out, Rsrc rs, uint64_t D0, uint64_t D,
+                                              uint64_t cap, uint4 o)
+{
+    if (D + 16 <= cap) {
+        if (CFWS_UNIFORM_STORE_AUX == 0) {
+            st16(out + D, o);
+        } else {
+            const u32x4 v = {o.x, o.y, o.z, o.w};
+            __builtin_amdgcn_raw_buffer_store_b128(v, rs, (int)(D - D0), 0, CFWS_UNIFORM_STORE_AUX);
+        }
+    } else {
+        for (uint32_t j = 0; D + j < cap; ++j) out[D + j] = (uint8_t)(u4_byte(o, (int)j));
+    }
+}
+
+// A header chunk: chunk byte 0 is byte `off` of frame f (f + 1 may start in
+// the chunk at byte t = W - off). Loads issued by header_prep, bytes by
+// header_finish.
+struct HeaderChunk {
+    uint4 A, B;
+    uint32_t k0, k1;
+    uint32_t ph, j_lo;
+};
+
+__device__ __forceinline__ void header_prep(const UniformFrames& U, uint64_t f, uint32_t off, HeaderChunk& h)
+{
+    const uint32_t t = U.W - off;
+    const uint32_t a = off < U.hs ? U.hs - off : 0u, b = t < 16u ? t : 16u;
+    const bool hasF = b > a;
+    const bool next = t < 16u && f + 1 < U.n;
+    const bool hasN = next && t + U.hs < 16u;
+    uint64_t s_lo = 0;
+    uint32_t npay = 0;
+    h.j_lo = 0;
+    if (hasF) {
+        s_lo = f * U.fs + (off + a - U.hs);
+        h.j_lo = a;
+        npay = (b - a) + (hasN ? 16u - (t + U.hs) : 0u);
+    } else if (hasN) {
+        s_lo = (f + 1) * U.fs;
+        h.j_lo = t + U.hs;
+        npay = 16u - h.j_lo;
+    }
+    const uint4 z = make_uint4(0, 0, 0, 0);
+    h.A = h.B = z;
+    h.ph = (uint32_t)(s_lo & 15u);
+    if (npay) {
+        const uint8_t* sp = U.src + (s_lo & ~uint64_t(15));
+        h.A = ld16(sp);
+        if (h.ph + npay > 16u) h.B = ld16(sp + 16);       // the block holds payload bytes of the chunk
+    }
+    h.k0 = U.keys ? U.keys[f] : 0u;
+    h.k1 = U.keys && next ? U.keys[f + 1] : 0u;
+}
+
+__device__ __forceinline__ uint4 header_finish(const UniformFrames& U, uint64_t f, uint32_t off, const HeaderChunk& h)
+{
+    const uint4 z = make_uint4(0, 0, 0, 0);
+    const uint32_t t = U.W - off;
+    const uint32_t a = off < U.hs ? U.hs - off : 0u, b = t < 16u ? t : 16u;
+    const bool hasF = b > a;
+    const bool next = t < 16u && f + 1 < U.n;
+    const uint32_t he = t + U.hs < 16u ? t + U.hs : 16u;
+    const bool hasN = next && he < 16u;
+    // Y[k] = source byte s_lo + (k - j_lo)
+    const uint4 Y = h.ph >= h.j_lo ? funnel16(h.A, h.B, h.ph - h.j_lo) : funnel16(z, h.A, 16u - (h.j_lo - h.ph));
+    uint4 o = z;
+    if (off < U.hs)                                           // f's header from its byte off
+        o = and4(funnel16(ws_header_words(U.fs, U.hb, h.k0), z, off), byte_range(0, U.hs - off));
+    if (hasF) {                                               // the end of f's payload
+        uint4 X = Y;
+        xor4(X, rotr8(h.k0, off + 16u - U.hs));
+        o = or4(o, and4(X, byte_range(a, b)));
+    }
+    if (next)                                                 // f + 1's header from chunk byte t
+        o = or4(o, and4(funnel16(z, ws_header_words(U.fs, U.hb, h.k1), 16u - t), byte_range(t, he)));
+    if (hasN) {                                               // the start of f + 1's payload
+        uint4 X = hasF ? funnel16(z, Y, 16u - U.hs) : Y;      // contiguous after f's: hs bytes on
+        xor4(X, rotr8(h.k1, 16u - (he & 3u)));
+        o = or4(o, and4(X, byte_range(he, 16u)));
+    }
+    return o;
+}
+
+__global__ void __launch_bounds__(kThreads)
+serialize_uniform_kernel(UniformFrames U, uint8_t* __restrict__ out, uint64_t cap, uint64_t* __restrict__ user_total)
+{
+    const uint32_t lane = threadIdx.x & 63u;
+    // wave-uniform values in scalar registers
+    const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const uint64_t wave = uint64_t(blockIdx.x) * kWaves + wv;
+    const uint64_t D0 = wave * kUniformSpan;
+    const uint64_t lim = U.total < cap ? U.total : cap;
+    if (wave == 0 && lane == 0 && user_total) *user_total = U.total;
+    if (D0 >= lim) return;
+    // the wave's first frame: D0 / W in double (D0 < 2^40), corrected
+    uint64_t F0 = (uint64_t)((double)D0 * U.invW);
+    if (F0 * U.W > D0) --F0;
+    else if ((F0 + 1) * U.W <= D0) ++F0;
+    F0 = (uint64_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)F0) |
+         (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(F0 >> 32)) << 32;
+    const uint64_t base = F0 * U.W;                           // <= D0
+    const uint32_t rel0 = (uint32_t)(D0 - base);              // < W
+    const uint64_t src0 = F0 * U.fs;
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc(out + D0, 0, (int)kUniformSpan, 0x00020000);
+
+    // frames whose header meets the span: fa .. fb (fb may be n: the chunk
+    // holding the batch's end past the last payload is handled as frame n's)
+    const uint64_t fa = (base + U.hs > D0) ? F0 : F0 + 1;
+    uint64_t fb = F0 + div_w(U, rel0 + kUniformSpan - 1);
+    if (fb > U.n) fb = U.n;
+    const uint32_t n_hdr = fa <= fb ? 2u * (uint32_t)(fb - fa + 1) : 0u;
+
+    // ---- issue every load: body chunks, then the first 64 header chunks
+    uint32_t q[kUniformUnroll], off[kUniformUnroll], key[kUniformUnroll];
+    bool body[kUniformUnroll];
+    uint4 A[kUniformUnroll], B[kUniformUnroll];
+#pragma unroll
+    for (int u = 0; u < kUniformUnroll; ++u) {
+        const uint32_t r = rel0 + 16u * (64u * u + lane);
+        q[u] = div_w(U, r);
+        off[u] = r - q[u] * U.W;
+        body[u] = D0 + 16ull * (64u * u + lane) < lim && off[u] >= U.hs && off[u] + 16u <= U.W;
+        A[u] = B[u] = make_uint4(0, 0, 0, 0);
+        key[u] = 0;
+        if (body[u]) {
+            const uint64_t s = src0 + uint64_t(q[u]) * U.fs + (off[u] - U.hs);
+            const uint8_t* sp = U.src + (s & ~uint64_t(15));
+            A[u] = ld16(sp);
+            if (s & 15u) B[u] = ld16(sp + 16);
+            key[u] = U.keys ? U.keys[F0 + q[u]] : 0u;
+        }
+    }
+    HeaderChunk h;
+    uint64_t hD = 0, hf = 0;
+    uint32_t hoff = 0;
+    bool hown = false;
+    auto header_lane = [&](uint32_t idx) {
+        // lane idx of the header pass: frame fa + idx / 2, its first or second header chunk
+        hown = false;
+        if (idx >= n_hdr) return;
+        const uint64_t fr = fa + idx / 2;
+        const uint64_t hstart = fr * U.W;
+        const uint64_t c1 = hstart >> 4, c2 = (hstart + U.hs - 1) >> 4;
+        if ((idx & 1u) && c2 == c1) return;
+        hD = ((idx & 1u) ? c2 : c1) << 4;
+        if (hD < D0 || hD >= D0 + kUniformSpan || hD >= lim) return;
+        hf = hD >= hstart ? fr : fr - 1;
+        hoff = (uint32_t)(hD - hf * U.W);
+        hown = true;
+        header_prep(U, hf, hoff, h);
+    };
+    header_lane(lane);
+
+    // ---- body chunks
+#pragma unroll
+    for (int u = 0; u < kUniformUnroll; ++u) {
+        if (!body[u]) continue;
+        const uint32_t ph = (uint32_t)((src0 + uint64_t(q[u]) * U.fs + (off[u] - U.hs)) & 15u);
+        uint4 o = ph ? funnel16(A[u], B[u], ph) : A[u];
+        xor4(o, rotr8(key[u], off[u] - U.hs));
+        uniform_store(out, rs, D0, D0 + 16ull * (64u * u + lane), cap, o);
+    }
+    // ---- header chunks, 64 at a time
+    for (uint32_t g = 0; g < n_hdr; g += 64) {
+        if (g) header_lane(g + lane);
+        if (hown) uniform_store(out, rs, D0, hD, cap, header_finish(U, hf, hoff, h));
+    }
+}
+
+// The 128-bit value (lo, hi) shifted up by `sh` bytes (0 <= sh < 16): byte j
+// moves to j + sh, zeros below.
+__device__ __forceinline__ uint4 shl16(uint4 v, uint32_t sh)
+{
+    const uint64_t lo = (uint64_t)v.x | (uint64_t)v.y << 32, hi = (uint64_t)v.z | (uint64_t)v.w << 32;
+    const uint32_t b = 8u * (sh & 7u);
+    const uint64_t l1 = b ? lo << b : lo;
+    const uint64_t h1 = b ? (hi << b) | (lo >> (64u - b)) : hi;
+    const uint64_t L = sh < 8 ? l1 : 0, H = sh < 8 ? h1 : l1;
+    return make_uint4((uint32_t)L, (uint32_t)(L >> 32), (uint32_t)H, (uint32_t)(H >> 32));
+}
+
+// Frames of 32 <= fs <= 65,535 payload bytes, fs a multiple of 16, masked or
+// not (headers of at most 8 bytes, payload starts 16-aligned in the source):
+// every chunk of the span, body or header, in one store round, so no 32-byte
+// sector of the wire is written in two parts. A header chunk is
+//   [f's body tail: bytes < q] [a header at q] [that frame's body head at q + hs]
+// (q = header start - chunk start, -7..15): the tail is the chunk's own
+// funnel of its source blocks (as a body chunk's), the header 8 bytes from
+// the frame's key, the head the NEXT chunk's first source block (that chunk
+// lies in the same body, whose source starts 16-aligned), taken over DPP --
+// the shape of general_region_ser_edges in cfws_kernels.h, with the frames
+// computed instead of read from a plan. The span's keys are read once (lane
+// j: frame F0 + j and F0 + 64 + j) and handed to chunks by ds_bpermute.
+#ifndef CFWS_UNIFORM_OCC
+#define CFWS_UNIFORM_OCC 1                 // __launch_bounds__ workgroups per CU (A/B knob)
+#endif
+#ifndef CFWS_UNIFORM_DPP_B
+#define CFWS_UNIFORM_DPP_B 1               // a body chunk's second block from the next lane: 256 B send 1.57 -> 1.53 ms (A/B knob)
+#endif
+__global__ void __launch_bounds__(kThreads, CFWS_UNIFORM_OCC)
+serialize_uniform_small_kernel(UniformFrames U, uint8_t* __restrict__ out, uint64_t cap,
+                               uint64_t* __restrict__ user_total)
+{
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const uint64_t wave = uint64_t(blockIdx.x) * kWaves + wv;
+    const uint64_t D0 = wave * kUniformSpan;
+    const uint64_t lim = U.total < cap ? U.total : cap;
+    if (wave == 0 && lane == 0 && user_total) *user_total = U.total;
+    if (D0 >= lim) return;
+    uint64_t F0 = (uint64_t)((double)D0 * U.invW);
+    if (F0 * U.W > D0) --F0;
+    else if ((F0 + 1) * U.W <= D0) ++F0;
+    F0 = (uint64_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)F0) |
+         (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(F0 >> 32)) << 32;
+    const uint32_t rel0 = (uint32_t)(D0 - F0 * U.W);
+    const uint64_t src0 = F0 * U.fs;
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc(out + D0, 0, (int)kUniformSpan, 0x00020000);
+    const uint32_t hs = U.hs, W = U.W;
+    // the span's keys: frames F0 .. F0 + 127 (W >= 38: at most 110 frames meet a 4 KiB span)
+    uint32_t kl0 = 0, kl1 = 0;
+    if (U.keys) {
+        if (F0 + lane < U.n) kl0 = U.keys[F0 + lane];
+        if (F0 + 64 + lane < U.n) kl1 = U.keys[F0 + 64 + lane];
+    }
+    auto key_of = [&](uint32_t j) {          // frame F0 + j's key, j < 128 (every lane active)
+        const uint32_t a = (uint32_t)__shfl((int)kl0, (int)(j & 63u), 64);
+        const uint32_t b = (uint32_t)__shfl((int)kl1, (int)(j & 63u), 64);
+        return j < 64 ? a : b;
+    };
+    uint32_t q[kUniformUnroll], off[kUniformUnroll], ph[kUniformUnroll];
+    bool fast[kUniformUnroll], tail[kUniformUnroll], live[kUniformUnroll];
+    uint4 A[kUniformUnroll], B[kUniformUnroll];
+    const uint4 z = make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int u = 0; u < kUniformUnroll; ++u) {
+        const uint32_t r = rel0 + 16u * (64u * u + lane);
+        q[u] = div_w(U, r);
+        off[u] = r - q[u] * W;
+        // chunks past the batch end are not written; their neighbours may need
+        // their block as a body head (a capacity cut inside the batch)
+        live[u] = D0 + 16ull * (64u * u + lane) < U.total;
+        fast[u] = off[u] >= hs && off[u] + 16u <= W;
+        tail[u] = !fast[u] && off[u] >= hs;                  // f's body, then f + 1's header
+        ph[u] = (off[u] - hs) & 15u;
+        A[u] = B[u] = z;
+        if (live[u] && (fast[u] || tail[u])) {
+            const uint8_t* sp = U.src + ((src0 + uint64_t(q[u]) * U.fs + (off[u] - hs)) & ~uint64_t(15));
+            A[u] = ld16(sp);
+            // the second block when the chunk's own bytes reach into it (with
+            // CFWS_UNIFORM_DPP_B, a body chunk followed by a chunk of the same
+            // body takes it from that chunk's lane instead)
+            const bool from_next = CFWS_UNIFORM_DPP_B && fast[u] && off[u] + 16u < W &&
+                                   !(lane == 63 && u == kUniformUnroll - 1);
+            if (ph[u] && !from_next && (fast[u] || ph[u] + (W - off[u]) > 16u)) B[u] = ld16(sp + 16);
+        }
+    }
+    // lane 63's last chunk takes a body head from the next span's first
+    // chunk: loaded here (the first block of that frame's payload)
+    uint4 hx = z;
+    {
+        constexpr int u = kUniformUnroll - 1;
+        const bool head = live[u] && !fast[u] && (off[u] < hs ? 16u > hs - off[u] : W - off[u] + hs < 16u) &&
+                          (off[u] < hs || F0 + q[u] + 1 < U.n);
+        if (lane == 63 && head) hx = ld16(U.src + (src0 + uint64_t(q[u] + (off[u] < hs ? 0u : 1u)) * U.fs));
+    }
+#pragma unroll
+    for (int u = 0; u < kUniformUnroll; ++u) {
+        const uint4 nextA = u + 1 < kUniformUnroll ? readlane4(A[u + 1 < kUniformUnroll ? u + 1 : u], 0) : hx;
+        const uint4 N = from_next_lane(A[u], nextA);        // every lane: DPP needs the full wave
+        const uint32_t kf = key_of(q[u]);
+        const uint32_t kn = key_of(q[u] + 1);
+        const uint64_t D = D0 + 16ull * (64u * u + lane);
+        if (D >= lim) continue;
+        const bool from_next = CFWS_UNIFORM_DPP_B && fast[u] && off[u] + 16u < W &&
+                               !(lane == 63 && u == kUniformUnroll - 1);
+        uint4 o = ph[u] ? funnel16(A[u], from_next ? N : B[u], ph[u]) : A[u];
+        xor4(o, rotr8(kf, off[u] - hs));
+        if (!fast[u]) {
+            // the header in the chunk: f's (the chunk starts inside it) or f + 1's
+            const bool own_hdr = off[u] < hs;
+            const bool has_hdr = own_hdr || F0 + q[u] + 1 < U.n;
+            const int qh = own_hdr ? -(int)off[u] : (int)(W - off[u]);          // -7 .. 15
+            const uint32_t kh = own_hdr ? kf : kn;
+            uint4 w = z;
+            if (!own_hdr) w = and4(o, byte_range(0, W - off[u]));              // f's body tail
+            if (has_hdr) {
+                const uint4 H = ws_header_words(U.fs, U.hb, kh);                   // hs <= 8 bytes
+                const uint64_t Hv = (uint64_t)H.x | (uint64_t)H.y << 32;
+                const uint4 Hs = qh >= 0 ? shl16(make_uint4(H.x, H.y, 0u, 0u), (uint32_t)qh)
+                                         : make_uint4((uint32_t)(Hv >> (8 * -qh)), (uint32_t)(Hv >> (8 * -qh) >> 32),
+                                                      0u, 0u);
+                w = or4(w, Hs);
+                const int sh = qh + (int)hs;                                       // its body head
+                if (sh < 16) {
+                    uint4 X = N;
+                    xor4(X, kh);
+                    w = or4(w, shl16(X, (uint32_t)sh));
+                }
+            }
+            o = w;
+        }
+        uniform_store(out, rs, D0, D, cap, o);
+    }
+}
+
+// W < 32: frames shorter than two chunks; every chunk byte by byte.
+__global__ void __launch_bounds__(kThreads)
+serialize_uniform_bytes_kernel(UniformFrames U, uint8_t* __restrict__ out, uint64_t cap,
+                               uint64_t* __restrict__ user_total)
+{
+    const uint64_t c = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
+    const uint64_t lim = U.total < cap ? U.total : cap;
+    if (c == 0 && user_total) *user_total = U.total;
+    const uint64_t D = c * 16;
+    if (D >= lim) return;
+    uint64_t f = D / U.W;
+    uint32_t off = (uint32_t)(D - f * U.W);
+    uint32_t w[4] = {0, 0, 0, 0};
+    uint32_t k = U.keys ? U.keys[f] : 0u;
+    uint4 H = ws_header_words(U.fs, U.hb, k);
+    for (int j = 0; j < 16; ++j) {
+        if (D + j >= U.total) break;
+        if (off == U.W) {
+            ++f;
+            off = 0;
+            k = U.keys ? U.keys[f] : 0u;
+            H = ws_header_words(U.fs, U.hb, k);
+        }
+        uint32_t b;
+        if (off < U.hs) {
+            b = u4_byte(H, (int)off);
+        } else {
+            const uint32_t p = off - U.hs;
+            b = (U.src[f * U.fs + p] ^ (k >> (8 * (p & 3u)))) & 0xffu;
+        }
+        w[j >> 2] |= b << (8 * (j & 3));
+        ++off;
+    }
+    const uint4 o = make_uint4(w[0], w[1], w[2], w[3]);
+    if (D + 16 <= cap)
+        st16(out + D, o);
+    else
+        for (uint32_t j = 0; D + j < cap; ++j) out[D + j] = (uint8_t)(u4_byte(o, (int)j));
+}
+
+}  // namespace
+
+extern "C" int cfws_serialize_uniform(const void* d_payload, const uint32_t* d_keys, size_t n, uint64_t fs,
+                                      uint8_t fin, uint8_t opcode, uint8_t mask, void* d_wire, uint64_t cap,
+                                      uint64_t* d_total, void* stream)
+{
+    const CfwsPassScope pass_scope;
+    if (int rc = check_init()) return rc;
+    if (fs > (1ull << 30)) return set_err(CFWS_ERROR_INVALID_ARGUMENT, "payload_size > 2^30", hipSuccess);
+    const uint32_t hs = 2u + (fs > 65535u ? 8u : (fs > 125u ? 2u : 0u)) + (mask ? 4u : 0u);
+    const uint64_t W = hs + fs;
+    if (n > (uint64_t(1) << 40) / W) return set_err(CFWS_ERROR_INVALID_ARGUMENT, "batch over 2^40 wire bytes",
+                                                    hipSuccess);
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    const uint64_t total = n * W;
+    if (n == 0 || cap == 0) {
+        if (d_total && hipMemcpyAsync(d_total, &total, 8, hipMemcpyHostToDevice, st) != hipSuccess)
+            return launch_check("serialize_uniform");
+        if (d_total && hipStreamSynchronize(st) != hipSuccess) return launch_check("serialize_uniform");
+        return CFWS_OK;
+    }
+    if (!d_wire || (fs && !d_payload) || (mask && !d_keys))
+        return set_err(CFWS_ERROR_INVALID_ARGUMENT, "null pointer", hipSuccess);
+    if (misaligned(fs ? d_payload : d_wire, d_wire))
+        return set_err(CFWS_ERROR_INVALID_ARGUMENT, "arenas must be 16-byte aligned", hipSuccess);
+    UniformFrames U;
+    U.src = static_cast<const uint8_t*>(d_payload);
+    U.keys = mask ? d_keys : nullptr;
+    U.n = n;
+    U.fs = fs;
+    U.hs = hs;
+    U.W = (uint32_t)W;
+    U.M = (uint32_t)(((uint64_t(1) << 32) + W - 1) / W);
+    U.hb = (uint32_t)(opcode | (fin ? 0x80u : 0u)) | (mask ? 0x100u : 0u);
+    U.total = total;
+    U.invW = 1.0 / (double)W;
+    const uint64_t lim = total < cap ? total : cap;
+    const CfwsPassTimer timer(st);
+    if (fs >= 32 && fs <= 65535 && fs % 16 == 0) {
+        const uint64_t waves = (lim + kUniformSpan - 1) / kUniformSpan;
+        const uint64_t blocks = (waves + kWaves - 1) / kWaves;
+        if (blocks > 0x7fffffffull) return set_err(CFWS_ERROR_INVALID_ARGUMENT, "batch too large", hipSuccess);
+        static const uint32_t lds = (uint32_t)env_knob("CFWS_UNIFORM_LDS", 0);   // residency cap (A/B knob)
+        serialize_uniform_small_kernel<<<(uint32_t)blocks, kThreads, lds, st>>>(U, static_cast<uint8_t*>(d_wire), cap,
+                                                                               d_total);
+    } else if (W >= 32) {
+        const uint64_t waves = (lim + kUniformSpan - 1) / kUniformSpan;
+        const uint64_t blocks = (waves + kWaves - 1) / kWaves;
+        if (blocks > 0x7fffffffull) return set_err(CFWS_ERROR_INVALID_ARGUMENT, "batch too large", hipSuccess);
+        // CFWS_UNIFORM_LDS: dynamic LDS per workgroup, a residency cap (A/B knob; 0 = none)
+        static const uint32_t lds = (uint32_t)env_knob("CFWS_UNIFORM_LDS", 0);
+        serialize_uniform_kernel<<<(uint32_t)blocks, kThreads, lds, st>>>(U, static_cast<uint8_t*>(d_wire), cap,
+                                                                        d_total);
+    } else {
+        const uint64_t chunks = (lim + 15) / 16;
+        serialize_uniform_bytes_kernel<<<grid_for(chunks, kThreads), kThreads, 0, st>>>(
+            U, static_cast<uint8_t*>(d_wire), cap, d_total);
+    }
+    return launch_check("serialize_uniform");
+}

@@ -101,6 +101,22 @@ int cfws_serialize_batch(const void* d_payload, cfws_frame_desc_t* d_desc,
                          uint64_t* d_wire_total, void* d_workspace,
                          size_t workspace_size, void* stream);
 
+/* ---- serialize a uniform batch (compact input) ----------------------------
+ * Every frame has the same payload_size, fin, opcode and mask: n sequential
+ * co_ws_frame_serialize calls (co_ws_frame.c:21-119) appending fixed-size
+ * messages to one co_byte_array, with no descriptor table and no plan.
+ * Frame i's payload is d_payload[i * payload_size, (i + 1) * payload_size)
+ * and its key d_keys[i] (wire order, as cfws_frame_desc_t.mask_key; NULL
+ * allowed when mask == 0); its frame is d_wire[i * W, (i + 1) * W), W =
+ * header size (2..14, co_ws_frame.c:34-91) + payload_size. One launch, no
+ * workspace; the bytes are those cfws_serialize_batch writes for the same
+ * frames. Wire bytes at or past wire_capacity are not written;
+ * *d_wire_total (may be NULL) = n * W. payload_size <= 2^31, n * W < 2^40. */
+int cfws_serialize_uniform(const void* d_payload, const uint32_t* d_keys, size_t n_frames,
+                           uint64_t payload_size, uint8_t fin, uint8_t opcode, uint8_t mask,
+                           void* d_wire, uint64_t wire_capacity, uint64_t* d_wire_total,
+                           void* stream);
+
 /* ---- deserialize (server unmask / client plain) --------------------------
  * plan:    parses the header at each d_frame_index[i] against wire_size,
  *          writes d_desc[i] and d_status[i] (reference codes) and lays the
@@ -159,6 +175,36 @@ int cfws_deserialize_slots(const void* d_wire, uint64_t wire_size,
                            cfws_frame_desc_t* d_desc, int32_t* d_status,
                            void* d_payload, uint64_t payload_capacity,
                            uint64_t* d_payload_total, void* stream);
+
+/* ---- compact per-frame output of the slot / scatter receives --------------
+ * What the reference's frame object carries (co_ws_frame_header_t:
+ * fin, opcode, payload_size, co_ws_frame.h:36-49) plus the status, in 8
+ * bytes instead of the 36 of a descriptor + status (the payload offset is
+ * the slot, or the caller's, and the key and header size are consumed by
+ * the unmask). payload_size is the parsed length, UINT32_MAX when it does
+ * not fit 32 bits (never for a COMPLETE frame: its payload fits its slot,
+ * <= 2^31); status is the int32 code cast to 16 bits (every code fits). */
+typedef struct cfws_frame_info {
+    uint32_t payload_size;
+    uint8_t  fin;
+    uint8_t  opcode;
+    int16_t  status;
+} cfws_frame_info_t;
+
+/* cfws_deserialize_slots / cfws_deserialize_scatter with d_info[i] (8-byte
+ * aligned) in place of d_desc[i] and d_status[i]: the same decisions, the
+ * same payload bytes; the fields equal the descriptor form's. */
+int cfws_deserialize_slots_info(const void* d_wire, uint64_t wire_size,
+                                const uint64_t* d_frame_index, size_t n_frames,
+                                uint64_t max_payload, uint64_t slot_bytes,
+                                cfws_frame_info_t* d_info, void* d_payload,
+                                uint64_t payload_capacity, uint64_t* d_payload_total,
+                                void* stream);
+int cfws_deserialize_scatter_info(const void* d_wire, uint64_t wire_size,
+                                  const uint64_t* d_frame_index, const uint64_t* d_payload_off,
+                                  size_t n_frames, uint64_t max_payload, uint64_t max_slot,
+                                  cfws_frame_info_t* d_info, void* d_payload,
+                                  uint64_t payload_capacity, void* stream);
 
 /* ---- deserialize, each payload to the caller's offset ---------------------
  * cfws_deserialize_slots with payload_off = d_payload_off[i] (the caller's
@@ -515,6 +561,15 @@ int cfws_device_copy(const void* d_src, void* d_dst, uint64_t n, void* stream);
  * a pending pair. Lets a caller time the one kernel of a multi-kernel call
  * that moves the bytes (bench.py's roofline figures). */
 int cfws_time_next_pass(void* start, void* stop);
+
+/* The kernel cfws_deserialize_batch's timed pass is for a call with these
+ * sizes (its pointers valid): "deserialize_small_kernel" (one launch for a
+ * small batch), "deserialize_plan_single_kernel<true>" (the fused plan +
+ * copy of batches of small frames) or "xform_kernel<1>" (the execute after
+ * the plan). The same rule the call applies, so a profile can name what it
+ * timed. A static string. */
+const char* cfws_deserialize_pass_kernel(size_t n_frames, uint64_t wire_size, uint32_t align,
+                                         uint32_t flags, uint64_t payload_capacity);
 
 /* ---- synthetic input (bench / tests) -------------------------------------
  * d_dst[i] = byte ((byte_base + i) % 8) of splitmix64 output number

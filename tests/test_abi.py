@@ -176,3 +176,17 @@ def test_link_level_dropin_fails_loudly_without_device():
     r = subprocess.run([exe, "77"], capture_output=True, text=True, timeout=60, env=env)
     assert r.returncode == 2
     assert "serialize failed size=65536 mask=1" in r.stdout
+
+
+def test_deserialize_pass_kernel_routes():
+    """cfws_deserialize_pass_kernel names the kernel cfws_deserialize_batch
+    times for a call of these sizes (host only: the same rule the call
+    applies, which bench.py reads instead of restating it)."""
+    from coldforce_amd import cfws
+    f = cfws.lib().cfws_deserialize_pass_kernel
+    assert f(1000, 1000 * 264, 16, 0, 1 << 20).decode() == "deserialize_small_kernel"
+    assert f(16 << 20, (16 << 20) * 264, 16, 0, 1 << 33).decode() == "deserialize_plan_single_kernel<true>"
+    assert f(16 << 20, (16 << 20) * 264, 1, 0, 1 << 33).decode() == "xform_kernel<1>"       # align < 16
+    assert f(65536, 65536 * 65550, 16, 0, 1 << 32).decode() == "xform_kernel<1>"           # large frames
+    assert f(16 << 20, (16 << 20) * 264, 16, cfws.DESERIALIZE_REASSEMBLE, 1 << 33).decode() == "xform_kernel<1>"
+    assert f(0, 0, 16, 0, 0).decode() == "xform_kernel<1>"

@@ -319,9 +319,9 @@ def _sha_device(t: "torch.Tensor", n: int) -> str:
     return h.hexdigest()
 
 
-@pytest.mark.parametrize("which", [0, 1, 2, 3, 4],
+@pytest.mark.parametrize("which", [0, 1, 2, 3, 4, 5],
                          ids=["4M_x_1KiB_text", "16M_x_256B_binary", "2M_x_2KiB_binary",
-                              "1398101_x_3KiB_binary", "1198372_x_3584B_text"])
+                              "1398101_x_3KiB_binary", "1198372_x_3584B_text", "8M_x_512B_binary"])
 def test_small_frame_reference_digests(which):
     """The small-frame batches the bench quotes (4,194,304 x 1 KiB TEXT,
     16,777,216 x 256 B BINARY, and the in-region send's range: 2,097,152 x
@@ -390,6 +390,35 @@ def test_small_frame_reference_digests(which):
     assert bool((st4 == 0).all())
     rolled = torch.roll(back[:n * fs].view(n, fs), shifts=-h, dims=0).reshape(-1)
     assert _sha_device(rolled, n * fs) == g["payload_sha256"]
+    del rolled
+    # the compact forms: the slot and scatter receives writing 8-byte
+    # cfws_frame_info_t entries (the payloads compared on the device with
+    # the arena the digest above pinned) ...
+    info = torch.empty((n, 8), dtype=torch.uint8, device="cuda")
+    for scatter in (False, True):
+        back.fill_(0xEE)
+        info.fill_(0xEE)
+        if scatter:
+            cfws.deserialize_scatter_info(wire, total, idx, dst, back, fs, info)
+        else:
+            cfws.deserialize_slots_info(wire, total, idx, back, fs, info)
+        torch.cuda.synchronize()
+        got = back[:n * fs].view(n, fs)
+        if scatter:
+            got = torch.roll(got, shifts=-h, dims=0)
+        assert torch.equal(got.reshape(-1), payload)
+        fi = info.view(torch.int64).view(-1)
+        exp = fs | 1 << 32 | g["opcode"] << 40          # payload_size, fin, opcode, status 0
+        assert bool((fi == exp).all())
+    del info
+    # ... and the uniform send (payload + one key per frame, no plan): the
+    # wire equals the one whose digest is checked above
+    keys_t = torch.from_numpy(desc["mask_key"].view(np.int32).copy()).cuda()
+    wire2 = torch.full_like(wire, 0xEE)
+    tot_u = torch.zeros(1, dtype=torch.int64, device="cuda")
+    cfws.serialize_uniform(payload, keys_t, n, fs, wire2, fin=True, opcode=g["opcode"], mask=True, total_t=tot_u)
+    torch.cuda.synchronize()
+    assert tot_u.item() == total and torch.equal(wire2, wire)
 
 
 def _roundtrip_digest(g, full=False):

@@ -10,7 +10,12 @@ payload arena at round16(capacity), and bytes past the capacity, past each
 payload's 16-byte round-up and in the slots of non-COMPLETE frames are
 checked to keep their sentinel. Slots up to 992 bytes take the window
 kernel with one block per lane, up to 2,016 with two, up to 4,064 with
-four, up to 8,160 with eight, larger ones the per-frame kernel."""
+four, up to 8,160 with eight, larger ones the per-frame kernel.
+
+Every case runs in both output forms (the `form` fixture): descriptors +
+statuses (cfws_deserialize_slots / _scatter) and the compact 8-byte
+cfws_frame_info_t (cfws_deserialize_slots_info / _scatter_info, in a guarded
+buffer of exactly 8 n bytes)."""
 import random
 
 import numpy as np
@@ -36,6 +41,16 @@ def device():
     if not _glib().guard_supported():
         pytest.skip("no HIP virtual memory management on this device")
     return torch.device("cuda", 0)
+
+
+FORM = {"form": "desc"}
+
+
+@pytest.fixture(params=["desc", "info"], autouse=True)
+def form(request):
+    FORM["form"] = request.param
+    yield request.param
+    FORM["form"] = "desc"
 
 
 @pytest.fixture
@@ -91,27 +106,45 @@ def run_slots(guards, wire, starts, slot, cap=None, wire_size=None, max_payload=
     w = guards(max(ws_n, 1), flush_end).upload(wire[:ws_n])
     out = guards(max(cap, 1), flush_end)
     idx = torch.from_numpy(np.asarray(starts, dtype=np.uint64).view(np.int64)).cuda()
-    if offs is None:
+    info = FORM["form"] == "info"
+    inf_b = guards(max(8 * n, 1), flush_end) if info else None
+    off_t = None if offs is None else torch.from_numpy(np.asarray(offs, dtype=np.uint64).view(np.int64)).cuda()
+    tot = None
+    if offs is None and info:
+        _, tot = cfws.deserialize_slots_info(w, ws_n, idx, out, slot, inf_b, max_payload=max_payload,
+                                             payload_capacity=cap)
+    elif offs is None:
         d_t, st_t, tot = cfws.deserialize_slots(w, ws_n, idx, out, slot, max_payload=max_payload,
                                                 payload_capacity=cap)
+    elif info:
+        cfws.deserialize_scatter_info(w, ws_n, idx, off_t, out, slot, inf_b, max_payload=max_payload,
+                                      payload_capacity=cap)
     else:
-        off_t = torch.from_numpy(np.asarray(offs, dtype=np.uint64).view(np.int64)).cuda()
         d_t, st_t = cfws.deserialize_scatter(w, ws_n, idx, off_t, out, slot, max_payload=max_payload,
                                              payload_capacity=cap)
-        tot = None
     torch.cuda.synchronize()
     e_arena, e_d, e_st, e_tot = expect_slots(wire, ws_n, starts, slot, cap, max_payload, offs)
     if tot is not None:
         assert int(tot.item()) == e_tot
-    st = st_t.cpu().numpy()
-    bad = np.nonzero(st != e_st)[0]
-    assert bad.size == 0, f"{bad.size} statuses differ, first {[(int(i), int(st[i]), int(e_st[i])) for i in bad[:6]]}"
-    d = cfws.desc_from_device(d_t)
-    for f in ("payload_off", "wire_off", "payload_size", "mask_key", "opcode", "header_size"):
-        assert np.array_equal(d[f], e_d[f]), f
     ok = e_st == O.PARSE_COMPLETE
-    for f in ("fin", "mask"):
-        assert np.array_equal(d[f][ok], e_d[f][ok]), f
+    if info:
+        fi = inf_b.download()[:8 * n].view(cfws.INFO_DTYPE)
+        st = fi["status"].astype(np.int32)
+        bad = np.nonzero(st != e_st)[0]
+        assert bad.size == 0, f"{bad.size} statuses differ, first {[(int(i), int(st[i]), int(e_st[i])) for i in bad[:6]]}"
+        e_ps = np.minimum(e_d["payload_size"], np.uint64(0xFFFFFFFF)).astype(np.uint32)
+        assert np.array_equal(fi["payload_size"], e_ps), "payload_size"
+        assert np.array_equal(fi["opcode"], e_d["opcode"]), "opcode"
+        assert np.array_equal(fi["fin"][ok], e_d["fin"][ok]), "fin"
+    else:
+        st = st_t.cpu().numpy()
+        bad = np.nonzero(st != e_st)[0]
+        assert bad.size == 0, f"{bad.size} statuses differ, first {[(int(i), int(st[i]), int(e_st[i])) for i in bad[:6]]}"
+        d = cfws.desc_from_device(d_t)
+        for f in ("payload_off", "wire_off", "payload_size", "mask_key", "opcode", "header_size"):
+            assert np.array_equal(d[f], e_d[f]), f
+        for f in ("fin", "mask"):
+            assert np.array_equal(d[f][ok], e_d[f][ok]), f
     got = out.download()
     bad = np.nonzero(got != e_arena)[0]
     assert bad.size == 0, f"{bad.size} arena bytes differ, first at {bad[:8]} (cap {cap})"
