@@ -19,6 +19,7 @@
 
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <mutex>
 #include <unordered_map>
 
@@ -122,14 +123,22 @@ int guard_free(uint64_t ptr)
     if (e != hipSuccess) return fail("hipDeviceSynchronize", e);
     if ((e = hipMemUnmap(g.mapped, g.mapped_n)) != hipSuccess) return fail("hipMemUnmap", e);
     if ((e = hipMemRelease(g.h)) != hipSuccess) return fail("hipMemRelease", e);
-    // The address range stays reserved for the rest of the process: on this
-    // stack (ROCm 7.2, gfx950) a range freed with hipMemAddressFree and handed
-    // out again by the next hipMemAddressReserve, with new memory mapped
-    // under it, was read by kernels through the old translation -- a
-    // serialize read a stale payload (the wire came out as key bytes over a
-    // constant) while hipMemcpy of the same range read the new bytes
-    // (tools/guard_debug.py --free, profiles/r05/guard_debug.txt). Never
-    // reusing a range keeps every buffer's first kernel on fresh addresses.
+    // GUARD_FREE_RANGES=1: release the range too (round 6's re-check of the
+    // finding below: tools/vmm_remap_probe.hip, profiles/r06/vmm/)
+    static const bool free_ranges = [] {
+        const char* v = getenv("GUARD_FREE_RANGES");
+        return v && v[0] == '1';
+    }();
+    if (free_ranges && (e = hipMemAddressFree(g.base, g.reserved)) != hipSuccess)
+        return fail("hipMemAddressFree", e);
+    // By default the address range stays reserved for the rest of the
+    // process: on this stack (ROCm 7.2, gfx950) new physical memory mapped at
+    // an address that earlier mapped other, still-allocated memory is read
+    // through the old translation, by kernels and by hipMemcpy. Round 6
+    // reproduced it with a plain copy kernel and no library code
+    // (tools/vmm_remap_probe.hip, profiles/r06/vmm/); with GUARD_FREE_RANGES=1
+    // tests/test_gpu_guard.py fails on its second test. Never reusing a range
+    // keeps every buffer's first kernel on fresh addresses.
     return 0;
 }
 

@@ -13,8 +13,19 @@
 // previous trial's pattern (a stale translation) -- and the same check by
 // hipMemcpy, which goes through the copy engines.
 //
+// --hold keeps each trial's physical allocation until the end of the run
+// (released after the next trial has mapped its own), so the next trial's
+// memory cannot be the same physical pages: a stale translation then reads
+// the previous pattern instead of (by luck) the same pages.
+//
 //   hipcc --offload-arch=gfx950 -O2 -o build/vmm_remap_probe tools/vmm_remap_probe.hip
-//   build/vmm_remap_probe [trials] [--keep]     (--keep: never free a range)
+// --remap reserves ONE range for the whole run and maps each trial's new
+// memory at the same address (unmap, then map the next handle): the pattern
+// of an allocator that grows and shrinks inside one reservation (torch's
+// expandable segments).
+//
+//   build/vmm_remap_probe [trials] [--keep] [--hold] [--remap]
+//   (--keep: never free a range)
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -43,7 +54,13 @@ static uint8_t pattern(int trial, uint64_t i) { return (uint8_t)(i * 131u + tria
 int main(int argc, char** argv)
 {
     const int trials = argc > 1 ? atoi(argv[1]) : 8;
-    const bool keep = argc > 2 && strcmp(argv[2], "--keep") == 0;
+    bool keep = false, hold = false, remap = false;
+    for (int i = 2; i < argc; ++i) {
+        keep |= strcmp(argv[i], "--keep") == 0;
+        hold |= strcmp(argv[i], "--hold") == 0;
+        remap |= strcmp(argv[i], "--remap") == 0;
+    }
+    std::vector<hipMemGenericAllocationHandle_t> held;
     int dev = 0;
     CHECK(hipSetDevice(dev));
     hipMemAllocationProp prop = {};
@@ -61,9 +78,11 @@ int main(int argc, char** argv)
     CHECK(hipMalloc(&dst, mapped_n));
     std::vector<uint8_t> host(mapped_n), got(mapped_n);
     void* prev_base = nullptr;
+    void* one = nullptr;
+    if (remap) CHECK(hipMemAddressReserve(&one, reserved, guard, nullptr, 0));
     for (int t = 0; t < trials; ++t) {
-        void* base = nullptr;
-        CHECK(hipMemAddressReserve(&base, reserved, guard, nullptr, 0));
+        void* base = one;
+        if (!remap) CHECK(hipMemAddressReserve(&base, reserved, guard, nullptr, 0));
         char* mapped = static_cast<char*>(base) + guard;
         hipMemGenericAllocationHandle_t h;
         CHECK(hipMemCreate(&h, mapped_n, &prop, 0));
@@ -92,18 +111,25 @@ int main(int argc, char** argv)
                 if (t > 0 && got[i] == pattern(t - 1, i)) ++stale;
             }
         }
-        printf("{\"trial\": %d, \"keep\": %s, \"range\": \"%p\", \"reused\": %s, \"kernel_bad_bytes\": %llu, "
-               "\"stale_bytes\": %llu, \"first_bad\": %lld, \"dma_bad_bytes\": %llu}\n",
-               t, keep ? "true" : "false", base, base == prev_base ? "true" : "false", (unsigned long long)bad,
+        printf("{\"trial\": %d, \"keep\": %s, \"hold\": %s, \"remap\": %s, \"range\": \"%p\", \"reused\": %s, "
+               "\"kernel_bad_bytes\": %llu, \"stale_bytes\": %llu, \"first_bad\": %lld, \"dma_bad_bytes\": %llu}\n",
+               t, keep ? "true" : "false", hold ? "true" : "false", remap ? "true" : "false", base,
+               base == prev_base ? "true" : "false",
+               (unsigned long long)bad,
                (unsigned long long)stale, first == ~uint64_t(0) ? -1LL : (long long)first,
                (unsigned long long)dma_bad);
         fflush(stdout);
         CHECK(hipDeviceSynchronize());
         CHECK(hipMemUnmap(mapped, mapped_n));
-        CHECK(hipMemRelease(h));
-        if (!keep) CHECK(hipMemAddressFree(base, reserved));
+        if (hold)
+            held.push_back(h);
+        else
+            CHECK(hipMemRelease(h));
+        if (!keep && !remap) CHECK(hipMemAddressFree(base, reserved));
         prev_base = base;
     }
+    if (remap) CHECK(hipMemAddressFree(one, reserved));
+    for (auto& h : held) CHECK(hipMemRelease(h));
     CHECK(hipFree(dst));
     return 0;
 }
