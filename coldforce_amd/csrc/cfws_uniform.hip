@@ -149,6 +149,15 @@ __device__ __forceinline__ uint4 header_finish(const UniformFrames& U, uint64_t 
     return o;
 }
 
+// The body chunk at D (round u of `lane`, frame byte `off`) is followed by a
+// body chunk of the same frame that this wave loads (lane + 1, or lane 0 of
+// round u + 1): its first source block is this chunk's second.
+__device__ __forceinline__ bool body_next_of(uint32_t hs, uint32_t W, int u, uint32_t lane, uint32_t off, uint64_t D,
+                                             uint64_t lim)
+{
+    return off + 32u <= W && off + 16u >= hs && D + 16 < lim && !(lane == 63 && u == kUniformUnroll - 1);
+}
+
 __global__ void __launch_bounds__(kThreads)
 serialize_uniform_kernel(UniformFrames U, uint8_t* __restrict__ out, uint64_t cap, uint64_t* __restrict__ user_total)
 {
@@ -173,6 +182,9 @@ serialize_uniform_kernel(UniformFrames U, uint8_t* __restrict__ out, uint64_t ca
 
     // frames whose header meets the span: fa .. fb (fb may be n: the chunk
     // holding the batch's end past the last payload is handled as frame n's)
+    auto body_next = [&](int u, uint32_t ln, uint32_t o, uint64_t D, uint64_t lm) {
+        return body_next_of(U.hs, U.W, u, ln, o, D, lm);
+    };
     const uint64_t fa = (base + U.hs > D0) ? F0 : F0 + 1;
     uint64_t fb = F0 + div_w(U, rel0 + kUniformSpan - 1);
     if (fb > U.n) fb = U.n;
@@ -194,10 +206,17 @@ serialize_uniform_kernel(UniformFrames U, uint8_t* __restrict__ out, uint64_t ca
             const uint64_t s = src0 + uint64_t(q[u]) * U.fs + (off[u] - U.hs);
             const uint8_t* sp = U.src + (s & ~uint64_t(15));
             A[u] = ld16(sp);
-            if (s & 15u) B[u] = ld16(sp + 16);
+            // the second block: the next chunk's own first block (over DPP)
+            // when that chunk is a body chunk of the same frame
+            if ((s & 15u) && !body_next(u, lane, off[u], D0 + 16ull * (64u * u + lane), lim)) B[u] = ld16(sp + 16);
             key[u] = U.keys ? U.keys[F0 + q[u]] : 0u;
         }
     }
+    uint4 N[kUniformUnroll];
+#pragma unroll
+    for (int u = 0; u < kUniformUnroll; ++u)          // every lane: DPP needs the full wave
+        N[u] = from_next_lane(A[u], u + 1 < kUniformUnroll ? readlane4(A[u + 1 < kUniformUnroll ? u + 1 : u], 0)
+                                                           : make_uint4(0, 0, 0, 0));
     HeaderChunk h;
     uint64_t hD = 0, hf = 0;
     uint32_t hoff = 0;
@@ -224,7 +243,8 @@ serialize_uniform_kernel(UniformFrames U, uint8_t* __restrict__ out, uint64_t ca
     for (int u = 0; u < kUniformUnroll; ++u) {
         if (!body[u]) continue;
         const uint32_t ph = (uint32_t)((src0 + uint64_t(q[u]) * U.fs + (off[u] - U.hs)) & 15u);
-        uint4 o = ph ? funnel16(A[u], B[u], ph) : A[u];
+        const bool nb = body_next(u, lane, off[u], D0 + 16ull * (64u * u + lane), lim);
+        uint4 o = ph ? funnel16(A[u], nb ? N[u] : B[u], ph) : A[u];
         xor4(o, rotr8(key[u], off[u] - U.hs));
         uniform_store(out, rs, D0, D0 + 16ull * (64u * u + lane), cap, o);
     }
@@ -412,6 +432,11 @@ serialize_uniform_bytes_kernel(UniformFrames U, uint8_t* __restrict__ out, uint6
         for (uint32_t j = 0; D + j < cap; ++j) out[D + j] = (uint8_t)(u4_byte(o, (int)j));
 }
 
+__global__ void uniform_total_kernel(uint64_t* __restrict__ user_total, uint64_t total)
+{
+    if (threadIdx.x == 0) *user_total = total;
+}
+
 }  // namespace
 
 extern "C" int cfws_serialize_uniform(const void* d_payload, const uint32_t* d_keys, size_t n, uint64_t fs,
@@ -428,10 +453,10 @@ extern "C" int cfws_serialize_uniform(const void* d_payload, const uint32_t* d_k
     hipStream_t st = static_cast<hipStream_t>(stream);
     const uint64_t total = n * W;
     if (n == 0 || cap == 0) {
-        if (d_total && hipMemcpyAsync(d_total, &total, 8, hipMemcpyHostToDevice, st) != hipSuccess)
-            return launch_check("serialize_uniform");
-        if (d_total && hipStreamSynchronize(st) != hipSuccess) return launch_check("serialize_uniform");
-        return CFWS_OK;
+        // nothing to write but the total: one thread stores it (no host
+        // copy, so nothing waits on the stream)
+        if (d_total) uniform_total_kernel<<<1, 64, 0, st>>>(d_total, total);
+        return launch_check("serialize_uniform");
     }
     if (!d_wire || (fs && !d_payload) || (mask && !d_keys))
         return set_err(CFWS_ERROR_INVALID_ARGUMENT, "null pointer", hipSuccess);

@@ -9,6 +9,9 @@
  *                 and the same frames through cfws_deserialize_slots (frame
  *                 i's payload at i * slot) and cfws_deserialize_scatter
  *                 (each payload to a buffer of its own size, last frame first)
+ *   uniform batch: n frames of 256 B through cfws_serialize_uniform (payload
+ *                 + one key per frame, no descriptors) and back through
+ *                 cfws_deserialize_slots_info (8-byte records)
  *
  * Checks that every payload comes back and that the wire equals what
  * sequential co_ws_frame_serialize calls (the drop-in, same library) append
@@ -185,11 +188,59 @@ int main(int argc, char** argv)
     for (size_t i = 0; scatter_ok && i < n; ++i)
         scatter_ok = status[i] == CFWS_PARSE_COMPLETE &&
                      memcmp(sc + off[i], payload + desc[i].payload_off, desc[i].payload_size) == 0;
+
+    /* a uniform batch: n BINARY frames of 256 B, masked; the wire must equal
+       the drop-in's appends for the same random() stream */
+    const uint64_t U = 256, UW = U + 8;                        /* 2 + 2 (BE16 length) + 4 key */
+    uint8_t* upay = malloc(n * U);
+    for (uint64_t k = 0; k < n * U; ++k) upay[k] = (uint8_t)(k * 40503u >> 7);
+    uint32_t* ukeys = malloc(n * sizeof *ukeys);
+    srandom(4242);
+    cfws_draw_mask_keys(n, NULL, ukeys);
+    co_byte_array_t uref = {0};
+    uref.element_size = 1;
+    uref.capacity = 8;
+    uref.buffer = malloc(8);
+    srandom(4242);
+    for (size_t i = 0; i < n; ++i)
+        if (!co_ws_frame_serialize(true, CO_WS_OPCODE_BINARY, true, upay + i * U, U, &uref)) return 1;
+    void *d_upay, *d_ukeys, *d_uwire, *d_uback, *d_uinfo, *d_ustarts;
+    CHECK(hipMalloc(&d_upay, n * U));
+    CHECK(hipMalloc(&d_ukeys, n * sizeof *ukeys));
+    CHECK(hipMalloc(&d_uwire, n * UW + 16));
+    CHECK(hipMalloc(&d_uback, n * U));
+    CHECK(hipMalloc(&d_uinfo, n * sizeof(cfws_frame_info_t)));
+    CHECK(hipMalloc(&d_ustarts, n * 8));
+    uint64_t* ustarts = malloc(n * 8);
+    for (size_t i = 0; i < n; ++i) ustarts[i] = i * UW;
+    CHECK(hipMemcpyAsync(d_upay, upay, n * U, hipMemcpyHostToDevice, st));
+    CHECK(hipMemcpyAsync(d_ukeys, ukeys, n * sizeof *ukeys, hipMemcpyHostToDevice, st));
+    CHECK(hipMemcpyAsync(d_ustarts, ustarts, n * 8, hipMemcpyHostToDevice, st));
+    CHECK(cfws_serialize_uniform(d_upay, (const uint32_t*)d_ukeys, n, U, 1, CO_WS_OPCODE_BINARY, 1, d_uwire,
+                                 n * UW + 16, d_total, st));
+    CHECK(cfws_deserialize_slots_info(d_uwire, n * UW, (const uint64_t*)d_ustarts, n,
+                                      CFWS_DEFAULT_MAX_RECEIVE_PAYLOAD_SIZE, U, (cfws_frame_info_t*)d_uinfo,
+                                      d_uback, n * U, NULL, st));
+    uint64_t utotal = 0;
+    CHECK(hipMemcpyAsync(&utotal, d_total, 8, hipMemcpyDeviceToHost, st));
+    CHECK(hipStreamSynchronize(st));
+    uint8_t* uwire = malloc(n * UW);
+    uint8_t* uback = malloc(n * U);
+    cfws_frame_info_t* uinfo = malloc(n * sizeof *uinfo);
+    CHECK(hipMemcpy(uwire, d_uwire, n * UW, hipMemcpyDeviceToHost));
+    CHECK(hipMemcpy(uback, d_uback, n * U, hipMemcpyDeviceToHost));
+    CHECK(hipMemcpy(uinfo, d_uinfo, n * sizeof *uinfo, hipMemcpyDeviceToHost));
+    int uniform_ok = utotal == n * UW && uref.count == n * UW && memcmp(uwire, uref.buffer, n * UW) == 0 &&
+                     memcmp(uback, upay, n * U) == 0;
+    for (size_t i = 0; uniform_ok && i < n; ++i)
+        uniform_ok = uinfo[i].status == CFWS_PARSE_COMPLETE && uinfo[i].payload_size == U && uinfo[i].fin == 1 &&
+                     uinfo[i].opcode == CO_WS_OPCODE_BINARY;
+
     printf("{\"frames\": %zu, \"payload_bytes\": %llu, \"wire_bytes\": %llu, "
            "\"wire_equals_dropin\": %s, \"indexed\": %llu, \"roundtrip\": %s, \"slots\": %s, "
-           "\"scatter\": %s}\n",
+           "\"scatter\": %s, \"uniform\": %s}\n",
            n, (unsigned long long)arena, (unsigned long long)wire_total, same ? "true" : "false",
            (unsigned long long)n_found, ok ? "true" : "false", slots_ok ? "true" : "false",
-           scatter_ok ? "true" : "false");
-    return ok && slots_ok && scatter_ok ? 0 : 2;
+           scatter_ok ? "true" : "false", uniform_ok ? "true" : "false");
+    return ok && slots_ok && scatter_ok && uniform_ok ? 0 : 2;
 }

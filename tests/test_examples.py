@@ -33,4 +33,4 @@ def test_example_roundtrip(n, maxlen):
     assert r.returncode == 0, r.stdout + r.stderr
     out = json.loads(r.stdout.strip().splitlines()[-1])
     assert out["frames"] == n and out["indexed"] == n
-    assert out["wire_equals_dropin"] and out["roundtrip"] and out["slots"] and out["scatter"]
+    assert out["wire_equals_dropin"] and out["roundtrip"] and out["slots"] and out["scatter"] and out["uniform"]
