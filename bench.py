@@ -70,6 +70,10 @@ def parse():
     ap.add_argument("--recv-info", action="store_true",
                     help="with --recv-slots / --recv-scatter: the compact 8-byte per-frame output "
                          "(cfws_deserialize_slots_info / _scatter_info) instead of descriptors + statuses")
+    ap.add_argument("--recv-uniform", action="store_true",
+                    help="config2: the slot receive of a uniform stream, frame i at i x its wire "
+                         "bytes with no index (cfws_deserialize_slots_uniform, compact output and a "
+                         "mismatch count); implies --recv-slots --recv-info")
     ap.add_argument("--keys", type=int, default=1 << 20, help="accept workload: client keys per GPU")
     ap.add_argument("--connections", type=int, default=16384, help="index workload: connections")
     ap.add_argument("--index-mib", type=int, default=1024, help="index workload: receive-buffer MiB")
@@ -847,6 +851,10 @@ def main():
     # batches of small frames (<= 512 B of wire per frame, no reassembly) the
     # fused plan + copy kernel of the receive,
     # deserialize_plan_single_kernel<true>
+    if args.recv_uniform:
+        if args.recv_scatter or args.workload != "config2":
+            sys.exit("bench.py: --recv-uniform is a config2 slot receive (no --recv-scatter)")
+        args.recv_slots = args.recv_info = True
     slot = W.round16(max(fs, 16)) if args.recv_slots or args.recv_scatter else 0
     if slot and (flags or slot != fs):
         sys.exit("bench.py: --recv-slots / --recv-scatter need config2 with a frame size that is a multiple of 16")
@@ -861,6 +869,8 @@ def main():
         sys.exit("bench.py: --send uniform needs config2 (a uniform batch)")
     keys_t = torch.from_numpy(desc_np["mask_key"].view(np.int32).copy()).to(dev) if uniform else None
     info_t = torch.empty((F, 8), dtype=torch.uint8, device=dev) if args.recv_info else None
+    stride = wire_total // F if args.recv_uniform else 0       # a uniform batch: W per frame
+    mismatch_t = torch.zeros(1, dtype=torch.int32, device=dev) if args.recv_uniform else None
     # the receive kernel the timed pass is, as the library routes the call
     recv_kernel = cfws.lib().cfws_deserialize_pass_kernel(F, wire_total, 16, flags, back.numel()).decode()
 
@@ -885,6 +895,9 @@ def main():
                 cfws.deserialize_scatter_info(wire, wire_total, index, dst_off, back, slot, info_t)
             elif dst_off is not None:
                 cfws.deserialize_scatter(wire, wire_total, index, dst_off, back, slot, desc_de, status)
+            elif stride:
+                cfws.deserialize_slots_uniform(wire, wire_total, F, stride, back, slot, info_t, tot_de,
+                                               mismatch_t)
             elif slot and info_t is not None:
                 cfws.deserialize_slots_info(wire, wire_total, index, back, slot, info_t, tot_de)
             elif slot:
@@ -912,6 +925,8 @@ def main():
         # the compact entries: payload_size, fin 1, opcode BINARY, status COMPLETE
         exp = fs | 1 << 32 | cfws.OPCODE_BINARY << 40
         ok_info = bool((info_t.view(torch.int64).view(-1) == exp).all().item())
+        if mismatch_t is not None:
+            ok_info = ok_info and int(mismatch_t.item()) == 0
         status.fill_(0 if ok_info else 1)
         if perm is None:
             tot_de.fill_(arena_bytes)
@@ -968,7 +983,7 @@ def main():
     # the PMC summary a traffic figure may come from: the same workload only
     traffic_key = (f"config2:{F}x{fs}" + (":uniform" if uniform else "")
                    + (":scatter" if perm is not None else ":slots" if slot else "")
-                   + (":info" if info_t is not None else "")
+                   + (":info" if info_t is not None else "") + (":implicit" if stride else "")
                    if args.workload == "config2" else
                    "config3" if args.workload == "config3" else f"config4:{F}x{fs}")
     rows = shard.gather_floats([local, arena_bytes, ser_ms, de_ms, alg_bytes], dev)
@@ -995,7 +1010,7 @@ def main():
                             f"{'_info' if info_t is not None else ''})"
                             if perm is not None else
                             f"; the receive into fixed {slot} B payload slots (cfws_deserialize_slots"
-                            f"{'_info' if info_t is not None else ''})"
+                            f"{'_uniform: no index' if stride else '_info' if info_t is not None else ''})"
                             if slot else "")
                          if args.workload == "config2" else
                          f"config4: shard {rank} of 8 of the 8 M x 64 KiB batch ({F} frames, "

@@ -51,7 +51,7 @@ BATCH_SYMBOLS = (
     "cfws_serialize_plan", "cfws_serialize_execute", "cfws_serialize_batch", "cfws_serialize_uniform",
     "cfws_deserialize_plan", "cfws_deserialize_execute", "cfws_deserialize_batch",
     "cfws_deserialize_slots", "cfws_deserialize_scatter", "cfws_deserialize_slots_info",
-    "cfws_deserialize_scatter_info", "cfws_xor_mask", "cfws_draw_mask_keys", "cfws_draw_mask_keys_seeded",
+    "cfws_deserialize_scatter_info", "cfws_deserialize_slots_uniform", "cfws_xor_mask", "cfws_draw_mask_keys", "cfws_draw_mask_keys_seeded",
     "cfws_release_thread_resources", "cfws_set_dropin_gpu_min", "cfws_dropin_gpu_min",
     "cfws_fill_splitmix", "cfws_pipeline_create", "cfws_pipeline_destroy",
     "cfws_pipeline_serialize", "cfws_pipeline_deserialize", "cfws_pipeline_receive",
@@ -127,6 +127,8 @@ def lib(path: str = LIB_PATH) -> C.CDLL:
         "cfws_deserialize_slots_info": ([_vp, _u64, _vp, _sz, _u64, _u64, _vp, _vp, _u64, _vp, _vp], C.c_int),
         "cfws_deserialize_scatter_info": ([_vp, _u64, _vp, _vp, _sz, _u64, _u64, _vp, _vp, _u64, _vp],
                                           C.c_int),
+        "cfws_deserialize_slots_uniform": ([_vp, _u64, _sz, _u64, _u64, _u64, _vp, _vp, _u64, _vp, _vp, _vp],
+                                           C.c_int),
         "cfws_encode_headers": ([_vp, _sz, _vp, _u64, _vp], C.c_int),
         "cfws_parse_headers": ([_vp, _u64, _vp, _sz, _u64, _vp, _vp, _vp], C.c_int),
         "cfws_mask_batch": ([_vp, _vp, _sz, _u64, _vp, _u64, _vp], C.c_int),
@@ -425,6 +427,28 @@ def deserialize_scatter_info(wire_t, wire_size: int, index_t, payload_off_t, pay
                                                _stream(stream)),
            "cfws_deserialize_scatter_info")
     return info_t
+
+
+def deserialize_slots_uniform(wire_t, wire_size: int, n: int, frame_stride: int, payload_t, slot_bytes: int,
+                              info_t=None, total_t=None, mismatch_t=None,
+                              max_payload: int = DEFAULT_MAX_PAYLOAD, payload_capacity: int | None = None,
+                              stream=None):
+    """cfws_deserialize_slots_uniform: the info slot receive with frame i at
+    i * frame_stride of the wire (no index). mismatch_t (one int32, may be
+    None): the frames that are not COMPLETE frames of frame_stride bytes.
+    Returns (info_t, total_t)."""
+    import torch
+    dev = wire_t.device
+    if info_t is None:
+        info_t = torch.empty((n, 8), dtype=torch.uint8, device=dev)
+    if total_t is None:
+        total_t = torch.zeros(1, dtype=torch.int64, device=dev)
+    cap = payload_t.numel() if payload_capacity is None else payload_capacity
+    _check(lib().cfws_deserialize_slots_uniform(_p(wire_t), wire_size, n, frame_stride, max_payload, slot_bytes,
+                                                _p(info_t), _p(payload_t), cap, _p(total_t), _p(mismatch_t),
+                                                _stream(stream)),
+           "cfws_deserialize_slots_uniform")
+    return info_t, total_t
 
 
 def info_from_device(t) -> np.ndarray:

@@ -905,8 +905,17 @@ __device__ __forceinline__ void slot_info(cfws_frame_info_t* info, uint64_t f, c
     reinterpret_cast<uint2*>(info)[f] = make_uint2(ps, w1);
 }
 
+// the uniform receive's check: lanes whose frame is not a COMPLETE frame of
+// exactly `stride` wire bytes, one atomic per wave that has any
+__device__ __forceinline__ void count_mismatch(uint32_t* mismatch, bool odd, uint32_t lane)
+{
+    const uint64_t b = __ballot(odd);
+    if (b && lane == 0) atomicAdd(mismatch, (uint32_t)__popcll(b));
+}
+
 // kInfo: write cfws_frame_info_t entries to `info` instead of descriptors
-// and statuses
+// and statuses; index null: frame i starts at i * stride and `mismatch`
+// (when not null) counts the frames that are not uniform frames
 template <int kSlotRounds, int kSub, bool kScatter, bool kInfo>
 __global__ void __launch_bounds__(kThreads)
 deserialize_slots_window_kernel(const uint8_t* __restrict__ wire, uint64_t wire_size,
@@ -914,7 +923,8 @@ deserialize_slots_window_kernel(const uint8_t* __restrict__ wire, uint64_t wire_
                                 uint64_t slot, uint32_t G, cfws_frame_desc_t* __restrict__ desc,
                                 int32_t* __restrict__ status, uint8_t* __restrict__ out, uint64_t capacity,
                                 uint64_t* __restrict__ user_total, const uint64_t* __restrict__ dst,
-                                cfws_frame_info_t* __restrict__ infos)
+                                cfws_frame_info_t* __restrict__ infos, uint64_t stride,
+                                uint32_t* __restrict__ mismatch)
 {
     const uint32_t lane = threadIdx.x & 63u;
     // kSub sub-windows of 64 lanes make 64 kSub virtual lanes, v = 64 sw +
@@ -930,14 +940,16 @@ deserialize_slots_window_kernel(const uint8_t* __restrict__ wire, uint64_t wire_
     }
     const uint32_t R = P * kSlotRounds <= 64 ? (uint32_t)kSlotRounds : 64u / P;
     const uint64_t FI = uint64_t(R) * P;                 // frames per wave-iteration
-    const uint64_t stride = uint64_t(gridDim.x) * kWaves * FI;
+    const uint64_t grid_frames = uint64_t(gridDim.x) * kWaves * FI;
     const uint4 z = make_uint4(0, 0, 0, 0);
     const bool b16 = wire_size >= 16;
     const uint64_t lastu = wire_size - 16;
-    for (uint64_t f0 = (uint64_t(blockIdx.x) * kWaves + (threadIdx.x >> 6)) * FI; f0 < n; f0 += stride) {
+    for (uint64_t f0 = (uint64_t(blockIdx.x) * kWaves + (threadIdx.x >> 6)) * FI; f0 < n; f0 += grid_frames) {
         const uint64_t fl = f0 + lane;
         const bool mine = lane < FI && fl < n;
-        const uint64_t wl = mine ? index[fl] : ~uint64_t(0);
+        // the frame's start: the index, or frame i at i * stride (the uniform
+        // receive: its window loads need no index load before them)
+        const uint64_t wl = !mine ? ~uint64_t(0) : index ? index[fl] : fl * stride;
         // the frame's payload offset: its slot, or the caller's (scatter)
         const uint64_t runl = !mine ? 0 : kScatter ? dst[fl] : fl * slot;
         // every round's window block, then each frame's header bytes
@@ -957,6 +969,7 @@ deserialize_slots_window_kernel(const uint8_t* __restrict__ wire, uint64_t wire_
         // lane l parses frame f0 + l; its round info: payload length (<= slot
         // < 2^16) | (phase + header size) << 16, zero when not copied
         uint32_t info = 0, key = 0;
+        bool odd = false;   // not a uniform frame at its place (mismatch count)
         if (mine) {
             cfws_frame_desc_t d;
             int32_t st;
@@ -981,7 +994,9 @@ deserialize_slots_window_kernel(const uint8_t* __restrict__ wire, uint64_t wire_
             if (st == CFWS_PARSE_COMPLETE && d.payload_size > 0)
                 info = (uint32_t)d.payload_size | ((uint32_t)(wl & 15u) + d.header_size) << 16;
             key = d.mask ? d.mask_key : 0u;
+            odd = st != CFWS_PARSE_COMPLETE || d.header_size + d.payload_size != stride;
         }
+        if (mismatch) count_mismatch(mismatch, odd, lane);
 #pragma unroll
         for (int u = 0; u < kSlotRounds; ++u) {
             if ((uint32_t)u >= R) break;   // wave-uniform
@@ -1029,14 +1044,15 @@ deserialize_slots_kernel(const uint8_t* __restrict__ wire, uint64_t wire_size, c
                          uint64_t n, uint64_t max_payload, uint64_t slot, cfws_frame_desc_t* __restrict__ desc,
                          int32_t* __restrict__ status, uint8_t* __restrict__ out, uint64_t capacity,
                          uint64_t* __restrict__ user_total, const uint64_t* __restrict__ dst,
-                         cfws_frame_info_t* __restrict__ info)
+                         cfws_frame_info_t* __restrict__ info, uint64_t stride, uint32_t* __restrict__ mismatch)
 {
     const uint64_t f = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
     uint64_t run = 0, src = 0;
     uint32_t len = 0, nb = 0, key = 0;
+    bool odd = false;
     if (f < n) {
         cfws_frame_desc_t d;
-        const uint64_t s0 = index[f];
+        const uint64_t s0 = index ? index[f] : f * stride;
         run = kScatter ? dst[f] : f * slot;
         const int32_t p = parse_ws_header(wire, wire_size, s0, max_payload, d);
         const int32_t st = kScatter ? scatter_rule(p, run, d.payload_size, slot, capacity)
@@ -1051,11 +1067,13 @@ deserialize_slots_kernel(const uint8_t* __restrict__ wire, uint64_t wire_size, c
             src = s0 + d.header_size;
             key = d.mask ? d.mask_key : 0u;
         }
+        odd = st != CFWS_PARSE_COMPLETE || d.header_size + d.payload_size != stride;
         if (f == n - 1 && user_total) {
             const uint64_t t = n * slot;
             *user_total = t < capacity ? t : capacity;
         }
     }
+    if (mismatch) count_mismatch(mismatch, odd, threadIdx.x & 63u);
     fused_item<kSlotUnroll>(wire, out, capacity, run, src, len, nb, key, threadIdx.x & 63u);
 }
 
@@ -1659,7 +1677,7 @@ namespace {
 int slots_impl(const void* d_wire, uint64_t wire_size, const uint64_t* d_index, const uint64_t* dst, size_t n,
                uint64_t max_payload, uint64_t slot, cfws_frame_desc_t* d_desc, int32_t* d_status,
                void* d_payload, uint64_t cap, uint64_t* d_total, void* stream, bool scatter, const char* what,
-               cfws_frame_info_t* d_info = nullptr)
+               cfws_frame_info_t* d_info = nullptr, uint64_t stride = 0, uint32_t* d_mismatch = nullptr)
 {
     if (int rc = check_init()) return rc;
     if (slot < 16 || (slot & 15) || slot > (1ull << 31))
@@ -1673,7 +1691,8 @@ int slots_impl(const void* d_wire, uint64_t wire_size, const uint64_t* d_index, 
         return CFWS_OK;
     }
     const bool info = d_info != nullptr;
-    if (!d_wire || !d_index || (!info && (!d_desc || !d_status)) || (cap && !d_payload) || (scatter && !dst))
+    if (!d_wire || (!d_index && !stride) || (!info && (!d_desc || !d_status)) || (cap && !d_payload) ||
+        (scatter && !dst))
         return set_err(CFWS_ERROR_INVALID_ARGUMENT, "null pointer", hipSuccess);
     if (misaligned(d_payload, d_wire))
         return set_err(CFWS_ERROR_INVALID_ARGUMENT, "arenas must be 16-byte aligned", hipSuccess);
@@ -1703,19 +1722,24 @@ int slots_impl(const void* d_wire, uint64_t wire_size, const uint64_t* d_index, 
             constexpr bool kIn = decltype(compact)::value;
             if (S == 8)
                 deserialize_slots_window_kernel<CFWS_SLOT_ROUNDS8, 8, kSc, kIn><<<grid, kThreads, 0, st>>>(
-                    w, wire_size, d_index, n, max_payload, slot, G, d_desc, d_status, out, cap, d_total, dst, d_info);
+                    w, wire_size, d_index, n, max_payload, slot, G, d_desc, d_status, out, cap, d_total, dst, d_info,
+                    stride, d_mismatch);
             else if (S == 4)
                 deserialize_slots_window_kernel<CFWS_SLOT_ROUNDS4, 4, kSc, kIn><<<grid, kThreads, 0, st>>>(
-                    w, wire_size, d_index, n, max_payload, slot, G, d_desc, d_status, out, cap, d_total, dst, d_info);
+                    w, wire_size, d_index, n, max_payload, slot, G, d_desc, d_status, out, cap, d_total, dst, d_info,
+                    stride, d_mismatch);
             else if (S == 2)
                 deserialize_slots_window_kernel<CFWS_SLOT_ROUNDS2, 2, kSc, kIn><<<grid, kThreads, 0, st>>>(
-                    w, wire_size, d_index, n, max_payload, slot, G, d_desc, d_status, out, cap, d_total, dst, d_info);
+                    w, wire_size, d_index, n, max_payload, slot, G, d_desc, d_status, out, cap, d_total, dst, d_info,
+                    stride, d_mismatch);
             else if (P > 1)
                 deserialize_slots_window_kernel<CFWS_SLOT_ROUNDS_MULTI, 1, kSc, kIn><<<grid, kThreads, 0, st>>>(
-                    w, wire_size, d_index, n, max_payload, slot, G, d_desc, d_status, out, cap, d_total, dst, d_info);
+                    w, wire_size, d_index, n, max_payload, slot, G, d_desc, d_status, out, cap, d_total, dst, d_info,
+                    stride, d_mismatch);
             else
                 deserialize_slots_window_kernel<CFWS_SLOT_ROUNDS, 1, kSc, kIn><<<grid, kThreads, 0, st>>>(
-                    w, wire_size, d_index, n, max_payload, slot, G, d_desc, d_status, out, cap, d_total, dst, d_info);
+                    w, wire_size, d_index, n, max_payload, slot, G, d_desc, d_status, out, cap, d_total, dst, d_info,
+                    stride, d_mismatch);
         };
         // the scatter form as its own instantiation: its per-round offset
         // shuffle, as a run-time branch in one kernel, cost the 1 KiB slot
@@ -1732,7 +1756,8 @@ int slots_impl(const void* d_wire, uint64_t wire_size, const uint64_t* d_index, 
         auto one = [&](auto scatter, auto compact) {
             deserialize_slots_kernel<decltype(scatter)::value, decltype(compact)::value>
                 <<<grid_for(n, kThreads), kThreads, 0, st>>>(w, wire_size, d_index, n, max_payload, slot, d_desc,
-                                                             d_status, out, cap, d_total, dst, d_info);
+                                                             d_status, out, cap, d_total, dst, d_info, stride,
+                                                             d_mismatch);
         };
         if (scatter && info)
             one(std::true_type{}, std::true_type{});
@@ -1787,6 +1812,21 @@ int cfws_deserialize_scatter_info(const void* d_wire, uint64_t wire_size, const 
     if (!d_info && n) return set_err(CFWS_ERROR_INVALID_ARGUMENT, "null pointer", hipSuccess);
     return slots_impl(d_wire, wire_size, d_index, d_payload_off, n, max_payload, max_slot, nullptr, nullptr,
                       d_payload, cap, nullptr, stream, true, "deserialize_scatter_info", d_info);
+}
+
+int cfws_deserialize_slots_uniform(const void* d_wire, uint64_t wire_size, size_t n, uint64_t stride,
+                                   uint64_t max_payload, uint64_t slot, cfws_frame_info_t* d_info, void* d_payload,
+                                   uint64_t cap, uint64_t* d_total, uint32_t* d_mismatch, void* stream)
+{
+    const CfwsPassScope pass_scope;
+    if (int rc = check_init()) return rc;
+    if (stride < 2 || (n && stride > (1ull << 63) / n))
+        return set_err(CFWS_ERROR_INVALID_ARGUMENT, "frame stride must be >= 2 and n * stride < 2^63", hipSuccess);
+    if (!d_info && n) return set_err(CFWS_ERROR_INVALID_ARGUMENT, "null pointer", hipSuccess);
+    if (d_mismatch && hipMemsetAsync(d_mismatch, 0, sizeof(uint32_t), static_cast<hipStream_t>(stream)) != hipSuccess)
+        return launch_check("deserialize_slots_uniform");
+    return slots_impl(d_wire, wire_size, nullptr, nullptr, n, max_payload, slot, nullptr, nullptr, d_payload, cap,
+                      d_total, stream, false, "deserialize_slots_uniform", d_info, stride, d_mismatch);
 }
 
 #if CFWS_PLAN_TRACE

@@ -11,7 +11,8 @@
  *                 (each payload to a buffer of its own size, last frame first)
  *   uniform batch: n frames of 256 B through cfws_serialize_uniform (payload
  *                 + one key per frame, no descriptors) and back through
- *                 cfws_deserialize_slots_info (8-byte records)
+ *                 cfws_deserialize_slots_uniform (frame i at i * its wire
+ *                 bytes, no index; 8-byte records and a mismatch count)
  *
  * Checks that every payload comes back and that the wire equals what
  * sequential co_ws_frame_serialize calls (the drop-in, same library) append
@@ -204,25 +205,24 @@ int main(int argc, char** argv)
     srandom(4242);
     for (size_t i = 0; i < n; ++i)
         if (!co_ws_frame_serialize(true, CO_WS_OPCODE_BINARY, true, upay + i * U, U, &uref)) return 1;
-    void *d_upay, *d_ukeys, *d_uwire, *d_uback, *d_uinfo, *d_ustarts;
+    void *d_upay, *d_ukeys, *d_uwire, *d_uback, *d_uinfo, *d_umis;
     CHECK(hipMalloc(&d_upay, n * U));
     CHECK(hipMalloc(&d_ukeys, n * sizeof *ukeys));
     CHECK(hipMalloc(&d_uwire, n * UW + 16));
     CHECK(hipMalloc(&d_uback, n * U));
     CHECK(hipMalloc(&d_uinfo, n * sizeof(cfws_frame_info_t)));
-    CHECK(hipMalloc(&d_ustarts, n * 8));
-    uint64_t* ustarts = malloc(n * 8);
-    for (size_t i = 0; i < n; ++i) ustarts[i] = i * UW;
+    CHECK(hipMalloc(&d_umis, sizeof(uint32_t)));
     CHECK(hipMemcpyAsync(d_upay, upay, n * U, hipMemcpyHostToDevice, st));
     CHECK(hipMemcpyAsync(d_ukeys, ukeys, n * sizeof *ukeys, hipMemcpyHostToDevice, st));
-    CHECK(hipMemcpyAsync(d_ustarts, ustarts, n * 8, hipMemcpyHostToDevice, st));
     CHECK(cfws_serialize_uniform(d_upay, (const uint32_t*)d_ukeys, n, U, 1, CO_WS_OPCODE_BINARY, 1, d_uwire,
                                  n * UW + 16, d_total, st));
-    CHECK(cfws_deserialize_slots_info(d_uwire, n * UW, (const uint64_t*)d_ustarts, n,
-                                      CFWS_DEFAULT_MAX_RECEIVE_PAYLOAD_SIZE, U, (cfws_frame_info_t*)d_uinfo,
-                                      d_uback, n * U, NULL, st));
+    CHECK(cfws_deserialize_slots_uniform(d_uwire, n * UW, n, UW, CFWS_DEFAULT_MAX_RECEIVE_PAYLOAD_SIZE, U,
+                                         (cfws_frame_info_t*)d_uinfo, d_uback, n * U, NULL, (uint32_t*)d_umis,
+                                         st));
     uint64_t utotal = 0;
+    uint32_t umis = 1;
     CHECK(hipMemcpyAsync(&utotal, d_total, 8, hipMemcpyDeviceToHost, st));
+    CHECK(hipMemcpyAsync(&umis, d_umis, 4, hipMemcpyDeviceToHost, st));
     CHECK(hipStreamSynchronize(st));
     uint8_t* uwire = malloc(n * UW);
     uint8_t* uback = malloc(n * U);
@@ -230,8 +230,8 @@ int main(int argc, char** argv)
     CHECK(hipMemcpy(uwire, d_uwire, n * UW, hipMemcpyDeviceToHost));
     CHECK(hipMemcpy(uback, d_uback, n * U, hipMemcpyDeviceToHost));
     CHECK(hipMemcpy(uinfo, d_uinfo, n * sizeof *uinfo, hipMemcpyDeviceToHost));
-    int uniform_ok = utotal == n * UW && uref.count == n * UW && memcmp(uwire, uref.buffer, n * UW) == 0 &&
-                     memcmp(uback, upay, n * U) == 0;
+    int uniform_ok = utotal == n * UW && umis == 0 && uref.count == n * UW &&
+                     memcmp(uwire, uref.buffer, n * UW) == 0 && memcmp(uback, upay, n * U) == 0;
     for (size_t i = 0; uniform_ok && i < n; ++i)
         uniform_ok = uinfo[i].status == CFWS_PARSE_COMPLETE && uinfo[i].payload_size == U && uinfo[i].fin == 1 &&
                      uinfo[i].opcode == CO_WS_OPCODE_BINARY;

@@ -206,6 +206,25 @@ int cfws_deserialize_scatter_info(const void* d_wire, uint64_t wire_size,
                                   cfws_frame_info_t* d_info, void* d_payload,
                                   uint64_t payload_capacity, void* stream);
 
+/* ---- slot receive of a uniform stream ------------------------------------
+ * cfws_deserialize_slots_info with the index implicit: frame i is parsed at
+ * i * frame_stride, as if d_frame_index[i] = i * frame_stride (the wire
+ * cfws_serialize_uniform writes, frame_stride its header + payload bytes).
+ * Same decisions, same d_info, payload and total as that indexed call; no
+ * index is read. *d_mismatch (may be NULL; the call zeroes it first) = the
+ * frames that are not COMPLETE frames of exactly frame_stride wire bytes.
+ * Zero means each frame i parsed COMPLETE and ends where frame i + 1 starts:
+ * the reference's receive loop (src/ws/co_ws_server.c:107-169 calling
+ * co_ws_frame_deserialize, src/ws/co_ws_frame.c:129-247) would have taken
+ * the same n frames from the start of the wire. Non-zero: the stream is not
+ * uniform there; index it (cfws_index_frames_batch) and use the indexed
+ * receive. frame_stride >= 2, n_frames * frame_stride < 2^63. */
+int cfws_deserialize_slots_uniform(const void* d_wire, uint64_t wire_size, size_t n_frames,
+                                   uint64_t frame_stride, uint64_t max_payload, uint64_t slot_bytes,
+                                   cfws_frame_info_t* d_info, void* d_payload,
+                                   uint64_t payload_capacity, uint64_t* d_payload_total,
+                                   uint32_t* d_mismatch, void* stream);
+
 /* ---- deserialize, each payload to the caller's offset ---------------------
  * cfws_deserialize_slots with payload_off = d_payload_off[i] (the caller's
  * own buffer for each frame, as the reference allocates one per frame,

@@ -114,3 +114,122 @@ def test_uniform_empty_and_arguments():
         cfws.serialize_uniform(pay, None, 1, (1 << 31) + 1, wire, mask=False)
     with pytest.raises(cfws.CodecError):                   # misaligned wire
         cfws.serialize_uniform(pay, None, 2, 10, wire[1:], mask=False)
+
+
+# ---- the receive of a uniform stream (cfws_deserialize_slots_uniform) ------
+# Frame i parsed at i * stride with no index: the expectation is the slot
+# receive's (test_gpu_slots.expect_slots, the oracle's packed receive with the
+# slot rule) over the index i * stride, the indexed info form on the same
+# buffers, and the mismatch count of frames that are not COMPLETE frames of
+# exactly `stride` bytes.
+
+def _recv(wire, wire_size, n, stride, slot, cap=None, max_payload=O.DEFAULT_MAX_PAYLOAD, count=True):
+    from test_gpu_slots import expect_slots
+    cap = n * slot if cap is None else cap
+    buf = np.full(W.round16(max(wire_size, 1)) + 32, SENT, np.uint8)
+    buf[:wire_size] = wire[:wire_size]
+    w = torch.from_numpy(buf).cuda()
+    out = torch.full((W.round16(max(cap, 1)) + 32,), SENT, dtype=torch.uint8, device="cuda")
+    out2 = torch.full_like(out, SENT)
+    info = torch.full((max(n, 1), 8), SENT, dtype=torch.uint8, device="cuda")
+    info2 = torch.full_like(info, SENT)
+    mm = torch.full((1,), 12345, dtype=torch.int32, device="cuda") if count else None
+    _, tot = cfws.deserialize_slots_uniform(w, wire_size, n, stride, out, slot, info, mismatch_t=mm,
+                                            max_payload=max_payload, payload_capacity=cap)
+    starts = np.arange(n, dtype=np.uint64) * np.uint64(stride)
+    if n:
+        idx = torch.from_numpy(starts.view(np.int64)).cuda()
+        _, tot2 = cfws.deserialize_slots_info(w, wire_size, idx, out2, slot, info2, max_payload=max_payload,
+                                              payload_capacity=cap)
+    torch.cuda.synchronize()
+    e_arena, e_d, e_st, e_tot = expect_slots(wire, wire_size, starts, slot, cap, max_payload)
+    assert int(tot.item()) == e_tot
+    fi = info.cpu().numpy()[:n].reshape(-1).view(cfws.INFO_DTYPE)
+    st = fi["status"].astype(np.int32)
+    bad = np.nonzero(st != e_st)[0]
+    assert bad.size == 0, f"{bad.size} statuses differ, first {[(int(i), int(st[i]), int(e_st[i])) for i in bad[:6]]}"
+    assert np.array_equal(fi["payload_size"], np.minimum(e_d["payload_size"], np.uint64(0xFFFFFFFF)).astype(np.uint32))
+    ok = e_st == O.PARSE_COMPLETE
+    assert np.array_equal(fi["opcode"], e_d["opcode"]) and np.array_equal(fi["fin"][ok], e_d["fin"][ok])
+    got = out.cpu().numpy()
+    lim = W.round16(max(cap, 1))
+    bad = np.nonzero(got[:lim] != e_arena)[0]
+    assert bad.size == 0, f"{bad.size} arena bytes differ, first at {bad[:8]} (cap {cap})"
+    assert (got[lim:] == SENT).all()
+    if n:
+        assert torch.equal(out, out2) and torch.equal(info, info2), "differs from the indexed info receive"
+        assert int(tot2.item()) == e_tot
+    odd = ~ok | (e_d["header_size"].astype(np.uint64) + e_d["payload_size"] != np.uint64(stride))
+    if count:
+        assert int(mm.item()) == int(odd.sum())
+    return e_st, int(odd.sum())
+
+
+@pytest.mark.parametrize("fs", [0, 1, 15, 16, 100, 125, 126, 240, 256, 512, 1000, 1024, 4064, 4096, 8160, 8161,
+                                65535, 65536, 200_003])
+@pytest.mark.parametrize("mask", [1, 0])
+def test_uniform_receive_sizes(fs, mask):
+    """The wire cfws_serialize_uniform writes, received with stride W into
+    slots of round16(fs): every frame COMPLETE, no mismatch, the payload
+    back; window kernels up to 8,160-byte slots, the per-frame kernel past."""
+    n = max(3, min(4000, (6 << 20) // (fs + 14)))
+    payload, keys, d = _frames(n, fs, mask, 1, 2, fs)
+    wire, _ = O.serialize_batch(payload, d)
+    stride = cfws.uniform_frame_bytes(fs, bool(mask))
+    slot = max(16, W.round16(fs))
+    st, odd = _recv(wire, len(wire), n, stride, slot)
+    assert (st == O.PARSE_COMPLETE).all() and odd == 0
+
+
+@pytest.mark.parametrize("stride", [2, 37, 262, 1000, 9001])
+def test_uniform_receive_non_uniform_wire(stride):
+    """A mixed batch (30-80 B frames, a 5,000-byte one every 97th) read at a
+    fixed stride: frames land anywhere in headers and payloads -- invalid
+    frames, MORE_DATA, OOM -- and the mismatch count says so."""
+    from test_gpu_guard import _seed21_batch
+    payload, desc = _seed21_batch(27)
+    wire, _ = O.serialize_batch(payload, desc.view(O.DESC_DTYPE))
+    n = min(len(desc), len(wire) // stride + 3)
+    for slot in (96, 5008):
+        _, odd = _recv(wire, len(wire), n, stride, slot)
+        assert odd > 0
+    _recv(wire, len(wire), n, stride, 96, max_payload=60)
+
+
+def test_uniform_receive_truncated_and_cut():
+    """The wire ends inside the last frames (MORE_DATA), slots too small for
+    the payloads (OOM), capacities inside slots: each such frame counts."""
+    n, fs = 3000, 256
+    payload, keys, d = _frames(n, fs, 1, 1, 2, 9)
+    wire, _ = O.serialize_batch(payload, d)
+    stride = cfws.uniform_frame_bytes(fs, True)
+    for cut, lost in ((len(wire) - 5, 1), (len(wire) - 3 * stride, 3), ((n - 10) * stride + 1, 10), (0, n)):
+        st, odd = _recv(wire, cut, n, stride, 256)
+        assert odd == lost and st[-1] == O.PARSE_MORE_DATA
+    _, odd = _recv(wire, len(wire), n, stride, 240)
+    assert odd == n
+    for cap in (n * 256 // 2 + 5, n * 256 - 3, 17, 0):
+        _, odd = _recv(wire, len(wire), n, stride, 256, cap=cap)
+        assert odd == n - min(cap, n * 256) // 256
+    _recv(wire, len(wire), n, stride, 256, count=False)
+
+
+def test_uniform_receive_arguments():
+    w = torch.zeros(64, dtype=torch.uint8, device="cuda")
+    out = torch.zeros(64, dtype=torch.uint8, device="cuda")
+    info = torch.zeros((4, 8), dtype=torch.uint8, device="cuda")
+    for stride in (0, 1):
+        with pytest.raises(cfws.CodecError):
+            cfws.deserialize_slots_uniform(w, 64, 4, stride, out, 16, info)
+    with pytest.raises(cfws.CodecError):                   # n * stride past 2^63
+        cfws.deserialize_slots_uniform(w, 64, 4, 1 << 62, out, 16, info)
+    with pytest.raises(cfws.CodecError):                   # slot not a multiple of 16
+        cfws.deserialize_slots_uniform(w, 64, 4, 20, out, 24, info)
+    rc = cfws.lib().cfws_deserialize_slots_uniform(cfws._p(w), 64, 4, 20, 1 << 20, 16, None, cfws._p(out), 64,
+                                                   None, None, cfws._stream(None))
+    assert rc == cfws.ERROR_INVALID_ARGUMENT                # no info entries
+    mm = torch.full((1,), 7, dtype=torch.int32, device="cuda")
+    tot = torch.full((1,), 7, dtype=torch.int64, device="cuda")
+    cfws.deserialize_slots_uniform(w, 64, 0, 20, out, 16, info, total_t=tot, mismatch_t=mm)
+    torch.cuda.synchronize()
+    assert mm.item() == 0 and tot.item() == 0
