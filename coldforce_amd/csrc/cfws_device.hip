@@ -1090,6 +1090,16 @@ uint32_t slot_sub2_g()
     return v;
 }
 
+// The receive without an index (cfws_deserialize_slots_uniform) keeps one
+// frame per round there: with no index load ahead of the window loads, 8 M
+// x 512 B takes 1.50 ms at one sub-window against 1.62 at two
+// (profiles/r06/compact/implicit/). A/B knob.
+uint32_t slot_sub2_g_implicit()
+{
+    static const uint32_t v = (uint32_t)env_knob("CFWS_SLOT_SUB2_G_IMPLICIT", 65);
+    return v;
+}
+
 // The same for four sub-windows: frames of CFWS_SLOT_SUB4_G (default 129:
 // off) to 85 lanes, three to 256 virtual lanes (A/B knob)
 uint32_t slot_sub4_g()
@@ -1703,9 +1713,10 @@ int slots_impl(const void* d_wire, uint64_t wire_size, const uint64_t* d_index, 
         // one wave-iteration of R P frames per wave (CFWS_SLOT_GRID caps the
         // workgroups: a grid-stride loop; A/B knob)
         const uint32_t G = (uint32_t)(slot / 16 + 2);
+        const uint32_t sub2 = d_index ? slot_sub2_g() : slot_sub2_g_implicit();
         const uint32_t S = G > 256 ? 8
                            : G > 128 || (G >= slot_sub4_g() && 256 / G >= 3) ? 4
-                           : G > 64 || (G >= slot_sub2_g() && 128 / G >= 3) ? 2 : 1;   // sub-windows
+                           : G > 64 || (G >= sub2 && 128 / G >= 3) ? 2 : 1;   // sub-windows
         const uint32_t P = 64 * S / G;
         const uint64_t RK = S == 8 ? CFWS_SLOT_ROUNDS8 : S == 4 ? CFWS_SLOT_ROUNDS4 : S == 2 ? CFWS_SLOT_ROUNDS2
                             : P > 1 ? CFWS_SLOT_ROUNDS_MULTI : CFWS_SLOT_ROUNDS;
