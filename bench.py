@@ -31,6 +31,7 @@ import argparse
 import json
 import math
 import os
+import statistics
 import sys
 import time
 
@@ -328,16 +329,19 @@ def bench_h2(args, rank, world, dev):
         torch.distributed.barrier()
     local = time.perf_counter() - t0
     elapsed = shard.max_over_ranks(local, dev)
-    send_ms = sum(e[0].elapsed_time(e[1]) for e in events) / args.steps
-    recv_ms = sum(e[2].elapsed_time(e[3]) for e in events) / args.steps
+    send_each = [e[0].elapsed_time(e[1]) for e in events]
+    recv_each = [e[2].elapsed_time(e[3]) for e in events]
+    send_ms, recv_ms = sum(send_each) / args.steps, sum(recv_each) / args.steps
     del events
     # algorithmic bytes per pass: read the payload n, write n plus every
     # header (WS + DATA) on the send; the receive reads what the send wrote
     # past the headers and writes n -- 2n + headers either way
     alg = F * fs + h2_total
     kern = {"h2_serialize_pass": {"kernel": "xform_kernel<3>", "ms": round(send_ms, 4),
+                                  "median_ms": round(statistics.median(send_each), 4),
                                   "GBps": round(alg / (send_ms * 1e-3) / 1e9, 1)},
             "h2_deserialize_pass": {"kernel": "xform_kernel<1>", "ms": round(recv_ms, 4),
+                                    "median_ms": round(statistics.median(recv_each), 4),
                                     "GBps": round(alg / (recv_ms * 1e-3) / 1e9, 1)}}
     dom = "h2_serialize_pass" if send_ms >= recv_ms else "h2_deserialize_pass"
     dom_ms = max(send_ms, recv_ms)
@@ -961,15 +965,18 @@ def main():
     copy_gbps = copy_rate(lambda: cfws.device_copy(payload, back, n_copy))
     torch_copy_gbps = copy_rate(lambda: back[:payload.numel()].copy_(payload))
 
-    ser_ms = sum(e[0].elapsed_time(e[1]) for e in events) / args.steps
-    de_ms = sum(e[2].elapsed_time(e[3]) for e in events) / args.steps
+    ser_each = [e[0].elapsed_time(e[1]) for e in events]
+    de_each = [e[2].elapsed_time(e[3]) for e in events]
+    ser_ms, de_ms = sum(ser_each) / args.steps, sum(de_each) / args.steps
     del events                               # HIP events freed while the runtime is up
     hdr = int(wire_total - arena_bytes)
     alg_bytes = 2 * arena_bytes + hdr       # read n + write n (+ headers) per launch
+    # ms: the mean over the timed steps (what rocprof's average compares
+    # with; roofline.achieved uses it), median_ms: SURVEY.md §8(d)'s median
     kern = {
-        "serialize_execute": {"ms": round(ser_ms, 4),
+        "serialize_execute": {"ms": round(ser_ms, 4), "median_ms": round(statistics.median(ser_each), 4),
                               "GBps": round(alg_bytes / (ser_ms * 1e-3) / 1e9, 1)},
-        "deserialize_execute": {"ms": round(de_ms, 4),
+        "deserialize_execute": {"ms": round(de_ms, 4), "median_ms": round(statistics.median(de_each), 4),
                                 "GBps": round(alg_bytes / (de_ms * 1e-3) / 1e9, 1)},
     }
     dom_name = "serialize_execute" if ser_ms >= de_ms else "deserialize_execute"
