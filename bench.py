@@ -838,7 +838,10 @@ def main():
         cfws.fill_splitmix(payload, PAYLOAD_SEED, byte_base)
     offs, wire_total = W.wire_layout(desc_np)
     wire = torch.empty(W.round16(wire_total), dtype=torch.uint8, device=dev)
-    back = torch.empty(payload.numel() + 64, dtype=torch.uint8, device=dev)
+    # config2 frames of a size that is not a multiple of 16: the packed
+    # receive (align 16) places payload i at i * round16(fs)
+    pstride = W.round16(fs) if args.workload == "config2" else fs
+    back = torch.empty(payload.numel() + F * (pstride - fs) + 64, dtype=torch.uint8, device=dev)
     desc_ser = cfws.desc_to_device(desc_np, dev)
     desc_de = torch.empty((F, 32), dtype=torch.uint8, device=dev)
     status = torch.empty(F, dtype=torch.int32, device=dev)
@@ -940,6 +943,10 @@ def main():
         verified = (int(tot_ser.item()) == wire_total and bool((status == 0).all().item())
                     and torch.equal(got.reshape(-1), payload[:arena_bytes]))
         del got
+    elif pstride != fs and not slot:
+        verified = (int(tot_ser.item()) == wire_total and int(tot_de.item()) == F * pstride
+                    and bool((status == 0).all().item())
+                    and torch.equal(back[:F * pstride].view(F, pstride)[:, :fs], payload[:arena_bytes].view(F, fs)))
     else:
         verified = (int(tot_ser.item()) == wire_total and int(tot_de.item()) == arena_bytes
                     and bool((status == 0).all().item())

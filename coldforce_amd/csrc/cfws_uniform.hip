@@ -80,6 +80,19 @@ __device__ __forceinline__ void uniform_store(uint8_t* __restrict__ out, Rsrc rs
     }
 }
 
+// Source blocks through a buffer resource whose base is the wave's first
+// frame's payload: a block that is not wanted gets an offset past the
+// resource's range and reads as zeros without a memory access, so every load
+// of the span is issued unconditionally. With a branch around a load, the
+// join made the compiler wait for all loads in flight after each round
+// (s_waitcnt vmcnt(0) for a register copy), serialising the rounds.
+constexpr uint32_t kNoLoad = 0x7ffffff0u;
+__device__ __forceinline__ uint4 src_ld16(__amdgpu_buffer_rsrc_t rs, uint32_t off)
+{
+    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)off, 0, 0);
+    return make_uint4(v[0], v[1], v[2], v[3]);
+}
+
 // A header chunk: chunk byte 0 is byte `off` of frame f (f + 1 may start in
 // the chunk at byte t = W - off). Loads issued by header_prep, bytes by
 // header_finish.
@@ -304,18 +317,10 @@ serialize_uniform_small_kernel(UniformFrames U, uint8_t* __restrict__ out, uint6
     const uint32_t rel0 = (uint32_t)(D0 - F0 * U.W);
     const uint64_t src0 = F0 * U.fs;
     const auto rs = __builtin_amdgcn_make_buffer_rsrc(out + D0, 0, (int)kUniformSpan, 0x00020000);
+    // payload source from frame F0's first byte (16-aligned: fs % 16 == 0)
+    const auto srs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(U.src + src0), 0, (int)kNoLoad,
+                                                       0x00020000);
     const uint32_t hs = U.hs, W = U.W;
-    // the span's keys: frames F0 .. F0 + 127 (W >= 38: at most 110 frames meet a 4 KiB span)
-    uint32_t kl0 = 0, kl1 = 0;
-    if (U.keys) {
-        if (F0 + lane < U.n) kl0 = U.keys[F0 + lane];
-        if (F0 + 64 + lane < U.n) kl1 = U.keys[F0 + 64 + lane];
-    }
-    auto key_of = [&](uint32_t j) {          // frame F0 + j's key, j < 128 (every lane active)
-        const uint32_t a = (uint32_t)__shfl((int)kl0, (int)(j & 63u), 64);
-        const uint32_t b = (uint32_t)__shfl((int)kl1, (int)(j & 63u), 64);
-        return j < 64 ? a : b;
-    };
     uint32_t q[kUniformUnroll], off[kUniformUnroll], ph[kUniformUnroll];
     bool fast[kUniformUnroll], tail[kUniformUnroll], live[kUniformUnroll];
     uint4 A[kUniformUnroll], B[kUniformUnroll];
@@ -331,27 +336,39 @@ serialize_uniform_small_kernel(UniformFrames U, uint8_t* __restrict__ out, uint6
         fast[u] = off[u] >= hs && off[u] + 16u <= W;
         tail[u] = !fast[u] && off[u] >= hs;                  // f's body, then f + 1's header
         ph[u] = (off[u] - hs) & 15u;
-        A[u] = B[u] = z;
-        if (live[u] && (fast[u] || tail[u])) {
-            const uint8_t* sp = U.src + ((src0 + uint64_t(q[u]) * U.fs + (off[u] - hs)) & ~uint64_t(15));
-            A[u] = ld16(sp);
-            // the second block when the chunk's own bytes reach into it (with
-            // CFWS_UNIFORM_DPP_B, a body chunk followed by a chunk of the same
-            // body takes it from that chunk's lane instead)
-            const bool from_next = CFWS_UNIFORM_DPP_B && fast[u] && off[u] + 16u < W &&
-                                   !(lane == 63 && u == kUniformUnroll - 1);
-            if (ph[u] && !from_next && (fast[u] || ph[u] + (W - off[u]) > 16u)) B[u] = ld16(sp + 16);
-        }
+        const bool ld = live[u] && (fast[u] || tail[u]);
+        const uint32_t so = (q[u] * (uint32_t)U.fs + (off[u] - hs)) & ~15u;   // < W + 4 KiB
+        A[u] = src_ld16(srs, ld ? so : kNoLoad);
+        // the second block when the chunk's own bytes reach into it (with
+        // CFWS_UNIFORM_DPP_B, a body chunk followed by a chunk of the same
+        // body takes it from that chunk's lane instead)
+        const bool from_next = CFWS_UNIFORM_DPP_B && fast[u] && off[u] + 16u < W &&
+                               !(lane == 63 && u == kUniformUnroll - 1);
+        const bool needB = ld && ph[u] && !from_next && (fast[u] || ph[u] + (W - off[u]) > 16u);
+        B[u] = src_ld16(srs, needB ? so + 16u : kNoLoad);
     }
     // lane 63's last chunk takes a body head from the next span's first
     // chunk: loaded here (the first block of that frame's payload)
-    uint4 hx = z;
+    uint4 hx;
     {
         constexpr int u = kUniformUnroll - 1;
         const bool head = live[u] && !fast[u] && (off[u] < hs ? 16u > hs - off[u] : W - off[u] + hs < 16u) &&
                           (off[u] < hs || F0 + q[u] + 1 < U.n);
-        if (lane == 63 && head) hx = ld16(U.src + (src0 + uint64_t(q[u] + (off[u] < hs ? 0u : 1u)) * U.fs));
+        hx = src_ld16(srs, lane == 63 && head ? (q[u] + (off[u] < hs ? 0u : 1u)) * (uint32_t)U.fs : kNoLoad);
     }
+    // the span's keys, after the payload loads: frames F0 .. F0 + 127 (W >=
+    // 38: at most 110 frames meet a 4 KiB span); keys null: a resource of no
+    // bytes, zeros
+    const auto krs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(U.keys ? U.keys + F0 : U.keys), 0,
+                                                       U.keys ? (int)(U.n - F0 < 128 ? 4 * (U.n - F0) : 512) : 0,
+                                                       0x00020000);
+    const uint32_t kl0 = __builtin_amdgcn_raw_buffer_load_b32(krs, (int)(4 * lane), 0, 0);
+    const uint32_t kl1 = __builtin_amdgcn_raw_buffer_load_b32(krs, (int)(4 * (64 + lane)), 0, 0);
+    auto key_of = [&](uint32_t j) {          // frame F0 + j's key, j < 128 (every lane active)
+        const uint32_t a = (uint32_t)__shfl((int)kl0, (int)(j & 63u), 64);
+        const uint32_t b = (uint32_t)__shfl((int)kl1, (int)(j & 63u), 64);
+        return j < 64 ? a : b;
+    };
 #pragma unroll
     for (int u = 0; u < kUniformUnroll; ++u) {
         const uint4 nextA = u + 1 < kUniformUnroll ? readlane4(A[u + 1 < kUniformUnroll ? u + 1 : u], 0) : hx;
