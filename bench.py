@@ -680,9 +680,19 @@ def spawn_ranks(args) -> int:
     127.0.0.1). Rank 0 prints the one JSON line; the exit status is the
     first failing rank's. If a rank fails, the others (blocked in a
     bookkeeping barrier) are given 30 s and then killed by PID."""
+    import signal
     import subprocess
     port = _free_port()
     procs = []
+
+    def stop(signum, frame):
+        # a launcher that signals this process (a time limit) ends the ranks too
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+        sys.exit(128 + signum)
+    signal.signal(signal.SIGTERM, stop)
+    signal.signal(signal.SIGINT, stop)
     for r in range(args.gpus):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
                    LOCAL_WORLD_SIZE=str(args.gpus), GROUP_RANK="0", MASTER_ADDR="127.0.0.1",

@@ -61,3 +61,34 @@ def test_spawned_ranks_fail_loudly_without_gpus():
     assert p.returncode != 0
     assert p.stdout.strip() == ""
     assert "has no GPU" in p.stderr
+
+
+def test_signalled_launcher_ends_its_ranks():
+    """A time limit that signals the launching process (SIGTERM) ends the
+    ranks it started as well: none is left running."""
+    import signal
+    import time
+
+    import psutil
+    env = dict(os.environ)
+    for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT", "CFWS_BENCH_LAUNCHER"):
+        env.pop(k, None)
+    p = subprocess.Popen([sys.executable, BENCH, "--gpus", "2", "--dry-run", "--steps", "100000", "--warmup", "0",
+                          "--frames", "65536"], cwd=ROOT, env=env, stdout=subprocess.DEVNULL,
+                         stderr=subprocess.DEVNULL)
+    try:
+        kids = []
+        for _ in range(300):
+            kids = psutil.Process(p.pid).children()
+            if len(kids) == 2:
+                break
+            time.sleep(0.1)
+        assert len(kids) == 2
+        time.sleep(1.0)
+        p.send_signal(signal.SIGTERM)
+        assert p.wait(timeout=60) == 128 + signal.SIGTERM
+        gone, alive = psutil.wait_procs(kids, timeout=30)
+        assert not alive
+    finally:
+        if p.poll() is None:
+            p.kill()
