@@ -999,7 +999,8 @@ def main():
     dom_name = "serialize_execute" if ser_ms >= de_ms else "deserialize_execute"
     dom_ms = max(ser_ms, de_ms)
     achieved = alg_bytes / (dom_ms * 1e-3) / 1e9
-    kernel_symbol = (("serialize_uniform_kernel" if uniform else "xform_kernel<0>")
+    kernel_symbol = ((cfws.lib().cfws_serialize_uniform_pass_kernel(fs, 1).decode() if uniform
+                      else "xform_kernel<0>")
                      if dom_name == "serialize_execute"
                      else "deserialize_slots_window_kernel" if 0 < slot <= 8160  # fixed slots
                      else "deserialize_slots_kernel" if slot

@@ -456,6 +456,33 @@ __global__ void uniform_total_kernel(uint64_t* __restrict__ user_total, uint64_t
 
 }  // namespace
 
+namespace {
+
+// the kernel a uniform batch takes (cfws_serialize_uniform and
+// cfws_serialize_uniform_pass_kernel)
+enum UniformRoute { kUniformSmall, kUniformGeneral, kUniformBytes };
+UniformRoute uniform_route(uint64_t fs, uint64_t W)
+{
+    if (fs >= 32 && fs <= 65535 && fs % 16 == 0) return kUniformSmall;
+    return W >= 32 ? kUniformGeneral : kUniformBytes;
+}
+
+uint32_t uniform_header_size(uint64_t fs, bool mask)
+{
+    return 2u + (fs > 65535u ? 8u : (fs > 125u ? 2u : 0u)) + (mask ? 4u : 0u);
+}
+
+}  // namespace
+
+extern "C" const char* cfws_serialize_uniform_pass_kernel(uint64_t fs, uint8_t mask)
+{
+    switch (uniform_route(fs, uniform_header_size(fs, mask) + fs)) {
+    case kUniformSmall: return "serialize_uniform_small_kernel";
+    case kUniformGeneral: return "serialize_uniform_kernel";
+    default: return "serialize_uniform_bytes_kernel";
+    }
+}
+
 extern "C" int cfws_serialize_uniform(const void* d_payload, const uint32_t* d_keys, size_t n, uint64_t fs,
                                       uint8_t fin, uint8_t opcode, uint8_t mask, void* d_wire, uint64_t cap,
                                       uint64_t* d_total, void* stream)
@@ -463,7 +490,7 @@ extern "C" int cfws_serialize_uniform(const void* d_payload, const uint32_t* d_k
     const CfwsPassScope pass_scope;
     if (int rc = check_init()) return rc;
     if (fs > (1ull << 30)) return set_err(CFWS_ERROR_INVALID_ARGUMENT, "payload_size > 2^30", hipSuccess);
-    const uint32_t hs = 2u + (fs > 65535u ? 8u : (fs > 125u ? 2u : 0u)) + (mask ? 4u : 0u);
+    const uint32_t hs = uniform_header_size(fs, mask);
     const uint64_t W = hs + fs;
     if (n > (uint64_t(1) << 40) / W) return set_err(CFWS_ERROR_INVALID_ARGUMENT, "batch over 2^40 wire bytes",
                                                     hipSuccess);
@@ -492,14 +519,15 @@ extern "C" int cfws_serialize_uniform(const void* d_payload, const uint32_t* d_k
     U.invW = 1.0 / (double)W;
     const uint64_t lim = total < cap ? total : cap;
     const CfwsPassTimer timer(st);
-    if (fs >= 32 && fs <= 65535 && fs % 16 == 0) {
+    const UniformRoute route = uniform_route(fs, W);
+    if (route == kUniformSmall) {
         const uint64_t waves = (lim + kUniformSpan - 1) / kUniformSpan;
         const uint64_t blocks = (waves + kWaves - 1) / kWaves;
         if (blocks > 0x7fffffffull) return set_err(CFWS_ERROR_INVALID_ARGUMENT, "batch too large", hipSuccess);
         static const uint32_t lds = (uint32_t)env_knob("CFWS_UNIFORM_LDS", 0);   // residency cap (A/B knob)
         serialize_uniform_small_kernel<<<(uint32_t)blocks, kThreads, lds, st>>>(U, static_cast<uint8_t*>(d_wire), cap,
                                                                                d_total);
-    } else if (W >= 32) {
+    } else if (route == kUniformGeneral) {
         const uint64_t waves = (lim + kUniformSpan - 1) / kUniformSpan;
         const uint64_t blocks = (waves + kWaves - 1) / kWaves;
         if (blocks > 0x7fffffffull) return set_err(CFWS_ERROR_INVALID_ARGUMENT, "batch too large", hipSuccess);

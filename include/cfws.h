@@ -590,6 +590,13 @@ int cfws_time_next_pass(void* start, void* stop);
 const char* cfws_deserialize_pass_kernel(size_t n_frames, uint64_t wire_size, uint32_t align,
                                          uint32_t flags, uint64_t payload_capacity);
 
+/* The kernel cfws_serialize_uniform launches for frames of payload_size
+ * bytes (masked or not): "serialize_uniform_small_kernel" (payloads of
+ * 32-65,535 bytes, multiples of 16), "serialize_uniform_kernel" (other
+ * frames of at least 32 wire bytes) or "serialize_uniform_bytes_kernel".
+ * The call's own rule. A static string. */
+const char* cfws_serialize_uniform_pass_kernel(uint64_t payload_size, uint8_t mask);
+
 /* ---- synthetic input (bench / tests) -------------------------------------
  * d_dst[i] = byte ((byte_base + i) % 8) of splitmix64 output number
  * (byte_base + i) / 8 for `seed`; byte_base must be a multiple of 8. */

@@ -190,3 +190,16 @@ def test_deserialize_pass_kernel_routes():
     assert f(65536, 65536 * 65550, 16, 0, 1 << 32).decode() == "xform_kernel<1>"           # large frames
     assert f(16 << 20, (16 << 20) * 264, 16, cfws.DESERIALIZE_REASSEMBLE, 1 << 33).decode() == "xform_kernel<1>"
     assert f(0, 0, 16, 0, 0).decode() == "xform_kernel<1>"
+
+
+def test_serialize_uniform_pass_kernel_routes():
+    """cfws_serialize_uniform_pass_kernel names the kernel
+    cfws_serialize_uniform launches (host only; bench.py's roofline name)."""
+    from coldforce_amd import cfws
+    f = cfws.lib().cfws_serialize_uniform_pass_kernel
+    for fs in (32, 256, 4096, 65520):
+        assert f(fs, 1).decode() == "serialize_uniform_small_kernel"
+    for fs, mask in ((65536, 1), (1000, 1), (4100, 0), (30, 1), (26, 1)):        # W >= 32
+        assert f(fs, mask).decode() == "serialize_uniform_kernel", (fs, mask)
+    for fs, mask in ((0, 1), (16, 1), (25, 1), (29, 0)):                        # W < 32
+        assert f(fs, mask).decode() == "serialize_uniform_bytes_kernel", (fs, mask)
