@@ -12,22 +12,23 @@
 // traffic at 256 B) and writes wire_off back into it.
 //
 // Each wave owns kUniformSpan bytes of wire (aligned 16-byte chunks, every
-// wire byte written once) in two phases:
-//  * body: lane l takes chunks l, l + 64, ... of the span; a chunk inside
-//    one payload is one or two aligned source loads, a funnel shift and the
-//    key XOR. Its frame comes from a multiply by a 32-bit reciprocal of W
-//    (host-computed) and one correction, relative to the wave's first frame.
-//  * headers: the chunks the body phase skipped are exactly the chunks that
-//    hold header bytes (frames of W >= 32 bytes: a chunk meets at most one
-//    header), one or two per frame; they are handed out one per lane --
-//    frame fr of the span to lanes 2 fr and 2 fr + 1 -- so a span of 16
-//    frames assembles its ~31 header chunks in one pass of that code rather
-//    than in every round of the body phase. Each holds the end of one
-//    payload, a header, and the start of the next payload: one source
-//    window (the two payload pieces are contiguous in the source), two keys.
-// All loads of both phases are issued before either computes.
-// Frames of W < 32 bytes (payloads up to 17-29 bytes) take a byte-wise
-// kernel.
+// wire byte written once); a chunk's frame comes from a multiply by a 32-bit
+// reciprocal of W (host-computed) and one correction, relative to the wave's
+// first frame. Three kernels, by frame size (uniform_route):
+//  * serialize_uniform_small_kernel, payloads of 32-65,535 bytes that are
+//    multiples of 16 (headers of at most 8 bytes, every payload 16-aligned in
+//    the source): every chunk of the span -- body or header -- in one store
+//    round, a header chunk assembled in registers from its own source blocks,
+//    the frame's key and the next chunk's first block (over DPP); every load
+//    issued before any computes (comment at the kernel).
+//  * serialize_uniform_kernel, any other frame of at least 32 wire bytes, in
+//    two phases: body chunks (one or two aligned source loads, a funnel shift
+//    and the key XOR), then the chunks the body phase skipped -- exactly the
+//    chunks that hold header bytes, one or two per frame -- handed out one
+//    per lane (frame fr of the span to lanes 2 fr and 2 fr + 1), each the end
+//    of one payload, a header and the start of the next payload.
+//  * serialize_uniform_bytes_kernel, frames of under 32 wire bytes (payloads
+//    up to 17-29 bytes): byte by byte.
 #include "cfws_kernels.h"
 
 namespace {
