@@ -47,7 +47,7 @@ assert INFO_DTYPE.itemsize == 8
 # Every function include/*.h declares (tests check the exports against the
 # headers themselves).
 BATCH_SYMBOLS = (
-    "cfws_init", "cfws_init_device", "cfws_device_copy", "cfws_time_next_pass", "cfws_deserialize_pass_kernel", "cfws_serialize_uniform_pass_kernel", "cfws_bind_thread_device", "cfws_thread_device", "cfws_last_error", "cfws_version", "cfws_workspace_size",
+    "cfws_init", "cfws_init_device", "cfws_device_copy", "cfws_time_next_pass", "cfws_deserialize_pass_kernel", "cfws_serialize_uniform_pass_kernel", "cfws_deserialize_slots_pass_kernel", "cfws_bind_thread_device", "cfws_thread_device", "cfws_last_error", "cfws_version", "cfws_workspace_size",
     "cfws_serialize_plan", "cfws_serialize_execute", "cfws_serialize_batch", "cfws_serialize_uniform",
     "cfws_deserialize_plan", "cfws_deserialize_execute", "cfws_deserialize_batch",
     "cfws_deserialize_slots", "cfws_deserialize_scatter", "cfws_deserialize_slots_info",
@@ -154,6 +154,7 @@ def lib(path: str = LIB_PATH) -> C.CDLL:
         "cfws_time_next_pass": ([_vp, _vp], C.c_int),
         "cfws_deserialize_pass_kernel": ([_sz, _u64, _u32, _u32, _u64], C.c_char_p),
         "cfws_serialize_uniform_pass_kernel": ([_u64, C.c_uint8], C.c_char_p),
+        "cfws_deserialize_slots_pass_kernel": ([_u64], C.c_char_p),
         "cfws_bind_thread_device": ([C.c_int], C.c_int),
         "cfws_thread_device": ([], C.c_int),
         "cfws_set_dropin_gpu_min": ([_sz], None),

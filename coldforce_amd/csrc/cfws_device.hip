@@ -1077,6 +1077,102 @@ deserialize_slots_kernel(const uint8_t* __restrict__ wire, uint64_t wire_size, c
     fused_item<kSlotUnroll>(wire, out, capacity, run, src, len, nb, key, threadIdx.x & 63u);
 }
 
+// Slots over kSlotWindow8Max, piece by piece: wave w copies piece w % pieces
+// (kSlotPiece bytes of slot) of frame w / pieces, so a 64 KiB frame is 32
+// waves' work and a launch has n x pieces waves. The per-frame kernel above
+// gives each wave the 64 frames its lanes parsed, one after another: 1,024
+// waves for 64 K frames, one per SIMD. Every wave of a frame parses its
+// header (one line, the same address in every lane); piece 0's lane 0 writes
+// the frame's descriptor + status or info entry and counts a mismatch.
+// 64 K x 64 KiB receive (profiles/r06/compact/slot_pieces/): per-frame
+// kernel 1.59-1.64 ms; pieces of 8 / 4 / 2 / 1 KiB 1.51-1.60 / 1.42-1.49 /
+// 1.35-1.36 / 2.13 ms; 2 KiB with write-through stores 1.31-1.32 (8 KiB
+// frames 1.38, against 1.51-1.64).
+#ifndef CFWS_SLOT_PIECE_AUX
+#define CFWS_SLOT_PIECE_AUX 19        // write-through (sc0 sc1 nt), as the WS receive; 0: the global nt store
+#endif
+#ifndef CFWS_SLOT_PIECE_UNROLL
+#define CFWS_SLOT_PIECE_UNROLL 2
+#endif
+constexpr int kSlotPieceUnroll = CFWS_SLOT_PIECE_UNROLL;            // rounds of loads in flight per wave
+constexpr uint64_t kSlotPiece = 64ull * 16 * kSlotPieceUnroll;     // 2 KiB
+template <bool kScatter, bool kInfo>
+__global__ void __launch_bounds__(kThreads)
+deserialize_slots_piece_kernel(const uint8_t* __restrict__ wire, uint64_t wire_size,
+                               const uint64_t* __restrict__ index, uint64_t n, uint64_t max_payload, uint64_t slot,
+                               cfws_frame_desc_t* __restrict__ desc, int32_t* __restrict__ status,
+                               uint8_t* __restrict__ out, uint64_t capacity, uint64_t* __restrict__ user_total,
+                               const uint64_t* __restrict__ dst, cfws_frame_info_t* __restrict__ info,
+                               uint64_t stride, uint32_t* __restrict__ mismatch, uint64_t pieces)
+{
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const uint4 z = make_uint4(0, 0, 0, 0);
+    const uint64_t waves = n * pieces;
+    for (uint64_t w = uint64_t(blockIdx.x) * kWaves + wv; w < waves; w += uint64_t(gridDim.x) * kWaves) {
+        const uint64_t f = w / pieces, piece = w - f * pieces;
+        cfws_frame_desc_t d;
+        const uint64_t s0 = index ? index[f] : f * stride;
+        const uint64_t run = kScatter ? dst[f] : f * slot;
+        const int32_t p = parse_ws_header(wire, wire_size, s0, max_payload, d);
+        const int32_t st = kScatter ? scatter_rule(p, run, d.payload_size, slot, capacity)
+                                    : slot_rule(p, run, d.payload_size, slot, capacity);
+        if (piece == 0 && lane == 0) {
+            if constexpr (kInfo)
+                slot_info(info, f, d, st);
+            else
+                slot_desc(desc, status, f, run, d, st);
+            if (f == n - 1 && user_total) {
+                const uint64_t t = n * slot;
+                *user_total = t < capacity ? t : capacity;
+            }
+            if (mismatch && (st != CFWS_PARSE_COMPLETE || d.header_size + d.payload_size != stride))
+                atomicAdd(mismatch, 1u);
+        }
+        if (st != CFWS_PARSE_COMPLETE) continue;             // wave-uniform: every lane parsed the same frame
+        const uint64_t len = d.payload_size;                 // <= slot <= 2^31
+        const uint64_t nb = (len + 15) & ~uint64_t(15);
+        const uint64_t c0 = piece * kSlotPiece;
+        if (c0 >= nb) continue;
+        const uint64_t src = s0 + d.header_size;
+        const uint32_t key = d.mask ? d.mask_key : 0u;
+        const uint32_t ph = (uint32_t)(src & 15u);
+        const auto prs = __builtin_amdgcn_make_buffer_rsrc(out + run + c0, 0, (int)kSlotPiece, 0x00020000);
+        uint4 A[kSlotPieceUnroll], E[kSlotPieceUnroll];
+        uint32_t need[kSlotPieceUnroll];
+        bool nl[kSlotPieceUnroll];
+#pragma unroll
+        for (int u = 0; u < kSlotPieceUnroll; ++u) {
+            const uint64_t k0 = c0 + (uint64_t)u * 1024 + 16 * lane;
+            need[u] = k0 < len ? (uint32_t)(len - k0 < 16 ? len - k0 : 16) : 0u;
+            nl[u] = lane != 63 && k0 + 16 < len;                 // the next lane loads the next block
+            const uint64_t s = src + k0;
+            A[u] = need[u] ? ld16(wire + (s & ~uint64_t(15))) : z;
+            E[u] = need[u] && ph && !nl[u] && ph + need[u] > 16 ? ld16(wire + (s & ~uint64_t(15)) + 16) : z;
+        }
+#pragma unroll
+        for (int u = 0; u < kSlotPieceUnroll; ++u) {
+            const uint4 nb4 = from_next_lane(A[u], E[u]);       // every lane: DPP needs the full wave
+            const uint64_t k0 = c0 + (uint64_t)u * 1024 + 16 * lane;
+            if (k0 >= nb) continue;
+            uint4 o = z;
+            if (need[u]) {
+                o = ph ? funnel16(A[u], nl[u] ? nb4 : E[u], ph) : A[u];
+                xor4(o, key);
+                if (need[u] < 16) o = and4(o, byte_range(0, need[u]));
+            }
+            if (CFWS_SLOT_PIECE_AUX != 0 && run + k0 + 16 <= capacity) {
+                // a buffer store over the wave's piece (cache policy CFWS_SLOT_PIECE_AUX)
+                const u32x4 v = {o.x, o.y, o.z, o.w};
+                __builtin_amdgcn_raw_buffer_store_b128(v, prs, (int)(k0 - c0), 0, CFWS_SLOT_PIECE_AUX);
+            } else {
+                fused_store(out, run + k0, capacity, o);
+            }
+        }
+    }
+}
+
+
 // Frames of at least CFWS_SLOT_SUB2_G lanes (default 33: slots of 496
 // bytes and more) that fit three to a 128-lane pair of sub-windows (up to
 // 42 lanes: slots up to 640 bytes) pack two sub-windows per round instead of
@@ -1112,6 +1208,23 @@ bool slots_window()
 {
     static const bool v = env_knob("CFWS_SLOTS_WINDOW", 1) != 0;
     return v;
+}
+
+bool slots_piece()
+{
+    static const bool v = env_knob("CFWS_SLOTS_PIECE", 1) != 0;
+    return v;
+}
+
+// the kernel a slot / scatter receive takes (slots_impl and
+// cfws_deserialize_slots_pass_kernel): windows up to kSlotWindow8Max-byte
+// slots, pieces past that (A/B knobs: CFWS_SLOTS_WINDOW=0, CFWS_SLOTS_PIECE=0
+// fall back to the per-frame kernel)
+enum SlotsRoute { kSlotsWindow, kSlotsPiece, kSlotsPerFrame };
+SlotsRoute slots_route(uint64_t slot)
+{
+    if (slot <= kSlotWindow8Max && slots_window()) return kSlotsWindow;
+    return slots_piece() ? kSlotsPiece : kSlotsPerFrame;
 }
 
 // Single-pass plans above kSelfScanBlocks blocks (CFWS_PLAN_SINGLE=0: the
@@ -1709,7 +1822,8 @@ int slots_impl(const void* d_wire, uint64_t wire_size, const uint64_t* d_index, 
     const uint8_t* w = static_cast<const uint8_t*>(d_wire);
     uint8_t* out = static_cast<uint8_t*>(d_payload);
     const CfwsPassTimer timer(st);
-    if (slot <= kSlotWindow8Max && slots_window()) {
+    const SlotsRoute route = slots_route(slot);
+    if (route == kSlotsWindow) {
         // one wave-iteration of R P frames per wave (CFWS_SLOT_GRID caps the
         // workgroups: a grid-stride loop; A/B knob)
         const uint32_t G = (uint32_t)(slot / 16 + 2);
@@ -1763,6 +1877,24 @@ int slots_impl(const void* d_wire, uint64_t wire_size, const uint64_t* d_index, 
             window(std::false_type{}, std::true_type{});
         else
             window(std::false_type{}, std::false_type{});
+    } else if (route == kSlotsPiece) {
+        const uint64_t pieces = (slot + kSlotPiece - 1) / kSlotPiece;
+        const uint64_t waves = n * pieces;
+        const uint64_t want = (waves + kWaves - 1) / kWaves;
+        const uint32_t grid = (uint32_t)(want < (1u << 22) ? want : (1u << 22));   // a grid-stride loop past that
+        auto piecewise = [&](auto scatter, auto compact) {
+            deserialize_slots_piece_kernel<decltype(scatter)::value, decltype(compact)::value>
+                <<<grid, kThreads, 0, st>>>(w, wire_size, d_index, n, max_payload, slot, d_desc, d_status, out, cap,
+                                            d_total, dst, d_info, stride, d_mismatch, pieces);
+        };
+        if (scatter && info)
+            piecewise(std::true_type{}, std::true_type{});
+        else if (scatter)
+            piecewise(std::true_type{}, std::false_type{});
+        else if (info)
+            piecewise(std::false_type{}, std::true_type{});
+        else
+            piecewise(std::false_type{}, std::false_type{});
     } else {
         auto one = [&](auto scatter, auto compact) {
             deserialize_slots_kernel<decltype(scatter)::value, decltype(compact)::value>
@@ -1838,6 +1970,15 @@ int cfws_deserialize_slots_uniform(const void* d_wire, uint64_t wire_size, size_
         return launch_check("deserialize_slots_uniform");
     return slots_impl(d_wire, wire_size, nullptr, nullptr, n, max_payload, slot, nullptr, nullptr, d_payload, cap,
                       d_total, stream, false, "deserialize_slots_uniform", d_info, stride, d_mismatch);
+}
+
+const char* cfws_deserialize_slots_pass_kernel(uint64_t slot)
+{
+    switch (slots_route(slot)) {
+    case kSlotsWindow: return "deserialize_slots_window_kernel";
+    case kSlotsPiece: return "deserialize_slots_piece_kernel";
+    default: return "deserialize_slots_kernel";
+    }
 }
 
 #if CFWS_PLAN_TRACE

@@ -590,6 +590,13 @@ int cfws_time_next_pass(void* start, void* stop);
 const char* cfws_deserialize_pass_kernel(size_t n_frames, uint64_t wire_size, uint32_t align,
                                          uint32_t flags, uint64_t payload_capacity);
 
+/* The kernel the slot / scatter receives (cfws_deserialize_slots*,
+ * cfws_deserialize_scatter*) launch for slots (max_slot) of this many bytes:
+ * "deserialize_slots_window_kernel" (up to 8,160 bytes) or
+ * "deserialize_slots_piece_kernel" (longer: one wave per 2 KiB piece of a
+ * frame's slot). The calls' own rule. A static string. */
+const char* cfws_deserialize_slots_pass_kernel(uint64_t slot_bytes);
+
 /* The kernel cfws_serialize_uniform launches for frames of payload_size
  * bytes (masked or not): "serialize_uniform_small_kernel" (payloads of
  * 32-65,535 bytes, multiples of 16), "serialize_uniform_kernel" (other

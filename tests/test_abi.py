@@ -203,3 +203,13 @@ def test_serialize_uniform_pass_kernel_routes():
         assert f(fs, mask).decode() == "serialize_uniform_kernel", (fs, mask)
     for fs, mask in ((0, 1), (16, 1), (25, 1), (29, 0)):                        # W < 32
         assert f(fs, mask).decode() == "serialize_uniform_bytes_kernel", (fs, mask)
+
+
+def test_deserialize_slots_pass_kernel_routes():
+    """cfws_deserialize_slots_pass_kernel names the slot receives' kernel."""
+    from coldforce_amd import cfws
+    f = cfws.lib().cfws_deserialize_slots_pass_kernel
+    for slot in (16, 256, 4064, 8160):
+        assert f(slot).decode() == "deserialize_slots_window_kernel"
+    for slot in (8176, 65536, 1 << 31):
+        assert f(slot).decode() == "deserialize_slots_piece_kernel"
