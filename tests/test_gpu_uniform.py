@@ -190,7 +190,7 @@ def test_uniform_receive_non_uniform_wire(stride):
     payload, desc = _seed21_batch(27)
     wire, _ = O.serialize_batch(payload, desc.view(O.DESC_DTYPE))
     n = min(len(desc), len(wire) // stride + 3)
-    for slot in (96, 5008):
+    for slot in (96, 5008, 9008):                       # window kernels; pieces past 8,160 B
         _, odd = _recv(wire, len(wire), n, stride, slot)
         assert odd > 0
     _recv(wire, len(wire), n, stride, 96, max_payload=60)
@@ -211,6 +211,9 @@ def test_uniform_receive_truncated_and_cut():
     for cap in (n * 256 // 2 + 5, n * 256 - 3, 17, 0):
         _, odd = _recv(wire, len(wire), n, stride, 256, cap=cap)
         assert odd == n - min(cap, n * 256) // 256
+    for cut in (len(wire) - 5, (n - 10) * stride + 1):        # the piece kernel (slots over 8,160 B)
+        _, odd = _recv(wire, cut, n, stride, 8192)
+        assert odd == (1 if cut == len(wire) - 5 else 10)
     _recv(wire, len(wire), n, stride, 256, count=False)
 
 
