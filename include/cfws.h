@@ -592,9 +592,11 @@ const char* cfws_deserialize_pass_kernel(size_t n_frames, uint64_t wire_size, ui
 
 /* The kernel the slot / scatter receives (cfws_deserialize_slots*,
  * cfws_deserialize_scatter*) launch for slots (max_slot) of this many bytes:
- * "deserialize_slots_window_kernel" (up to 8,160 bytes) or
- * "deserialize_slots_piece_kernel" (longer: one wave per 2 KiB piece of a
- * frame's slot). The calls' own rule. A static string. */
+ * "deserialize_slots_piece_kernel" (one wave per 2 KiB piece of a frame's
+ * slot: slots over 8,160 bytes, and from 2 KiB those that are multiples of
+ * 128 filling at least 85 % of their pieces) or
+ * "deserialize_slots_window_kernel" (the rest). The calls' own rule. A
+ * static string. */
 const char* cfws_deserialize_slots_pass_kernel(uint64_t slot_bytes);
 
 /* The kernel cfws_serialize_uniform launches for frames of payload_size

@@ -209,7 +209,7 @@ def test_deserialize_slots_pass_kernel_routes():
     """cfws_deserialize_slots_pass_kernel names the slot receives' kernel."""
     from coldforce_amd import cfws
     f = cfws.lib().cfws_deserialize_slots_pass_kernel
-    for slot in (16, 256, 4064, 8160):
-        assert f(slot).decode() == "deserialize_slots_window_kernel"
-    for slot in (8176, 65536, 1 << 31):
-        assert f(slot).decode() == "deserialize_slots_piece_kernel"
+    for slot in (16, 256, 1024, 2560, 3072, 4064, 5120, 8160):
+        assert f(slot).decode() == "deserialize_slots_window_kernel", slot
+    for slot in (2048, 3584, 4096, 6144, 7680, 8176, 65536, 1 << 31):   # pieces >= 85 % used, on 128-B lines
+        assert f(slot).decode() == "deserialize_slots_piece_kernel", slot
