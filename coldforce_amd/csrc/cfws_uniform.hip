@@ -11,8 +11,8 @@
 // descriptor per frame in its plan and again in its execute (14 % more read
 // traffic at 256 B) and writes wire_off back into it.
 //
-// Each wave owns kUniformSpan bytes of wire (aligned 16-byte chunks, every
-// wire byte written once); a chunk's frame comes from a multiply by a 32-bit
+// Each wave owns a span of wire (4 KiB in the small kernel, 2 KiB in the
+// general one; aligned 16-byte chunks, every wire byte written once); a chunk's frame comes from a multiply by a 32-bit
 // reciprocal of W (host-computed) and one correction, relative to the wave's
 // first frame. Three kernels, by frame size (uniform_route):
 //  * serialize_uniform_small_kernel, payloads of 32-65,535 bytes that are
@@ -38,6 +38,14 @@ namespace {
 #endif
 constexpr int kUniformUnroll = CFWS_UNIFORM_UNROLL;               // body chunks per lane
 constexpr uint32_t kUniformSpan = 64u * 16u * kUniformUnroll;    // wire bytes per wave
+// serialize_uniform_kernel's own (2 KiB spans: 4,100 B frames 1.70 -> 1.51
+// ms, 1,000 B 1.83 -> 1.75, 64 KiB 1.455 -> 1.44; the small kernel lost 2 %
+// at 256 B with them, profiles/r06/compact/uniform_general/spans.txt)
+#ifndef CFWS_UNIFORM_GEN_UNROLL
+#define CFWS_UNIFORM_GEN_UNROLL 2
+#endif
+constexpr int kGenUnroll = CFWS_UNIFORM_GEN_UNROLL;
+constexpr uint32_t kGenSpan = 64u * 16u * kGenUnroll;
 #ifndef CFWS_UNIFORM_STORE_AUX
 #define CFWS_UNIFORM_STORE_AUX 19                                 // write-through, as the WS send (st16_region)
 #endif
@@ -169,7 +177,7 @@ __device__ __forceinline__ uint4 header_finish(const UniformFrames& U, uint64_t 
 __device__ __forceinline__ bool body_next_of(uint32_t hs, uint32_t W, int u, uint32_t lane, uint32_t off, uint64_t D,
                                              uint64_t lim)
 {
-    return off + 32u <= W && off + 16u >= hs && D + 16 < lim && !(lane == 63 && u == kUniformUnroll - 1);
+    return off + 32u <= W && off + 16u >= hs && D + 16 < lim && !(lane == 63 && u == kGenUnroll - 1);
 }
 
 __global__ void __launch_bounds__(kThreads)
@@ -179,7 +187,7 @@ serialize_uniform_kernel(UniformFrames U, uint8_t* __restrict__ out, uint64_t ca
     // wave-uniform values in scalar registers
     const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const uint64_t wave = uint64_t(blockIdx.x) * kWaves + wv;
-    const uint64_t D0 = wave * kUniformSpan;
+    const uint64_t D0 = wave * kGenSpan;
     const uint64_t lim = U.total < cap ? U.total : cap;
     if (wave == 0 && lane == 0 && user_total) *user_total = U.total;
     if (D0 >= lim) return;
@@ -192,7 +200,7 @@ serialize_uniform_kernel(UniformFrames U, uint8_t* __restrict__ out, uint64_t ca
     const uint64_t base = F0 * U.W;                           // <= D0
     const uint32_t rel0 = (uint32_t)(D0 - base);              // < W
     const uint64_t src0 = F0 * U.fs;
-    const auto rs = __builtin_amdgcn_make_buffer_rsrc(out + D0, 0, (int)kUniformSpan, 0x00020000);
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc(out + D0, 0, (int)kGenSpan, 0x00020000);
 
     // frames whose header meets the span: fa .. fb (fb may be n: the chunk
     // holding the batch's end past the last payload is handled as frame n's)
@@ -200,16 +208,16 @@ serialize_uniform_kernel(UniformFrames U, uint8_t* __restrict__ out, uint64_t ca
         return body_next_of(U.hs, U.W, u, ln, o, D, lm);
     };
     const uint64_t fa = (base + U.hs > D0) ? F0 : F0 + 1;
-    uint64_t fb = F0 + div_w(U, rel0 + kUniformSpan - 1);
+    uint64_t fb = F0 + div_w(U, rel0 + kGenSpan - 1);
     if (fb > U.n) fb = U.n;
     const uint32_t n_hdr = fa <= fb ? 2u * (uint32_t)(fb - fa + 1) : 0u;
 
     // ---- issue every load: body chunks, then the first 64 header chunks
-    uint32_t q[kUniformUnroll], off[kUniformUnroll], key[kUniformUnroll];
-    bool body[kUniformUnroll];
-    uint4 A[kUniformUnroll], B[kUniformUnroll];
+    uint32_t q[kGenUnroll], off[kGenUnroll], key[kGenUnroll];
+    bool body[kGenUnroll];
+    uint4 A[kGenUnroll], B[kGenUnroll];
 #pragma unroll
-    for (int u = 0; u < kUniformUnroll; ++u) {
+    for (int u = 0; u < kGenUnroll; ++u) {
         const uint32_t r = rel0 + 16u * (64u * u + lane);
         q[u] = div_w(U, r);
         off[u] = r - q[u] * U.W;
@@ -226,10 +234,10 @@ serialize_uniform_kernel(UniformFrames U, uint8_t* __restrict__ out, uint64_t ca
             key[u] = U.keys ? U.keys[F0 + q[u]] : 0u;
         }
     }
-    uint4 N[kUniformUnroll];
+    uint4 N[kGenUnroll];
 #pragma unroll
-    for (int u = 0; u < kUniformUnroll; ++u)          // every lane: DPP needs the full wave
-        N[u] = from_next_lane(A[u], u + 1 < kUniformUnroll ? readlane4(A[u + 1 < kUniformUnroll ? u + 1 : u], 0)
+    for (int u = 0; u < kGenUnroll; ++u)          // every lane: DPP needs the full wave
+        N[u] = from_next_lane(A[u], u + 1 < kGenUnroll ? readlane4(A[u + 1 < kGenUnroll ? u + 1 : u], 0)
                                                            : make_uint4(0, 0, 0, 0));
     HeaderChunk h;
     uint64_t hD = 0, hf = 0;
@@ -244,7 +252,7 @@ serialize_uniform_kernel(UniformFrames U, uint8_t* __restrict__ out, uint64_t ca
         const uint64_t c1 = hstart >> 4, c2 = (hstart + U.hs - 1) >> 4;
         if ((idx & 1u) && c2 == c1) return;
         hD = ((idx & 1u) ? c2 : c1) << 4;
-        if (hD < D0 || hD >= D0 + kUniformSpan || hD >= lim) return;
+        if (hD < D0 || hD >= D0 + kGenSpan || hD >= lim) return;
         hf = hD >= hstart ? fr : fr - 1;
         hoff = (uint32_t)(hD - hf * U.W);
         hown = true;
@@ -254,7 +262,7 @@ serialize_uniform_kernel(UniformFrames U, uint8_t* __restrict__ out, uint64_t ca
 
     // ---- body chunks
 #pragma unroll
-    for (int u = 0; u < kUniformUnroll; ++u) {
+    for (int u = 0; u < kGenUnroll; ++u) {
         if (!body[u]) continue;
         const uint32_t ph = (uint32_t)((src0 + uint64_t(q[u]) * U.fs + (off[u] - U.hs)) & 15u);
         const bool nb = body_next(u, lane, off[u], D0 + 16ull * (64u * u + lane), lim);
@@ -529,7 +537,7 @@ extern "C" int cfws_serialize_uniform(const void* d_payload, const uint32_t* d_k
         serialize_uniform_small_kernel<<<(uint32_t)blocks, kThreads, lds, st>>>(U, static_cast<uint8_t*>(d_wire), cap,
                                                                                d_total);
     } else if (route == kUniformGeneral) {
-        const uint64_t waves = (lim + kUniformSpan - 1) / kUniformSpan;
+        const uint64_t waves = (lim + kGenSpan - 1) / kGenSpan;
         const uint64_t blocks = (waves + kWaves - 1) / kWaves;
         if (blocks > 0x7fffffffull) return set_err(CFWS_ERROR_INVALID_ARGUMENT, "batch too large", hipSuccess);
         // CFWS_UNIFORM_LDS: dynamic LDS per workgroup, a residency cap (A/B knob; 0 = none)
