@@ -33,14 +33,10 @@
 
 namespace {
 
-#ifndef CFWS_UNIFORM_UNROLL
-#define CFWS_UNIFORM_UNROLL 4
-#endif
-constexpr int kUniformUnroll = CFWS_UNIFORM_UNROLL;               // body chunks per lane
-constexpr uint32_t kUniformSpan = 64u * 16u * kUniformUnroll;    // wire bytes per wave
-// serialize_uniform_kernel's own (2 KiB spans: 4,100 B frames 1.70 -> 1.51
-// ms, 1,000 B 1.83 -> 1.75, 64 KiB 1.455 -> 1.44; the small kernel lost 2 %
-// at 256 B with them, profiles/r06/compact/uniform_general/spans.txt)
+// serialize_uniform_small_kernel<kU> spans kU KiB of wire per wave (4 or 2,
+// small_span); serialize_uniform_kernel 2 KiB (4,100 B frames 1.70 -> 1.51
+// ms, 1,000 B 1.83 -> 1.75, 64 KiB 1.455 -> 1.44 against 4 KiB;
+// profiles/r06/compact/uniform_general/spans.txt)
 #ifndef CFWS_UNIFORM_GEN_UNROLL
 #define CFWS_UNIFORM_GEN_UNROLL 2
 #endif
@@ -307,6 +303,7 @@ __device__ __forceinline__ uint4 shl16(uint4 v, uint32_t sh)
 #ifndef CFWS_UNIFORM_DPP_B
 #define CFWS_UNIFORM_DPP_B 1               // a body chunk's second block from the next lane: 256 B send 1.57 -> 1.53 ms (A/B knob)
 #endif
+template <int kU>
 __global__ void __launch_bounds__(kThreads, CFWS_UNIFORM_OCC)
 serialize_uniform_small_kernel(UniformFrames U, uint8_t* __restrict__ out, uint64_t cap,
                                uint64_t* __restrict__ user_total)
@@ -314,7 +311,7 @@ serialize_uniform_small_kernel(UniformFrames U, uint8_t* __restrict__ out, uint6
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const uint64_t wave = uint64_t(blockIdx.x) * kWaves + wv;
-    const uint64_t D0 = wave * kUniformSpan;
+    const uint64_t D0 = wave * (64u * 16u * kU);
     const uint64_t lim = U.total < cap ? U.total : cap;
     if (wave == 0 && lane == 0 && user_total) *user_total = U.total;
     if (D0 >= lim) return;
@@ -325,17 +322,17 @@ serialize_uniform_small_kernel(UniformFrames U, uint8_t* __restrict__ out, uint6
          (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(F0 >> 32)) << 32;
     const uint32_t rel0 = (uint32_t)(D0 - F0 * U.W);
     const uint64_t src0 = F0 * U.fs;
-    const auto rs = __builtin_amdgcn_make_buffer_rsrc(out + D0, 0, (int)kUniformSpan, 0x00020000);
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc(out + D0, 0, (int)(64u * 16u * kU), 0x00020000);
     // payload source from frame F0's first byte (16-aligned: fs % 16 == 0)
     const auto srs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(U.src + src0), 0, (int)kNoLoad,
                                                        0x00020000);
     const uint32_t hs = U.hs, W = U.W;
-    uint32_t q[kUniformUnroll], off[kUniformUnroll], ph[kUniformUnroll];
-    bool fast[kUniformUnroll], tail[kUniformUnroll], live[kUniformUnroll];
-    uint4 A[kUniformUnroll], B[kUniformUnroll];
+    uint32_t q[kU], off[kU], ph[kU];
+    bool fast[kU], tail[kU], live[kU];
+    uint4 A[kU], B[kU];
     const uint4 z = make_uint4(0, 0, 0, 0);
 #pragma unroll
-    for (int u = 0; u < kUniformUnroll; ++u) {
+    for (int u = 0; u < kU; ++u) {
         const uint32_t r = rel0 + 16u * (64u * u + lane);
         q[u] = div_w(U, r);
         off[u] = r - q[u] * W;
@@ -352,7 +349,7 @@ serialize_uniform_small_kernel(UniformFrames U, uint8_t* __restrict__ out, uint6
         // CFWS_UNIFORM_DPP_B, a body chunk followed by a chunk of the same
         // body takes it from that chunk's lane instead)
         const bool from_next = CFWS_UNIFORM_DPP_B && fast[u] && off[u] + 16u < W &&
-                               !(lane == 63 && u == kUniformUnroll - 1);
+                               !(lane == 63 && u == kU - 1);
         const bool needB = ld && ph[u] && !from_next && (fast[u] || ph[u] + (W - off[u]) > 16u);
         B[u] = src_ld16(srs, needB ? so + 16u : kNoLoad);
     }
@@ -360,7 +357,7 @@ serialize_uniform_small_kernel(UniformFrames U, uint8_t* __restrict__ out, uint6
     // chunk: loaded here (the first block of that frame's payload)
     uint4 hx;
     {
-        constexpr int u = kUniformUnroll - 1;
+        constexpr int u = kU - 1;
         const bool head = live[u] && !fast[u] && (off[u] < hs ? 16u > hs - off[u] : W - off[u] + hs < 16u) &&
                           (off[u] < hs || F0 + q[u] + 1 < U.n);
         hx = src_ld16(srs, lane == 63 && head ? (q[u] + (off[u] < hs ? 0u : 1u)) * (uint32_t)U.fs : kNoLoad);
@@ -379,15 +376,15 @@ serialize_uniform_small_kernel(UniformFrames U, uint8_t* __restrict__ out, uint6
         return j < 64 ? a : b;
     };
 #pragma unroll
-    for (int u = 0; u < kUniformUnroll; ++u) {
-        const uint4 nextA = u + 1 < kUniformUnroll ? readlane4(A[u + 1 < kUniformUnroll ? u + 1 : u], 0) : hx;
+    for (int u = 0; u < kU; ++u) {
+        const uint4 nextA = u + 1 < kU ? readlane4(A[u + 1 < kU ? u + 1 : u], 0) : hx;
         const uint4 N = from_next_lane(A[u], nextA);        // every lane: DPP needs the full wave
         const uint32_t kf = key_of(q[u]);
         const uint32_t kn = key_of(q[u] + 1);
         const uint64_t D = D0 + 16ull * (64u * u + lane);
         if (D >= lim) continue;
         const bool from_next = CFWS_UNIFORM_DPP_B && fast[u] && off[u] + 16u < W &&
-                               !(lane == 63 && u == kUniformUnroll - 1);
+                               !(lane == 63 && u == kU - 1);
         uint4 o = ph[u] ? funnel16(A[u], from_next ? N : B[u], ph[u]) : A[u];
         xor4(o, rotr8(kf, off[u] - hs));
         if (!fast[u]) {
@@ -476,6 +473,15 @@ UniformRoute uniform_route(uint64_t fs, uint64_t W)
     return W >= 32 ? kUniformGeneral : kUniformBytes;
 }
 
+// the small kernel's span per wave: 2 KiB from CFWS_UNIFORM_SPAN2_MIN-byte
+// payloads (1 / 4 KiB frames 2 / 4.5 % faster than at 4 KiB; 256 B 0.5 %
+// slower), 4 KiB below
+uint64_t small_span(uint64_t fs)
+{
+    static const uint64_t min2 = (uint64_t)env_knob("CFWS_UNIFORM_SPAN2_MIN", 1024);   // A/B knob
+    return fs >= min2 ? 2048 : 4096;
+}
+
 uint32_t uniform_header_size(uint64_t fs, bool mask)
 {
     return 2u + (fs > 65535u ? 8u : (fs > 125u ? 2u : 0u)) + (mask ? 4u : 0u);
@@ -530,12 +536,17 @@ extern "C" int cfws_serialize_uniform(const void* d_payload, const uint32_t* d_k
     const CfwsPassTimer timer(st);
     const UniformRoute route = uniform_route(fs, W);
     if (route == kUniformSmall) {
-        const uint64_t waves = (lim + kUniformSpan - 1) / kUniformSpan;
+        const uint64_t span = small_span(fs);
+        const uint64_t waves = (lim + span - 1) / span;
         const uint64_t blocks = (waves + kWaves - 1) / kWaves;
         if (blocks > 0x7fffffffull) return set_err(CFWS_ERROR_INVALID_ARGUMENT, "batch too large", hipSuccess);
         static const uint32_t lds = (uint32_t)env_knob("CFWS_UNIFORM_LDS", 0);   // residency cap (A/B knob)
-        serialize_uniform_small_kernel<<<(uint32_t)blocks, kThreads, lds, st>>>(U, static_cast<uint8_t*>(d_wire), cap,
-                                                                               d_total);
+        if (small_span(fs) == 2048)
+            serialize_uniform_small_kernel<2><<<(uint32_t)blocks, kThreads, lds, st>>>(
+                U, static_cast<uint8_t*>(d_wire), cap, d_total);
+        else
+            serialize_uniform_small_kernel<4><<<(uint32_t)blocks, kThreads, lds, st>>>(
+                U, static_cast<uint8_t*>(d_wire), cap, d_total);
     } else if (route == kUniformGeneral) {
         const uint64_t waves = (lim + kGenSpan - 1) / kGenSpan;
         const uint64_t blocks = (waves + kWaves - 1) / kWaves;
