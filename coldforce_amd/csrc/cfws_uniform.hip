@@ -551,8 +551,13 @@ extern "C" int cfws_serialize_uniform(const void* d_payload, const uint32_t* d_k
         const uint64_t waves = (lim + kGenSpan - 1) / kGenSpan;
         const uint64_t blocks = (waves + kWaves - 1) / kWaves;
         if (blocks > 0x7fffffffull) return set_err(CFWS_ERROR_INVALID_ARGUMENT, "batch too large", hipSuccess);
-        // CFWS_UNIFORM_LDS: dynamic LDS per workgroup, a residency cap (A/B knob; 0 = none)
-        static const uint32_t lds = (uint32_t)env_knob("CFWS_UNIFORM_LDS", 0);
+        // dynamic LDS per workgroup, a residency cap: frames of 32 KiB and
+        // more run at 5 workgroups per CU (64 / 128 KiB 1.44 -> 1.39 ms; 4 per
+        // CU 1.50; 16 KiB level; 1,000 / 4,100 B 21-30 % slower capped,
+        // profiles/r06/compact/uniform_general/lds.txt). CFWS_UNIFORM_LDS
+        // overrides (A/B knob; 0 = none).
+        static const int64_t lds_knob = env_knob("CFWS_UNIFORM_LDS", -1);
+        const uint32_t lds = lds_knob >= 0 ? (uint32_t)lds_knob : W >= 32768 ? 32000u : 0u;
         serialize_uniform_kernel<<<(uint32_t)blocks, kThreads, lds, st>>>(U, static_cast<uint8_t*>(d_wire), cap,
                                                                         d_total);
     } else {
