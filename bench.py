@@ -1002,7 +1002,7 @@ def main():
     kernel_symbol = ((cfws.lib().cfws_serialize_uniform_pass_kernel(fs, 1).decode() if uniform
                       else "xform_kernel<0>")
                      if dom_name == "serialize_execute"
-                     else cfws.lib().cfws_deserialize_slots_pass_kernel(slot).decode() if slot
+                     else cfws.lib().cfws_deserialize_slots_pass_kernel(F, wire_total, slot).decode() if slot
                      else recv_kernel if not flags else "xform_kernel<1>")
     # the PMC summary a traffic figure may come from: the same workload only
     traffic_key = (f"config2:{F}x{fs}" + (":uniform" if uniform else "")

@@ -154,7 +154,7 @@ def lib(path: str = LIB_PATH) -> C.CDLL:
         "cfws_time_next_pass": ([_vp, _vp], C.c_int),
         "cfws_deserialize_pass_kernel": ([_sz, _u64, _u32, _u32, _u64], C.c_char_p),
         "cfws_serialize_uniform_pass_kernel": ([_u64, C.c_uint8], C.c_char_p),
-        "cfws_deserialize_slots_pass_kernel": ([_u64], C.c_char_p),
+        "cfws_deserialize_slots_pass_kernel": ([_sz, _u64, _u64], C.c_char_p),
         "cfws_bind_thread_device": ([C.c_int], C.c_int),
         "cfws_thread_device": ([], C.c_int),
         "cfws_set_dropin_gpu_min": ([_sz], None),

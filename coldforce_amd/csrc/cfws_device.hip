@@ -1077,9 +1077,16 @@ deserialize_slots_kernel(const uint8_t* __restrict__ wire, uint64_t wire_size, c
     fused_item<kSlotUnroll>(wire, out, capacity, run, src, len, nb, key, threadIdx.x & 63u);
 }
 
-// Slots over kSlotWindow8Max, piece by piece: wave w copies piece w % pieces
-// (kSlotPiece bytes of slot) of frame w / pieces, so a 64 KiB frame is 32
-// waves' work and a launch has n x pieces waves. The per-frame kernel above
+// Slots over kSlotWindow8Max, piece by piece: wave w copies piece w % P of
+// frame w / P (kSlotPiece bytes of slot), so a 64 KiB frame is 32 waves'
+// work and a launch has n x P waves. P is the slot's piece count; when the
+// batch's frames are shorter on average (wire bytes / frames) P is that
+// average's piece count and each wave takes pieces w % P, w % P + P, ...
+// (kLoop), so a large slot holding short payloads does not cost a wave per
+// piece of the slot. Batches averaging under one piece per frame take the
+// per-frame kernel, which packs short frames into shared wave-instructions
+// (slots_route; tools/slot_sparse_probe.py: 1 M x 256 B in 16 KiB slots
+// 0.13 ms there against 0.59 one wave per frame). The per-frame kernel above
 // gives each wave the 64 frames its lanes parsed, one after another: 1,024
 // waves for 64 K frames, one per SIMD. Every wave of a frame parses its
 // header (one line, the same address in every lane); piece 0's lane 0 writes
@@ -1096,7 +1103,7 @@ deserialize_slots_kernel(const uint8_t* __restrict__ wire, uint64_t wire_size, c
 #endif
 constexpr int kSlotPieceUnroll = CFWS_SLOT_PIECE_UNROLL;            // rounds of loads in flight per wave
 constexpr uint64_t kSlotPiece = 64ull * 16 * kSlotPieceUnroll;     // 2 KiB
-template <bool kScatter, bool kInfo>
+template <bool kScatter, bool kInfo, bool kLoop>
 __global__ void __launch_bounds__(kThreads)
 deserialize_slots_piece_kernel(const uint8_t* __restrict__ wire, uint64_t wire_size,
                                const uint64_t* __restrict__ index, uint64_t n, uint64_t max_payload, uint64_t slot,
@@ -1132,46 +1139,49 @@ deserialize_slots_piece_kernel(const uint8_t* __restrict__ wire, uint64_t wire_s
         if (st != CFWS_PARSE_COMPLETE) continue;             // wave-uniform: every lane parsed the same frame
         const uint64_t len = d.payload_size;                 // <= slot <= 2^31
         const uint64_t nb = (len + 15) & ~uint64_t(15);
-        const uint64_t c0 = piece * kSlotPiece;
-        if (c0 >= nb) continue;
         const uint64_t src = s0 + d.header_size;
         const uint32_t key = d.mask ? d.mask_key : 0u;
         const uint32_t ph = (uint32_t)(src & 15u);
-        const auto prs = __builtin_amdgcn_make_buffer_rsrc(out + run + c0, 0, (int)kSlotPiece, 0x00020000);
-        uint4 A[kSlotPieceUnroll], E[kSlotPieceUnroll];
-        uint32_t need[kSlotPieceUnroll];
-        bool nl[kSlotPieceUnroll];
+        // this wave's piece of the frame (kLoop: pieces piece, piece + P, ...;
+        // without, the loop body once: the straight-line form measured 7 %
+        // faster when every frame fills its slot)
+        for (uint64_t c0 = piece * kSlotPiece; c0 < nb; c0 += pieces * kSlotPiece) {
+            const auto prs = __builtin_amdgcn_make_buffer_rsrc(out + run + c0, 0, (int)kSlotPiece, 0x00020000);
+            uint4 A[kSlotPieceUnroll], E[kSlotPieceUnroll];
+            uint32_t need[kSlotPieceUnroll];
+            bool nl[kSlotPieceUnroll];
 #pragma unroll
-        for (int u = 0; u < kSlotPieceUnroll; ++u) {
-            const uint64_t k0 = c0 + (uint64_t)u * 1024 + 16 * lane;
-            need[u] = k0 < len ? (uint32_t)(len - k0 < 16 ? len - k0 : 16) : 0u;
-            nl[u] = lane != 63 && k0 + 16 < len;                 // the next lane loads the next block
-            const uint64_t s = src + k0;
-            A[u] = need[u] ? ld16(wire + (s & ~uint64_t(15))) : z;
-            E[u] = need[u] && ph && !nl[u] && ph + need[u] > 16 ? ld16(wire + (s & ~uint64_t(15)) + 16) : z;
-        }
+            for (int u = 0; u < kSlotPieceUnroll; ++u) {
+                const uint64_t k0 = c0 + (uint64_t)u * 1024 + 16 * lane;
+                need[u] = k0 < len ? (uint32_t)(len - k0 < 16 ? len - k0 : 16) : 0u;
+                nl[u] = lane != 63 && k0 + 16 < len;                 // the next lane loads the next block
+                const uint64_t s = src + k0;
+                A[u] = need[u] ? ld16(wire + (s & ~uint64_t(15))) : z;
+                E[u] = need[u] && ph && !nl[u] && ph + need[u] > 16 ? ld16(wire + (s & ~uint64_t(15)) + 16) : z;
+            }
 #pragma unroll
-        for (int u = 0; u < kSlotPieceUnroll; ++u) {
-            const uint4 nb4 = from_next_lane(A[u], E[u]);       // every lane: DPP needs the full wave
-            const uint64_t k0 = c0 + (uint64_t)u * 1024 + 16 * lane;
-            if (k0 >= nb) continue;
-            uint4 o = z;
-            if (need[u]) {
-                o = ph ? funnel16(A[u], nl[u] ? nb4 : E[u], ph) : A[u];
-                xor4(o, key);
-                if (need[u] < 16) o = and4(o, byte_range(0, need[u]));
+            for (int u = 0; u < kSlotPieceUnroll; ++u) {
+                const uint4 nb4 = from_next_lane(A[u], E[u]);       // every lane: DPP needs the full wave
+                const uint64_t k0 = c0 + (uint64_t)u * 1024 + 16 * lane;
+                if (k0 >= nb) continue;
+                uint4 o = z;
+                if (need[u]) {
+                    o = ph ? funnel16(A[u], nl[u] ? nb4 : E[u], ph) : A[u];
+                    xor4(o, key);
+                    if (need[u] < 16) o = and4(o, byte_range(0, need[u]));
+                }
+                if (CFWS_SLOT_PIECE_AUX != 0 && run + k0 + 16 <= capacity) {
+                    // a buffer store over the wave's piece (cache policy CFWS_SLOT_PIECE_AUX)
+                    const u32x4 v = {o.x, o.y, o.z, o.w};
+                    __builtin_amdgcn_raw_buffer_store_b128(v, prs, (int)(k0 - c0), 0, CFWS_SLOT_PIECE_AUX);
+                } else {
+                    fused_store(out, run + k0, capacity, o);
+                }
             }
-            if (CFWS_SLOT_PIECE_AUX != 0 && run + k0 + 16 <= capacity) {
-                // a buffer store over the wave's piece (cache policy CFWS_SLOT_PIECE_AUX)
-                const u32x4 v = {o.x, o.y, o.z, o.w};
-                __builtin_amdgcn_raw_buffer_store_b128(v, prs, (int)(k0 - c0), 0, CFWS_SLOT_PIECE_AUX);
-            } else {
-                fused_store(out, run + k0, capacity, o);
-            }
+            if (!kLoop) break;
         }
     }
 }
-
 
 // Frames of at least CFWS_SLOT_SUB2_G lanes (default 33: slots of 496
 // bytes and more) that fit three to a 128-lane pair of sub-windows (up to
@@ -1235,12 +1245,16 @@ bool piece_pays(uint64_t slot)
     return slot % 128 == 0 && 20 * slot >= 17 * pieces * kSlotPiece;
 }
 
-SlotsRoute slots_route(uint64_t slot)
+SlotsRoute slots_route(uint64_t slot, uint64_t n, uint64_t wire_size)
 {
     static const uint64_t piece_min = (uint64_t)env_knob("CFWS_SLOTS_PIECE_MIN", 2048);   // A/B knob
-    const bool piece = slots_piece() && slot >= piece_min && (slot > kSlotWindow8Max || piece_pays(slot));
+    // the batch's average frame (wire bytes): pieces pay for frames that
+    // fill them, not for short frames in large slots
+    const uint64_t avg = n ? wire_size / n : 0;
+    const bool piece = slots_piece() && slot >= piece_min &&
+                       (slot > kSlotWindow8Max ? avg >= kSlotPiece : piece_pays(slot) && 20 * avg >= 17 * slot);
     if (slot <= kSlotWindow8Max && slots_window() && !piece) return kSlotsWindow;
-    return slots_piece() ? kSlotsPiece : kSlotsPerFrame;
+    return piece ? kSlotsPiece : kSlotsPerFrame;
 }
 
 // Single-pass plans above kSelfScanBlocks blocks (CFWS_PLAN_SINGLE=0: the
@@ -1838,7 +1852,7 @@ int slots_impl(const void* d_wire, uint64_t wire_size, const uint64_t* d_index, 
     const uint8_t* w = static_cast<const uint8_t*>(d_wire);
     uint8_t* out = static_cast<uint8_t*>(d_payload);
     const CfwsPassTimer timer(st);
-    const SlotsRoute route = slots_route(slot);
+    const SlotsRoute route = slots_route(slot, n, wire_size);
     if (route == kSlotsWindow) {
         // one wave-iteration of R P frames per wave (CFWS_SLOT_GRID caps the
         // workgroups: a grid-stride loop; A/B knob)
@@ -1894,14 +1908,25 @@ int slots_impl(const void* d_wire, uint64_t wire_size, const uint64_t* d_index, 
         else
             window(std::false_type{}, std::false_type{});
     } else if (route == kSlotsPiece) {
-        const uint64_t pieces = (slot + kSlotPiece - 1) / kSlotPiece;
+        // waves per frame: the slot's pieces, at most the pieces of the
+        // batch's average frame (its wire bytes; at least one)
+        const uint64_t slot_pieces = (slot + kSlotPiece - 1) / kSlotPiece;
+        const uint64_t avg_pieces = (wire_size / n + kSlotPiece - 1) / kSlotPiece;
+        const uint64_t pieces = avg_pieces < 1 ? 1 : avg_pieces < slot_pieces ? avg_pieces : slot_pieces;
+        const bool loop = pieces < slot_pieces;
         const uint64_t waves = n * pieces;
         const uint64_t want = (waves + kWaves - 1) / kWaves;
         const uint32_t grid = (uint32_t)(want < (1u << 22) ? want : (1u << 22));   // a grid-stride loop past that
         auto piecewise = [&](auto scatter, auto compact) {
-            deserialize_slots_piece_kernel<decltype(scatter)::value, decltype(compact)::value>
-                <<<grid, kThreads, 0, st>>>(w, wire_size, d_index, n, max_payload, slot, d_desc, d_status, out, cap,
-                                            d_total, dst, d_info, stride, d_mismatch, pieces);
+            constexpr bool kSc = decltype(scatter)::value, kIn = decltype(compact)::value;
+            if (loop)
+                deserialize_slots_piece_kernel<kSc, kIn, true><<<grid, kThreads, 0, st>>>(
+                    w, wire_size, d_index, n, max_payload, slot, d_desc, d_status, out, cap, d_total, dst, d_info,
+                    stride, d_mismatch, pieces);
+            else
+                deserialize_slots_piece_kernel<kSc, kIn, false><<<grid, kThreads, 0, st>>>(
+                    w, wire_size, d_index, n, max_payload, slot, d_desc, d_status, out, cap, d_total, dst, d_info,
+                    stride, d_mismatch, pieces);
         };
         if (scatter && info)
             piecewise(std::true_type{}, std::true_type{});
@@ -1988,9 +2013,9 @@ int cfws_deserialize_slots_uniform(const void* d_wire, uint64_t wire_size, size_
                       d_total, stream, false, "deserialize_slots_uniform", d_info, stride, d_mismatch);
 }
 
-const char* cfws_deserialize_slots_pass_kernel(uint64_t slot)
+const char* cfws_deserialize_slots_pass_kernel(size_t n, uint64_t wire_size, uint64_t slot)
 {
-    switch (slots_route(slot)) {
+    switch (slots_route(slot, n, wire_size)) {
     case kSlotsWindow: return "deserialize_slots_window_kernel";
     case kSlotsPiece: return "deserialize_slots_piece_kernel";
     default: return "deserialize_slots_kernel";

@@ -591,13 +591,15 @@ const char* cfws_deserialize_pass_kernel(size_t n_frames, uint64_t wire_size, ui
                                          uint32_t flags, uint64_t payload_capacity);
 
 /* The kernel the slot / scatter receives (cfws_deserialize_slots*,
- * cfws_deserialize_scatter*) launch for slots (max_slot) of this many bytes:
- * "deserialize_slots_piece_kernel" (one wave per 2 KiB piece of a frame's
- * slot: slots over 8,160 bytes, and from 2 KiB those that are multiples of
- * 128 filling at least 85 % of their pieces) or
- * "deserialize_slots_window_kernel" (the rest). The calls' own rule. A
- * static string. */
-const char* cfws_deserialize_slots_pass_kernel(uint64_t slot_bytes);
+ * cfws_deserialize_scatter*) launch for n_frames frames in wire_size bytes
+ * and slots (max_slot) of slot_bytes: "deserialize_slots_piece_kernel" (one
+ * wave per 2 KiB piece of a frame's slot: slots over 8,160 bytes whose frames
+ * average at least 2 KiB, and from 2 KiB slots that are multiples of 128
+ * filling at least 85 % of their pieces, with frames averaging 85 % of the
+ * slot), "deserialize_slots_window_kernel" (other slots up to 8,160 bytes) or
+ * "deserialize_slots_kernel" (other slots over 8,160 bytes: short frames in
+ * large slots). The calls' own rule. A static string. */
+const char* cfws_deserialize_slots_pass_kernel(size_t n_frames, uint64_t wire_size, uint64_t slot_bytes);
 
 /* The kernel cfws_serialize_uniform launches for frames of payload_size
  * bytes (masked or not): "serialize_uniform_small_kernel" (payloads of

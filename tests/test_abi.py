@@ -209,7 +209,12 @@ def test_deserialize_slots_pass_kernel_routes():
     """cfws_deserialize_slots_pass_kernel names the slot receives' kernel."""
     from coldforce_amd import cfws
     f = cfws.lib().cfws_deserialize_slots_pass_kernel
+    full = lambda slot: f(1000, 1000 * (slot + 8), slot).decode()           # frames that fill their slots
     for slot in (16, 256, 1024, 2560, 3072, 4064, 5120, 8160):
-        assert f(slot).decode() == "deserialize_slots_window_kernel", slot
+        assert full(slot) == "deserialize_slots_window_kernel", slot
     for slot in (2048, 3584, 4096, 6144, 7680, 8176, 65536, 1 << 31):   # pieces >= 85 % used, on 128-B lines
-        assert f(slot).decode() == "deserialize_slots_piece_kernel", slot
+        assert full(slot) == "deserialize_slots_piece_kernel", slot
+    # short frames in large slots
+    assert f(1000, 1000 * 264, 4096).decode() == "deserialize_slots_window_kernel"
+    assert f(1000, 1000 * 264, 16384).decode() == "deserialize_slots_kernel"
+    assert f(1000, 1000 * 4104, 65536).decode() == "deserialize_slots_piece_kernel"

@@ -236,3 +236,18 @@ def test_uniform_receive_arguments():
     cfws.deserialize_slots_uniform(w, 64, 0, 20, out, 16, info, total_t=tot, mismatch_t=mm)
     torch.cuda.synchronize()
     assert mm.item() == 0 and tot.item() == 0
+
+
+@pytest.mark.parametrize("fs,slot", [(4096, 16384), (3000, 65536), (2100, 8192), (9000, 20480), (1000, 16384),
+                                     (256, 4096)])
+def test_uniform_receive_slots_larger_than_frames(fs, slot):
+    """Frames shorter than their slots: the piece kernel with fewer waves per
+    frame than the slot has pieces (each wave taking every P-th piece), the
+    window kernel, or the per-frame kernel, as the batch's average frame
+    routes it -- against the oracle and the indexed receive."""
+    n = 700
+    payload, keys, d = _frames(n, fs, 1, 1, 2, fs + slot)
+    wire, _ = O.serialize_batch(payload, d)
+    stride = cfws.uniform_frame_bytes(fs, True)
+    st, odd = _recv(wire, len(wire), n, stride, slot)
+    assert (st == O.PARSE_COMPLETE).all() and odd == 0
