@@ -596,9 +596,11 @@ const char* cfws_deserialize_pass_kernel(size_t n_frames, uint64_t wire_size, ui
  * wave per 2 KiB piece of a frame's slot: slots over 8,160 bytes whose frames
  * average at least 2 KiB, and from 2 KiB slots that are multiples of 128
  * filling at least 85 % of their pieces, with frames averaging 85 % of the
- * slot), "deserialize_slots_window_kernel" (other slots up to 8,160 bytes) or
- * "deserialize_slots_kernel" (other slots over 8,160 bytes: short frames in
- * large slots). The calls' own rule. A static string. */
+ * slot), "deserialize_slots_kernel" (short frames in large slots: frames
+ * averaging under 2 KiB in slots over 8,160 bytes; frames of up to 1 KiB
+ * filling under half their slot, or under 80 % of a slot of 1 KiB or more)
+ * or "deserialize_slots_window_kernel" (the rest). The calls' own rule. A
+ * static string. */
 const char* cfws_deserialize_slots_pass_kernel(size_t n_frames, uint64_t wire_size, uint64_t slot_bytes);
 
 /* The kernel cfws_serialize_uniform launches for frames of payload_size

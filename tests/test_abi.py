@@ -214,7 +214,10 @@ def test_deserialize_slots_pass_kernel_routes():
         assert full(slot) == "deserialize_slots_window_kernel", slot
     for slot in (2048, 3584, 4096, 6144, 7680, 8176, 65536, 1 << 31):   # pieces >= 85 % used, on 128-B lines
         assert full(slot) == "deserialize_slots_piece_kernel", slot
-    # short frames in large slots
-    assert f(1000, 1000 * 264, 4096).decode() == "deserialize_slots_window_kernel"
+    # frames shorter than their slots
+    assert f(1000, 1000 * 264, 4096).decode() == "deserialize_slots_kernel"        # 6 % full
+    assert f(1000, 1000 * 776, 1024).decode() == "deserialize_slots_kernel"        # 76 % of a 1 KiB slot
+    assert f(1000, 1000 * 134, 256).decode() == "deserialize_slots_window_kernel"  # 52 % of 256 B
+    assert f(1000, 1000 * 2056, 4096).decode() == "deserialize_slots_window_kernel"  # 2 KiB frames
     assert f(1000, 1000 * 264, 16384).decode() == "deserialize_slots_kernel"
     assert f(1000, 1000 * 4104, 65536).decode() == "deserialize_slots_piece_kernel"
