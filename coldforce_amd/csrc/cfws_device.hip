@@ -1252,7 +1252,7 @@ SlotsRoute slots_route(uint64_t slot, uint64_t n, uint64_t wire_size)
     // fill them, not for short frames in large slots
     const uint64_t avg = n ? wire_size / n : 0;
     const bool piece = slots_piece() && slot >= piece_min &&
-                       (slot > kSlotWindow8Max ? avg >= kSlotPiece : piece_pays(slot) && 20 * avg >= 17 * slot);
+                       (slot > kSlotWindow8Max ? avg > 1040 : piece_pays(slot) && 20 * avg >= 17 * slot);
     // a window spans the whole slot, whatever the frame: frames of up to
     // 1 KiB filling under half their slot (under 80 % of a slot of 1 KiB or
     // more) take the per-frame kernel, which packs them into shared

@@ -594,10 +594,10 @@ const char* cfws_deserialize_pass_kernel(size_t n_frames, uint64_t wire_size, ui
  * cfws_deserialize_scatter*) launch for n_frames frames in wire_size bytes
  * and slots (max_slot) of slot_bytes: "deserialize_slots_piece_kernel" (one
  * wave per 2 KiB piece of a frame's slot: slots over 8,160 bytes whose frames
- * average at least 2 KiB, and from 2 KiB slots that are multiples of 128
+ * average over 1,040 bytes, and from 2 KiB slots that are multiples of 128
  * filling at least 85 % of their pieces, with frames averaging 85 % of the
  * slot), "deserialize_slots_kernel" (short frames in large slots: frames
- * averaging under 2 KiB in slots over 8,160 bytes; frames of up to 1 KiB
+ * averaging up to 1,040 bytes in slots over 8,160 bytes; frames of up to 1 KiB
  * filling under half their slot, or under 80 % of a slot of 1 KiB or more)
  * or "deserialize_slots_window_kernel" (the rest). The calls' own rule. A
  * static string. */

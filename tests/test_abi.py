@@ -221,3 +221,5 @@ def test_deserialize_slots_pass_kernel_routes():
     assert f(1000, 1000 * 2056, 4096).decode() == "deserialize_slots_window_kernel"  # 2 KiB frames
     assert f(1000, 1000 * 264, 16384).decode() == "deserialize_slots_kernel"
     assert f(1000, 1000 * 4104, 65536).decode() == "deserialize_slots_piece_kernel"
+    assert f(1000, 1000 * 1508, 16384).decode() == "deserialize_slots_piece_kernel"   # one wave per frame
+    assert f(1000, 1000 * 1032, 16384).decode() == "deserialize_slots_kernel"
