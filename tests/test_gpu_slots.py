@@ -289,6 +289,23 @@ def test_scatter_permuted(guards, max_slot):
     run_slots(guards, wire, starts, max_slot, cap=cap, offs=offs)
 
 
+@pytest.mark.parametrize("fs,max_slot", [(9000, 9008), (4096, 4096), (2048, 2048), (20000, 20480), (3000, 16384)])
+def test_scatter_pieces(guards, fs, max_slot):
+    """The piece kernel through the scatter form (frames that fill their
+    slots, or average past 1 KiB in slots over 8,160 B): shuffled
+    destinations with gaps, and a capacity that cuts the last slots."""
+    n = max(40, min(600, (6 << 20) // max_slot))
+    desc = W.uniform_batch(n, fs, 5, opcode=cfws.OPCODE_BINARY)
+    payload = O.fill_splitmix(n * fs, 0x5EED0005, 0)
+    wire, starts = _wire_of(payload, desc)
+    assert cfws.lib().cfws_deserialize_slots_pass_kernel(n, len(wire), max_slot).decode() == \
+        "deserialize_slots_piece_kernel"
+    rng = np.random.default_rng(fs)
+    offs, cap = _scatter_offsets(n, max_slot, rng)
+    run_slots(guards, wire, starts, max_slot, cap=cap, offs=offs)
+    run_slots(guards, wire, starts, max_slot, cap=cap - 3 * max_slot - 5, offs=offs)
+
+
 def test_scatter_bad_offsets(guards):
     """Offsets that are not multiples of 16, that end past the capacity, or
     that are near 2^64 (no wrap): OUT_OF_MEMORY, nothing written for them."""
